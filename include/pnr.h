@@ -1,0 +1,150 @@
+/*
+ * pnr.h -- C ABI of the MI355X (gfx950) neural volume renderer `libpnr.so`.
+ *
+ * Drop-in boundary for the `render_batch_ray` hot path of thua919/pointNeRF-SLAM
+ * (src/utils/Renderer.py + src/common.py + src/conv_onet/models/decoder.py).  The Python
+ * host mirror `pnr` (pointnerf-slam_amd/pnr/) binds these symbols with ctypes; any other
+ * FFI (cgo, JNI, N-API) can bind them the same way -- see INTEGRATION.md.
+ *
+ * Conventions
+ *  - Every pointer argument is a DEVICE pointer owned by the caller, except `pnr_render_params`
+ *    and the `const float* const*` parameter-table arrays, which are HOST structs holding device
+ *    pointers.  The library allocates no device memory and keeps no per-call state; scratch comes
+ *    from the caller's workspace (size from the matching *_workspace_bytes query).
+ *  - `stream` is a hipStream_t passed as void* (0 = legacy default stream).  All calls are
+ *    asynchronous and stream-ordered; they are re-entrant (no global mutable state except a
+ *    per-thread cache of rocBLAS handles used by pnr_render_bwd / pnr_mlp_bwd).
+ *  - Return value: 0 on success, a negative PNR_E* code on argument errors, or a positive
+ *    hipError_t when a launch fails.  No exception ever crosses the ABI.
+ *  - Dtypes follow the reference exactly: sample depths z / points / depth / variance are
+ *    float64, rays / colours / densities / MLP weights are float32.
+ *
+ * Decoder parameter table (`params[11]`), the reference state_dict order
+ * (src/conv_onet/models/decoder.py:128-159; src/conv_onet/config.py:29-31):
+ *    0 embedder._B            (3,93)      1 pts_linears.0.weight (256,93)   2 pts_linears.0.bias (256)
+ *    3 pts_linears.1.weight   (256,256)   4 pts_linears.1.bias   (256)
+ *    5 pts_linears.2.weight   (256,256)   6 pts_linears.2.bias   (256)
+ *    7 pts_linears.3.weight   (256,256)   8 pts_linears.3.bias   (256)
+ *    9 output_linear.weight   (4,256)    10 output_linear.bias   (4)
+ * all contiguous row-major float32.
+ */
+#ifndef PNR_H_
+#define PNR_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PNR_ABI_VERSION 1
+#define PNR_N_PARAMS 11
+#define PNR_MAX_SAMPLES 64      /* N_samples + N_importance per ray */
+
+enum {
+  PNR_OK = 0,
+  PNR_E_ARG = -1,        /* bad argument (null pointer, negative size, unsupported config) */
+  PNR_E_WORKSPACE = -2,  /* workspace smaller than *_workspace_bytes */
+  PNR_E_BLAS = -3,       /* rocBLAS failure */
+};
+
+/* Renderer configuration: the cfg keys Renderer.__init__ reads (src/utils/Renderer.py:6-21)
+ * plus host-computed torch.linspace tables (Renderer.py:157, common.py:33). */
+typedef struct pnr_render_params {
+  int32_t n_samples;        /* cfg['rendering']['N_samples']  (<= 64)            */
+  int32_t n_importance;     /* cfg['rendering']['N_importance'] (n_samples+n_importance <= 64) */
+  int32_t lindisp;          /* cfg['rendering']['lindisp']                       */
+  int32_t far_mode;         /* 0: clamp far to max(1.2*gt) of THIS batch (Renderer.py:112);
+                               1: clamp to `far_clamp` (global max supplied by a sharded caller) */
+  double bound[6];          /* slam.bound (3,2) float64 row-major: x0,x1,y0,y1,z0,z1   */
+  double far_clamp;         /* used when far_mode == 1                                 */
+  float t_vals[PNR_MAX_SAMPLES];   /* torch.linspace(0,1,n_samples) float32           */
+  float u_vals[PNR_MAX_SAMPLES];   /* torch.linspace(0,1,n_importance) float32        */
+  int32_t save_for_backward;       /* keep MLP activations in the workspace for pnr_render_bwd */
+  int32_t need_ray_grads;          /* backward also produces dL/drays_o, dL/drays_d (tracking) */
+} pnr_render_params;
+
+/* ---- library identity -------------------------------------------------------------------- */
+int pnr_abi_version(void);
+const char* pnr_build_info(void);
+
+/* ---- decoder: MLP.forward / eval_points -------------------------------------------------- */
+/* Number of float32 words of the packed (MFMA-fragment-ordered) weight image. */
+size_t pnr_mlp_packed_floats(void);
+/* Builds the packed image from the 11 reference tensors (params: host array of device ptrs).
+ * Must be re-run after every optimizer step (the image is a pure function of the weights). */
+int pnr_mlp_pack(const float* const* params, float* packed, void* stream);
+
+/* Renderer.eval_points (src/utils/Renderer.py:23-61): raw[P,4] = MLP(p) with raw[:,3] := 100
+ * where p is not strictly inside `bound6`.  p float64 (P,3). */
+int pnr_eval_points(const float* packed, const double* p, int64_t P, const double* bound6,
+                    float* raw_out, void* stream);
+/* Same for float32 points (MLP.forward on f32 input, decoder.py:177-203); bound6 may be NULL
+ * (then no masking).  The mask comparison is done in float32 as torch does for f32 points. */
+int pnr_eval_points_f32(const float* packed, const float* p, int64_t P, const double* bound6,
+                        float* raw_out, void* stream);
+
+/* MLP.forward with autograd (decoder.py:177-203 on float32 points, no bound mask): the forward
+ * keeps activations in `ws` (size pnr_mlp_train_workspace_bytes(P)); pnr_mlp_bwd consumes them.
+ * g_raw (P,4) float32; grads accumulated (+=); g_p (P,3) written when non-NULL. */
+size_t pnr_mlp_train_workspace_bytes(int64_t P);
+int pnr_mlp_fwd_train(const float* packed, const float* p, int64_t P, float* raw_out, void* ws, size_t ws_bytes,
+                      void* stream);
+size_t pnr_mlp_bwd_workspace_bytes(int64_t P);
+int pnr_mlp_bwd(const float* packed, int64_t P, const float* g_raw, float* const* grads, float* g_p, void* ws,
+                size_t ws_bytes, void* bwd_ws, size_t bwd_bytes, void* stream);
+
+/* ---- render_batch_ray (src/utils/Renderer.py:63-203) ------------------------------------- */
+size_t pnr_render_workspace_bytes(const pnr_render_params* prm, int64_t n_rays);
+/* Forward.  depth, var: float64 (N); rgb float32 (N,3).  gt_depth may be NULL (gt_depth=None).
+ * The workspace must stay untouched between this call and pnr_render_bwd. */
+int pnr_render_fwd(const pnr_render_params* prm, const float* packed,
+                   const float* rays_o, const float* rays_d, const float* gt_depth, int64_t n_rays,
+                   double* depth, double* var, float* rgb,
+                   void* workspace, size_t ws_bytes, void* stream);
+/* Backward of the final (44-sample) pass.  Inputs are dL/ddepth, dL/dvar (float64, may be NULL
+ * = zero), dL/drgb (float32, may be NULL).  Outputs: `grads` = host array of 11 device pointers
+ * receiving dL/dparam (ACCUMULATED: +=, reference layout), g_rays_o / g_rays_d (N,3) float32
+ * written (not accumulated) when prm->need_ray_grads, else ignored (may be NULL).
+ * `params` = the same 11 raw tensors (needed for the transposed weight images). */
+size_t pnr_render_bwd_workspace_bytes(const pnr_render_params* prm, int64_t n_rays);
+int pnr_render_bwd(const pnr_render_params* prm, const float* packed, const float* const* params,
+                   const float* rays_o, const float* rays_d, int64_t n_rays,
+                   const double* g_depth, const double* g_var, const float* g_rgb,
+                   float* const* grads, float* g_rays_o, float* g_rays_d,
+                   void* workspace, size_t ws_bytes,
+                   void* bwd_workspace, size_t bwd_ws_bytes, void* stream);
+
+/* ---- Renderer.regulation (src/utils/Renderer.py:263-301) --------------------------------- */
+/* sigma[N*n_samples] = density at z = lower + (upper-lower)*t_rand in [0, 0.85*gt], float32 z.
+ * t_rand (N, n_samples) float32 replaces the reference's torch.rand draw (Renderer.py:293). */
+size_t pnr_regulation_workspace_bytes(const pnr_render_params* prm, int64_t n_rays);
+int pnr_regulation_fwd(const pnr_render_params* prm, const float* packed,
+                       const float* rays_o, const float* rays_d, const float* gt_depth,
+                       const float* t_rand, int64_t n_rays, float* sigma,
+                       void* workspace, size_t ws_bytes, void* stream);
+size_t pnr_regulation_bwd_workspace_bytes(const pnr_render_params* prm, int64_t n_rays);
+int pnr_regulation_bwd(const pnr_render_params* prm, const float* packed, const float* const* params,
+                       const float* rays_o, const float* rays_d, int64_t n_rays,
+                       const float* g_sigma, float* const* grads, float* g_rays_o, float* g_rays_d,
+                       void* workspace, size_t ws_bytes,
+                       void* bwd_workspace, size_t bwd_ws_bytes, void* stream);
+
+/* ---- rays (src/common.py:74-89, 248-266) ------------------------------------------------- */
+/* Full-frame rays, row-major (H,W,3) float32; c2w (3,4) or (4,4) float32 row-major on device. */
+int pnr_get_rays(int32_t H, int32_t W, float fx, float fy, float cx, float cy, const float* c2w,
+                 float* rays_o, float* rays_d, void* stream);
+/* Rays for pixel coordinates i (column), j (row), float32 (n). */
+int pnr_rays_from_uv(const float* i, const float* j, int64_t n, float fx, float fy, float cx, float cy,
+                     const float* c2w, float* rays_o, float* rays_d, void* stream);
+
+/* ---- optimizer (src/Mapper.py:498-502, 657-662: torch.optim.Adam, default betas/eps) ----- */
+/* One Adam step over `n` float32 words: p -= lr * mhat / (sqrt(vhat) + eps).  step >= 1. */
+int pnr_adam_step(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1,
+                  float beta2, float eps, int64_t step, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PNR_H_ */

@@ -1,0 +1,507 @@
+// capi.cpp -- extern "C" entry points of libpnr.so (declared in include/pnr.h).
+//
+// Orchestrates the kernels of mlp.hip / render.hip for one render_batch_ray call
+// (src/utils/Renderer.py:63-203):
+//   gt_max -> coarse_z -> MLP(coarse points) -> pdf (importance z) -> MLP(importance points)
+//   -> fine (sort + compositing)
+// The first pass's 32 points are NOT re-evaluated in the second pass (the reference does,
+// Renderer.py:193-196): the same float64 depth gives the same float32 MLP input and the same
+// output, so the fine pass gathers them from the coarse results through the sort order.
+//
+// Backward: compositing backward -> per point dL/draw -> (chunks of <= kBwdChunk points)
+// delta chain kernel -> weight-gradient GEMMs on rocBLAS (sgemm / sgemv, accumulate) ->
+// optional ray gradients.
+#include <hip/hip_runtime.h>
+#include <rocblas/rocblas.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+
+#include "pnr_internal.h"
+
+namespace pnr {
+int launch_gt_max(const float*, int64_t, float*, hipStream_t);
+int launch_coarse_z(const pnr_render_params&, const float*, const float*, const float*, const float*, int64_t,
+                    double*, double*, hipStream_t);
+int launch_pdf(const pnr_render_params&, const float*, const double*, const float*, int64_t, double*, hipStream_t);
+int launch_fine(const pnr_render_params&, const float*, const double*, const double*, const float*, const float*,
+                int64_t, double*, double*, float*, uint8_t*, hipStream_t);
+int launch_fine_bwd(const pnr_render_params&, const float*, const double*, const double*, const float*,
+                    const float*, const uint8_t*, const uint8_t*, const uint8_t*, int64_t, const double*,
+                    const double*, const float*, float*, float*, float*, hipStream_t);
+int launch_ray_grads_f64(const float*, const double*, int, const double*, int, const float*, const float*,
+                         const float*, int64_t, float*, float*, hipStream_t);
+int launch_ray_grads_f32(const float*, const float*, int, const float*, int64_t, float*, float*, hipStream_t);
+int launch_reg_z(const pnr_render_params&, const float*, const float*, int64_t, float*, hipStream_t);
+int launch_extract_sigma(const float*, int64_t, float*, hipStream_t);
+int launch_gout_sigma(const float*, const uint8_t*, int64_t, float*, hipStream_t);
+int launch_get_rays(int, int, float, float, float, float, const float*, float*, float*, hipStream_t);
+int launch_rays_from_uv(const float*, const float*, int64_t, float, float, float, float, const float*, float*,
+                        float*, hipStream_t);
+int launch_adam(float*, const float*, float*, float*, int64_t, float, float, float, float, float, hipStream_t);
+}  // namespace pnr
+
+using namespace pnr;
+
+namespace {
+
+constexpr size_t kAlign = 256;
+constexpr int64_t kBwdChunk = 1 << 20;  // points per delta-chain / GEMM chunk
+
+inline size_t align_up(size_t x) { return (x + kAlign - 1) / kAlign * kAlign; }
+inline int64_t pad128(int64_t x) { return (x + 127) / 128 * 128; }
+
+// Linear carve of a caller-provided workspace.
+struct Carver {
+  char* base;
+  size_t off = 0;
+  explicit Carver(void* b) : base(static_cast<char*>(b)) {}
+  template <typename T>
+  T* take(size_t count) {
+    T* p = base ? reinterpret_cast<T*>(base + off) : nullptr;
+    off += align_up(count * sizeof(T));
+    return p;
+  }
+};
+
+bool valid_prm(const pnr_render_params* p) {
+  return p && p->n_samples >= 2 && p->n_importance >= 0 && p->n_samples + p->n_importance <= PNR_MAX_SAMPLES;
+}
+
+// Forward workspace of render_batch_ray.
+struct RenderWS {
+  float* gmax;
+  double* z;       // [N*S coarse | N*I importance]
+  float* raw;      // float4 per point, same order
+  uint8_t* ord;    // [N][64]
+  double* far;     // [N]
+  int64_t pc_pad;  // first saved column of the importance segment (coarse points padded to 128)
+  SaveArgs save;   // when save_for_backward; columns [0,pc_pad) coarse, [pc_pad, ld) importance
+};
+
+SaveArgs carve_save(Carver& c, int64_t ld) {
+  SaveArgs s{};
+  s.ld = ld;
+  s.p0 = 0;
+  s.eT = c.take<float>(kFourierPad * ld);
+  s.hT = c.take<float>((size_t)4 * kHidden * ld);
+  s.xT = c.take<float>(3 * ld);
+  s.inside = c.take<uint8_t>(ld);
+  s.masks = c.take<uint4>((size_t)4 * (ld / 32) * 64);
+  return s;
+}
+
+RenderWS carve_render(const pnr_render_params* prm, int64_t n, void* ws, size_t* bytes) {
+  Carver c(ws);
+  RenderWS w{};
+  const int64_t P = n * (prm->n_samples + prm->n_importance);
+  w.gmax = c.take<float>(1);
+  w.z = c.take<double>(P);
+  w.raw = c.take<float>(P * 4);
+  w.ord = c.take<uint8_t>(n * PNR_MAX_SAMPLES);
+  w.far = c.take<double>(n);
+  w.pc_pad = pad128(n * prm->n_samples);
+  if (prm->save_for_backward) w.save = carve_save(c, w.pc_pad + pad128(n * prm->n_importance));
+  if (bytes) *bytes = c.off;
+  return w;
+}
+
+// Backward scratch shared by render and regulation.
+struct BwdWS {
+  float* g_out;   // [P] float4
+  float* g_x;     // [P][3]
+  float* g_nrm;   // [N]
+  float* dT;      // [4][256][C]
+  float* gargT;   // [96][C]
+  float* goutT;   // [4][C]
+  float* ones;    // [C]
+  int64_t C;
+};
+
+BwdWS carve_bwd(int64_t P, int64_t n, void* ws, size_t* bytes) {
+  Carver c(ws);
+  BwdWS b{};
+  b.C = P < kBwdChunk ? ((P + 127) / 128) * 128 : kBwdChunk;
+  if (b.C < 128) b.C = 128;
+  b.g_out = c.take<float>(P * 4);
+  b.g_x = c.take<float>(P * 3);
+  b.g_nrm = c.take<float>(n);
+  b.dT = c.take<float>((size_t)4 * kHidden * b.C);
+  b.gargT = c.take<float>(kFourierPad * b.C);
+  b.goutT = c.take<float>(4 * b.C);
+  b.ones = c.take<float>(b.C);
+  if (bytes) *bytes = c.off;
+  return b;
+}
+
+// ---- rocBLAS ------------------------------------------------------------------------------
+rocblas_handle blas_handle(hipStream_t st) {
+  thread_local rocblas_handle h = nullptr;
+  if (!h && rocblas_create_handle(&h) != rocblas_status_success) return nullptr;
+  rocblas_set_stream(h, st);
+  return h;
+}
+
+// row-major C[M][Nc] (ldc) += A[M][K] (lda) * B[Nc][K]^T (ldb)
+bool gemm_abt(rocblas_handle h, int M, int Nc, int64_t K, const float* A, int64_t lda, const float* B,
+              int64_t ldb, float* C, int64_t ldc) {
+  const float one = 1.f;
+  return rocblas_sgemm(h, rocblas_operation_transpose, rocblas_operation_none, Nc, M, (rocblas_int)K, &one, B,
+                       (rocblas_int)ldb, A, (rocblas_int)lda, &one, C, (rocblas_int)ldc) == rocblas_status_success;
+}
+// y[M] += sum_k A[M][k]  (row-major A, lda)
+bool rowsum(rocblas_handle h, int M, int64_t K, const float* A, int64_t lda, const float* ones, float* y) {
+  const float one = 1.f;
+  return rocblas_sgemv(h, rocblas_operation_transpose, (rocblas_int)K, M, &one, A, (rocblas_int)lda, ones, 1, &one,
+                       y, 1) == rocblas_status_success;
+}
+
+__global__ void k_fill(float* p, int64_t n, float v) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[i] = v;
+}
+
+// Shared backward core over P points with saved activations `sv` and dL/draw in b.g_out.
+int mlp_backward_core(const float* packed, const SaveArgs& sv, int64_t P, BwdWS& b, float* const* grads,
+                      bool want_gx, hipStream_t st) {
+  rocblas_handle h = blas_handle(st);
+  if (!h) return PNR_E_BLAS;
+  hipLaunchKernelGGL(k_fill, dim3((unsigned)((b.C + 255) / 256)), dim3(256), 0, st, b.ones, b.C, 1.f);
+  for (int64_t p0 = 0; p0 < P; p0 += b.C) {
+    const int64_t C = (P - p0) < b.C ? (P - p0) : b.C;
+    BwdArgs a;
+    a.g_out = b.g_out + p0 * 4;
+    a.masks = sv.masks;
+    a.xT = sv.xT;
+    a.dT = b.dT;
+    a.gargT = b.gargT;
+    a.g_x = want_gx ? b.g_x + p0 * 3 : nullptr;
+    a.goutT = b.goutT;
+    a.ld = sv.ld;
+    a.p0 = p0;
+    a.ld_d = b.C;
+    int rc = launch_mlp_bwd(packed, a, C, st);
+    if (rc) return rc;
+    const int64_t ld = sv.ld, ldd = b.C;
+    const float* h1 = sv.hT + p0;
+    bool ok = true;
+    // output layer: dWo (4x256) += goutT (4xC) . h4^T ; dbo += rowsum(goutT)
+    ok &= gemm_abt(h, 4, kHidden, C, b.goutT, ldd, h1 + 3 * (int64_t)kHidden * ld, ld, grads[9], kHidden);
+    ok &= rowsum(h, 4, C, b.goutT, ldd, b.ones, grads[10]);
+    // hidden layers: dW_l += delta_{l+1} . h_l^T   (W3: delta4.h3, W2: delta3.h2, W1: delta2.h1)
+    for (int l = 3; l >= 1; --l) {
+      const float* dl = b.dT + (int64_t)l * kHidden * ldd;  // delta_{l+1}
+      ok &= gemm_abt(h, kHidden, kHidden, C, dl, ldd, h1 + (int64_t)(l - 1) * kHidden * ld, ld, grads[1 + 2 * l],
+                     kHidden);
+      ok &= rowsum(h, kHidden, C, dl, ldd, b.ones, grads[2 + 2 * l]);
+    }
+    // first layer: dW0 (256x93) += delta1 . e^T ; db0
+    ok &= gemm_abt(h, kHidden, kFourier, C, b.dT, ldd, sv.eT + p0, ld, grads[1], kFourier);
+    ok &= rowsum(h, kHidden, C, b.dT, ldd, b.ones, grads[2]);
+    // Fourier: dB (3x93) += x^T . g_arg  ->  row-major C[3][93] += xT (3xC) . gargT(93xC)^T
+    ok &= gemm_abt(h, 3, kFourier, C, sv.xT + p0, ld, b.gargT, ldd, grads[0], kFourier);
+    if (!ok) return PNR_E_BLAS;
+  }
+  return hip_status(hipGetLastError());
+}
+
+bool check_params(const float* const* params) {
+  if (!params) return false;
+  for (int i = 0; i < PNR_N_PARAMS; ++i)
+    if (!params[i]) return false;
+  return true;
+}
+
+}  // namespace
+
+extern "C" {
+
+int pnr_abi_version(void) { return PNR_ABI_VERSION; }
+
+const char* pnr_build_info(void) {
+  return "libpnr gfx950: fp32 v_mfma_f32_32x32x2_f32 fused decoder, LDS-streamed weights; "
+         "thread-per-ray compositing; rocBLAS weight-gradient GEMMs";
+}
+
+size_t pnr_mlp_packed_floats(void) { return (size_t)kPackedFloats; }
+
+int pnr_mlp_pack(const float* const* params, float* packed, void* stream) {
+  if (!check_params(params) || !packed) return PNR_E_ARG;
+  RawParams rp;
+  for (int i = 0; i < PNR_N_PARAMS; ++i) rp.p[i] = params[i];
+  return launch_pack(rp, packed, (hipStream_t)stream);
+}
+
+int pnr_eval_points(const float* packed, const double* p, int64_t P, const double* bound6, float* raw_out,
+                    void* stream) {
+  if (!packed || P < 0 || (P > 0 && (!p || !raw_out))) return PNR_E_ARG;
+  PointSrc s{};
+  s.pts = p;
+  s.use_bound = bound6 != nullptr;
+  if (bound6) memcpy(s.bound, bound6, sizeof(s.bound));
+  return launch_mlp_fwd(packed, s, kPtsF64, P, raw_out, nullptr, (hipStream_t)stream);
+}
+
+int pnr_eval_points_f32(const float* packed, const float* p, int64_t P, const double* bound6, float* raw_out,
+                        void* stream) {
+  if (!packed || P < 0 || (P > 0 && (!p || !raw_out))) return PNR_E_ARG;
+  PointSrc s{};
+  s.pts = p;
+  s.use_bound = bound6 != nullptr;
+  if (bound6) memcpy(s.bound, bound6, sizeof(s.bound));
+  return launch_mlp_fwd(packed, s, kPtsF32, P, raw_out, nullptr, (hipStream_t)stream);
+}
+
+size_t pnr_mlp_train_workspace_bytes(int64_t P) {
+  if (P < 0) return 0;
+  Carver c(nullptr);
+  carve_save(c, pad128(P));
+  return c.off;
+}
+
+int pnr_mlp_fwd_train(const float* packed, const float* p, int64_t P, float* raw_out, void* ws, size_t ws_bytes,
+                      void* stream) {
+  if (!packed || P < 0 || (P > 0 && (!p || !raw_out || !ws))) return PNR_E_ARG;
+  if (P == 0) return PNR_OK;
+  Carver c(ws);
+  SaveArgs sv = carve_save(c, pad128(P));
+  if (ws_bytes < c.off) return PNR_E_WORKSPACE;
+  PointSrc s{};
+  s.pts = p;
+  s.use_bound = 0;
+  return launch_mlp_fwd(packed, s, kPtsF32, P, raw_out, &sv, (hipStream_t)stream);
+}
+
+size_t pnr_mlp_bwd_workspace_bytes(int64_t P) {
+  if (P < 0) return 0;
+  size_t b = 0;
+  carve_bwd(pad128(P), 1, nullptr, &b);
+  return b;
+}
+
+int pnr_mlp_bwd(const float* packed, int64_t P, const float* g_raw, float* const* grads, float* g_p, void* ws,
+                size_t ws_bytes, void* bwd_ws, size_t bwd_bytes, void* stream) {
+  if (!packed || P < 0 || (P > 0 && (!g_raw || !grads || !ws || !bwd_ws))) return PNR_E_ARG;
+  if (P == 0) return PNR_OK;
+  for (int i = 0; i < PNR_N_PARAMS; ++i)
+    if (!grads[i]) return PNR_E_ARG;
+  Carver c(ws);
+  SaveArgs sv = carve_save(c, pad128(P));
+  size_t bneed = 0;
+  BwdWS b = carve_bwd(sv.ld, 1, bwd_ws, &bneed);
+  if (ws_bytes < c.off || bwd_bytes < bneed) return PNR_E_WORKSPACE;
+  hipStream_t st = (hipStream_t)stream;
+  if (hipMemsetAsync(b.g_out, 0, (size_t)sv.ld * 16, st) != hipSuccess) return (int)hipGetLastError();
+  if (hipMemcpyAsync(b.g_out, g_raw, (size_t)P * 16, hipMemcpyDeviceToDevice, st) != hipSuccess)
+    return (int)hipGetLastError();
+  int rc = mlp_backward_core(packed, sv, sv.ld, b, grads, g_p != nullptr, st);
+  if (rc) return rc;
+  if (g_p && hipMemcpyAsync(g_p, b.g_x, (size_t)P * 12, hipMemcpyDeviceToDevice, st) != hipSuccess)
+    return (int)hipGetLastError();
+  return PNR_OK;
+}
+
+size_t pnr_render_workspace_bytes(const pnr_render_params* prm, int64_t n_rays) {
+  if (!valid_prm(prm) || n_rays < 0) return 0;
+  size_t b = 0;
+  carve_render(prm, n_rays, nullptr, &b);
+  return b;
+}
+
+int pnr_render_fwd(const pnr_render_params* prm, const float* packed, const float* rays_o, const float* rays_d,
+                   const float* gt_depth, int64_t n, double* depth, double* var, float* rgb, void* workspace,
+                   size_t ws_bytes, void* stream) {
+  if (!valid_prm(prm) || !packed || n < 0) return PNR_E_ARG;
+  if (n == 0) return PNR_OK;
+  if (!rays_o || !rays_d || !depth || !var || !rgb || !workspace) return PNR_E_ARG;
+  if (prm->n_importance > 0 && prm->n_samples < 3) return PNR_E_ARG;
+  size_t need = 0;
+  RenderWS w = carve_render(prm, n, workspace, &need);
+  if (ws_bytes < need) return PNR_E_WORKSPACE;
+  hipStream_t st = (hipStream_t)stream;
+  const int S = prm->n_samples, I = prm->n_importance;
+  int rc = 0;
+  if (gt_depth && prm->far_mode == 0) rc = launch_gt_max(gt_depth, n, w.gmax, st);
+  if (rc) return rc;
+  rc = launch_coarse_z(*prm, rays_o, rays_d, gt_depth, w.gmax, n, w.z, w.far, st);
+  if (rc) return rc;
+  PointSrc src{};
+  src.rays_o = rays_o;
+  src.rays_d = rays_d;
+  src.use_bound = 1;
+  memcpy(src.bound, prm->bound, sizeof(src.bound));
+  src.z = w.z;
+  src.spr = S;
+  const SaveArgs* sv = prm->save_for_backward ? &w.save : nullptr;
+  rc = launch_mlp_fwd(packed, src, kRaysZ64, n * S, w.raw, sv, st);
+  if (rc) return rc;
+  double* zi = w.z + n * S;
+  float* rawi = w.raw + n * S * 4;
+  if (I > 0) {
+    rc = launch_pdf(*prm, rays_d, w.z, w.raw, n, zi, st);
+    if (rc) return rc;
+    src.z = zi;
+    src.spr = I;
+    SaveArgs s2{};
+    if (sv) {
+      s2 = *sv;
+      s2.p0 = w.pc_pad;
+      sv = &s2;
+    }
+    rc = launch_mlp_fwd(packed, src, kRaysZ64, n * I, rawi, sv, st);
+    if (rc) return rc;
+  }
+  return launch_fine(*prm, rays_d, w.z, zi, w.raw, rawi, n, depth, var, rgb, w.ord, st);
+}
+
+size_t pnr_render_bwd_workspace_bytes(const pnr_render_params* prm, int64_t n_rays) {
+  if (!valid_prm(prm) || n_rays < 0) return 0;
+  size_t b = 0;
+  carve_bwd(pad128(n_rays * prm->n_samples) + pad128(n_rays * prm->n_importance), n_rays, nullptr, &b);
+  return b;
+}
+
+int pnr_render_bwd(const pnr_render_params* prm, const float* packed, const float* const* params,
+                   const float* rays_o, const float* rays_d, int64_t n, const double* g_depth, const double* g_var,
+                   const float* g_rgb, float* const* grads, float* g_rays_o, float* g_rays_d, void* workspace,
+                   size_t ws_bytes, void* bwd_ws, size_t bwd_bytes, void* stream) {
+  (void)params;
+  (void)rays_o;
+  if (!valid_prm(prm) || !packed || n < 0 || !prm->save_for_backward) return PNR_E_ARG;
+  if (n == 0) return PNR_OK;
+  if (!grads || !workspace || !bwd_ws || !rays_d) return PNR_E_ARG;
+  for (int i = 0; i < PNR_N_PARAMS; ++i)
+    if (!grads[i]) return PNR_E_ARG;
+  if (prm->need_ray_grads && (!g_rays_o || !g_rays_d)) return PNR_E_ARG;
+  size_t need = 0, bneed = 0;
+  RenderWS w = carve_render(prm, n, workspace, &need);
+  const int S = prm->n_samples, I = prm->n_importance;
+  const int64_t ld = w.save.ld;
+  BwdWS b = carve_bwd(ld, n, bwd_ws, &bneed);
+  if (ws_bytes < need || bwd_bytes < bneed) return PNR_E_WORKSPACE;
+  hipStream_t st = (hipStream_t)stream;
+  const double* zi = w.z + n * S;
+  const float* rawi = w.raw + n * S * 4;
+  const int64_t pc = w.pc_pad;
+  if (hipMemsetAsync(b.g_out, 0, (size_t)ld * 16, st) != hipSuccess) return (int)hipGetLastError();
+  int rc = launch_fine_bwd(*prm, rays_d, w.z, zi, w.raw, rawi, w.save.inside, w.save.inside + pc, w.ord, n,
+                           g_depth, g_var, g_rgb, b.g_out, b.g_out + pc * 4, b.g_nrm, st);
+  if (rc) return rc;
+  rc = mlp_backward_core(packed, w.save, ld, b, grads, prm->need_ray_grads != 0, st);
+  if (rc) return rc;
+  if (prm->need_ray_grads)
+    rc = launch_ray_grads_f64(rays_d, w.z, S, zi, I, b.g_x, b.g_x + pc * 3, b.g_nrm, n, g_rays_o, g_rays_d, st);
+  return rc;
+}
+
+// ---- regulation ---------------------------------------------------------------------------
+namespace {
+struct RegWS {
+  float* z;
+  float* raw;
+  SaveArgs save;
+};
+RegWS carve_reg(const pnr_render_params* prm, int64_t n, void* ws, size_t* bytes) {
+  Carver c(ws);
+  RegWS w{};
+  const int64_t P = n * prm->n_samples;
+  w.z = c.take<float>(P);
+  w.raw = c.take<float>(P * 4);
+  if (prm->save_for_backward) w.save = carve_save(c, pad128(P));
+  if (bytes) *bytes = c.off;
+  return w;
+}
+}  // namespace
+
+size_t pnr_regulation_workspace_bytes(const pnr_render_params* prm, int64_t n_rays) {
+  if (!valid_prm(prm) || n_rays < 0) return 0;
+  size_t b = 0;
+  carve_reg(prm, n_rays, nullptr, &b);
+  return b;
+}
+
+int pnr_regulation_fwd(const pnr_render_params* prm, const float* packed, const float* rays_o, const float* rays_d,
+                       const float* gt_depth, const float* t_rand, int64_t n, float* sigma, void* workspace,
+                       size_t ws_bytes, void* stream) {
+  if (!valid_prm(prm) || !packed || n < 0) return PNR_E_ARG;
+  if (n == 0) return PNR_OK;
+  if (!rays_o || !rays_d || !gt_depth || !t_rand || !sigma || !workspace) return PNR_E_ARG;
+  size_t need = 0;
+  RegWS w = carve_reg(prm, n, workspace, &need);
+  if (ws_bytes < need) return PNR_E_WORKSPACE;
+  hipStream_t st = (hipStream_t)stream;
+  int rc = launch_reg_z(*prm, gt_depth, t_rand, n, w.z, st);
+  if (rc) return rc;
+  PointSrc src{};
+  src.rays_o = rays_o;
+  src.rays_d = rays_d;
+  src.use_bound = 1;
+  memcpy(src.bound, prm->bound, sizeof(src.bound));
+  src.z = w.z;
+  src.spr = prm->n_samples;
+  const int64_t P = n * prm->n_samples;
+  rc = launch_mlp_fwd(packed, src, kRaysZ32, P, w.raw, prm->save_for_backward ? &w.save : nullptr, st);
+  if (rc) return rc;
+  return launch_extract_sigma(w.raw, P, sigma, st);
+}
+
+size_t pnr_regulation_bwd_workspace_bytes(const pnr_render_params* prm, int64_t n_rays) {
+  if (!valid_prm(prm) || n_rays < 0) return 0;
+  size_t b = 0;
+  carve_bwd(pad128(n_rays * prm->n_samples), n_rays, nullptr, &b);
+  return b;
+}
+
+int pnr_regulation_bwd(const pnr_render_params* prm, const float* packed, const float* const* params,
+                       const float* rays_o, const float* rays_d, int64_t n, const float* g_sigma,
+                       float* const* grads, float* g_rays_o, float* g_rays_d, void* workspace, size_t ws_bytes,
+                       void* bwd_ws, size_t bwd_bytes, void* stream) {
+  (void)params;
+  (void)rays_o;
+  if (!valid_prm(prm) || !packed || n < 0 || !prm->save_for_backward) return PNR_E_ARG;
+  if (n == 0) return PNR_OK;
+  if (!grads || !workspace || !bwd_ws || !g_sigma) return PNR_E_ARG;
+  for (int i = 0; i < PNR_N_PARAMS; ++i)
+    if (!grads[i]) return PNR_E_ARG;
+  if (prm->need_ray_grads && (!g_rays_o || !g_rays_d || !rays_d)) return PNR_E_ARG;
+  size_t need = 0, bneed = 0;
+  RegWS w = carve_reg(prm, n, workspace, &need);
+  const int64_t P = n * prm->n_samples;
+  const int64_t ld = w.save.ld;
+  BwdWS b = carve_bwd(ld, n, bwd_ws, &bneed);
+  if (ws_bytes < need || bwd_bytes < bneed) return PNR_E_WORKSPACE;
+  hipStream_t st = (hipStream_t)stream;
+  if (hipMemsetAsync(b.g_out, 0, (size_t)ld * 16, st) != hipSuccess) return (int)hipGetLastError();
+  int rc = launch_gout_sigma(g_sigma, w.save.inside, P, b.g_out, st);
+  if (rc) return rc;
+  rc = mlp_backward_core(packed, w.save, ld, b, grads, prm->need_ray_grads != 0, st);
+  if (rc) return rc;
+  if (prm->need_ray_grads) rc = launch_ray_grads_f32(rays_d, w.z, prm->n_samples, b.g_x, n, g_rays_o, g_rays_d, st);
+  return rc;
+}
+
+// ---- rays / optimizer ------------------------------------------------------------------------
+int pnr_get_rays(int32_t H, int32_t W, float fx, float fy, float cx, float cy, const float* c2w, float* rays_o,
+                 float* rays_d, void* stream) {
+  if (H < 0 || W < 0 || !c2w || !rays_o || !rays_d) return PNR_E_ARG;
+  return launch_get_rays(H, W, fx, fy, cx, cy, c2w, rays_o, rays_d, (hipStream_t)stream);
+}
+
+int pnr_rays_from_uv(const float* i, const float* j, int64_t n, float fx, float fy, float cx, float cy,
+                     const float* c2w, float* rays_o, float* rays_d, void* stream) {
+  if (n < 0 || (n > 0 && (!i || !j || !c2w || !rays_o || !rays_d))) return PNR_E_ARG;
+  return launch_rays_from_uv(i, j, n, fx, fy, cx, cy, c2w, rays_o, rays_d, (hipStream_t)stream);
+}
+
+int pnr_adam_step(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1, float beta2,
+                  float eps, int64_t step, void* stream) {
+  if (n < 0 || step < 1 || (n > 0 && (!p || !g || !m || !v))) return PNR_E_ARG;
+  const double bc1 = 1.0 - std::pow((double)beta1, (double)step);
+  const double bc2 = 1.0 - std::pow((double)beta2, (double)step);
+  const float step_size = (float)((double)lr / bc1);
+  const float bc2_sqrt = (float)std::sqrt(bc2);
+  return launch_adam(p, g, m, v, n, beta1, beta2, eps, step_size, bc2_sqrt, (hipStream_t)stream);
+}
+
+}  // extern "C"

@@ -1,0 +1,502 @@
+// mlp.hip -- fused decoder kernels for gfx950 (MI355X).
+//
+//   k_pack      : raw state_dict tensors -> MFMA-fragment-ordered weight image (pnr_internal.h)
+//   k_mlp_fwd   : point generation (Renderer.py:177-179 / 296-298), bound mask (Renderer.py:43-57),
+//                 Fourier features (decoder.py:26-30), 4 hidden layers + output layer
+//                 (decoder.py:189-203), optional activation save for the backward pass
+//   k_mlp_bwd   : delta chain  g_h4 = Wo^T g_out, delta_l = (W^T delta_{l+1}) * [h_l > 0],
+//                 g_arg = (W0^T delta_1) * cos(x@B), optional dL/dx = B g_arg
+//
+// One workgroup = 4 waves (one per SIMD) = 128 points; each wave keeps its 32 points' hidden
+// activations (8 tiles x 16 fp32) in registers and accumulates the next layer in 8 MFMA tiles
+// (v_mfma_f32_32x32x2_f32: exact fp32 fma chain).  Weights stream through a double-buffered
+// 2 x 32 KiB LDS ring filled by global_load_lds (lane-linear, the image is pre-permuted).
+#include "pnr_internal.h"
+
+namespace pnr {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+#define PNR_FP_STRICT _Pragma("clang fp contract(off)")
+
+// ---------------------------------------------------------------------------------------------
+// Packing
+// ---------------------------------------------------------------------------------------------
+__global__ void k_pack(RawParams rp, float* __restrict__ out) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= kPackedFloats) return;
+  float v = 0.f;
+  auto frag = [](int64_t i, int& kc, int& t, int& r, int& lane, int tiles) {
+    // [kc][t][rq][lane][4]
+    const int64_t per_chunk = (int64_t)tiles * 1024;
+    kc = (int)(i / per_chunk);
+    int64_t rem = i % per_chunk;
+    t = (int)(rem / 1024);
+    rem %= 1024;
+    const int rq = (int)(rem / 256);
+    lane = (int)((rem % 256) / 4);
+    r = rq * 4 + (int)(rem % 4);
+  };
+  int kc, t, r, lane;
+  if (idx < kOffOF) {  // forward hidden images
+    int layer;
+    int64_t i;
+    if (idx < kOffL1F) { layer = 0; i = idx - kOffL0F; }
+    else if (idx < kOffL2F) { layer = 1; i = idx - kOffL1F; }
+    else if (idx < kOffL3F) { layer = 2; i = idx - kOffL2F; }
+    else { layer = 3; i = idx - kOffL3F; }
+    frag(i, kc, t, r, lane, 8);
+    const int row = 32 * t + (lane & 31);
+    const int col = 32 * kc + perm(r, lane >> 5);
+    const float* W = rp.p[1 + 2 * layer];
+    if (layer == 0) v = col < kFourier ? W[row * kFourier + col] : 0.f;
+    else v = W[row * kHidden + col];
+  } else if (idx < kOffB0) {  // output layer forward image [kc][rq][lane][4]
+    frag(idx - kOffOF, kc, t, r, lane, 1);
+    const int row = lane & 31;
+    const int col = 32 * kc + perm(r, lane >> 5);
+    v = row < 4 ? rp.p[9][row * kHidden + col] : 0.f;
+  } else if (idx < kOffBO) {  // bias images [t][rq][lane][4]
+    const int layer = (int)((idx - kOffB0) / kBiasFloats);
+    frag((idx - kOffB0) % kBiasFloats, kc, t, r, lane, 8);
+    v = rp.p[2 + 2 * layer][32 * t + perm(r, lane >> 5)];
+  } else if (idx < kOffFB) {  // output bias [rq][lane][4]
+    frag(idx - kOffBO, kc, t, r, lane, 1);
+    const int u = perm(r, lane >> 5);
+    v = u < 4 ? rp.p[10][u] : 0.f;
+  } else if (idx < kOffOT) {  // Fourier B padded [3][96]
+    const int i = (int)(idx - kOffFB);
+    const int c = i / kFourierPad, k = i % kFourierPad;
+    v = k < kFourier ? rp.p[0][c * kFourier + k] : 0.f;
+  } else if (idx < kOffL3T) {  // Wo^T [t][lane][4]: k-steps r = 0..3 only
+    const int i = (int)(idx - kOffOT);
+    t = i / 256;
+    lane = (i % 256) / 4;
+    r = i % 4;
+    const int o = perm(r, lane >> 5);
+    v = o < 4 ? rp.p[9][o * kHidden + 32 * t + (lane & 31)] : 0.f;
+  } else if (idx < kOffL0T) {  // W_l^T, l = 3,2,1
+    const int which = (int)((idx - kOffL3T) / (8 * kChunkFloats));  // 0:W3 1:W2 2:W1
+    frag((idx - kOffL3T) % (8 * kChunkFloats), kc, t, r, lane, 8);
+    const float* W = rp.p[7 - 2 * which];
+    const int row = 32 * t + (lane & 31);         // input unit of W
+    const int col = 32 * kc + perm(r, lane >> 5);  // output unit of W (the K index here)
+    v = W[col * kHidden + row];
+  } else {  // W0^T, 3 out tiles
+    frag(idx - kOffL0T, kc, t, r, lane, 3);
+    const int row = 32 * t + (lane & 31);
+    const int col = 32 * kc + perm(r, lane >> 5);
+    v = row < kFourier ? rp.p[1][col * kFourier + row] : 0.f;
+  }
+  out[idx] = v;
+}
+
+int launch_pack(const RawParams& rp, float* packed, hipStream_t st) {
+  const int threads = 256;
+  const int blocks = (int)((kPackedFloats + threads - 1) / threads);
+  hipLaunchKernelGGL(k_pack, dim3(blocks), dim3(threads), 0, st, rp, packed);
+  return hip_status(hipGetLastError());
+}
+
+// ---------------------------------------------------------------------------------------------
+// Building blocks
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ f32x16 mfma(float a, float b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
+
+// The weight image is one contiguous stream per kernel; `sp` is this lane's cursor into it
+// (stream base + wave*256 + lane*4 floats).  stage() copies the next `nfloats` (multiple of 1024)
+// into LDS with global_load_lds_dwordx4 (lane-linear destination) and advances the cursor.
+__device__ __forceinline__ void stage(const float*& sp, float* dst, int nfloats) {
+  const int w = wave_id();
+  const int n = nfloats >> 10;
+  for (int i = 0; i < n; ++i)
+    __builtin_amdgcn_global_load_lds((const void*)(sp + i * 1024), (lds_ptr_t)(dst + (i * 4 + w) * 256), 16, 0, 0);
+  sp += nfloats;
+}
+
+// acc[t] += A(chunk, tile t) * act  over the 16 k-steps of one 32-row input tile.
+// A fragments are read from LDS one r-quad ahead (ds_read_b128, conflict-free lane-linear
+// image); the sched barriers keep at most two r-quads of A (2 x NT x 4 VGPRs) live.
+template <int NT>
+__device__ __forceinline__ void load_a(const float* chunk, int rq, float4 (&a)[NT]) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int t = 0; t < NT; ++t) a[t] = *reinterpret_cast<const float4*>(chunk + ((t * 4 + rq) * 64 + lane) * 4);
+}
+template <int NT>
+__device__ __forceinline__ void mfma_rq(const float4 (&a)[NT], const float (&b)[16], int rq, f32x16 (&acc)[NT]) {
+#pragma unroll
+  for (int t = 0; t < NT; ++t) acc[t] = mfma(a[t].x, b[4 * rq + 0], acc[t]);
+#pragma unroll
+  for (int t = 0; t < NT; ++t) acc[t] = mfma(a[t].y, b[4 * rq + 1], acc[t]);
+#pragma unroll
+  for (int t = 0; t < NT; ++t) acc[t] = mfma(a[t].z, b[4 * rq + 2], acc[t]);
+#pragma unroll
+  for (int t = 0; t < NT; ++t) acc[t] = mfma(a[t].w, b[4 * rq + 3], acc[t]);
+}
+template <int NT>
+__device__ __forceinline__ void mfma_chunk(const float* chunk, const float (&b)[16], f32x16 (&acc)[NT]) {
+  float4 a0[NT], a1[NT];
+  load_a<NT>(chunk, 0, a0);
+  load_a<NT>(chunk, 1, a1);
+  mfma_rq<NT>(a0, b, 0, acc);
+  __builtin_amdgcn_sched_barrier(0);
+  load_a<NT>(chunk, 2, a0);
+  mfma_rq<NT>(a1, b, 1, acc);
+  __builtin_amdgcn_sched_barrier(0);
+  load_a<NT>(chunk, 3, a1);
+  mfma_rq<NT>(a0, b, 2, acc);
+  __builtin_amdgcn_sched_barrier(0);
+  mfma_rq<NT>(a1, b, 3, acc);
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// One layer: NCH input tiles streamed as NCH LDS chunks of `chf` floats from the cursor; the
+// chunk after the last one (`nxf` floats, 0 = none) is prefetched during the last compute.
+// Buffer parity START: chunk c lives in buffer (START + c) & 1.
+template <int NCH, int NT, int START>
+__device__ __forceinline__ void layer(float* lds, const float*& sp, int chf, int nxf, const float (&act)[8][16],
+                                      f32x16 (&acc)[NT]) {
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    __syncthreads();
+    float* cur = lds + ((START + c) & 1) * kChunkFloats;
+    float* oth = lds + ((START + c + 1) & 1) * kChunkFloats;
+    if (c + 1 < NCH) stage(sp, oth, chf);
+    else if (nxf > 0) stage(sp, oth, nxf);
+    mfma_chunk<NT>(cur, act[c], acc);
+    // Pin the accumulators here: without it hipcc defers half of the MFMA chains past the next
+    // s_barrier (MFMAs touch no memory), keeps their A fragments alive and spills ~250 VGPRs.
+#pragma unroll
+    for (int t = 0; t < NT; ++t) asm volatile("" : "+a"(acc[t]));
+  }
+}
+
+template <int NT>
+__device__ __forceinline__ void zero_acc(f32x16 (&acc)[NT]) {
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+}
+
+// act = relu(acc + bias), bias image [t][rq][lane][4]; one tile of bias live at a time
+__device__ __forceinline__ void bias_relu(const f32x16 (&acc)[8], const float* __restrict__ img, float (&act)[8][16]) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+#pragma unroll
+    for (int rq = 0; rq < 4; ++rq) {
+      const float4 b = *reinterpret_cast<const float4*>(img + ((t * 4 + rq) * 64 + lane) * 4);
+      const float v0 = acc[t][4 * rq + 0] + b.x, v1 = acc[t][4 * rq + 1] + b.y;
+      const float v2 = acc[t][4 * rq + 2] + b.z, v3 = acc[t][4 * rq + 3] + b.w;
+      act[t][4 * rq + 0] = v0 > 0.f ? v0 : 0.f;
+      act[t][4 * rq + 1] = v1 > 0.f ? v1 : 0.f;
+      act[t][4 * rq + 2] = v2 > 0.f ? v2 : 0.f;
+      act[t][4 * rq + 3] = v3 > 0.f ? v3 : 0.f;
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// store NT tiles of the register activation into a unit-major [rows][ld] buffer at column col.
+// Rows of register r are 32t + perm(r,hh): walk one pointer (deltas 1,1,1,5 rows) so that the
+// compiler does not materialise 128 separate 64-bit row addresses.
+template <int NT>
+__device__ __forceinline__ void save_tiles(float* __restrict__ base, int64_t ld, int64_t col,
+                                           const float (&act)[8][16]) {
+  const int lane = threadIdx.x & 63, hh = lane >> 5;
+  float* q = base + (int64_t)(4 * hh) * ld + col;
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      *q = act[t][r];
+      q += ((r & 3) == 3 ? 5 : 1) * ld;
+    }
+}
+
+// ReLU mask of one lane: bit (t&1)*16 + r of word t>>1 is [act[t][r] > 0]; the wave tile's
+// 64 lanes store one uint4 each (1 KiB per 32 points per layer).
+__device__ __forceinline__ void save_mask(uint4* __restrict__ words, const float (&act)[8][16]) {
+  uint32_t w[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+  for (int t = 0; t < 8; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) w[t >> 1] |= (act[t][r] > 0.f ? 1u : 0u) << ((t & 1) * 16 + r);
+  words[threadIdx.x & 63] = make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Forward
+// ---------------------------------------------------------------------------------------------
+struct FwdArgs {
+  const float* packed;
+  PointSrc src;
+  int64_t P;
+  float* raw;
+  SaveArgs save;
+  int do_save;
+};
+
+template <int MODE>
+__device__ __forceinline__ void load_point(const PointSrc& s, int64_t p, float& x0, float& x1, float& x2,
+                                           bool& inside) {
+  PNR_FP_STRICT
+  if (MODE == kPtsF64 || MODE == kRaysZ64) {
+    double q0, q1, q2;
+    if (MODE == kPtsF64) {
+      const double* pp = reinterpret_cast<const double*>(s.pts) + p * 3;
+      q0 = pp[0]; q1 = pp[1]; q2 = pp[2];
+    } else {
+      const int64_t ray = p / s.spr;
+      const double z = reinterpret_cast<const double*>(s.z)[p];
+      // torch: rays_o[...,None,:] + rays_d[...,None,:] * z[...,:,None], promoted to float64
+      q0 = (double)s.rays_o[ray * 3 + 0] + (double)s.rays_d[ray * 3 + 0] * z;
+      q1 = (double)s.rays_o[ray * 3 + 1] + (double)s.rays_d[ray * 3 + 1] * z;
+      q2 = (double)s.rays_o[ray * 3 + 2] + (double)s.rays_d[ray * 3 + 2] * z;
+    }
+    inside = true;
+    if (s.use_bound)
+      inside = (q0 < s.bound[1]) && (q0 > s.bound[0]) && (q1 < s.bound[3]) && (q1 > s.bound[2]) &&
+               (q2 < s.bound[5]) && (q2 > s.bound[4]);
+    x0 = (float)q0; x1 = (float)q1; x2 = (float)q2;
+  } else {
+    if (MODE == kPtsF32) {
+      const float* pp = reinterpret_cast<const float*>(s.pts) + p * 3;
+      x0 = pp[0]; x1 = pp[1]; x2 = pp[2];
+    } else {
+      const int64_t ray = p / s.spr;
+      const float z = reinterpret_cast<const float*>(s.z)[p];
+      x0 = s.rays_o[ray * 3 + 0] + s.rays_d[ray * 3 + 0] * z;
+      x1 = s.rays_o[ray * 3 + 1] + s.rays_d[ray * 3 + 1] * z;
+      x2 = s.rays_o[ray * 3 + 2] + s.rays_d[ray * 3 + 2] * z;
+    }
+    inside = true;
+    if (s.use_bound)  // a float32 tensor compared with a 0-dim float64 tensor compares in float32
+      inside = (x0 < (float)s.bound[1]) && (x0 > (float)s.bound[0]) && (x1 < (float)s.bound[3]) &&
+               (x1 > (float)s.bound[2]) && (x2 < (float)s.bound[5]) && (x2 > (float)s.bound[4]);
+  }
+}
+
+// torch CPU computes the K=3 product x @ B as fma(x2,B2, fma(x1,B1, x0*B0)) (verified bitwise)
+__device__ __forceinline__ float fourier_arg(const float* __restrict__ FB, int k, float x0, float x1, float x2) {
+  PNR_FP_STRICT
+  float a = x0 * FB[k];
+  a = __builtin_fmaf(x1, FB[kFourierPad + k], a);
+  a = __builtin_fmaf(x2, FB[2 * kFourierPad + k], a);
+  return a;
+}
+
+template <int MODE>
+__global__ __launch_bounds__(256, 1) void k_mlp_fwd(FwdArgs a) {
+  __shared__ __attribute__((aligned(16))) float lds[2 * kChunkFloats];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, hh = lane >> 5, j = lane & 31;
+  const int64_t p = (int64_t)blockIdx.x * 128 + wave * 32 + j;
+  const bool valid = p < a.P;
+  const float* __restrict__ W = a.packed;
+
+  const float* sp = W + kOffL0F + wave_id() * 256 + lane * 4;  // weight stream cursor
+  stage(sp, lds, kChunkFloats);  // chunk 0 of layer 0 -> buffer 0
+
+  float x0 = 0.f, x1 = 0.f, x2 = 0.f;
+  bool inside = false;
+  if (valid) load_point<MODE>(a.src, p, x0, x1, x2, inside);
+
+  float act[8][16];
+  const float* FB = W + kOffFB;
+#pragma unroll
+  for (int t = 0; t < 3; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int k = 32 * t + perm(r, hh);
+      act[t][r] = k < kFourier ? sinf(fourier_arg(FB, k, x0, x1, x2)) : 0.f;
+    }
+  // training saves cover every point of the (128-padded) grid: padded columns get finite
+  // activations of x = 0 and a zero gradient later, so the weight GEMMs may include them
+  const bool save = a.do_save;
+  const int64_t col = a.save.p0 + p;
+  // first saved column of this wave (p0 is a multiple of 128) -> its 64 mask slots
+  const int64_t mask_word0 = ((a.save.p0 + (int64_t)blockIdx.x * 128) / 32 + wave_id()) * 64;
+  if (save) {
+    save_tiles<3>(a.save.eT, a.save.ld, col, act);
+    if (hh == 0) {
+      a.save.xT[col] = x0;
+      a.save.xT[a.save.ld + col] = x1;
+      a.save.xT[2 * a.save.ld + col] = x2;
+      a.save.inside[col] = inside ? 1 : 0;
+    }
+  }
+
+  f32x16 acc[8];
+  zero_acc<8>(acc);
+  layer<3, 8, 0>(lds, sp, kChunkFloats, kChunkFloats, act, acc);
+  bias_relu(acc, W + kOffB0, act);
+  if (a.do_save) {
+    save_mask(a.save.masks + mask_word0, act);
+    save_tiles<8>(a.save.hT, a.save.ld, col, act);
+  }
+
+  // hidden layers 1..3 (pts_linears.1..3); each starts in buffer 1 (layer 0 used 3 chunks)
+  for (int L = 1; L <= 3; ++L) {
+    const int nxf = L < 3 ? kChunkFloats : kSmallChunkFloats;
+    zero_acc<8>(acc);
+    layer<8, 8, 1>(lds, sp, kChunkFloats, nxf, act, acc);
+    bias_relu(acc, W + kOffB0 + (int64_t)L * kBiasFloats, act);
+    if (a.do_save) {
+      save_mask(a.save.masks + (int64_t)L * (a.save.ld / 32) * 64 + mask_word0, act);
+      save_tiles<8>(a.save.hT + (int64_t)L * kHidden * a.save.ld, a.save.ld, col, act);
+    }
+  }
+
+  f32x16 out[1];
+  zero_acc<1>(out);
+  layer<8, 1, 1>(lds, sp, kSmallChunkFloats, 0, act, out);
+  // rows 0..3 of the output tile live in lanes 0..31, registers 0..3
+  if (valid && hh == 0) {
+    const float4 bo = *reinterpret_cast<const float4*>(W + kOffBO + lane * 4);
+    float4 o = make_float4(out[0][0] + bo.x, out[0][1] + bo.y, out[0][2] + bo.z, inside ? out[0][3] + bo.w : 100.f);
+    reinterpret_cast<float4*>(a.raw)[p] = o;
+  }
+}
+
+int launch_mlp_fwd(const float* packed, const PointSrc& src, int mode, int64_t P, float* raw,
+                   const SaveArgs* save, hipStream_t st) {
+  if (P <= 0) return 0;
+  FwdArgs a;
+  a.packed = packed;
+  a.src = src;
+  a.P = P;
+  a.raw = raw;
+  a.do_save = save != nullptr;
+  if (save) a.save = *save;
+  else a.save = SaveArgs{nullptr, nullptr, nullptr, nullptr, 0, 0};
+  const dim3 grid((unsigned)((P + 127) / 128)), block(256);
+  switch (mode) {
+    case kPtsF64: hipLaunchKernelGGL(k_mlp_fwd<kPtsF64>, grid, block, 0, st, a); break;
+    case kPtsF32: hipLaunchKernelGGL(k_mlp_fwd<kPtsF32>, grid, block, 0, st, a); break;
+    case kRaysZ64: hipLaunchKernelGGL(k_mlp_fwd<kRaysZ64>, grid, block, 0, st, a); break;
+    case kRaysZ32: hipLaunchKernelGGL(k_mlp_fwd<kRaysZ32>, grid, block, 0, st, a); break;
+    default: return PNR_E_ARG;
+  }
+  return hip_status(hipGetLastError());
+}
+
+// ---------------------------------------------------------------------------------------------
+// Backward delta chain
+// ---------------------------------------------------------------------------------------------
+// act = acc * [h > 0]; the ReLU mask comes from the forward's per-lane bit words
+__device__ __forceinline__ void relu_grad(const f32x16 (&acc)[8], const uint4* __restrict__ words,
+                                          float (&act)[8][16]) {
+  const uint4 m = words[threadIdx.x & 63];
+  const uint32_t w[4] = {m.x, m.y, m.z, m.w};
+#pragma unroll
+  for (int t = 0; t < 8; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) act[t][r] = ((w[t >> 1] >> ((t & 1) * 16 + r)) & 1u) ? acc[t][r] : 0.f;
+}
+
+__global__ __launch_bounds__(256, 1) void k_mlp_bwd(const float* __restrict__ W, BwdArgs a, int64_t P) {
+  __shared__ __attribute__((aligned(16))) float lds[2 * kChunkFloats];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, hh = lane >> 5, j = lane & 31;
+  const int64_t p = (int64_t)blockIdx.x * 128 + wave * 32 + j;  // chunk-local point
+  const bool valid = p < P;
+  const int64_t col = a.p0 + p;   // column in the saved activations
+  const int64_t dcol = p;         // column in the delta buffers
+  const int64_t mstride = (a.ld / 32) * 64;  // mask slots per layer
+  const uint4* mk = a.masks + ((a.p0 + (int64_t)blockIdx.x * 128) / 32 + wave_id()) * 64;
+
+  const float* sp = W + kOffL3T + wave_id() * 256 + lane * 4;  // weight stream cursor
+  stage(sp, lds, kChunkFloats);  // W3^T chunk 0 -> buffer 0 (lands during the Wo^T step)
+
+  // g_h4 = Wo^T g_out  (K = 4: k-steps r = 0..3, lane half 0 carries o = r)
+  float g[4] = {0.f, 0.f, 0.f, 0.f};
+  if (valid && hh == 0) {
+    const float4 go = reinterpret_cast<const float4*>(a.g_out)[p];
+    g[0] = go.x; g[1] = go.y; g[2] = go.z; g[3] = go.w;
+  }
+  if (valid && hh == 0) {
+#pragma unroll
+    for (int o = 0; o < 4; ++o) a.goutT[(int64_t)o * a.ld_d + dcol] = g[o];
+  }
+  f32x16 acc[8];
+  zero_acc<8>(acc);
+  {
+    const float* OT = W + kOffOT;
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const float4 w4 = *reinterpret_cast<const float4*>(OT + (t * 64 + lane) * 4);
+      acc[t] = mfma(w4.x, g[0], acc[t]);
+      acc[t] = mfma(w4.y, g[1], acc[t]);
+      acc[t] = mfma(w4.z, g[2], acc[t]);
+      acc[t] = mfma(w4.w, g[3], acc[t]);
+    }
+  }
+  float act[8][16];
+  relu_grad(acc, mk + 3 * mstride, act);   // delta4
+  if (valid) save_tiles<8>(a.dT + 3 * (int64_t)kHidden * a.ld_d, a.ld_d, dcol, act);
+
+  // delta3 = W3^T delta4 * [h3>0]; delta2; delta1  (images L3T, L2T, L1T; 8 chunks each)
+  // chunk parity: L3T starts in buffer 0, 8 chunks -> every image starts in buffer 0
+  for (int s = 0; s < 3; ++s) {  // s=0: W3^T -> delta3 (uses h3), s=1: W2^T -> delta2, s=2: W1^T -> delta1
+    const int nxf = s < 2 ? kChunkFloats : (int)kL0TChunkFloats;
+    zero_acc<8>(acc);
+    layer<8, 8, 0>(lds, sp, kChunkFloats, nxf, act, acc);
+    const int hl = 2 - s;  // h3 -> index 2, h2 -> 1, h1 -> 0
+    relu_grad(acc, mk + hl * mstride, act);
+    if (valid) save_tiles<8>(a.dT + (int64_t)hl * kHidden * a.ld_d, a.ld_d, dcol, act);
+  }
+
+  // g_e = W0^T delta1 : 3 output tiles (96 rows, 93 valid)
+  f32x16 ge[3];
+  zero_acc<3>(ge);
+  layer<8, 3, 0>(lds, sp, (int)kL0TChunkFloats, 0, act, ge);
+
+  // g_arg = g_e * cos(x@B); g_x = B g_arg
+  float x0 = 0.f, x1 = 0.f, x2 = 0.f;
+  if (valid) {
+    x0 = a.xT[col];
+    x1 = a.xT[a.ld + col];
+    x2 = a.xT[2 * a.ld + col];
+  }
+  const float* FB = W + kOffFB;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f;
+#pragma unroll
+  for (int t = 0; t < 3; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int k = 32 * t + perm(r, hh);
+      float gv = 0.f;
+      if (k < kFourier) {
+        gv = ge[t][r] * cosf(fourier_arg(FB, k, x0, x1, x2));
+        s0 = __builtin_fmaf(FB[k], gv, s0);
+        s1 = __builtin_fmaf(FB[kFourierPad + k], gv, s1);
+        s2 = __builtin_fmaf(FB[2 * kFourierPad + k], gv, s2);
+      }
+      if (valid) a.gargT[(int64_t)k * a.ld_d + dcol] = gv;
+    }
+  if (a.g_x != nullptr) {
+    s0 += __shfl_xor(s0, 32);
+    s1 += __shfl_xor(s1, 32);
+    s2 += __shfl_xor(s2, 32);
+    if (valid && hh == 0) {
+      a.g_x[p * 3 + 0] = s0;
+      a.g_x[p * 3 + 1] = s1;
+      a.g_x[p * 3 + 2] = s2;
+    }
+  }
+}
+
+int launch_mlp_bwd(const float* packed, const BwdArgs& a, int64_t P, hipStream_t st) {
+  if (P <= 0) return 0;
+  const dim3 grid((unsigned)((P + 127) / 128)), block(256);
+  hipLaunchKernelGGL(k_mlp_bwd, grid, block, 0, st, packed, a, P);
+  return hip_status(hipGetLastError());
+}
+
+}  // namespace pnr

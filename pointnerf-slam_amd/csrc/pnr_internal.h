@@ -1,0 +1,112 @@
+// pnr_internal.h -- shared constants, packed-weight layout and launch helpers of libpnr.so.
+//
+// MLP = the iMAP* decoder of src/conv_onet/models/decoder.py:91-203 under
+// src/conv_onet/config.py:29-31: Fourier(3->93, sin) -> 93->256 -> 3x(256->256) -> 256->4,
+// ReLU after every hidden layer, no skips, no output activation.
+//
+// Execution model of the MLP kernels (see DESIGN.md "MLP kernel"): one wave owns 32 points,
+// the point index sits on the MFMA column (lane & 31), the hidden units sit in registers.
+// A hidden activation h (256 x 32 points) is 8 accumulator tiles of v_mfma_f32_32x32x2_f32:
+//   lane l = 32*hh + j holds, in tile t, register r:  unit 32*t + perm(r,hh), point j
+//   perm(r,hh) = (r&3) + 8*(r>>2) + 4*hh                       (gfx950 32x32 C/D layout)
+// The NEXT layer consumes that accumulator directly as its B operand (k-step r of tile t uses
+// register r: lane half hh supplies k = 32t + perm(r,hh)), so activations never leave the
+// registers.  The weights (A operand) are pre-permuted on the device into exactly the lane
+// order each MFMA needs and streamed through LDS in 32 KiB chunks by global_load_lds.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/pnr.h"
+
+namespace pnr {
+
+constexpr int kHidden = 256;
+constexpr int kFourier = 93;     // decoder.py:129
+constexpr int kFourierPad = 96;  // 3 tiles of 32
+constexpr int kTiles = kHidden / 32;
+constexpr int kChunkFloats = 8192;       // one 32 KiB LDS chunk = 8 tiles x 16 k-steps x 64 lanes
+constexpr int kSmallChunkFloats = 1024;  // output layer: 1 tile x 16 k-steps x 64 lanes
+
+// ---- packed image offsets (floats) -------------------------------------------------------
+// forward A images: [chunk kc][tile t][rq][lane][4]
+constexpr int64_t kOffL0F = 0;                                   // 3 chunks
+constexpr int64_t kOffL1F = kOffL0F + 3 * kChunkFloats;          // 8 chunks each
+constexpr int64_t kOffL2F = kOffL1F + 8 * kChunkFloats;
+constexpr int64_t kOffL3F = kOffL2F + 8 * kChunkFloats;
+constexpr int64_t kOffOF = kOffL3F + 8 * kChunkFloats;           // 8 small chunks
+// bias images: [tile][rq][lane][4]
+constexpr int64_t kBiasFloats = kTiles * 4 * 64 * 4;             // 8192
+constexpr int64_t kOffB0 = kOffOF + 8 * kSmallChunkFloats;
+constexpr int64_t kOffB1 = kOffB0 + kBiasFloats;
+constexpr int64_t kOffB2 = kOffB1 + kBiasFloats;
+constexpr int64_t kOffB3 = kOffB2 + kBiasFloats;
+constexpr int64_t kOffBO = kOffB3 + kBiasFloats;                 // [rq][lane][4] 1024
+constexpr int64_t kOffFB = kOffBO + 1024;                        // Fourier B padded [3][96]
+// backward (transposed) A images
+constexpr int64_t kOffOT = kOffFB + 3 * kFourierPad;             // Wo^T: [tile][lane][4] 2048
+constexpr int64_t kOffL3T = kOffOT + 2048;                       // W3^T: 8 chunks
+constexpr int64_t kOffL2T = kOffL3T + 8 * kChunkFloats;
+constexpr int64_t kOffL1T = kOffL2T + 8 * kChunkFloats;
+constexpr int64_t kL0TChunkFloats = 3 * 4 * 64 * 4;              // 3 out tiles: 3072
+constexpr int64_t kOffL0T = kOffL1T + 8 * kChunkFloats;          // W0^T: 8 chunks of 3072
+constexpr int64_t kPackedFloats = kOffL0T + 8 * kL0TChunkFloats;
+
+__host__ __device__ inline int perm(int r, int hh) { return (r & 3) + 8 * (r >> 2) + 4 * hh; }
+
+// Device views of the 11 reference tensors (src/conv_onet/models/decoder.py state_dict order).
+struct RawParams {
+  const float* p[PNR_N_PARAMS];
+};
+
+// Where the MLP reads its points from.
+enum PointMode : int {
+  kPtsF64 = 0,      // explicit float64 points (eval_points)
+  kPtsF32 = 1,      // explicit float32 points (MLP.forward on f32 / masked in f32)
+  kRaysZ64 = 2,     // p = o + d * z, z float64 (render_batch_ray)
+  kRaysZ32 = 3,     // p = o + d * z, z float32 (regulation)
+};
+
+struct PointSrc {
+  const void* pts;      // kPtsF64/kPtsF32: (P,3)
+  const float* rays_o;  // ray modes: (N,3)
+  const float* rays_d;
+  const void* z;        // ray modes: (N, spr) float64 or float32, point p -> ray p / spr
+  int32_t spr;          // samples per ray
+  int32_t use_bound;
+  double bound[6];
+};
+
+// Activation save area for training (unit-major, leading dimension ld = total points).
+struct SaveArgs {
+  float* eT;       // [96][ld]
+  float* hT;       // [4][256][ld]  (h1..h4)
+  float* xT;       // [3][ld]        f32 MLP input
+  uint8_t* inside; // [ld]
+  uint4* masks;    // [4][ld/32][64 lanes] ReLU bit words of h1..h4 (mlp.hip save_mask)
+  int64_t ld;      // multiple of 128
+  int64_t p0;      // column of point 0 of this launch (multiple of 128)
+};
+
+int launch_mlp_fwd(const float* packed, const PointSrc& src, int mode, int64_t P, float* raw,
+                   const SaveArgs* save, hipStream_t st);
+
+struct BwdArgs {
+  const float* g_out;  // (P,4) dL/draw, sigma channel already zeroed where masked
+  const uint4* masks;  // [4][ld/32][64]
+  const float* xT;     // [3][ld]
+  float* dT;           // [4][256][ld_d]  delta1..delta4
+  float* gargT;        // [96][ld_d]      dL/d(x@B) (pre-sin argument)
+  float* g_x;          // (P,3) dL/dx or nullptr
+  float* goutT;        // [4][ld_d]       transposed copy of g_out for the dWo GEMM
+  int64_t ld;          // leading dim of saved activations
+  int64_t p0;          // first saved column handled by this launch
+  int64_t ld_d;        // leading dim of delta buffers (chunk-local, column 0 = p0)
+};
+int launch_mlp_bwd(const float* packed, const BwdArgs& a, int64_t P, hipStream_t st);
+
+int launch_pack(const RawParams& rp, float* packed, hipStream_t st);
+
+inline int hip_status(hipError_t e) { return e == hipSuccess ? 0 : (int)e; }
+
+}  // namespace pnr

@@ -1,0 +1,481 @@
+// render.hip -- ray-level kernels of the renderer (thread per ray; cheap next to the MLP).
+//
+//   k_gt_max          max(1.2 * gt_depth) of the batch              Renderer.py:112
+//   k_coarse_z        near/far + stratified depths (float64)         Renderer.py:90-116, 157-171
+//   k_pdf             coarse compositing weights + inverse-CDF       common.py:204-245, 19-63;
+//                     importance depths (float64)                    Renderer.py:186-190
+//   k_fine            sort(cat(z, z_samples)) + final compositing    Renderer.py:191-201
+//   k_fine_bwd        compositing backward -> dL/draw per point       (autograd of common.py:224-244)
+//   k_ray_grads       dL/drays_o, dL/drays_d (tracking)              Renderer.py:177-178, common.py:230
+//   k_reg_z           regulation depths (float32, jittered)          Renderer.py:280-294
+//   k_get_rays        full-frame / per-pixel rays                    common.py:74-89, 248-266
+//   k_adam            torch.optim.Adam step                          Mapper.py:498-502, 657-662
+//
+// Arithmetic follows torch's CPU semantics where it is observable: python scalars are applied
+// in float32, cumprod / cumsum accumulate in float64 and round per element, x@B for K=3 and
+// |d| are fma chains, and no floating-point contraction is allowed elsewhere (fp contract off).
+#include <math.h>
+
+#include "pnr_internal.h"
+
+#pragma clang fp contract(off)
+
+namespace pnr {
+
+__device__ __forceinline__ double max_nan(double a, double b) { return (a != a || b != b) ? NAN : (a > b ? a : b); }
+__device__ __forceinline__ double min_nan(double a, double b) { return (a != a || b != b) ? NAN : (a < b ? a : b); }
+__device__ __forceinline__ float relu(float x) { return x > 0.f ? x : 0.f; }
+
+__device__ __forceinline__ float ray_norm(const float* d) {
+  return sqrtf(__builtin_fmaf(d[2], d[2], __builtin_fmaf(d[1], d[1], d[0] * d[0])));
+}
+
+// ---------------------------------------------------------------------------------------------
+__global__ void k_gt_max(const float* __restrict__ gt, int64_t n, float* __restrict__ out) {
+  __shared__ float red[1024];
+  float m = -INFINITY;
+  for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
+    const float v = gt[i] * 1.2f;
+    m = (v > m || v != v) ? v : m;
+  }
+  red[threadIdx.x] = m;
+  __syncthreads();
+  for (int s = blockDim.x / 2; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) {
+      const float o = red[threadIdx.x + s];
+      const float c = red[threadIdx.x];
+      red[threadIdx.x] = (o > c || o != o) ? o : c;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *out = red[0];
+}
+
+// near/far and the stratified z of the first pass.  z: (N, S) float64.
+__global__ void k_coarse_z(pnr_render_params prm, const float* __restrict__ ro, const float* __restrict__ rd,
+                           const float* __restrict__ gt, const float* __restrict__ gmax, int64_t n_rays,
+                           double* __restrict__ z, double* __restrict__ far_out) {
+  const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= n_rays) return;
+  double fb = 0.0;
+  for (int a = 0; a < 3; ++a) {
+    const double o = (double)ro[n * 3 + a], d = (double)rd[n * 3 + a];
+    const double t0 = (prm.bound[2 * a] - o) / d;
+    const double t1 = (prm.bound[2 * a + 1] - o) / d;
+    const double mx = max_nan(t0, t1);
+    fb = a == 0 ? mx : min_nan(fb, mx);
+  }
+  fb = fb + 0.01;
+  double far = fb;
+  float nearf = 0.01f;
+  if (gt != nullptr) {
+    const double hi = prm.far_mode == 1 ? prm.far_clamp : (double)(*gmax);
+    far = fb != fb ? fb : (fb < 0.0 ? 0.0 : fb);  // clamp(min=0)
+    far = far != far ? far : (far > hi ? hi : far);
+    nearf = gt[n] * 0.01f;
+  }
+  if (far_out) far_out[n] = far;
+  const int S = prm.n_samples;
+  for (int s = 0; s < S; ++s) {
+    const float t = prm.t_vals[s];
+    double zz;
+    if (!prm.lindisp) {
+      zz = (double)(nearf * (1.f - t)) + far * (double)t;
+    } else {
+      const float inv_near = gt != nullptr ? 1.f / nearf : 100.f;
+      zz = 1.0 / ((double)(inv_near * (1.f - t)) + (1.0 / far) * (double)t);
+    }
+    z[n * S + s] = zz;
+  }
+}
+
+// Compositing weights of one ray (common.py:224-240), sorted sample order given by `src`.
+// Writes w (float) into wl[q*stride].  Returns nothing else; used by the coarse pass.
+struct RaySamples {
+  const double* zc; const double* zi; const float4* rc; const float4* ri;
+  int S;
+};
+
+// ---------------------------------------------------------------------------------------------
+// coarse weights -> sample_pdf -> z_samples (N, I) float64
+__global__ __launch_bounds__(64) void k_pdf(pnr_render_params prm, const float* __restrict__ rd,
+                                            const double* __restrict__ zc, const float4* __restrict__ rawc,
+                                            int64_t n_rays, double* __restrict__ zi) {
+  __shared__ float wl[PNR_MAX_SAMPLES][64];
+  __shared__ float cdf[PNR_MAX_SAMPLES][64];
+  const int tid = threadIdx.x;
+  const int64_t n = (int64_t)blockIdx.x * 64 + tid;
+  if (n >= n_rays) return;
+  const int S = prm.n_samples, I = prm.n_importance;
+  const double* z = zc + n * S;
+  const float4* raw = rawc + n * S;
+  const float nrm = ray_norm(rd + n * 3);
+  double T = 1.0;
+  for (int q = 0; q < S; ++q) {
+    const float dz = q < S - 1 ? (float)(z[q + 1] - z[q]) : 1e10f;
+    const float delta = dz * nrm;
+    const float a = 1.f - expf(-relu(raw[q].w) * delta);
+    wl[q][tid] = a * (float)T;
+    T *= (double)(1.f - a + 1e-10f);
+  }
+  // sample_pdf(bins = mid(z) (S-1), weights[1:-1] (S-2))
+  const int M = S - 2;
+  float sum = 0.f;
+  for (int m = 0; m < M; ++m) sum += wl[m + 1][tid] + 1e-5f;
+  double acc = 0.0;
+  cdf[0][tid] = 0.f;
+  for (int m = 0; m < M; ++m) {
+    acc += (double)((wl[m + 1][tid] + 1e-5f) / sum);
+    cdf[m + 1][tid] = (float)acc;
+  }
+  for (int k = 0; k < I; ++k) {
+    const float u = prm.u_vals[k];
+    // searchsorted(cdf, u, right=True): first index with cdf > u (binary search over M+1 entries)
+    int lo = 0, hi = M + 1;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (cdf[mid][tid] <= u) lo = mid + 1; else hi = mid;
+    }
+    const int below = lo - 1 > 0 ? lo - 1 : 0;
+    const int above = lo < M ? lo : M;
+    const float c0 = cdf[below][tid], c1 = cdf[above][tid];
+    float denom = c1 - c0;
+    if (denom < 1e-5f) denom = 1.f;
+    const float t = (u - c0) / denom;
+    const double b0 = .5 * (z[below + 1] + z[below]);
+    const double b1 = .5 * (z[above + 1] + z[above]);
+    zi[n * I + k] = b0 + (double)t * (b1 - b0);
+  }
+}
+
+// NaN-aware strict order used for torch.sort (NaN sorts last)
+__device__ __forceinline__ bool lt_nan(double a, double b) { return (a < b) || (a == a && b != b); }
+__device__ __forceinline__ bool eq_nan(double a, double b) { return (a == b) || (a != a && b != b); }
+
+// Sort the S+I depths of ray n into ascending order; ord[q] = source index (< S: coarse).
+__device__ void sort_ray(const double* zc, const double* zi, int S, int I, double (*zl)[64], uint8_t (*ord)[64],
+                         int tid) {
+  const int M = S + I;
+  for (int m = 0; m < M; ++m) zl[m][tid] = m < S ? zc[m] : zi[m - S];
+  for (int i = 0; i < M; ++i) {
+    const double v = zl[i][tid];
+    int r = 0;
+    for (int m = 0; m < M; ++m) {
+      const double w = zl[m][tid];
+      r += (lt_nan(w, v) || (eq_nan(w, v) && m < i)) ? 1 : 0;
+    }
+    ord[r][tid] = (uint8_t)i;
+  }
+}
+
+// final pass: depth/var (float64), rgb (float32); saves the sort order for the backward
+__global__ __launch_bounds__(64) void k_fine(pnr_render_params prm, const float* __restrict__ rd,
+                                             const double* __restrict__ zc, const double* __restrict__ zi,
+                                             const float4* __restrict__ rawc, const float4* __restrict__ rawi,
+                                             int64_t n_rays, double* __restrict__ depth, double* __restrict__ var,
+                                             float* __restrict__ rgb, uint8_t* __restrict__ ord_out) {
+  __shared__ double zl[PNR_MAX_SAMPLES][64];
+  __shared__ uint8_t ord[PNR_MAX_SAMPLES][64];
+  __shared__ float wl[PNR_MAX_SAMPLES][64];
+  const int tid = threadIdx.x;
+  const int64_t n = (int64_t)blockIdx.x * 64 + tid;
+  if (n >= n_rays) return;
+  const int S = prm.n_samples, I = prm.n_importance, M = S + I;
+  sort_ray(zc + n * S, zi + n * I, S, I, zl, ord, tid);
+  const float nrm = ray_norm(rd + n * 3);
+  double T = 1.0, D = 0.0;
+  float r0 = 0.f, r1 = 0.f, r2 = 0.f;
+  for (int q = 0; q < M; ++q) {
+    const int s = ord[q][tid];
+    const double zq = zl[s][tid];
+    const float dz = q < M - 1 ? (float)(zl[ord[q + 1][tid]][tid] - zq) : 1e10f;
+    const float4 c = s < S ? rawc[n * S + s] : rawi[n * I + (s - S)];
+    const float a = 1.f - expf(-relu(c.w) * (dz * nrm));
+    const float w = a * (float)T;
+    T *= (double)(1.f - a + 1e-10f);
+    wl[q][tid] = w;
+    r0 += w * c.x; r1 += w * c.y; r2 += w * c.z;
+    D += (double)w * zq;
+  }
+  double V = 0.0;
+  for (int q = 0; q < M; ++q) {
+    const double dd = zl[ord[q][tid]][tid] - D;
+    V += (double)wl[q][tid] * dd * dd;
+  }
+  depth[n] = D;
+  var[n] = V;
+  rgb[n * 3 + 0] = r0; rgb[n * 3 + 1] = r1; rgb[n * 3 + 2] = r2;
+  if (ord_out)
+    for (int q = 0; q < M; ++q) ord_out[n * PNR_MAX_SAMPLES + q] = ord[q][tid];
+}
+
+// Backward of the final compositing: writes dL/draw (float4) for every coarse and importance
+// point, sigma channel zeroed where the point was outside the bound (Renderer.py:57 assigns
+// the density, so no gradient reaches the MLP there); g_nrm[n] = dL/d|rays_d|.
+__global__ __launch_bounds__(64) void k_fine_bwd(pnr_render_params prm, const float* __restrict__ rd,
+                                                 const double* __restrict__ zc, const double* __restrict__ zi,
+                                                 const float4* __restrict__ rawc, const float4* __restrict__ rawi,
+                                                 const uint8_t* __restrict__ insc, const uint8_t* __restrict__ insi,
+                                                 const uint8_t* __restrict__ ord_in, int64_t n_rays,
+                                                 const double* __restrict__ g_depth, const double* __restrict__ g_var,
+                                                 const float* __restrict__ g_rgb, float4* __restrict__ goc,
+                                                 float4* __restrict__ goi, float* __restrict__ g_nrm) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x;
+  const int64_t n = (int64_t)blockIdx.x * 64 + tid;
+  const int S = prm.n_samples, I = prm.n_importance, M = S + I;
+  double* zs = reinterpret_cast<double*>(smem);                 // [M][64]
+  float* wl = reinterpret_cast<float*>(zs + M * 64);            // [M][64]
+  float* al = wl + M * 64;
+  float* Tl = al + M * 64;
+  float* dzl = Tl + M * 64;
+  if (n >= n_rays) return;
+  const uint8_t* ord = ord_in + n * PNR_MAX_SAMPLES;
+  const float* dvec = rd + n * 3;
+  const float nrm = ray_norm(dvec);
+  auto zsrc = [&](int s) { return s < S ? zc[n * S + s] : zi[n * I + (s - S)]; };
+  auto rsrc = [&](int s) { return s < S ? rawc[n * S + s] : rawi[n * I + (s - S)]; };
+  double T = 1.0, D = 0.0;
+  for (int q = 0; q < M; ++q) zs[q * 64 + tid] = zsrc(ord[q]);
+  for (int q = 0; q < M; ++q) {
+    const double zq = zs[q * 64 + tid];
+    const float dz = q < M - 1 ? (float)(zs[(q + 1) * 64 + tid] - zq) : 1e10f;
+    const float4 c = rsrc(ord[q]);
+    const float a = 1.f - expf(-relu(c.w) * (dz * nrm));
+    const float w = a * (float)T;
+    Tl[q * 64 + tid] = (float)T;
+    T *= (double)(1.f - a + 1e-10f);
+    wl[q * 64 + tid] = w;
+    al[q * 64 + tid] = a;
+    dzl[q * 64 + tid] = dz;
+    D += (double)w * zq;
+  }
+  const double gd = g_depth ? g_depth[n] : 0.0;
+  const double gv = g_var ? g_var[n] : 0.0;
+  const float gr0 = g_rgb ? g_rgb[n * 3 + 0] : 0.f;
+  const float gr1 = g_rgb ? g_rgb[n * 3 + 1] : 0.f;
+  const float gr2 = g_rgb ? g_rgb[n * 3 + 2] : 0.f;
+  double sdev = 0.0;
+  for (int q = 0; q < M; ++q) sdev += (double)wl[q * 64 + tid] * (zs[q * 64 + tid] - D);
+  const double gD = gd - 2.0 * gv * sdev;  // d var / d depth = -2 sum w (z - depth)
+  float R = 0.f, gn = 0.f;
+  for (int q = M - 1; q >= 0; --q) {
+    const int s = ord[q];
+    const float4 c = rsrc(s);
+    const double zq = zs[q * 64 + tid];
+    const double dd = zq - D;
+    const float w = wl[q * 64 + tid];
+    const float gw = (gr0 * c.x + gr1 * c.y + gr2 * c.z) + (float)(gD * zq) + (float)(gv * dd * dd);
+    const float a = al[q * 64 + tid];
+    const float ga = Tl[q * 64 + tid] * (gw - R);
+    R = gw * a + (1.f - a + 1e-10f) * R;
+    const float dz = dzl[q * 64 + tid];
+    const float delta = dz * nrm;
+    const float sr = relu(c.w);
+    const float ex = expf(-sr * delta);
+    float gs = c.w > 0.f ? ga * ex * delta : 0.f;
+    const bool inside = s < S ? insc[n * S + s] != 0 : insi[n * I + (s - S)] != 0;
+    if (!inside) gs = 0.f;
+    gn += (ga * ex * sr) * dz;
+    const float4 go = make_float4(gr0 * w, gr1 * w, gr2 * w, gs);
+    if (s < S) goc[n * S + s] = go; else goi[n * I + (s - S)] = go;
+  }
+  if (g_nrm) g_nrm[n] = gn;
+}
+
+// dL/drays_o = sum_s dL/dx_s ; dL/drays_d = sum_s dL/dx_s * z_s + g_nrm * d/|d|
+template <typename ZT>
+__global__ void k_ray_grads(const float* __restrict__ rd, const ZT* __restrict__ za, int sa, const ZT* __restrict__ zb,
+                            int sb, const float* __restrict__ gxa, const float* __restrict__ gxb,
+                            const float* __restrict__ g_nrm, int64_t n_rays, float* __restrict__ g_o,
+                            float* __restrict__ g_d) {
+  const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= n_rays) return;
+  double o[3] = {0, 0, 0}, d[3] = {0, 0, 0};
+  for (int s = 0; s < sa; ++s)
+    for (int c = 0; c < 3; ++c) {
+      const double g = gxa[(n * sa + s) * 3 + c];
+      o[c] += g;
+      d[c] += g * (double)za[n * sa + s];
+    }
+  for (int s = 0; s < sb; ++s)
+    for (int c = 0; c < 3; ++c) {
+      const double g = gxb[(n * sb + s) * 3 + c];
+      o[c] += g;
+      d[c] += g * (double)zb[n * sb + s];
+    }
+  const float* dv = rd + n * 3;
+  float gn = g_nrm ? g_nrm[n] : 0.f;
+  const float nrm = ray_norm(dv);
+  for (int c = 0; c < 3; ++c) {
+    g_o[n * 3 + c] = (float)o[c];
+    const float extra = (g_nrm && nrm > 0.f) ? gn * dv[c] / nrm : 0.f;
+    g_d[n * 3 + c] = (float)d[c] + extra;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// regulation (Renderer.py:280-294): float32 z in [0, 0.85*gt], jittered by t_rand
+__global__ void k_reg_z(pnr_render_params prm, const float* __restrict__ gt, const float* __restrict__ t_rand,
+                        int64_t n_rays, float* __restrict__ z) {
+  const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= n_rays) return;
+  const int S = prm.n_samples;
+  const float far = gt[n] * 0.85f;
+  auto z0 = [&](int s) { return (0.0f * (1.f - prm.t_vals[s])) + far * prm.t_vals[s]; };
+  for (int s = 0; s < S; ++s) {
+    const float zs = z0(s);
+    const float lower = s > 0 ? .5f * (zs + z0(s - 1)) : zs;
+    const float upper = s < S - 1 ? .5f * (z0(s + 1) + zs) : zs;
+    z[n * S + s] = lower + (upper - lower) * t_rand[n * S + s];
+  }
+}
+
+__global__ void k_extract_sigma(const float4* __restrict__ raw, int64_t P, float* __restrict__ sigma) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p < P) sigma[p] = raw[p].w;
+}
+
+__global__ void k_gout_sigma(const float* __restrict__ g_sigma, const uint8_t* __restrict__ inside, int64_t P,
+                             float4* __restrict__ g_out) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p < P) g_out[p] = make_float4(0.f, 0.f, 0.f, inside[p] ? g_sigma[p] : 0.f);
+}
+
+// ---------------------------------------------------------------------------------------------
+// rays: dirs = [(i-cx)/fx, -(j-cy)/fy, -1]; rays_d = sum(dirs * c2w[:3,:3], -1); rays_o = c2w[:3,3]
+__device__ __forceinline__ void make_ray(float i, float j, float fx, float fy, float cx, float cy,
+                                         const float* __restrict__ c2w, int ld, float* o, float* d) {
+  const float dx = (i - cx) / fx, dy = -((j - cy) / fy), dzv = -1.f;
+  for (int r = 0; r < 3; ++r) {
+    // torch.sum over the last dim of 3 products: ((a0 + a1) + a2), products rounded
+    const float p0 = dx * c2w[r * ld + 0], p1 = dy * c2w[r * ld + 1], p2 = dzv * c2w[r * ld + 2];
+    d[r] = (p0 + p1) + p2;
+    o[r] = c2w[r * ld + 3];
+  }
+}
+
+__global__ void k_get_rays(int H, int W, float fx, float fy, float cx, float cy, const float* __restrict__ c2w,
+                           float* __restrict__ ro, float* __restrict__ rd) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= (int64_t)H * W) return;
+  const int row = (int)(k / W), col = (int)(k % W);
+  make_ray((float)col, (float)row, fx, fy, cx, cy, c2w, 4, ro + k * 3, rd + k * 3);
+}
+
+__global__ void k_rays_from_uv(const float* __restrict__ ii, const float* __restrict__ jj, int64_t n, float fx,
+                               float fy, float cx, float cy, const float* __restrict__ c2w, float* __restrict__ ro,
+                               float* __restrict__ rd) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  make_ray(ii[k], jj[k], fx, fy, cx, cy, c2w, 4, ro + k * 3, rd + k * 3);
+}
+
+// torch.optim.Adam (amsgrad=False, weight_decay=0), single-tensor semantics
+__global__ void k_adam(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                       float* __restrict__ v, int64_t n, float beta1, float beta2, float eps, float step_size,
+                       float bc2_sqrt) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float gi = g[i];
+  float mi = m[i];
+  mi = mi + (1.f - beta1) * (gi - mi);           // exp_avg.lerp_(grad, 1-beta1)
+  float vi = v[i] * beta2 + (1.f - beta2) * gi * gi;  // exp_avg_sq.mul_(b2).addcmul_(g, g, 1-b2)
+  m[i] = mi;
+  v[i] = vi;
+  const float denom = sqrtf(vi) / bc2_sqrt + eps;
+  p[i] = p[i] + (-step_size) * (mi / denom);
+}
+
+// ---------------------------------------------------------------------------------------------
+// launchers
+// ---------------------------------------------------------------------------------------------
+static inline unsigned nblk(int64_t n, int b) { return (unsigned)((n + b - 1) / b); }
+
+int launch_gt_max(const float* gt, int64_t n, float* out, hipStream_t st) {
+  hipLaunchKernelGGL(k_gt_max, dim3(1), dim3(1024), 0, st, gt, n, out);
+  return hip_status(hipGetLastError());
+}
+int launch_coarse_z(const pnr_render_params& prm, const float* ro, const float* rd, const float* gt,
+                    const float* gmax, int64_t n, double* z, double* far_out, hipStream_t st) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(k_coarse_z, dim3(nblk(n, 128)), dim3(128), 0, st, prm, ro, rd, gt, gmax, n, z, far_out);
+  return hip_status(hipGetLastError());
+}
+int launch_pdf(const pnr_render_params& prm, const float* rd, const double* zc, const float* rawc, int64_t n,
+               double* zi, hipStream_t st) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(k_pdf, dim3(nblk(n, 64)), dim3(64), 0, st, prm, rd, zc, (const float4*)rawc, n, zi);
+  return hip_status(hipGetLastError());
+}
+int launch_fine(const pnr_render_params& prm, const float* rd, const double* zc, const double* zi,
+                const float* rawc, const float* rawi, int64_t n, double* depth, double* var, float* rgb,
+                uint8_t* ord, hipStream_t st) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(k_fine, dim3(nblk(n, 64)), dim3(64), 0, st, prm, rd, zc, zi, (const float4*)rawc,
+                     (const float4*)rawi, n, depth, var, rgb, ord);
+  return hip_status(hipGetLastError());
+}
+int launch_fine_bwd(const pnr_render_params& prm, const float* rd, const double* zc, const double* zi,
+                    const float* rawc, const float* rawi, const uint8_t* insc, const uint8_t* insi,
+                    const uint8_t* ord, int64_t n, const double* gd, const double* gv, const float* grgb,
+                    float* goc, float* goi, float* g_nrm, hipStream_t st) {
+  if (n <= 0) return 0;
+  const int M = prm.n_samples + prm.n_importance;
+  const size_t sh = (size_t)M * 64 * (8 + 4 * 4);
+  hipLaunchKernelGGL(k_fine_bwd, dim3(nblk(n, 64)), dim3(64), sh, st, prm, rd, zc, zi, (const float4*)rawc,
+                     (const float4*)rawi, insc, insi, ord, n, gd, gv, grgb, (float4*)goc, (float4*)goi, g_nrm);
+  return hip_status(hipGetLastError());
+}
+int launch_ray_grads_f64(const float* rd, const double* za, int sa, const double* zb, int sb, const float* gxa,
+                         const float* gxb, const float* g_nrm, int64_t n, float* g_o, float* g_d, hipStream_t st) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(k_ray_grads<double>, dim3(nblk(n, 128)), dim3(128), 0, st, rd, za, sa, zb, sb, gxa, gxb, g_nrm,
+                     n, g_o, g_d);
+  return hip_status(hipGetLastError());
+}
+int launch_ray_grads_f32(const float* rd, const float* za, int sa, const float* gxa, int64_t n, float* g_o,
+                         float* g_d, hipStream_t st) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(k_ray_grads<float>, dim3(nblk(n, 128)), dim3(128), 0, st, rd, za, sa, (const float*)nullptr, 0,
+                     gxa, (const float*)nullptr, (const float*)nullptr, n, g_o, g_d);
+  return hip_status(hipGetLastError());
+}
+int launch_reg_z(const pnr_render_params& prm, const float* gt, const float* t_rand, int64_t n, float* z,
+                 hipStream_t st) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(k_reg_z, dim3(nblk(n, 128)), dim3(128), 0, st, prm, gt, t_rand, n, z);
+  return hip_status(hipGetLastError());
+}
+int launch_extract_sigma(const float* raw, int64_t P, float* sigma, hipStream_t st) {
+  if (P <= 0) return 0;
+  hipLaunchKernelGGL(k_extract_sigma, dim3(nblk(P, 256)), dim3(256), 0, st, (const float4*)raw, P, sigma);
+  return hip_status(hipGetLastError());
+}
+int launch_gout_sigma(const float* g_sigma, const uint8_t* inside, int64_t P, float* g_out, hipStream_t st) {
+  if (P <= 0) return 0;
+  hipLaunchKernelGGL(k_gout_sigma, dim3(nblk(P, 256)), dim3(256), 0, st, g_sigma, inside, P, (float4*)g_out);
+  return hip_status(hipGetLastError());
+}
+int launch_get_rays(int H, int W, float fx, float fy, float cx, float cy, const float* c2w, float* ro, float* rd,
+                    hipStream_t st) {
+  const int64_t n = (int64_t)H * W;
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(k_get_rays, dim3(nblk(n, 256)), dim3(256), 0, st, H, W, fx, fy, cx, cy, c2w, ro, rd);
+  return hip_status(hipGetLastError());
+}
+int launch_rays_from_uv(const float* i, const float* j, int64_t n, float fx, float fy, float cx, float cy,
+                        const float* c2w, float* ro, float* rd, hipStream_t st) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(k_rays_from_uv, dim3(nblk(n, 256)), dim3(256), 0, st, i, j, n, fx, fy, cx, cy, c2w, ro, rd);
+  return hip_status(hipGetLastError());
+}
+int launch_adam(float* p, const float* g, float* m, float* v, int64_t n, float beta1, float beta2, float eps,
+                float step_size, float bc2_sqrt, hipStream_t st) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(k_adam, dim3(nblk(n, 256)), dim3(256), 0, st, p, g, m, v, n, beta1, beta2, eps, step_size,
+                     bc2_sqrt);
+  return hip_status(hipGetLastError());
+}
+
+}  // namespace pnr

@@ -1,0 +1,114 @@
+"""ctypes binding of libpnr.so (the C ABI declared in include/pnr.h).
+
+The library is built in-tree (`pointnerf-slam_amd/pnr/libpnr.so`, see the Makefile) and loaded
+lazily on first use, after torch, so that it shares torch's HIP runtime (same SONAME).  There is
+no fallback: if the library is missing or cannot be loaded every GPU entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'libpnr.so')
+MAX_SAMPLES = 64
+N_PARAMS = 11
+
+c_void_p = ctypes.c_void_p
+c_int64 = ctypes.c_int64
+c_int32 = ctypes.c_int32
+c_size_t = ctypes.c_size_t
+c_float = ctypes.c_float
+
+
+class RenderParams(ctypes.Structure):
+    """Mirror of `pnr_render_params` (include/pnr.h)."""
+    _fields_ = [
+        ('n_samples', c_int32), ('n_importance', c_int32), ('lindisp', c_int32), ('far_mode', c_int32),
+        ('bound', ctypes.c_double * 6), ('far_clamp', ctypes.c_double),
+        ('t_vals', c_float * MAX_SAMPLES), ('u_vals', c_float * MAX_SAMPLES),
+        ('save_for_backward', c_int32), ('need_ray_grads', c_int32),
+    ]
+
+
+PtrArray = c_void_p * N_PARAMS
+
+# name -> (restype, argtypes)
+_SIGS = {
+    'pnr_abi_version': (ctypes.c_int, []),
+    'pnr_build_info': (ctypes.c_char_p, []),
+    'pnr_mlp_packed_floats': (c_size_t, []),
+    'pnr_mlp_pack': (ctypes.c_int, [PtrArray, c_void_p, c_void_p]),
+    'pnr_eval_points': (ctypes.c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p]),
+    'pnr_eval_points_f32': (ctypes.c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p]),
+    'pnr_mlp_train_workspace_bytes': (c_size_t, [c_int64]),
+    'pnr_mlp_fwd_train': (ctypes.c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_size_t, c_void_p]),
+    'pnr_mlp_bwd_workspace_bytes': (c_size_t, [c_int64]),
+    'pnr_mlp_bwd': (ctypes.c_int, [c_void_p, c_int64, c_void_p, PtrArray, c_void_p, c_void_p, c_size_t,
+                                   c_void_p, c_size_t, c_void_p]),
+    'pnr_render_workspace_bytes': (c_size_t, [ctypes.POINTER(RenderParams), c_int64]),
+    'pnr_render_fwd': (ctypes.c_int, [ctypes.POINTER(RenderParams), c_void_p, c_void_p, c_void_p, c_void_p, c_int64,
+                                      c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
+    'pnr_render_bwd_workspace_bytes': (c_size_t, [ctypes.POINTER(RenderParams), c_int64]),
+    'pnr_render_bwd': (ctypes.c_int, [ctypes.POINTER(RenderParams), c_void_p, c_void_p, c_void_p, c_void_p, c_int64,
+                                      c_void_p, c_void_p, c_void_p, PtrArray, c_void_p, c_void_p,
+                                      c_void_p, c_size_t, c_void_p, c_size_t, c_void_p]),
+    'pnr_regulation_workspace_bytes': (c_size_t, [ctypes.POINTER(RenderParams), c_int64]),
+    'pnr_regulation_fwd': (ctypes.c_int, [ctypes.POINTER(RenderParams), c_void_p, c_void_p, c_void_p, c_void_p,
+                                          c_void_p, c_int64, c_void_p, c_void_p, c_size_t, c_void_p]),
+    'pnr_regulation_bwd_workspace_bytes': (c_size_t, [ctypes.POINTER(RenderParams), c_int64]),
+    'pnr_regulation_bwd': (ctypes.c_int, [ctypes.POINTER(RenderParams), c_void_p, c_void_p, c_void_p, c_void_p,
+                                          c_int64, c_void_p, PtrArray, c_void_p, c_void_p, c_void_p, c_size_t,
+                                          c_void_p, c_size_t, c_void_p]),
+    'pnr_get_rays': (ctypes.c_int, [c_int32, c_int32, c_float, c_float, c_float, c_float, c_void_p, c_void_p,
+                                    c_void_p, c_void_p]),
+    'pnr_rays_from_uv': (ctypes.c_int, [c_void_p, c_void_p, c_int64, c_float, c_float, c_float, c_float, c_void_p,
+                                        c_void_p, c_void_p, c_void_p]),
+    'pnr_adam_step': (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_float, c_float, c_float,
+                                     c_float, c_int64, c_void_p]),
+}
+SYMBOLS = tuple(_SIGS)
+
+_lib = None
+_lock = threading.Lock()
+
+
+def load(path: str = LIB_PATH):
+    """Load (once) and return the ctypes library; raises RuntimeError if it is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(path):
+                raise RuntimeError(f'pnr: HIP library {path} not built (run `make -C pointnerf-slam_amd`)')
+            lib = ctypes.CDLL(path)
+            for name, (res, args) in _SIGS.items():
+                fn = getattr(lib, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = lib
+    return _lib
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        kind = {-1: 'bad argument', -2: 'workspace too small', -3: 'rocBLAS failure'}.get(rc, f'hipError {rc}')
+        raise RuntimeError(f'pnr: {what} failed ({kind})')
+
+
+def ptr(t) -> c_void_p:
+    return c_void_p(0 if t is None else t.data_ptr())
+
+
+def stream_of(device=None) -> c_void_p:
+    return c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def require_cuda(*tensors):
+    for t in tensors:
+        if t is not None and not t.is_cuda:
+            raise RuntimeError('pnr: the renderer runs on the MI355X HIP path only; got a CPU tensor '
+                               '(the CPU restatement lives in oracle/, test infrastructure only)')

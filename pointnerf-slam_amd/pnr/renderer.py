@@ -1,0 +1,292 @@
+"""Drop-in `Renderer` (src/utils/Renderer.py:5-301) running on libpnr.so.
+
+Same constructor and method signatures as the reference; every method dispatches to the C ABI
+(include/pnr.h) through autograd Functions:
+
+  eval_points       -> pnr_eval_points            Renderer.py:23-61
+  render_batch_ray  -> pnr_render_fwd / _bwd      Renderer.py:63-203
+  render_img        -> pnr_get_rays + fwd chunks  Renderer.py:205-260
+  regulation        -> pnr_regulation_fwd / _bwd  Renderer.py:263-301
+
+The decoder must be `pnr.decoder.MLP` (or any module exposing `ordered_params()` with the
+reference state_dict tensors).  Inputs must be CUDA tensors: there is no CPU path here (the CPU
+restatement in oracle/ is test infrastructure only).
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+from .packing import PackedMLP
+
+_GRAD_SHAPES = ((3, 93), (256, 93), (256,), (256, 256), (256,), (256, 256), (256,), (256, 256), (256,), (4, 256),
+                (4,))
+
+
+def _linspace_table(n):
+    """torch.linspace(0,1,n) float32 exactly as the reference computes it (Renderer.py:157)."""
+    out = [0.0] * _lib.MAX_SAMPLES
+    if n > 0:
+        for i, v in enumerate(torch.linspace(0., 1., steps=n).tolist()):
+            out[i] = v
+    return out
+
+
+def _decoder_params(decoders):
+    if hasattr(decoders, 'ordered_params'):
+        return decoders.ordered_params()
+    from .decoder import PARAM_ORDER
+    sd = dict(decoders.named_parameters())
+    return [sd[k] for k in PARAM_ORDER]
+
+
+def _packer(decoders):
+    pk = getattr(decoders, '_packed', None)
+    if pk is None:
+        pk = PackedMLP()
+        try:
+            decoders._packed = pk
+        except AttributeError:
+            pass
+    return pk
+
+
+class _RenderFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, prm_bytes, packer, rays_o, rays_d, gt_depth, far_clamp, *params):
+        lib = _lib.load()
+        prm = _lib.RenderParams.from_buffer_copy(prm_bytes)
+        n = rays_o.shape[0]
+        dev = rays_o.device
+        packed = packer.image(params)
+        need = any(ctx.needs_input_grad)  # (inside forward grad mode is off; ask autograd)
+        prm.save_for_backward = 1 if need else 0
+        prm.need_ray_grads = 1 if (ctx.needs_input_grad[2] or ctx.needs_input_grad[3]) else 0
+        if far_clamp is not None:
+            prm.far_mode = 1
+            prm.far_clamp = float(far_clamp)
+        ws = torch.empty(lib.pnr_render_workspace_bytes(ctypes_ref(prm), n), dtype=torch.uint8, device=dev)
+        depth = torch.empty(n, dtype=torch.float64, device=dev)
+        var = torch.empty(n, dtype=torch.float64, device=dev)
+        rgb = torch.empty((n, 3), dtype=torch.float32, device=dev)
+        _lib.check(lib.pnr_render_fwd(ctypes_ref(prm), _lib.ptr(packed), _lib.ptr(rays_o), _lib.ptr(rays_d),
+                                      _lib.ptr(gt_depth), n, _lib.ptr(depth), _lib.ptr(var), _lib.ptr(rgb),
+                                      _lib.ptr(ws), ws.numel(), _lib.stream_of(dev)), 'render_fwd')
+        if need:
+            ctx.prm = bytes(prm)
+            ctx.save_for_backward(ws, packed, rays_o, rays_d)
+        return depth, var, rgb
+
+    @staticmethod
+    def backward(ctx, g_depth, g_var, g_rgb):
+        lib = _lib.load()
+        ws, packed, rays_o, rays_d = ctx.saved_tensors
+        prm = _lib.RenderParams.from_buffer_copy(ctx.prm)
+        n = rays_o.shape[0]
+        dev = rays_o.device
+        grads = [torch.zeros(s, device=dev, dtype=torch.float32) for s in _GRAD_SHAPES]
+        g_o = g_d = None
+        if prm.need_ray_grads:
+            g_o = torch.empty((n, 3), device=dev, dtype=torch.float32)
+            g_d = torch.empty((n, 3), device=dev, dtype=torch.float32)
+        bws = torch.empty(lib.pnr_render_bwd_workspace_bytes(ctypes_ref(prm), n), dtype=torch.uint8, device=dev)
+        arr = _lib.PtrArray(*[g.data_ptr() for g in grads])
+        gd = None if g_depth is None else g_depth.contiguous()
+        gv = None if g_var is None else g_var.contiguous()
+        gc = None if g_rgb is None else g_rgb.contiguous()
+        _lib.check(lib.pnr_render_bwd(ctypes_ref(prm), _lib.ptr(packed), None, _lib.ptr(rays_o), _lib.ptr(rays_d),
+                                      n, _lib.ptr(gd), _lib.ptr(gv), _lib.ptr(gc), arr, _lib.ptr(g_o),
+                                      _lib.ptr(g_d), _lib.ptr(ws), ws.numel(), _lib.ptr(bws), bws.numel(),
+                                      _lib.stream_of(dev)), 'render_bwd')
+        return (None, None, g_o, g_d, None, None, *grads)
+
+
+class _RegulationFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, prm_bytes, packer, rays_o, rays_d, gt_depth, t_rand, *params):
+        lib = _lib.load()
+        prm = _lib.RenderParams.from_buffer_copy(prm_bytes)
+        n = rays_o.shape[0]
+        dev = rays_o.device
+        packed = packer.image(params)
+        need = any(ctx.needs_input_grad)  # (inside forward grad mode is off; ask autograd)
+        prm.save_for_backward = 1 if need else 0
+        prm.need_ray_grads = 1 if (ctx.needs_input_grad[2] or ctx.needs_input_grad[3]) else 0
+        ws = torch.empty(lib.pnr_regulation_workspace_bytes(ctypes_ref(prm), n), dtype=torch.uint8, device=dev)
+        sigma = torch.empty(n * prm.n_samples, dtype=torch.float32, device=dev)
+        _lib.check(lib.pnr_regulation_fwd(ctypes_ref(prm), _lib.ptr(packed), _lib.ptr(rays_o), _lib.ptr(rays_d),
+                                          _lib.ptr(gt_depth), _lib.ptr(t_rand), n, _lib.ptr(sigma), _lib.ptr(ws),
+                                          ws.numel(), _lib.stream_of(dev)), 'regulation_fwd')
+        if need:
+            ctx.prm = bytes(prm)
+            ctx.save_for_backward(ws, packed, rays_o, rays_d)
+        return sigma
+
+    @staticmethod
+    def backward(ctx, g_sigma):
+        lib = _lib.load()
+        ws, packed, rays_o, rays_d = ctx.saved_tensors
+        prm = _lib.RenderParams.from_buffer_copy(ctx.prm)
+        n = rays_o.shape[0]
+        dev = rays_o.device
+        grads = [torch.zeros(s, device=dev, dtype=torch.float32) for s in _GRAD_SHAPES]
+        g_o = g_d = None
+        if prm.need_ray_grads:
+            g_o = torch.empty((n, 3), device=dev, dtype=torch.float32)
+            g_d = torch.empty((n, 3), device=dev, dtype=torch.float32)
+        bws = torch.empty(lib.pnr_regulation_bwd_workspace_bytes(ctypes_ref(prm), n), dtype=torch.uint8, device=dev)
+        arr = _lib.PtrArray(*[g.data_ptr() for g in grads])
+        _lib.check(lib.pnr_regulation_bwd(ctypes_ref(prm), _lib.ptr(packed), None, _lib.ptr(rays_o),
+                                          _lib.ptr(rays_d), n, _lib.ptr(g_sigma.contiguous()), arr, _lib.ptr(g_o),
+                                          _lib.ptr(g_d), _lib.ptr(ws), ws.numel(), _lib.ptr(bws), bws.numel(),
+                                          _lib.stream_of(dev)), 'regulation_bwd')
+        return (None, None, g_o, g_d, None, None, *grads)
+
+
+def ctypes_ref(prm):
+    import ctypes
+    return ctypes.byref(prm)
+
+
+class Renderer(object):
+    """src/utils/Renderer.py:5-21 (same signature and cfg keys)."""
+
+    def __init__(self, cfg, args, slam, points_batch_size=500000, ray_batch_size=100000):
+        self.ray_batch_size = ray_batch_size
+        self.points_batch_size = points_batch_size
+        self.lindisp = cfg['rendering']['lindisp']
+        self.perturb = cfg['rendering']['perturb']
+        self.N_samples = cfg['rendering']['N_samples']
+        self.N_surface = cfg['rendering']['N_surface']
+        self.N_importance = cfg['rendering']['N_importance']
+        self.scale = cfg['scale']
+        self.occupancy = cfg['occupancy']
+        self.nice = False
+        self.bound = slam.bound
+        self.H, self.W, self.fx, self.fy, self.cx, self.cy = slam.H, slam.W, slam.fx, slam.fy, slam.cx, slam.cy
+        if self.N_surface > 0 or self.occupancy or self.perturb > 0.:
+            raise NotImplementedError('pnr.Renderer: N_surface>0 / occupancy / perturb>0 are not on the '
+                                      'configs/pointNeRF_slam.yaml path (SURVEY.md section 8)')
+        if self.N_samples + self.N_importance > _lib.MAX_SAMPLES or self.N_samples < 3:
+            raise ValueError('pnr.Renderer: need 3 <= N_samples and N_samples + N_importance <= 64')
+
+    # -- helpers --------------------------------------------------------------------------------
+    def _bound6(self):
+        b = self.bound
+        b = b.detach().cpu().double().reshape(3, 2) if isinstance(b, torch.Tensor) else torch.tensor(b).double()
+        return [float(v) for v in b.reshape(-1)]
+
+    def params(self, n_samples=None, n_importance=None):
+        prm = _lib.RenderParams()
+        prm.n_samples = self.N_samples if n_samples is None else n_samples
+        prm.n_importance = self.N_importance if n_importance is None else n_importance
+        prm.lindisp = 1 if self.lindisp else 0
+        prm.far_mode = 0
+        for i, v in enumerate(self._bound6()):
+            prm.bound[i] = v
+        for i, v in enumerate(_linspace_table(prm.n_samples)):
+            prm.t_vals[i] = v
+        for i, v in enumerate(_linspace_table(prm.n_importance)):
+            prm.u_vals[i] = v
+        return prm
+
+    # -- reference API ------------------------------------------------------------------------------
+    def eval_points(self, p, decoders, c=None, stage='color', device='cuda:0'):
+        """Renderer.py:23-61: raw (P,4) float32, density := 100 outside the bound (strict)."""
+        _lib.require_cuda(p)
+        lib = _lib.load()
+        packed = _packer(decoders).image(_decoder_params(decoders))
+        P = p.shape[0]
+        raw = torch.empty((P, 4), dtype=torch.float32, device=p.device)
+        import ctypes
+        bound = (ctypes.c_double * 6)(*self._bound6())
+        if p.dtype == torch.float64:
+            fn = lib.pnr_eval_points
+        else:
+            fn = lib.pnr_eval_points_f32
+            p = p.float()
+        _lib.check(fn(_lib.ptr(packed), _lib.ptr(p.contiguous()), P, bound, _lib.ptr(raw), _lib.stream_of(p.device)),
+                   'eval_points')
+        return raw
+
+    def render_batch_ray(self, c, decoders, rays_d, rays_o, device, stage, gt_depth=None, far_clamp=None):
+        """Renderer.py:63-203 -> (depth f64 (N,), uncertainty f64 (N,), color f32 (N,3)).
+
+        `far_clamp` (extension, default None = reference behaviour) overrides the batch-global
+        max(1.2*gt) of Renderer.py:112 -- used by a ray-sharded caller to keep 1-GPU semantics."""
+        _lib.require_cuda(rays_o, rays_d, gt_depth)
+        rays_o = rays_o.float().contiguous()
+        rays_d = rays_d.float().contiguous()
+        gt = None if gt_depth is None else gt_depth.reshape(-1).float().contiguous()
+        prm = self.params()
+        params = _decoder_params(decoders)
+        return _RenderFn.apply(bytes(prm), _packer(decoders), rays_o, rays_d, gt, far_clamp, *params)
+
+    def render_img(self, c, decoders, c2w, device, stage, gt_depth=None):
+        """Renderer.py:205-260: full frame in ray_batch_size chunks, float64 depth/uncertainty."""
+        with torch.no_grad():
+            H, W = self.H, self.W
+            rays_o, rays_d = get_rays(H, W, self.fx, self.fy, self.cx, self.cy, c2w, device)
+            rays_o = rays_o.reshape(-1, 3)
+            rays_d = rays_d.reshape(-1, 3)
+            gt = None if gt_depth is None else gt_depth.reshape(-1)
+            ds, vs, cs = [], [], []
+            for i in range(0, rays_d.shape[0], self.ray_batch_size):
+                g = None if gt is None else gt[i:i + self.ray_batch_size]
+                d, v, col = self.render_batch_ray(c, decoders, rays_d[i:i + self.ray_batch_size],
+                                                  rays_o[i:i + self.ray_batch_size], device, stage, gt_depth=g)
+                ds.append(d.double()); vs.append(v.double()); cs.append(col)
+            return (torch.cat(ds).reshape(H, W), torch.cat(vs).reshape(H, W), torch.cat(cs).reshape(H, W, 3))
+
+    def regulation(self, c, decoders, rays_d, rays_o, gt_depth, device, stage='color', t_rand=None):
+        """Renderer.py:263-301: density at N_samples jittered depths in [0, 0.85*gt].
+        `t_rand` (extension) supplies the jitter; default draws torch.rand on the device."""
+        _lib.require_cuda(rays_o, rays_d, gt_depth)
+        rays_o = rays_o.float().contiguous()
+        rays_d = rays_d.float().contiguous()
+        gt = gt_depth.reshape(-1).float().contiguous()
+        n = rays_o.shape[0]
+        if t_rand is None:
+            t_rand = torch.rand((n, self.N_samples), device=rays_o.device)
+        t_rand = t_rand.float().contiguous()
+        prm = self.params(n_importance=0)
+        params = _decoder_params(decoders)
+        return _RegulationFn.apply(bytes(prm), _packer(decoders), rays_o, rays_d, gt, t_rand, *params)
+
+
+def get_rays(H, W, fx, fy, cx, cy, c2w, device):
+    """src/common.py:248-266 on the device: (H,W,3) rays_o, rays_d float32."""
+    lib = _lib.load()
+    if not isinstance(c2w, torch.Tensor):
+        c2w = torch.as_tensor(c2w)
+    c2w = c2w.to(device=device, dtype=torch.float32)
+    if c2w.shape[0] == 3:
+        c2w = torch.cat([c2w, torch.tensor([[0., 0., 0., 1.]], device=c2w.device)], 0)
+    c2w = c2w.contiguous()
+    _lib.require_cuda(c2w)
+    ro = torch.empty((H, W, 3), dtype=torch.float32, device=c2w.device)
+    rd = torch.empty((H, W, 3), dtype=torch.float32, device=c2w.device)
+    _lib.check(lib.pnr_get_rays(H, W, float(fx), float(fy), float(cx), float(cy), _lib.ptr(c2w), _lib.ptr(ro),
+                                _lib.ptr(rd), _lib.stream_of(c2w.device)), 'get_rays')
+    return ro, rd
+
+
+def get_rays_from_uv(i, j, c2w, H, W, fx, fy, cx, cy, device):
+    """src/common.py:74-89 on the device: rays for pixel coordinates (i column, j row)."""
+    lib = _lib.load()
+    if not isinstance(c2w, torch.Tensor):
+        c2w = torch.as_tensor(c2w)
+    c2w = c2w.to(device=device, dtype=torch.float32)
+    if c2w.shape[0] == 3:
+        c2w = torch.cat([c2w, torch.tensor([[0., 0., 0., 1.]], device=c2w.device)], 0)
+    c2w = c2w.contiguous()
+    i = i.reshape(-1).float().contiguous()
+    j = j.reshape(-1).float().contiguous()
+    _lib.require_cuda(c2w, i, j)
+    n = i.shape[0]
+    ro = torch.empty((n, 3), dtype=torch.float32, device=c2w.device)
+    rd = torch.empty((n, 3), dtype=torch.float32, device=c2w.device)
+    _lib.check(lib.pnr_rays_from_uv(_lib.ptr(i), _lib.ptr(j), n, float(fx), float(fy), float(cx), float(cy),
+                                    _lib.ptr(c2w), _lib.ptr(ro), _lib.ptr(rd), _lib.stream_of(c2w.device)),
+               'rays_from_uv')
+    return ro, rd

@@ -1,0 +1,91 @@
+"""Host-side logic of the pnr mirror that needs no GPU: config loading, pose helpers, bound,
+linspace tables, decoder construction / state_dict compatibility, CPU-tensor refusal."""
+import os
+import sys
+import types
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import REPO, load_golden, golden_params
+
+sys.path.insert(0, os.path.join(REPO, 'pointnerf-slam_amd'))
+import pnr  # noqa: E402
+from pnr import renderer as R  # noqa: E402
+from oracle import ref_render as ref  # noqa: E402
+
+
+def test_linspace_tables_match_torch():
+    for n in (1, 2, 12, 32, 44, 64):
+        t = R._linspace_table(n)
+        assert np.array_equal(np.array(t[:n], dtype=np.float32), torch.linspace(0., 1., n).numpy())
+
+
+def test_scaled_bound_matches_golden():
+    s = load_golden('scene.npz')
+    b = pnr.scaled_bound(s['bound_cfg'], float(s['scale']), float(s['bound_divisible']))
+    assert torch.equal(b, torch.from_numpy(s['bound']))
+
+
+def test_pose_helpers_roundtrip():
+    s = load_golden('scene.npz')
+    for c2w in s['poses']:
+        t = pnr.get_tensor_from_camera(torch.from_numpy(c2w))
+        RT = pnr.get_camera_from_tensor(t)
+        np.testing.assert_allclose(RT.numpy(), c2w[:3, :4], atol=2e-6)
+        np.testing.assert_allclose(RT.numpy(), ref.camera_from_tensor(t).numpy(), atol=0)
+
+
+def test_decoder_state_dict_compat():
+    params = golden_params('trained')
+    dec = pnr.MLP(dim=3, c_dim=0, color=True, hidden_size=256, skips=[], n_blocks=4, pos_embedding_method='fourier')
+    assert set(dec.state_dict().keys()) == set(params.keys())
+    dec.load_state_dict(params)
+    assert sum(p.numel() for p in dec.parameters()) == 222747
+    import copy
+    dec2 = copy.deepcopy(dec)
+    assert all(torch.equal(a, b) for a, b in zip(dec.parameters(), dec2.parameters()))
+    dec.share_memory()
+    with pytest.raises(NotImplementedError):
+        pnr.MLP(c_dim=32, color=True, skips=[], n_blocks=4, hidden_size=256)
+
+
+def test_get_model_from_cfg():
+    dec = pnr.get_model(pnr.ROOM0_CFG, nice=False)
+    assert isinstance(dec, pnr.MLP)
+    with pytest.raises(NotImplementedError):
+        pnr.get_model(pnr.ROOM0_CFG, nice=True)
+
+
+def test_load_config_inherit(tmp_path):
+    (tmp_path / 'base.yaml').write_text('rendering:\n  N_samples: 32\n  N_importance: 12\nscale: 1\n')
+    (tmp_path / 'mid.yaml').write_text(f'inherit_from: {tmp_path}/base.yaml\nscale: 0.1\n')
+    (tmp_path / 'leaf.yaml').write_text(f'inherit_from: {tmp_path}/mid.yaml\nrendering:\n  N_samples: 16\n')
+    cfg = pnr.load_config(str(tmp_path / 'leaf.yaml'))
+    assert cfg['scale'] == 0.1 and cfg['rendering'] == {'N_samples': 16, 'N_importance': 12}
+
+
+def test_renderer_refuses_cpu_tensors():
+    s = load_golden('scene.npz')
+    slam = types.SimpleNamespace(bound=torch.from_numpy(s['bound']), H=680, W=1200, fx=600., fy=600., cx=599.5,
+                                 cy=339.5)
+    r = pnr.Renderer(pnr.ROOM0_CFG, None, slam)
+    dec = pnr.get_model(pnr.ROOM0_CFG, nice=False)
+    with pytest.raises(RuntimeError, match='HIP path only'):
+        r.render_batch_ray({}, dec, torch.zeros(4, 3), torch.zeros(4, 3), 'cpu', 'color')
+    with pytest.raises(RuntimeError, match='HIP path only'):
+        dec(torch.zeros(1, 5, 3))
+    prm = r.params()
+    assert prm.n_samples == 32 and prm.n_importance == 12 and list(prm.bound)[:2] == [float(s['bound'][0, 0]),
+                                                                                       float(s['bound'][0, 1])]
+
+
+def test_renderer_rejects_out_of_scope_cfg():
+    s = load_golden('scene.npz')
+    slam = types.SimpleNamespace(bound=torch.from_numpy(s['bound']), H=1, W=1, fx=1., fy=1., cx=0., cy=0.)
+    import copy
+    cfg = copy.deepcopy(pnr.ROOM0_CFG)
+    cfg['rendering']['N_surface'] = 4
+    with pytest.raises(NotImplementedError):
+        pnr.Renderer(cfg, None, slam)
