@@ -1,0 +1,214 @@
+#!/usr/bin/env python3
+"""Benchmark: rendered rays/s per mapping iteration (BASELINE.json metric) on MI355X.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload map|fwd] [--rays R]
+
+Workload `map` (default; SURVEY.md 8(d) "S-map"): one full Mapper iteration of
+src/Mapper.py:507-662 for the effective room0 config (configs/pointNeRF_slam.yaml +
+configs/Replica/room0_point.yaml: 32 stratified + 12 importance samples, gt-depth near/far,
+regulation with 32 jittered samples, L1 depth + 0.05 L1 colour + 0.0005 |sigma|, backward,
+Adam lr 2e-4) over R rays per GPU (default 307,200 = one 640x480 pixel batch), fp32.
+Workload `fwd` ("S-fwd"): render_batch_ray forward, 640x480 rays x 64 stratified samples.
+
+Data: synthetic.  Decoder = the trained room0 weights committed as a golden fixture
+(tests/golden/weights.npz, from the reference's own checkpoint) -- random init if absent; rays
+from room0 pose gt_c2w_list[1000] through ScanNet-style 640x480 intrinsics; gt depth U[0.05,0.6]
+with 10% zeros; gt colour U[0,1]; seed 0 + rank.
+
+Multi-GPU (torchrun, one process per GPU, RCCL): every rank maps its own R rays (weak
+scaling); per step one scalar all_reduce(MAX) (global far clamp) and one 891 KB gradient
+all_reduce(SUM).  Rank 0 prints ONE JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, 'pointnerf-slam_amd'))
+sys.path.insert(0, REPO)
+
+METRIC = 'rendered rays/sec per mapping iter (Replica room0); PSNR Δ vs ref ≤0.1 dB'
+FP32_MFMA_PEAK_TF = 157.3          # MI355X_MICROARCH.md: f32 MFMA dense = f32 vector peak
+HBM_PEAK_GBS = 8000.0
+FLOP_PER_POINT_FWD = 443438        # 2 x (279 + 23,808 + 3 x 65,536 + 1,024) MAC
+FLOP_PER_POINT_BWD = 442880        # delta chain: 2 x (1,024 + 3 x 65,536 + 23,808) MAC
+W, H = 640, 480
+FX, FY, CX, CY = 577.59, 578.73, 318.91, 242.68   # configs/ScanNet/scannet.yaml:30-35
+
+
+def load_scene():
+    s = np.load(os.path.join(REPO, 'tests', 'golden', 'scene.npz'))
+    bound = torch.from_numpy(s['bound'])
+    pose = torch.from_numpy(s['poses'][2])            # room0 gt_c2w_list[1000]
+    wpath = os.path.join(REPO, 'tests', 'golden', 'weights.npz')
+    params = None
+    if os.path.exists(wpath):
+        w = np.load(wpath)
+        params = {k[len('trained/'):]: torch.from_numpy(w[k]) for k in w.files if k.startswith('trained/')}
+    return bound, pose, params
+
+
+def synth_batch(n, rank, pose, dev, seed=0):
+    g = torch.Generator().manual_seed(seed + 1000 * rank)
+    pix = torch.randint(0, W * H, (n,), generator=g)
+    i, j = (pix % W).float(), (pix // W).float()
+    dirs = torch.stack([(i - CX) / FX, -(j - CY) / FY, -torch.ones_like(i)], -1)
+    rd = torch.sum(dirs[:, None, :] * pose[:3, :3], -1)
+    ro = pose[:3, 3].expand(rd.shape)
+    gt = torch.rand(n, generator=g) * 0.55 + 0.05
+    gt[torch.rand(n, generator=g) < 0.1] = 0.0
+    col = torch.rand((n, 3), generator=g)
+    return (ro.contiguous().to(dev), rd.contiguous().to(dev), gt.to(dev), col.to(dev))
+
+
+def cpu_baseline(bound, pose, params, workload, n_rays=2048, reps=3):
+    """The oracle (oracle/ref_render.py, a bit-exact restatement of the reference CPU path pinned
+    by tests/test_oracle_golden.py) timed on this host: bounded sample, median of `reps`."""
+    from oracle import ref_render as ref
+    cores = torch.get_num_threads()
+    ro, rd, gt, col = [t.cpu() for t in synth_batch(n_rays, 0, pose, 'cpu', seed=7)]
+    p = {k: v.clone().requires_grad_(workload == 'map') for k, v in params.items()}
+    opt = torch.optim.Adam(list(p.values()), lr=2e-4) if workload == 'map' else None
+
+    def step():
+        if workload == 'map':
+            opt.zero_grad()
+            d, v, c = ref.render_batch_ray(p, rd, ro, bound, gt_depth=gt)
+            sig = ref.regulation(p, rd, ro, gt, bound)
+            ref.mapping_loss(d, c, gt, col, sig).backward()
+            opt.step()
+        else:
+            with torch.no_grad():
+                ref.render_batch_ray(p, rd, ro, bound, n_samples=64, n_importance=0)
+
+    step()
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        step()
+        ts.append(time.perf_counter() - t0)
+    t = float(np.median(ts))
+    return {'value': round(n_rays / t, 1), 'unit': 'rays/s', 'cores': cores, 'kind': 'port',
+            'sample': f'{workload} step on {n_rays} rays, oracle (torch CPU restatement of src/utils/Renderer.py), '
+                      f'median of {reps} after 1 warm-up, {cores} threads'}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=5)
+    ap.add_argument('--warmup', type=int, default=2)
+    ap.add_argument('--workload', choices=['map', 'fwd'], default='map')
+    ap.add_argument('--rays', type=int, default=W * H, help='rays per GPU per step')
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    args = ap.parse_args()
+
+    import pnr
+    from pnr import dist as pdist
+    from pnr._lib import timing_read
+    from pnr.mapping import MapStep
+
+    rank, world, local = pdist.init()
+    dev = torch.device('cuda', local)
+    torch.cuda.set_device(dev)
+    lib = pnr.library()
+    bound, pose, params = load_scene()
+    import types
+    slam = types.SimpleNamespace(bound=bound, H=H, W=W, fx=FX, fy=FY, cx=CX, cy=CY)
+    cfg = pnr.ROOM0_CFG
+    if args.workload == 'fwd':
+        import copy
+        cfg = copy.deepcopy(cfg)
+        cfg['rendering']['N_samples'], cfg['rendering']['N_importance'] = 64, 0
+    renderer = pnr.Renderer(cfg, None, slam)
+    dec = pnr.get_model(cfg, nice=False)
+    if params is not None:
+        dec.load_state_dict(params)
+    dec = dec.to(dev)
+    ddp = pdist.DataParallel()
+    ro, rd, gt, col = synth_batch(args.rays, rank, pose, dev)
+    n = args.rays
+
+    if args.workload == 'map':
+        mstep = MapStep(renderer, dec, lr=cfg['mapping']['imap_decoders_lr'],
+                        w_color_loss=cfg['mapping']['w_color_loss'], ddp=ddp if world > 1 else None)
+
+        def step():
+            t_rand = torch.rand((n, cfg['rendering']['N_samples']), device=dev)
+            mstep(ro, rd, gt, col, t_rand)
+    else:
+        def step():
+            with torch.no_grad():
+                renderer.render_batch_ray({}, dec, rd, ro, dev, 'color', gt_depth=None)
+
+    for _ in range(args.warmup):
+        step()
+    ddp.barrier()
+    torch.cuda.synchronize()
+    lib.pnr_timing_enable(1)
+    timing_read(0), timing_read(1)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    ddp.barrier()
+    el = time.perf_counter() - t0
+    lib.pnr_timing_enable(0)
+    kt = {'mlp_fwd': timing_read(0), 'mlp_bwd': timing_read(1)}
+    t = torch.tensor([el], device=dev, dtype=torch.float64)
+    if world > 1:
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+    el = float(t.item())
+    ms_per_step = el / args.steps * 1e3
+    value = n * world / (el / args.steps)
+
+    # roofline of the dominant hand-written kernel (fused MLP fwd or delta chain), per launch
+    best = None
+    for name, (launches, ms, units) in kt.items():
+        if launches == 0:
+            continue
+        fl = FLOP_PER_POINT_FWD if name == 'mlp_fwd' else FLOP_PER_POINT_BWD
+        cand = {'kernel': 'k_mlp_fwd' if name == 'mlp_fwd' else 'k_mlp_bwd', 'launches': launches,
+                'avg_ms': ms / launches, 'share_of_step': ms / (el * 1e3),
+                'achieved': fl * units / launches / (ms / launches * 1e-3) / 1e12}
+        if best is None or ms > best['_ms']:
+            best = dict(cand, _ms=ms)
+    roofline = None
+    if best is not None:
+        roofline = {'bound': 'mfma', 'achieved': round(best['achieved'], 2), 'peak': FP32_MFMA_PEAK_TF,
+                    'unit': 'TFLOP/s', 'frac': round(best['achieved'] / FP32_MFMA_PEAK_TF, 4), 'traffic': None,
+                    'kernel': best['kernel'], 'avg_launch_ms': round(best['avg_ms'], 3),
+                    'launches': best['launches'], 'kernel_share_of_step': round(best['share_of_step'], 3)}
+
+    if rank == 0:
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline and params is not None:
+            cpu = cpu_baseline(bound, pose, params, args.workload)
+        samples = '32+12 (+32 regulation)' if args.workload == 'map' else '64'
+        out = {
+            'metric': METRIC, 'value': round(value, 1), 'unit': 'rays/s', 'n_gpus': world, 'steps': args.steps,
+            'warmup': args.warmup, 'ms_per_step': round(ms_per_step, 3), 'higher_is_better': True, 'scaling': 'weak',
+            'vs_baseline': None, 'dtype': 'fp32',
+            'data': 'synthetic (640x480 ScanNet-intrinsics rays at room0 pose 1000, U[0.05,0.6] gt depth, trained '
+                    'room0 decoder fixture)',
+            'config': {'workload': ('S-map: full mapping iteration (render+regulation+L1 losses+backward+Adam)'
+                                    if args.workload == 'map' else 'S-fwd: render_batch_ray forward'),
+                       'rays_per_gpu': n, 'global_batch': n * world, 'samples_per_ray': samples,
+                       'parallelism': f'dp{world}'},
+            'roofline': roofline, 'cpu_baseline': cpu,
+            'kernels': {k: {'launches': v[0], 'ms': round(v[1], 3), 'units': v[2]} for k, v in kt.items()},
+        }
+        if cpu is not None:
+            out['speedup_vs_cpu'] = round(value / cpu['value'], 1)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

@@ -144,6 +144,15 @@ int pnr_rays_from_uv(const float* i, const float* j, int64_t n, float fx, float 
 int pnr_adam_step(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1,
                   float beta2, float eps, int64_t step, void* stream);
 
+/* ---- diagnostics (not on the reference API) ----------------------------------------------- */
+/* Kernel timing: while enabled, every launch of the timed kernels is bracketed by hipEvents on
+ * its own stream.  pnr_timing_read synchronises those events and returns, for `kernel`
+ * (0 = fused MLP forward k_mlp_fwd, 1 = MLP delta-chain k_mlp_bwd, 2 = ray kernels), the launch
+ * count, the summed device milliseconds and the summed number of points (MLP) or rays processed,
+ * then clears that kernel's record.  Process-global, mutex-protected; off by default. */
+int pnr_timing_enable(int on);
+int pnr_timing_read(int kernel, int64_t* launches, double* ms, int64_t* units);
+
 #ifdef __cplusplus
 }
 #endif

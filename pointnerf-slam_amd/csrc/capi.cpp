@@ -9,14 +9,15 @@
 // output, so the fine pass gathers them from the coarse results through the sort order.
 //
 // Backward: compositing backward -> per point dL/draw -> (chunks of <= kBwdChunk points)
-// delta chain kernel -> weight-gradient GEMMs on rocBLAS (sgemm / sgemv, accumulate) ->
-// optional ray gradients.
+// delta chain kernel (mlp.hip) -> split-K weight-gradient MFMA GEMMs (wgrad.hip, atomically
+// accumulated) -> optional ray gradients.
 #include <hip/hip_runtime.h>
-#include <rocblas/rocblas.h>
 
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <mutex>
+#include <vector>
 
 #include "pnr_internal.h"
 
@@ -40,14 +41,49 @@ int launch_get_rays(int, int, float, float, float, float, const float*, float*, 
 int launch_rays_from_uv(const float*, const float*, int64_t, float, float, float, float, const float*, float*,
                         float*, hipStream_t);
 int launch_adam(float*, const float*, float*, float*, int64_t, float, float, float, float, float, hipStream_t);
+int launch_wgrad(int MT, int NT, const float* A, int64_t lda, int ma, const float* B, int64_t ldb, int nb, int64_t K,
+                 float* C, int64_t ldc, float* bias, hipStream_t st);
 }  // namespace pnr
 
 using namespace pnr;
 
+// ---- diagnostics: kernel timing --------------------------------------------------------------
+namespace {
+struct TimedLaunch {
+  hipEvent_t a, b;
+  int64_t units;
+};
+std::mutex g_tmu;
+bool g_timing = false;
+std::vector<TimedLaunch> g_tl[kTimeKinds];
+}  // namespace
+
+namespace pnr {
+TimingScope::TimingScope(int k, int64_t u, hipStream_t s) : st(s), kind(k), units(u) {
+  bool on;
+  {
+    std::lock_guard<std::mutex> g(g_tmu);
+    on = g_timing;
+  }
+  if (!on) return;
+  if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) {
+    a = b = nullptr;
+    return;
+  }
+  (void)hipEventRecord(a, st);
+}
+TimingScope::~TimingScope() {
+  if (!a) return;
+  (void)hipEventRecord(b, st);
+  std::lock_guard<std::mutex> g(g_tmu);
+  g_tl[kind].push_back({a, b, units});
+}
+}  // namespace pnr
+
 namespace {
 
 constexpr size_t kAlign = 256;
-constexpr int64_t kBwdChunk = 1 << 20;  // points per delta-chain / GEMM chunk
+constexpr int64_t kBwdChunk = 1 << 22;  // points per delta-chain / GEMM chunk (4.5 KB each)
 
 inline size_t align_up(size_t x) { return (x + kAlign - 1) / kAlign * kAlign; }
 inline int64_t pad128(int64_t x) { return (x + 127) / 128 * 128; }
@@ -115,7 +151,6 @@ struct BwdWS {
   float* dT;      // [4][256][C]
   float* gargT;   // [96][C]
   float* goutT;   // [4][C]
-  float* ones;    // [C]
   int64_t C;
 };
 
@@ -130,31 +165,8 @@ BwdWS carve_bwd(int64_t P, int64_t n, void* ws, size_t* bytes) {
   b.dT = c.take<float>((size_t)4 * kHidden * b.C);
   b.gargT = c.take<float>(kFourierPad * b.C);
   b.goutT = c.take<float>(4 * b.C);
-  b.ones = c.take<float>(b.C);
   if (bytes) *bytes = c.off;
   return b;
-}
-
-// ---- rocBLAS ------------------------------------------------------------------------------
-rocblas_handle blas_handle(hipStream_t st) {
-  thread_local rocblas_handle h = nullptr;
-  if (!h && rocblas_create_handle(&h) != rocblas_status_success) return nullptr;
-  rocblas_set_stream(h, st);
-  return h;
-}
-
-// row-major C[M][Nc] (ldc) += A[M][K] (lda) * B[Nc][K]^T (ldb)
-bool gemm_abt(rocblas_handle h, int M, int Nc, int64_t K, const float* A, int64_t lda, const float* B,
-              int64_t ldb, float* C, int64_t ldc) {
-  const float one = 1.f;
-  return rocblas_sgemm(h, rocblas_operation_transpose, rocblas_operation_none, Nc, M, (rocblas_int)K, &one, B,
-                       (rocblas_int)ldb, A, (rocblas_int)lda, &one, C, (rocblas_int)ldc) == rocblas_status_success;
-}
-// y[M] += sum_k A[M][k]  (row-major A, lda)
-bool rowsum(rocblas_handle h, int M, int64_t K, const float* A, int64_t lda, const float* ones, float* y) {
-  const float one = 1.f;
-  return rocblas_sgemv(h, rocblas_operation_transpose, (rocblas_int)K, M, &one, A, (rocblas_int)lda, ones, 1, &one,
-                       y, 1) == rocblas_status_success;
 }
 
 __global__ void k_fill(float* p, int64_t n, float v) {
@@ -165,9 +177,6 @@ __global__ void k_fill(float* p, int64_t n, float v) {
 // Shared backward core over P points with saved activations `sv` and dL/draw in b.g_out.
 int mlp_backward_core(const float* packed, const SaveArgs& sv, int64_t P, BwdWS& b, float* const* grads,
                       bool want_gx, hipStream_t st) {
-  rocblas_handle h = blas_handle(st);
-  if (!h) return PNR_E_BLAS;
-  hipLaunchKernelGGL(k_fill, dim3((unsigned)((b.C + 255) / 256)), dim3(256), 0, st, b.ones, b.C, 1.f);
   for (int64_t p0 = 0; p0 < P; p0 += b.C) {
     const int64_t C = (P - p0) < b.C ? (P - p0) : b.C;
     BwdArgs a;
@@ -185,23 +194,21 @@ int mlp_backward_core(const float* packed, const SaveArgs& sv, int64_t P, BwdWS&
     if (rc) return rc;
     const int64_t ld = sv.ld, ldd = b.C;
     const float* h1 = sv.hT + p0;
-    bool ok = true;
     // output layer: dWo (4x256) += goutT (4xC) . h4^T ; dbo += rowsum(goutT)
-    ok &= gemm_abt(h, 4, kHidden, C, b.goutT, ldd, h1 + 3 * (int64_t)kHidden * ld, ld, grads[9], kHidden);
-    ok &= rowsum(h, 4, C, b.goutT, ldd, b.ones, grads[10]);
-    // hidden layers: dW_l += delta_{l+1} . h_l^T   (W3: delta4.h3, W2: delta3.h2, W1: delta2.h1)
-    for (int l = 3; l >= 1; --l) {
-      const float* dl = b.dT + (int64_t)l * kHidden * ldd;  // delta_{l+1}
-      ok &= gemm_abt(h, kHidden, kHidden, C, dl, ldd, h1 + (int64_t)(l - 1) * kHidden * ld, ld, grads[1 + 2 * l],
-                     kHidden);
-      ok &= rowsum(h, kHidden, C, dl, ldd, b.ones, grads[2 + 2 * l]);
-    }
+    rc = launch_wgrad(1, 8, b.goutT, ldd, 4, h1 + 3 * (int64_t)kHidden * ld, ld, kHidden, C, grads[9], kHidden,
+                      grads[10], st);
+    if (rc) return rc;
+    // hidden layers: dW_l += delta_{l+1} . h_l^T  (W3: delta4.h3, W2: delta3.h2, W1: delta2.h1)
+    for (int l = 3; l >= 1 && rc == 0; --l)
+      rc = launch_wgrad(8, 8, b.dT + (int64_t)l * kHidden * ldd, ldd, kHidden, h1 + (int64_t)(l - 1) * kHidden * ld,
+                        ld, kHidden, C, grads[1 + 2 * l], kHidden, grads[2 + 2 * l], st);
+    if (rc) return rc;
     // first layer: dW0 (256x93) += delta1 . e^T ; db0
-    ok &= gemm_abt(h, kHidden, kFourier, C, b.dT, ldd, sv.eT + p0, ld, grads[1], kFourier);
-    ok &= rowsum(h, kHidden, C, b.dT, ldd, b.ones, grads[2]);
-    // Fourier: dB (3x93) += x^T . g_arg  ->  row-major C[3][93] += xT (3xC) . gargT(93xC)^T
-    ok &= gemm_abt(h, 3, kFourier, C, sv.xT + p0, ld, b.gargT, ldd, grads[0], kFourier);
-    if (!ok) return PNR_E_BLAS;
+    rc = launch_wgrad(8, 3, b.dT, ldd, kHidden, sv.eT + p0, ld, kFourier, C, grads[1], kFourier, grads[2], st);
+    if (rc) return rc;
+    // Fourier: dB (3x93) += x . g_arg^T
+    rc = launch_wgrad(1, 3, sv.xT + p0, ld, 3, b.gargT, ldd, kFourier, C, grads[0], kFourier, nullptr, st);
+    if (rc) return rc;
   }
   return hip_status(hipGetLastError());
 }
@@ -218,6 +225,35 @@ bool check_params(const float* const* params) {
 extern "C" {
 
 int pnr_abi_version(void) { return PNR_ABI_VERSION; }
+
+int pnr_timing_enable(int on) {
+  std::lock_guard<std::mutex> g(g_tmu);
+  g_timing = on != 0;
+  return PNR_OK;
+}
+
+int pnr_timing_read(int kernel, int64_t* launches, double* ms, int64_t* units) {
+  if (kernel < 0 || kernel >= kTimeKinds || !launches || !ms || !units) return PNR_E_ARG;
+  std::vector<TimedLaunch> v;
+  {
+    std::lock_guard<std::mutex> g(g_tmu);
+    v.swap(g_tl[kernel]);
+  }
+  double tot = 0.0;
+  int64_t u = 0;
+  for (auto& t : v) {
+    float e = 0.f;
+    (void)hipEventSynchronize(t.b);
+    if (hipEventElapsedTime(&e, t.a, t.b) == hipSuccess) tot += e;
+    u += t.units;
+    (void)hipEventDestroy(t.a);
+    (void)hipEventDestroy(t.b);
+  }
+  *launches = (int64_t)v.size();
+  *ms = tot;
+  *units = u;
+  return PNR_OK;
+}
 
 const char* pnr_build_info(void) {
   return "libpnr gfx950: fp32 v_mfma_f32_32x32x2_f32 fused decoder, LDS-streamed weights; "

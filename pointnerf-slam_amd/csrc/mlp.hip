@@ -377,6 +377,7 @@ int launch_mlp_fwd(const float* packed, const PointSrc& src, int mode, int64_t P
   if (save) a.save = *save;
   else a.save = SaveArgs{nullptr, nullptr, nullptr, nullptr, 0, 0};
   const dim3 grid((unsigned)((P + 127) / 128)), block(256);
+  TimingScope ts(kTimeMlpFwd, P, st);
   switch (mode) {
     case kPtsF64: hipLaunchKernelGGL(k_mlp_fwd<kPtsF64>, grid, block, 0, st, a); break;
     case kPtsF32: hipLaunchKernelGGL(k_mlp_fwd<kPtsF32>, grid, block, 0, st, a); break;
@@ -495,6 +496,7 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd(const float* __restrict__ W,
 int launch_mlp_bwd(const float* packed, const BwdArgs& a, int64_t P, hipStream_t st) {
   if (P <= 0) return 0;
   const dim3 grid((unsigned)((P + 127) / 128)), block(256);
+  TimingScope ts(kTimeMlpBwd, P, st);
   hipLaunchKernelGGL(k_mlp_bwd, grid, block, 0, st, packed, a, P);
   return hip_status(hipGetLastError());
 }

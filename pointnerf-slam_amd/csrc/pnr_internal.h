@@ -109,4 +109,15 @@ int launch_pack(const RawParams& rp, float* packed, hipStream_t st);
 
 inline int hip_status(hipError_t e) { return e == hipSuccess ? 0 : (int)e; }
 
+// Diagnostics: bracket a launch with hipEvents when pnr_timing_enable(1) (capi.cpp).
+enum TimedKernel : int { kTimeMlpFwd = 0, kTimeMlpBwd = 1, kTimeRay = 2, kTimeKinds = 3 };
+struct TimingScope {
+  hipEvent_t a = nullptr, b = nullptr;
+  hipStream_t st;
+  int kind;
+  int64_t units;
+  TimingScope(int kind, int64_t units, hipStream_t st);
+  ~TimingScope();
+};
+
 }  // namespace pnr

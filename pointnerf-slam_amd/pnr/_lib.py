@@ -68,8 +68,18 @@ _SIGS = {
                                         c_void_p, c_void_p, c_void_p]),
     'pnr_adam_step': (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_float, c_float, c_float,
                                      c_float, c_int64, c_void_p]),
+    'pnr_timing_enable': (ctypes.c_int, [ctypes.c_int]),
+    'pnr_timing_read': (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(c_int64), ctypes.POINTER(ctypes.c_double),
+                                       ctypes.POINTER(c_int64)]),
 }
 SYMBOLS = tuple(_SIGS)
+
+
+def timing_read(kernel: int):
+    """(launches, device ms, units) recorded for `kernel` since the last read (pnr_timing_read)."""
+    n, ms, u = c_int64(0), ctypes.c_double(0.0), c_int64(0)
+    check(load().pnr_timing_read(kernel, ctypes.byref(n), ctypes.byref(ms), ctypes.byref(u)), 'timing_read')
+    return n.value, ms.value, u.value
 
 _lib = None
 _lock = threading.Lock()

@@ -1,0 +1,96 @@
+"""One Mapper iteration on the HIP path (src/Mapper.py:335-694).
+
+`MapStep` is the inner loop body of Mapper.optimize_map for the imap* decoder
+(src/Mapper.py:507-662): render the sampled rays with gt depth (Renderer.render_batch_ray,
+:623-624), L1 depth over gt>0 + w_color * L1 colour (:641-646), 0.0005 * |sigma| of the
+regulation query (:650-655), backward, Adam step with lr = imap_decoders_lr (:540, :657-662).
+
+The decoder parameters live in ONE flat float32 buffer (and so do their grads), so a data-
+parallel caller reduces a single 891 KB buffer per step and Adam is one kernel
+(pnr_adam_step).  `ddp` (pnr.dist.DataParallel) adds the cross-GPU gradient all-reduce and the
+global far clamp; without it the step is single-GPU and bit-identical to the reference order of
+operations of a 1-process Mapper.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+
+
+class FlatParams:
+    """Re-seat every parameter of `module` (and its .grad) as a view of one flat buffer."""
+
+    def __init__(self, params):
+        self.params = list(params)
+        n = sum(p.numel() for p in self.params)
+        dev = self.params[0].device
+        self.data = torch.empty(n, device=dev, dtype=torch.float32)
+        self.grad = torch.zeros(n, device=dev, dtype=torch.float32)
+        off = 0
+        for p in self.params:
+            k = p.numel()
+            self.data[off:off + k].copy_(p.detach().reshape(-1))
+            p.data = self.data[off:off + k].view_as(p)
+            p.grad = self.grad[off:off + k].view_as(p)
+            off += k
+        self.numel = n
+
+    def zero_grad(self):
+        self.grad.zero_()
+
+
+class Adam:
+    """torch.optim.Adam(lr, betas=(0.9, 0.999), eps=1e-8) over a FlatParams buffer, one launch."""
+
+    def __init__(self, flat: FlatParams, lr: float, betas=(0.9, 0.999), eps=1e-8, on_update=None):
+        self.flat = flat
+        self.on_update = on_update
+        self.lr = lr
+        self.b1, self.b2 = betas
+        self.eps = eps
+        self.m = torch.zeros_like(flat.data)
+        self.v = torch.zeros_like(flat.data)
+        self.step_count = 0
+
+    def step(self):
+        self.step_count += 1
+        lib = _lib.load()
+        f = self.flat
+        _lib.check(lib.pnr_adam_step(_lib.ptr(f.data), _lib.ptr(f.grad), _lib.ptr(self.m), _lib.ptr(self.v), f.numel,
+                                     self.lr, self.b1, self.b2, self.eps, self.step_count,
+                                     _lib.stream_of(f.data.device)), 'adam_step')
+        if self.on_update is not None:  # weights changed behind autograd: drop the packed image
+            self.on_update()
+
+
+class MapStep:
+    def __init__(self, renderer, decoder, lr=2e-4, w_color_loss=0.05, w_reg=0.0005, ddp=None):
+        self.renderer = renderer
+        self.decoder = decoder
+        self.flat = FlatParams(decoder.ordered_params())
+        self.opt = Adam(self.flat, lr, on_update=decoder._packed.invalidate)
+        self.w_color = w_color_loss
+        self.w_reg = w_reg
+        self.ddp = ddp
+
+    def loss(self, rays_o, rays_d, gt_depth, gt_color, t_rand=None, far_clamp=None):
+        r, dec = self.renderer, self.decoder
+        dev = rays_o.device
+        d, _, c = r.render_batch_ray({}, dec, rays_d, rays_o, dev, 'color', gt_depth, far_clamp=far_clamp)
+        m = gt_depth > 0
+        loss = torch.abs(gt_depth[m] - d[m]).sum()
+        loss = loss + self.w_color * torch.abs(gt_color - c).sum()
+        sigma = r.regulation({}, dec, rays_d, rays_o, gt_depth, dev, 'color', t_rand=t_rand)
+        return loss + self.w_reg * torch.abs(sigma).sum()
+
+    def __call__(self, rays_o, rays_d, gt_depth, gt_color, t_rand=None):
+        self.flat.zero_grad()
+        far_clamp = self.ddp.global_far_clamp(gt_depth) if self.ddp is not None else None
+        loss = self.loss(rays_o, rays_d, gt_depth, gt_color, t_rand, far_clamp)
+        loss.backward()
+        if self.ddp is not None:
+            self.ddp.allreduce_(self.flat.grad)
+        self.opt.step()
+        return loss.detach()
+

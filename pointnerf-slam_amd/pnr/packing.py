@@ -16,6 +16,10 @@ class PackedMLP:
         self._key = None
         self._img = None
 
+    def invalidate(self):
+        """Force a re-pack (weights were written in place outside autograd, e.g. pnr_adam_step)."""
+        self._key = None
+
     def image(self, params) -> torch.Tensor:
         key = tuple((t.data_ptr(), t._version, t.device.index) for t in params)
         if self._img is not None and key == self._key:
