@@ -114,7 +114,7 @@ def main():
     from pnr.mapping import MapStep
 
     rank, world, local = pdist.init()
-    dev = torch.device('cuda', local)
+    dev = torch.device('cuda', local % torch.cuda.device_count())
     torch.cuda.set_device(dev)
     lib = pnr.library()
     bound, pose, params = load_scene()

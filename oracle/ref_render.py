@@ -207,9 +207,10 @@ def sample_pdf(bins: torch.Tensor, weights: torch.Tensor, n: int, det: bool = Tr
     return bins_g[..., 0] + t * (bins_g[..., 1] - bins_g[..., 0])
 
 
-def near_far(rays_o, rays_d, bound: torch.Tensor, n_samples: int, gt_depth=None):
+def near_far(rays_o, rays_d, bound: torch.Tensor, n_samples: int, gt_depth=None, far_clamp=None):
     """src/utils/Renderer.py:90-116.  near: 0.01 (python float) or 0.01*gt (N,S) f32;
-    far: (N,1) f64 box exit + 0.01, clamped to [0, max(1.2*gt)] (batch-global) when gt given."""
+    far: (N,1) f64 box exit + 0.01, clamped to [0, max(1.2*gt)] (batch-global) when gt given.
+    `far_clamp` replaces that batch max (the sharded-batch extension of pnr.Renderer)."""
     with torch.no_grad():
         t = (bound.unsqueeze(0) - rays_o.detach().unsqueeze(-1)) / rays_d.detach().unsqueeze(-1)
         far_bb = torch.min(torch.max(t, dim=2)[0], dim=1)[0].unsqueeze(-1) + 0.01
@@ -217,16 +218,17 @@ def near_far(rays_o, rays_d, bound: torch.Tensor, n_samples: int, gt_depth=None)
         return 0.01, far_bb
     g = gt_depth.reshape(-1, 1)
     near = g.repeat(1, n_samples) * 0.01
-    far = torch.clamp(far_bb, 0, (g * 1.2).max())
+    hi = (g * 1.2).max() if far_clamp is None else torch.tensor(far_clamp, dtype=torch.float64)
+    far = torch.clamp(far_bb, 0, hi)
     return near, far
 
 
 def render_batch_ray(params: Params, rays_d, rays_o, bound, n_samples=32, n_importance=12,
                      gt_depth=None, perturb=0.0, lindisp=False, t_rand=None,
-                     return_extras=False, points_batch_size=500000):
+                     return_extras=False, points_batch_size=500000, far_clamp=None):
     """src/utils/Renderer.py:63-203 (N_surface=0 path; occupancy=False).
     Returns (depth f64 (N,), uncertainty f64 (N,), color f32 (N,3)) [, extras]."""
-    near, far = near_far(rays_o, rays_d, bound, n_samples, gt_depth)
+    near, far = near_far(rays_o, rays_d, bound, n_samples, gt_depth, far_clamp)
     t_vals = torch.linspace(0., 1., steps=n_samples)
     if not lindisp:
         z = near * (1. - t_vals) + far * t_vals

@@ -1,0 +1,106 @@
+"""Data-parallel mapping step on CPU with the gloo backend, world size 2.
+
+Each rank takes a contiguous shard of the rays, uses pnr.dist.DataParallel for the two
+collectives of a mapping iteration (all_reduce MAX of the far clamp, all_reduce SUM of the flat
+gradient) and computes its shard's loss gradient with the CPU oracle.  The reduced gradient must
+equal the single-process full-batch gradient: this is the sharding contract the GPU path
+(pnr.mapping.MapStep with ddp) relies on."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from conftest import REPO, load_golden, golden_params
+
+sys.path.insert(0, os.path.join(REPO, 'pointnerf-slam_amd'))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _flat_grad(params):
+    return torch.cat([params[k].grad.reshape(-1) for k in sorted(params)])
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    sys.path.insert(0, REPO)
+    sys.path.insert(0, os.path.join(REPO, 'pointnerf-slam_amd'))
+    torch.set_num_threads(1)
+    from pnr import dist as pdist
+    from oracle import ref_render as ref
+    r, w, _ = pdist.init(backend='gloo')
+    assert (r, w) == (rank, world)
+    G = load_golden('grads.npz')
+    S = load_golden('scene.npz')
+    bound = torch.from_numpy(S['bound'])
+    n = 96
+    a, b = pdist.shard_bounds(n, rank, world)
+    ro = torch.from_numpy(G['map_rays_o'][:n][a:b].copy())
+    rd = torch.from_numpy(G['map_rays_d'][:n][a:b].copy())
+    gt = torch.from_numpy(G['map_gt_depth'][:n][a:b].copy())
+    gc = torch.from_numpy(G['map_gt_color'][:n][a:b].copy())
+    tr = torch.from_numpy(G['map_t_rand'][:n][a:b].copy())
+    ddp = pdist.DataParallel()
+    fc = ddp.global_far_clamp(gt)
+    params = {k: v.clone().requires_grad_(True) for k, v in golden_params('trained').items()}
+    d, v, c = ref.render_batch_ray(params, rd, ro, bound, gt_depth=gt, far_clamp=fc)
+    sig = ref.regulation(params, rd, ro, gt, bound, t_rand=tr)
+    ref.mapping_loss(d, c, gt, gc, sig).backward()
+    g = _flat_grad(params)
+    ddp.allreduce_(g)
+    if rank == 0:
+        q.put((fc, g.numpy()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_shard_bounds():
+    from pnr.dist import shard_bounds
+    for n in (0, 1, 7, 96, 1001):
+        for w in (1, 2, 3, 8):
+            cuts = [shard_bounds(n, r, w) for r in range(w)]
+            assert cuts[0][0] == 0 and cuts[-1][1] == n
+            assert all(cuts[i][1] == cuts[i + 1][0] for i in range(w - 1))
+            assert max(b - a for a, b in cuts) - min(b - a for a, b in cuts) <= 1
+
+
+def test_dp_mapping_grads_match_single_process():
+    from oracle import ref_render as ref
+    torch.set_num_threads(2)
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    fc, g_dp = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=300)
+        assert p.exitcode == 0
+    G = load_golden('grads.npz')
+    S = load_golden('scene.npz')
+    bound = torch.from_numpy(S['bound'])
+    n = 96
+    gt = torch.from_numpy(G['map_gt_depth'][:n].copy())
+    assert fc == float((gt * 1.2).max())
+    params = {k: v.clone().requires_grad_(True) for k, v in golden_params('trained').items()}
+    d, v, c = ref.render_batch_ray(params, torch.from_numpy(G['map_rays_d'][:n].copy()),
+                                   torch.from_numpy(G['map_rays_o'][:n].copy()), bound, gt_depth=gt)
+    sig = ref.regulation(params, torch.from_numpy(G['map_rays_d'][:n].copy()),
+                         torch.from_numpy(G['map_rays_o'][:n].copy()), gt, bound,
+                         t_rand=torch.from_numpy(G['map_t_rand'][:n].copy()))
+    ref.mapping_loss(d, c, gt, torch.from_numpy(G['map_gt_color'][:n].copy()), sig).backward()
+    g_full = _flat_grad(params).numpy()
+    np.testing.assert_allclose(g_dp, g_full, rtol=1e-4, atol=1e-6 * np.abs(g_full).max())
