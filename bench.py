@@ -151,7 +151,7 @@ def main():
     ddp.barrier()
     torch.cuda.synchronize()
     lib.pnr_timing_enable(1)
-    timing_read(0), timing_read(1)
+    timing_read(0), timing_read(1), timing_read(3)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
@@ -159,7 +159,7 @@ def main():
     ddp.barrier()
     el = time.perf_counter() - t0
     lib.pnr_timing_enable(0)
-    kt = {'mlp_fwd': timing_read(0), 'mlp_bwd': timing_read(1)}
+    kt = {'mlp_fwd': timing_read(0), 'mlp_bwd': timing_read(1), 'wgrad': timing_read(3)}
     t = torch.tensor([el], device=dev, dtype=torch.float64)
     if world > 1:
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
@@ -170,7 +170,7 @@ def main():
     # roofline of the dominant hand-written kernel (fused MLP fwd or delta chain), per launch
     best = None
     for name, (launches, ms, units) in kt.items():
-        if launches == 0:
+        if launches == 0 or name == 'wgrad':
             continue
         fl = FLOP_PER_POINT_FWD if name == 'mlp_fwd' else FLOP_PER_POINT_BWD
         cand = {'kernel': 'k_mlp_fwd' if name == 'mlp_fwd' else 'k_mlp_bwd', 'launches': launches,

@@ -147,7 +147,8 @@ int pnr_adam_step(float* p, const float* g, float* m, float* v, int64_t n, float
 /* ---- diagnostics (not on the reference API) ----------------------------------------------- */
 /* Kernel timing: while enabled, every launch of the timed kernels is bracketed by hipEvents on
  * its own stream.  pnr_timing_read synchronises those events and returns, for `kernel`
- * (0 = fused MLP forward k_mlp_fwd, 1 = MLP delta-chain k_mlp_bwd, 2 = ray kernels), the launch
+ * (0 = fused MLP forward k_mlp_fwd, 1 = MLP delta-chain k_mlp_bwd, 2 = ray kernels, 3 = weight-
+ * gradient GEMMs k_wgrad, units = points of the K dimension), the launch
  * count, the summed device milliseconds and the summed number of points (MLP) or rays processed,
  * then clears that kernel's record.  Process-global, mutex-protected; off by default. */
 int pnr_timing_enable(int on);

@@ -29,20 +29,19 @@ int launch_pdf(const pnr_render_params&, const float*, const double*, const floa
 int launch_fine(const pnr_render_params&, const float*, const double*, const double*, const float*, const float*,
                 int64_t, double*, double*, float*, uint8_t*, hipStream_t);
 int launch_fine_bwd(const pnr_render_params&, const float*, const double*, const double*, const float*,
-                    const float*, const uint8_t*, const uint8_t*, const uint8_t*, int64_t, const double*,
+                    const float*, const float4*, const float4*, const uint8_t*, int64_t, const double*,
                     const double*, const float*, float*, float*, float*, hipStream_t);
 int launch_ray_grads_f64(const float*, const double*, int, const double*, int, const float*, const float*,
                          const float*, int64_t, float*, float*, hipStream_t);
 int launch_ray_grads_f32(const float*, const float*, int, const float*, int64_t, float*, float*, hipStream_t);
 int launch_reg_z(const pnr_render_params&, const float*, const float*, int64_t, float*, hipStream_t);
 int launch_extract_sigma(const float*, int64_t, float*, hipStream_t);
-int launch_gout_sigma(const float*, const uint8_t*, int64_t, float*, hipStream_t);
+int launch_gout_sigma(const float*, const float4*, int64_t, float*, hipStream_t);
 int launch_get_rays(int, int, float, float, float, float, const float*, float*, float*, hipStream_t);
 int launch_rays_from_uv(const float*, const float*, int64_t, float, float, float, float, const float*, float*,
                         float*, hipStream_t);
 int launch_adam(float*, const float*, float*, float*, int64_t, float, float, float, float, float, hipStream_t);
-int launch_wgrad(int MT, int NT, const float* A, int64_t lda, int ma, const float* B, int64_t ldb, int nb, int64_t K,
-                 float* C, int64_t ldc, float* bias, hipStream_t st);
+
 }  // namespace pnr
 
 using namespace pnr;
@@ -120,10 +119,9 @@ SaveArgs carve_save(Carver& c, int64_t ld) {
   SaveArgs s{};
   s.ld = ld;
   s.p0 = 0;
-  s.eT = c.take<float>(kFourierPad * ld);
-  s.hT = c.take<float>((size_t)4 * kHidden * ld);
-  s.xT = c.take<float>(3 * ld);
-  s.inside = c.take<uint8_t>(ld);
+  s.eP = c.take<float>(kFourierPad * ld);
+  s.hP = c.take<float>((size_t)4 * kHidden * ld);
+  s.xP = c.take<float4>(ld);
   s.masks = c.take<uint4>((size_t)4 * (ld / 32) * 64);
   return s;
 }
@@ -148,9 +146,8 @@ struct BwdWS {
   float* g_out;   // [P] float4
   float* g_x;     // [P][3]
   float* g_nrm;   // [N]
-  float* dT;      // [4][256][C]
-  float* gargT;   // [96][C]
-  float* goutT;   // [4][C]
+  float* dP;      // [4][C][256]
+  float* gargP;   // [C][96]
   int64_t C;
 };
 
@@ -162,9 +159,8 @@ BwdWS carve_bwd(int64_t P, int64_t n, void* ws, size_t* bytes) {
   b.g_out = c.take<float>(P * 4);
   b.g_x = c.take<float>(P * 3);
   b.g_nrm = c.take<float>(n);
-  b.dT = c.take<float>((size_t)4 * kHidden * b.C);
-  b.gargT = c.take<float>(kFourierPad * b.C);
-  b.goutT = c.take<float>(4 * b.C);
+  b.dP = c.take<float>((size_t)4 * kHidden * b.C);
+  b.gargP = c.take<float>(kFourierPad * b.C);
   if (bytes) *bytes = c.off;
   return b;
 }
@@ -182,32 +178,33 @@ int mlp_backward_core(const float* packed, const SaveArgs& sv, int64_t P, BwdWS&
     BwdArgs a;
     a.g_out = b.g_out + p0 * 4;
     a.masks = sv.masks;
-    a.xT = sv.xT;
-    a.dT = b.dT;
-    a.gargT = b.gargT;
+    a.xP = sv.xP;
+    a.dP = b.dP;
+    a.gargP = b.gargP;
     a.g_x = want_gx ? b.g_x + p0 * 3 : nullptr;
-    a.goutT = b.goutT;
     a.ld = sv.ld;
     a.p0 = p0;
     a.ld_d = b.C;
     int rc = launch_mlp_bwd(packed, a, C, st);
     if (rc) return rc;
-    const int64_t ld = sv.ld, ldd = b.C;
-    const float* h1 = sv.hT + p0;
-    // output layer: dWo (4x256) += goutT (4xC) . h4^T ; dbo += rowsum(goutT)
-    rc = launch_wgrad(1, 8, b.goutT, ldd, 4, h1 + 3 * (int64_t)kHidden * ld, ld, kHidden, C, grads[9], kHidden,
-                      grads[10], st);
+    const float* hp = sv.hP + p0 * kHidden;  // h_l rows of this chunk: hp + l_idx * ld * 256
+    const int64_t hstride = sv.ld * kHidden;
+    const int64_t dstride = b.C * kHidden;
+    // output layer: dWo (4x256) += g_out^T h4 ; dbo += colsum(g_out)
+    rc = launch_wgrad(kWgradOut, b.g_out + p0 * 4, 4, hp + 3 * hstride, kHidden, C, grads[9], kHidden, grads[10], st);
     if (rc) return rc;
-    // hidden layers: dW_l += delta_{l+1} . h_l^T  (W3: delta4.h3, W2: delta3.h2, W1: delta2.h1)
+    // hidden layers: dW_l += delta_{l+1}^T h_l  (W3: delta4.h3, W2: delta3.h2, W1: delta2.h1)
     for (int l = 3; l >= 1 && rc == 0; --l)
-      rc = launch_wgrad(8, 8, b.dT + (int64_t)l * kHidden * ldd, ldd, kHidden, h1 + (int64_t)(l - 1) * kHidden * ld,
-                        ld, kHidden, C, grads[1 + 2 * l], kHidden, grads[2 + 2 * l], st);
+      rc = launch_wgrad(kWgradHidden, b.dP + l * dstride, kHidden, hp + (l - 1) * hstride, kHidden, C,
+                        grads[1 + 2 * l], kHidden, grads[2 + 2 * l], st);
     if (rc) return rc;
-    // first layer: dW0 (256x93) += delta1 . e^T ; db0
-    rc = launch_wgrad(8, 3, b.dT, ldd, kHidden, sv.eT + p0, ld, kFourier, C, grads[1], kFourier, grads[2], st);
+    // first layer: dW0 (256x93) += delta1^T e ; db0
+    rc = launch_wgrad(kWgradFirst, b.dP, kHidden, sv.eP + p0 * kFourierPad, kFourier, C, grads[1], kFourier,
+                      grads[2], st);
     if (rc) return rc;
-    // Fourier: dB (3x93) += x . g_arg^T
-    rc = launch_wgrad(1, 3, sv.xT + p0, ld, 3, b.gargT, ldd, kFourier, C, grads[0], kFourier, nullptr, st);
+    // Fourier: dB (3x93) += x^T g_arg   (x rows are float4 (x0,x1,x2,inside): 3 of 4 used)
+    rc = launch_wgrad(kWgradFourier, reinterpret_cast<const float*>(sv.xP + p0), 3, b.gargP, kFourier, C, grads[0],
+                      kFourier, nullptr, st);
     if (rc) return rc;
   }
   return hip_status(hipGetLastError());
@@ -421,7 +418,7 @@ int pnr_render_bwd(const pnr_render_params* prm, const float* packed, const floa
   const float* rawi = w.raw + n * S * 4;
   const int64_t pc = w.pc_pad;
   if (hipMemsetAsync(b.g_out, 0, (size_t)ld * 16, st) != hipSuccess) return (int)hipGetLastError();
-  int rc = launch_fine_bwd(*prm, rays_d, w.z, zi, w.raw, rawi, w.save.inside, w.save.inside + pc, w.ord, n,
+  int rc = launch_fine_bwd(*prm, rays_d, w.z, zi, w.raw, rawi, w.save.xP, w.save.xP + pc, w.ord, n,
                            g_depth, g_var, g_rgb, b.g_out, b.g_out + pc * 4, b.g_nrm, st);
   if (rc) return rc;
   rc = mlp_backward_core(packed, w.save, ld, b, grads, prm->need_ray_grads != 0, st);
@@ -509,7 +506,7 @@ int pnr_regulation_bwd(const pnr_render_params* prm, const float* packed, const 
   if (ws_bytes < need || bwd_bytes < bneed) return PNR_E_WORKSPACE;
   hipStream_t st = (hipStream_t)stream;
   if (hipMemsetAsync(b.g_out, 0, (size_t)ld * 16, st) != hipSuccess) return (int)hipGetLastError();
-  int rc = launch_gout_sigma(g_sigma, w.save.inside, P, b.g_out, st);
+  int rc = launch_gout_sigma(g_sigma, w.save.xP, P, b.g_out, st);
   if (rc) return rc;
   rc = mlp_backward_core(packed, w.save, ld, b, grads, prm->need_ray_grads != 0, st);
   if (rc) return rc;

@@ -111,12 +111,37 @@ __device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane
 // The weight image is one contiguous stream per kernel; `sp` is this lane's cursor into it
 // (stream base + wave*256 + lane*4 floats).  stage() copies the next `nfloats` (multiple of 1024)
 // into LDS with global_load_lds_dwordx4 (lane-linear destination) and advances the cursor.
+//
+// The DMA is issued from inline asm ON PURPOSE: when hipcc sees a global_load_lds it cannot tell
+// which LDS bytes it writes, so it waits vmcnt(0) before the next ds_read -- i.e. it waits for
+// the PREFETCH of chunk c+1 before computing chunk c, exposing the whole load latency (measured:
+// 26% of the kernel).  Hidden from hipcc, the DMA is ordered only by the explicit
+// `s_waitcnt vmcnt(N); s_barrier` at the top of each chunk (sync_chunk), N = stores issued
+// after the DMA that may stay in flight (activation saves).
+__device__ __forceinline__ void glds16(const float* gsrc, uint32_t lds_byte) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(gsrc), "s"(lds_byte) : "memory");
+}
+
+__device__ __forceinline__ uint32_t lds_addr(const float* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) float*)p;
+}
+
 __device__ __forceinline__ void stage(const float*& sp, float* dst, int nfloats) {
   const int w = wave_id();
   const int n = nfloats >> 10;
-  for (int i = 0; i < n; ++i)
-    __builtin_amdgcn_global_load_lds((const void*)(sp + i * 1024), (lds_ptr_t)(dst + (i * 4 + w) * 256), 16, 0, 0);
+  const uint32_t base = lds_addr(dst) + (uint32_t)(w * 256 * 4);
+  for (int i = 0; i < n; ++i) glds16(sp + i * 1024, base + (uint32_t)(i * 4096));
   sp += nfloats;
+}
+
+// Wait for this wave's DMA of the current chunk (all but the N youngest VMEM ops), then meet the
+// other waves: after it every wave's DMA into the chunk has landed and every wave has finished
+// reading the buffer that the next stage() overwrites.
+template <int N>
+__device__ __forceinline__ void sync_chunk() {
+  asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
 }
 
 // acc[t] += A(chunk, tile t) * act  over the 16 k-steps of one 32-row input tile.
@@ -158,13 +183,15 @@ __device__ __forceinline__ void mfma_chunk(const float* chunk, const float (&b)[
 
 // One layer: NCH input tiles streamed as NCH LDS chunks of `chf` floats from the cursor; the
 // chunk after the last one (`nxf` floats, 0 = none) is prefetched during the last compute.
-// Buffer parity START: chunk c lives in buffer (START + c) & 1.
-template <int NCH, int NT, int START>
+// Buffer parity START: chunk c lives in buffer (START + c) & 1.  `stores0` (runtime, wave-
+// uniform) tells the first chunk's sync that N0 stores were issued after its DMA.
+template <int NCH, int NT, int START, int N0>
 __device__ __forceinline__ void layer(float* lds, const float*& sp, int chf, int nxf, const float (&act)[8][16],
-                                      f32x16 (&acc)[NT]) {
+                                      f32x16 (&acc)[NT], bool stores0) {
 #pragma unroll
   for (int c = 0; c < NCH; ++c) {
-    __syncthreads();
+    if (c == 0 && stores0) sync_chunk<N0>();
+    else sync_chunk<0>();
     float* cur = lds + ((START + c) & 1) * kChunkFloats;
     float* oth = lds + ((START + c + 1) & 1) * kChunkFloats;
     if (c + 1 < NCH) stage(sp, oth, chf);
@@ -204,21 +231,18 @@ __device__ __forceinline__ void bias_relu(const f32x16 (&acc)[8], const float* _
   }
 }
 
-// store NT tiles of the register activation into a unit-major [rows][ld] buffer at column col.
-// Rows of register r are 32t + perm(r,hh): walk one pointer (deltas 1,1,1,5 rows) so that the
-// compiler does not materialise 128 separate 64-bit row addresses.
-template <int NT>
-__device__ __forceinline__ void save_tiles(float* __restrict__ base, int64_t ld, int64_t col,
-                                           const float (&act)[8][16]) {
-  const int lane = threadIdx.x & 63, hh = lane >> 5;
-  float* q = base + (int64_t)(4 * hh) * ld + col;
+// store NT tiles of the register activation into a point-major [rows][W] buffer (row = point):
+// registers 4q..4q+3 of tile t are units 32t + 8q + 4hh + {0..3}, one 16-B store each.
+template <int NT, int W>
+__device__ __forceinline__ void save_tiles(float* __restrict__ row, const float (&act)[8][16]) {
+  const int hh = (threadIdx.x >> 5) & 1;
+  float* q0 = row + 4 * hh;
 #pragma unroll
   for (int t = 0; t < NT; ++t)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      *q = act[t][r];
-      q += ((r & 3) == 3 ? 5 : 1) * ld;
-    }
+    for (int q = 0; q < 4; ++q)
+      *reinterpret_cast<float4*>(q0 + 32 * t + 8 * q) =
+          make_float4(act[t][4 * q], act[t][4 * q + 1], act[t][4 * q + 2], act[t][4 * q + 3]);
 }
 
 // ReLU mask of one lane: bit (t&1)*16 + r of word t>>1 is [act[t][r] > 0]; the wave tile's
@@ -243,6 +267,11 @@ struct FwdArgs {
   SaveArgs save;
   int do_save;
 };
+
+// VMEM stores issued between a layer's prefetch DMA and the next layer's first sync (a lower
+// bound is safe: it only makes the wait stricter): e + x saves = 13, mask + h saves = 33,
+// delta saves = 32.
+constexpr int kStoresE = 12, kStoresH = 32, kStoresD = 31;
 
 template <int MODE>
 __device__ __forceinline__ void load_point(const PointSrc& s, int64_t p, float& x0, float& x1, float& x2,
@@ -324,39 +353,34 @@ __global__ __launch_bounds__(256, 1) void k_mlp_fwd(FwdArgs a) {
   // first saved column of this wave (p0 is a multiple of 128) -> its 64 mask slots
   const int64_t mask_word0 = ((a.save.p0 + (int64_t)blockIdx.x * 128) / 32 + wave_id()) * 64;
   if (save) {
-    save_tiles<3>(a.save.eT, a.save.ld, col, act);
-    if (hh == 0) {
-      a.save.xT[col] = x0;
-      a.save.xT[a.save.ld + col] = x1;
-      a.save.xT[2 * a.save.ld + col] = x2;
-      a.save.inside[col] = inside ? 1 : 0;
-    }
+    save_tiles<3, kFourierPad>(a.save.eP + col * kFourierPad, act);
+    if (hh == 0) a.save.xP[col] = make_float4(x0, x1, x2, inside ? 1.f : 0.f);
   }
 
   f32x16 acc[8];
   zero_acc<8>(acc);
-  layer<3, 8, 0>(lds, sp, kChunkFloats, kChunkFloats, act, acc);
+  layer<3, 8, 0, kStoresE>(lds, sp, kChunkFloats, kChunkFloats, act, acc, save);
   bias_relu(acc, W + kOffB0, act);
   if (a.do_save) {
     save_mask(a.save.masks + mask_word0, act);
-    save_tiles<8>(a.save.hT, a.save.ld, col, act);
+    save_tiles<8, kHidden>(a.save.hP + col * kHidden, act);
   }
 
   // hidden layers 1..3 (pts_linears.1..3); each starts in buffer 1 (layer 0 used 3 chunks)
   for (int L = 1; L <= 3; ++L) {
     const int nxf = L < 3 ? kChunkFloats : kSmallChunkFloats;
     zero_acc<8>(acc);
-    layer<8, 8, 1>(lds, sp, kChunkFloats, nxf, act, acc);
+    layer<8, 8, 1, kStoresH>(lds, sp, kChunkFloats, nxf, act, acc, a.do_save);
     bias_relu(acc, W + kOffB0 + (int64_t)L * kBiasFloats, act);
     if (a.do_save) {
       save_mask(a.save.masks + (int64_t)L * (a.save.ld / 32) * 64 + mask_word0, act);
-      save_tiles<8>(a.save.hT + (int64_t)L * kHidden * a.save.ld, a.save.ld, col, act);
+      save_tiles<8, kHidden>(a.save.hP + ((int64_t)L * a.save.ld + col) * kHidden, act);
     }
   }
 
   f32x16 out[1];
   zero_acc<1>(out);
-  layer<8, 1, 1>(lds, sp, kSmallChunkFloats, 0, act, out);
+  layer<8, 1, 1, kStoresH>(lds, sp, kSmallChunkFloats, 0, act, out, a.do_save);
   // rows 0..3 of the output tile live in lanes 0..31, registers 0..3
   if (valid && hh == 0) {
     const float4 bo = *reinterpret_cast<const float4*>(W + kOffBO + lane * 4);
@@ -410,6 +434,9 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd(const float* __restrict__ W,
   const int64_t col = a.p0 + p;   // column in the saved activations
   const int64_t dcol = p;         // column in the delta buffers
   const int64_t mstride = (a.ld / 32) * 64;  // mask slots per layer
+  // delta saves are skipped for invalid lanes only; a wave with no valid lane issues no store
+  // instruction at all, so the relaxed first-chunk wait is used only when some lane is valid
+  const bool valid_any = __builtin_amdgcn_readfirstlane((int)((int64_t)blockIdx.x * 128 + wave_id() * 32 < P));
   const uint4* mk = a.masks + ((a.p0 + (int64_t)blockIdx.x * 128) / 32 + wave_id()) * 64;
 
   const float* sp = W + kOffL3T + wave_id() * 256 + lane * 4;  // weight stream cursor
@@ -420,10 +447,6 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd(const float* __restrict__ W,
   if (valid && hh == 0) {
     const float4 go = reinterpret_cast<const float4*>(a.g_out)[p];
     g[0] = go.x; g[1] = go.y; g[2] = go.z; g[3] = go.w;
-  }
-  if (valid && hh == 0) {
-#pragma unroll
-    for (int o = 0; o < 4; ++o) a.goutT[(int64_t)o * a.ld_d + dcol] = g[o];
   }
   f32x16 acc[8];
   zero_acc<8>(acc);
@@ -440,33 +463,33 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd(const float* __restrict__ W,
   }
   float act[8][16];
   relu_grad(acc, mk + 3 * mstride, act);   // delta4
-  if (valid) save_tiles<8>(a.dT + 3 * (int64_t)kHidden * a.ld_d, a.ld_d, dcol, act);
+  if (valid) save_tiles<8, kHidden>(a.dP + (3 * a.ld_d + dcol) * kHidden, act);
 
   // delta3 = W3^T delta4 * [h3>0]; delta2; delta1  (images L3T, L2T, L1T; 8 chunks each)
   // chunk parity: L3T starts in buffer 0, 8 chunks -> every image starts in buffer 0
   for (int s = 0; s < 3; ++s) {  // s=0: W3^T -> delta3 (uses h3), s=1: W2^T -> delta2, s=2: W1^T -> delta1
     const int nxf = s < 2 ? kChunkFloats : (int)kL0TChunkFloats;
     zero_acc<8>(acc);
-    layer<8, 8, 0>(lds, sp, kChunkFloats, nxf, act, acc);
+    layer<8, 8, 0, kStoresD>(lds, sp, kChunkFloats, nxf, act, acc, valid_any);
     const int hl = 2 - s;  // h3 -> index 2, h2 -> 1, h1 -> 0
     relu_grad(acc, mk + hl * mstride, act);
-    if (valid) save_tiles<8>(a.dT + (int64_t)hl * kHidden * a.ld_d, a.ld_d, dcol, act);
+    if (valid) save_tiles<8, kHidden>(a.dP + ((int64_t)hl * a.ld_d + dcol) * kHidden, act);
   }
 
   // g_e = W0^T delta1 : 3 output tiles (96 rows, 93 valid)
   f32x16 ge[3];
   zero_acc<3>(ge);
-  layer<8, 3, 0>(lds, sp, (int)kL0TChunkFloats, 0, act, ge);
+  layer<8, 3, 0, kStoresD>(lds, sp, (int)kL0TChunkFloats, 0, act, ge, valid_any);
 
   // g_arg = g_e * cos(x@B); g_x = B g_arg
   float x0 = 0.f, x1 = 0.f, x2 = 0.f;
   if (valid) {
-    x0 = a.xT[col];
-    x1 = a.xT[a.ld + col];
-    x2 = a.xT[2 * a.ld + col];
+    const float4 xv = a.xP[col];
+    x0 = xv.x; x1 = xv.y; x2 = xv.z;
   }
   const float* FB = W + kOffFB;
   float s0 = 0.f, s1 = 0.f, s2 = 0.f;
+  float garg[8][16];  // only tiles 0..2 used (save_tiles layout)
 #pragma unroll
   for (int t = 0; t < 3; ++t)
 #pragma unroll
@@ -479,8 +502,9 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd(const float* __restrict__ W,
         s1 = __builtin_fmaf(FB[kFourierPad + k], gv, s1);
         s2 = __builtin_fmaf(FB[2 * kFourierPad + k], gv, s2);
       }
-      if (valid) a.gargT[(int64_t)k * a.ld_d + dcol] = gv;
+      garg[t][r] = gv;
     }
+  if (valid) save_tiles<3, kFourierPad>(a.gargP + dcol * kFourierPad, garg);
   if (a.g_x != nullptr) {
     s0 += __shfl_xor(s0, 32);
     s1 += __shfl_xor(s1, 32);

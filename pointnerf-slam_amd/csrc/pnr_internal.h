@@ -77,15 +77,15 @@ struct PointSrc {
   double bound[6];
 };
 
-// Activation save area for training (unit-major, leading dimension ld = total points).
+// Activation save area for training, POINT-major (row p = one point), ld = total points
+// (multiple of 128; padded points hold finite activations of x = 0 and get zero gradient).
 struct SaveArgs {
-  float* eT;       // [96][ld]
-  float* hT;       // [4][256][ld]  (h1..h4)
-  float* xT;       // [3][ld]        f32 MLP input
-  uint8_t* inside; // [ld]
+  float* eP;       // [ld][96]        Fourier features sin(x@B)
+  float* hP;       // [4][ld][256]    h1..h4
+  float4* xP;      // [ld]            (x0, x1, x2, inside ? 1 : 0), f32 MLP input
   uint4* masks;    // [4][ld/32][64 lanes] ReLU bit words of h1..h4 (mlp.hip save_mask)
-  int64_t ld;      // multiple of 128
-  int64_t p0;      // column of point 0 of this launch (multiple of 128)
+  int64_t ld;
+  int64_t p0;      // first point (row) of this launch (multiple of 128)
 };
 
 int launch_mlp_fwd(const float* packed, const PointSrc& src, int mode, int64_t P, float* raw,
@@ -94,23 +94,27 @@ int launch_mlp_fwd(const float* packed, const PointSrc& src, int mode, int64_t P
 struct BwdArgs {
   const float* g_out;  // (P,4) dL/draw, sigma channel already zeroed where masked
   const uint4* masks;  // [4][ld/32][64]
-  const float* xT;     // [3][ld]
-  float* dT;           // [4][256][ld_d]  delta1..delta4
-  float* gargT;        // [96][ld_d]      dL/d(x@B) (pre-sin argument)
+  const float4* xP;    // [ld] saved MLP inputs
+  float* dP;           // [4][ld_d][256]  delta1..delta4, point-major, chunk-local rows
+  float* gargP;        // [ld_d][96]      dL/d(x@B) (pre-sin argument)
   float* g_x;          // (P,3) dL/dx or nullptr
-  float* goutT;        // [4][ld_d]       transposed copy of g_out for the dWo GEMM
-  int64_t ld;          // leading dim of saved activations
-  int64_t p0;          // first saved column handled by this launch
-  int64_t ld_d;        // leading dim of delta buffers (chunk-local, column 0 = p0)
+  int64_t ld;          // rows of the saved activations
+  int64_t p0;          // first saved row handled by this launch
+  int64_t ld_d;        // rows of the delta buffers (chunk size)
 };
 int launch_mlp_bwd(const float* packed, const BwdArgs& a, int64_t P, hipStream_t st);
 
 int launch_pack(const RawParams& rp, float* packed, hipStream_t st);
 
+// weight-gradient GEMM shapes (wgrad.hip): C[MA][NB] += A[K][WA]^T B[K][WB]
+enum WgradKind : int { kWgradHidden = 0, kWgradFirst = 1, kWgradOut = 2, kWgradFourier = 3 };
+int launch_wgrad(int kind, const float* A, int ma, const float* B, int nb, int64_t K, float* C, int64_t ldc,
+                 float* bias, hipStream_t st);
+
 inline int hip_status(hipError_t e) { return e == hipSuccess ? 0 : (int)e; }
 
 // Diagnostics: bracket a launch with hipEvents when pnr_timing_enable(1) (capi.cpp).
-enum TimedKernel : int { kTimeMlpFwd = 0, kTimeMlpBwd = 1, kTimeRay = 2, kTimeKinds = 3 };
+enum TimedKernel : int { kTimeMlpFwd = 0, kTimeMlpBwd = 1, kTimeRay = 2, kTimeWgrad = 3, kTimeKinds = 4 };
 struct TimingScope {
   hipEvent_t a = nullptr, b = nullptr;
   hipStream_t st;

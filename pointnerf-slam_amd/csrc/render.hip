@@ -89,13 +89,6 @@ __global__ void k_coarse_z(pnr_render_params prm, const float* __restrict__ ro, 
   }
 }
 
-// Compositing weights of one ray (common.py:224-240), sorted sample order given by `src`.
-// Writes w (float) into wl[q*stride].  Returns nothing else; used by the coarse pass.
-struct RaySamples {
-  const double* zc; const double* zi; const float4* rc; const float4* ri;
-  int S;
-};
-
 // ---------------------------------------------------------------------------------------------
 // coarse weights -> sample_pdf -> z_samples (N, I) float64
 __global__ __launch_bounds__(64) void k_pdf(pnr_render_params prm, const float* __restrict__ rd,
@@ -215,7 +208,7 @@ __global__ __launch_bounds__(64) void k_fine(pnr_render_params prm, const float*
 __global__ __launch_bounds__(64) void k_fine_bwd(pnr_render_params prm, const float* __restrict__ rd,
                                                  const double* __restrict__ zc, const double* __restrict__ zi,
                                                  const float4* __restrict__ rawc, const float4* __restrict__ rawi,
-                                                 const uint8_t* __restrict__ insc, const uint8_t* __restrict__ insi,
+                                                 const float4* __restrict__ insc, const float4* __restrict__ insi,
                                                  const uint8_t* __restrict__ ord_in, int64_t n_rays,
                                                  const double* __restrict__ g_depth, const double* __restrict__ g_var,
                                                  const float* __restrict__ g_rgb, float4* __restrict__ goc,
@@ -274,7 +267,7 @@ __global__ __launch_bounds__(64) void k_fine_bwd(pnr_render_params prm, const fl
     const float sr = relu(c.w);
     const float ex = expf(-sr * delta);
     float gs = c.w > 0.f ? ga * ex * delta : 0.f;
-    const bool inside = s < S ? insc[n * S + s] != 0 : insi[n * I + (s - S)] != 0;
+    const bool inside = s < S ? insc[n * S + s].w != 0.f : insi[n * I + (s - S)].w != 0.f;
     if (!inside) gs = 0.f;
     gn += (ga * ex * sr) * dz;
     const float4 go = make_float4(gr0 * w, gr1 * w, gr2 * w, gs);
@@ -336,10 +329,10 @@ __global__ void k_extract_sigma(const float4* __restrict__ raw, int64_t P, float
   if (p < P) sigma[p] = raw[p].w;
 }
 
-__global__ void k_gout_sigma(const float* __restrict__ g_sigma, const uint8_t* __restrict__ inside, int64_t P,
+__global__ void k_gout_sigma(const float* __restrict__ g_sigma, const float4* __restrict__ xP, int64_t P,
                              float4* __restrict__ g_out) {
   const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (p < P) g_out[p] = make_float4(0.f, 0.f, 0.f, inside[p] ? g_sigma[p] : 0.f);
+  if (p < P) g_out[p] = make_float4(0.f, 0.f, 0.f, xP[p].w != 0.f ? g_sigma[p] : 0.f);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -417,7 +410,7 @@ int launch_fine(const pnr_render_params& prm, const float* rd, const double* zc,
   return hip_status(hipGetLastError());
 }
 int launch_fine_bwd(const pnr_render_params& prm, const float* rd, const double* zc, const double* zi,
-                    const float* rawc, const float* rawi, const uint8_t* insc, const uint8_t* insi,
+                    const float* rawc, const float* rawi, const float4* insc, const float4* insi,
                     const uint8_t* ord, int64_t n, const double* gd, const double* gv, const float* grgb,
                     float* goc, float* goi, float* g_nrm, hipStream_t st) {
   if (n <= 0) return 0;
@@ -452,7 +445,7 @@ int launch_extract_sigma(const float* raw, int64_t P, float* sigma, hipStream_t 
   hipLaunchKernelGGL(k_extract_sigma, dim3(nblk(P, 256)), dim3(256), 0, st, (const float4*)raw, P, sigma);
   return hip_status(hipGetLastError());
 }
-int launch_gout_sigma(const float* g_sigma, const uint8_t* inside, int64_t P, float* g_out, hipStream_t st) {
+int launch_gout_sigma(const float* g_sigma, const float4* inside, int64_t P, float* g_out, hipStream_t st) {
   if (P <= 0) return 0;
   hipLaunchKernelGGL(k_gout_sigma, dim3(nblk(P, 256)), dim3(256), 0, st, g_sigma, inside, P, (float4*)g_out);
   return hip_status(hipGetLastError());

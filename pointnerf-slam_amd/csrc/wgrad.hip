@@ -1,19 +1,21 @@
-// wgrad.hip -- weight-gradient GEMMs of the decoder backward (replaces rocBLAS).
+// wgrad.hip -- weight-gradient GEMMs of the decoder backward.
 //
-//   C[MA][NB] += A[MA][K] * B[NB][K]^T        (A, B unit-major: row u holds K points)
-//   bias[MA]  += sum_k A[MA][k]               (optional)
+//   C[MA][NB] += A[K][MA]^T * B[K][NB]        (A, B point-major: row k = one point)
+//   bias[MA]  += sum_k A[k][MA]               (optional)
 //
-// The K dimension (points) is huge (up to millions) and MA, NB <= 256, so the work is split
-// over K: each workgroup owns KS consecutive points, streams them in tiles of 32 points through
-// a double-buffered LDS image laid out point-major ([k][u], conflict-free MFMA operand reads),
-// keeps its whole MA x NB partial in accumulator registers (v_mfma_f32_32x32x2_f32, exact fp32)
-// and adds it into C with float atomics once at the end.
+// K (points) is huge (up to millions) and MA, NB <= 256, so the work is split over K: each
+// workgroup owns KS consecutive points and streams them in tiles of 32 points.  A tile of a
+// point-major operand is one contiguous block (32 x MA floats), copied linearly into LDS with
+// 16-B loads/stores (register double-buffering); the MFMA operand reads of that [k][u] image are
+// conflict-free (lanes read consecutive units).  The whole MA x NB partial stays in accumulator
+// registers (v_mfma_f32_32x32x2_f32, exact fp32) and is added into C with one float atomic per
+// element at the end.
 //
 // Used for (src/conv_onet/models/decoder.py:149-159 parameters):
-//   dW3 = delta4 . h3^T, dW2 = delta3 . h2^T, dW1 = delta2 . h1^T      MA = NB = 256
-//   dW0 = delta1 . e^T                                                  MA = 256, NB = 96 (93 used)
-//   dWo = g_out . h4^T                                                  MA = 4,   NB = 256
-//   dB  = x . g_arg^T                                                   MA = 3,   NB = 96 (93 used)
+//   dW3 = delta4^T h3, dW2 = delta3^T h2, dW1 = delta2^T h1     MA = NB = 256
+//   dW0 = delta1^T e                                            MA = 256, NB = 96 (93 used)
+//   dWo = g_out^T h4                                            MA = 4,   NB = 256
+//   dB  = x^T g_arg                                             MA = 4 (3 used), NB = 96 (93 used)
 #include "pnr_internal.h"
 
 namespace pnr {
@@ -22,118 +24,119 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int kKT = 32;  // points per LDS tile
 
-template <int MT, int NT>
+template <int MT, int NT, int WA, int WB>
 struct WgradCfg {
-  static constexpr int MA_PAD = 32 * MT;
-  static constexpr int NB_PAD = 32 * NT;
-  static constexpr int SA = MA_PAD + 1;  // LDS row stride (floats): +1 makes the transposing
-  static constexpr int SB = NB_PAD + 1;  // ds_write_b32 and the operand reads conflict-free
   static constexpr int TILES = MT * NT;
-  static constexpr int TPW = (TILES + 3) / 4;  // output tiles per wave (round robin)
-  static constexpr int A_FLOATS = kKT * SA;
-  static constexpr int B_FLOATS = kKT * SB;
+  // wave w owns row tiles [w*RW, w*RW+RW) x all NT col tiles (MT >= 4), or col tiles
+  // [w*CW, w*CW+CW) of the single row tile (MT == 1): per k-step it reads RW A and CW B
+  // fragments for RW*CW MFMAs
+  static constexpr int RW = MT >= 4 ? MT / 4 : 1;
+  static constexpr int CW = MT >= 4 ? NT : (NT + 3) / 4;
+  static constexpr int TPW = RW * CW;
+  static constexpr int A_FLOATS = kKT * WA;
+  static constexpr int B_FLOATS = kKT * WB;
   static constexpr int STAGE = A_FLOATS + B_FLOATS;
+  static constexpr int A_V4 = (A_FLOATS / 4 + 255) / 256;  // float4 per thread per tile
+  static constexpr int B_V4 = (B_FLOATS / 4 + 255) / 256;
 };
 
 struct WgradArgs {
-  const float* A;
-  int64_t lda;
-  int ma;          // valid rows of A (<= 32*MT)
-  const float* B;
-  int64_t ldb;
-  int nb;          // valid rows of B (<= 32*NT) -- also the number of C columns written
-  int64_t K;       // points
+  const float* A;  // [K][WA]
+  int ma;          // valid columns of A (rows of C)
+  const float* B;  // [K][WB]
+  int nb;          // valid columns of B (columns of C)
+  int64_t K;
   int64_t ks;      // points per workgroup (multiple of kKT)
   float* C;
   int64_t ldc;
-  float* bias;     // optional row sums of A
+  float* bias;     // optional column sums of A
 };
 
-// Tile load: 8 threads share one 32-point row segment (one float4 each), so every wave
-// instruction reads 8 whole 128-B lines.  Thread t covers rows rep*32 + t/8, rep < NREP.
-template <int NREP>
-__device__ __forceinline__ void load_tile(const float* __restrict__ src, int64_t ld, int nrows, int64_t k0,
-                                          int64_t ke, float4 (&v)[NREP]) {
-  const int t = threadIdx.x, q = t & 7;
-  const int64_t k = k0 + 4 * q;
+// load one 32-point tile (rows k0.. of a [K][W] operand) as float4 per thread, zero past ke
+template <int W, int NV4>
+__device__ __forceinline__ void load_tile(const float* __restrict__ src, int64_t k0, int64_t ke, float4 (&v)[NV4]) {
+  constexpr int N4 = kKT * W / 4;
+  const int64_t lim = (ke - k0) * W / 4;  // valid float4 of this tile
+  const float4* s4 = reinterpret_cast<const float4*>(src + k0 * W);
 #pragma unroll
-  for (int rep = 0; rep < NREP; ++rep) {
-    const int row = rep * 32 + (t >> 3);
-    if (row < nrows && k + 4 <= ke) {
-      v[rep] = *reinterpret_cast<const float4*>(src + (int64_t)row * ld + k);
-    } else {
-      float e[4] = {0.f, 0.f, 0.f, 0.f};
-      if (row < nrows)
-#pragma unroll
-        for (int c = 0; c < 4; ++c)
-          if (k + c < ke) e[c] = src[(int64_t)row * ld + k + c];
-      v[rep] = make_float4(e[0], e[1], e[2], e[3]);
-    }
+  for (int q = 0; q < NV4; ++q) {
+    const int e = q * 256 + threadIdx.x;
+    v[q] = (e < N4 && e < lim) ? s4[e] : make_float4(0.f, 0.f, 0.f, 0.f);
   }
 }
 
-// transpose into the point-major LDS image: lds[k][row], row stride S
-template <int NREP, int S>
-__device__ __forceinline__ void store_tile(float* lds, const float4 (&v)[NREP]) {
-  const int t = threadIdx.x, q = t & 7;
+template <int W, int NV4>
+__device__ __forceinline__ void store_tile(float* lds, const float4 (&v)[NV4]) {
+  constexpr int N4 = kKT * W / 4;
 #pragma unroll
-  for (int rep = 0; rep < NREP; ++rep) {
-    const int row = rep * 32 + (t >> 3);
-    float* d = lds + (4 * q) * S + row;
-    d[0] = v[rep].x;
-    d[S] = v[rep].y;
-    d[2 * S] = v[rep].z;
-    d[3 * S] = v[rep].w;
+  for (int q = 0; q < NV4; ++q) {
+    const int e = q * 256 + threadIdx.x;
+    if (e < N4) reinterpret_cast<float4*>(lds)[e] = v[q];
   }
 }
 
-template <int MT, int NT>
+template <int MT, int NT, int WA, int WB>
 __global__ __launch_bounds__(256, 1) void k_wgrad(WgradArgs a) {
-  using Cfg = WgradCfg<MT, NT>;
-  constexpr int RA = MT * 32 / 32, RB = NT * 32 / 32;  // row reps per 256 threads (32 rows each)
+  using Cfg = WgradCfg<MT, NT, WA, WB>;
   __shared__ __attribute__((aligned(16))) float lds[2 * Cfg::STAGE];
   const int lane = threadIdx.x & 63, hh = lane >> 5, i = lane & 31;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t kb = (int64_t)blockIdx.x * a.ks;
   const int64_t ke = kb + a.ks < a.K ? kb + a.ks : a.K;
+  const int tr0 = MT >= 4 ? w * Cfg::RW : 0;
+  const int tc0 = MT >= 4 ? 0 : w * Cfg::CW;
 
   f32x16 acc[Cfg::TPW];
 #pragma unroll
   for (int q = 0; q < Cfg::TPW; ++q)
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[q][r] = 0.f;
-  float rsum[RA];
-#pragma unroll
-  for (int r = 0; r < RA; ++r) rsum[r] = 0.f;
+  float csum = 0.f;  // bias: thread u < ma sums column u of A
 
-  float4 va[RA], vb[RB];
-  load_tile<RA>(a.A, a.lda, a.ma, kb, ke, va);
-  load_tile<RB>(a.B, a.ldb, a.nb, kb, ke, vb);
+  float4 va[Cfg::A_V4], vb[Cfg::B_V4];
+  load_tile<WA, Cfg::A_V4>(a.A, kb, ke, va);
+  load_tile<WB, Cfg::B_V4>(a.B, kb, ke, vb);
   int buf = 0;
   for (int64_t k0 = kb; k0 < ke; k0 += kKT) {
     float* la = lds + buf * Cfg::STAGE;
     float* lb = la + Cfg::A_FLOATS;
-    store_tile<RA, Cfg::SA>(la, va);
-    store_tile<RB, Cfg::SB>(lb, vb);
-#pragma unroll
-    for (int r = 0; r < RA; ++r) rsum[r] += (va[r].x + va[r].y) + (va[r].z + va[r].w);
+    store_tile<WA, Cfg::A_V4>(la, va);
+    store_tile<WB, Cfg::B_V4>(lb, vb);
     __syncthreads();
     if (k0 + kKT < ke) {  // prefetch the next tile into registers while this one computes
-      load_tile<RA>(a.A, a.lda, a.ma, k0 + kKT, ke, va);
-      load_tile<RB>(a.B, a.ldb, a.nb, k0 + kKT, ke, vb);
+      load_tile<WA, Cfg::A_V4>(a.A, k0 + kKT, ke, va);
+      load_tile<WB, Cfg::B_V4>(a.B, k0 + kKT, ke, vb);
+    }
+    if (a.bias && (int)threadIdx.x < a.ma) {  // column sums, 4 independent chains
+      float c0 = 0.f, c1 = 0.f, c2 = 0.f, c3 = 0.f;
+#pragma unroll
+      for (int k = 0; k < kKT; k += 4) {
+        c0 += la[(k + 0) * WA + threadIdx.x];
+        c1 += la[(k + 1) * WA + threadIdx.x];
+        c2 += la[(k + 2) * WA + threadIdx.x];
+        c3 += la[(k + 3) * WA + threadIdx.x];
+      }
+      csum += (c0 + c1) + (c2 + c3);
     }
 #pragma unroll
     for (int kk = 0; kk < kKT / 2; ++kk) {
       const int kr = 2 * kk + hh;
+      float av[Cfg::RW], bv[Cfg::CW];
 #pragma unroll
-      for (int q = 0; q < Cfg::TPW; ++q) {
-        const int id = w + 4 * q;
-        if (Cfg::TILES % 4 != 0 && id >= Cfg::TILES) continue;
-        const int ti = id / NT, tj = id % NT;
-        const float av = la[kr * Cfg::SA + 32 * ti + i];
-        const float bv = lb[kr * Cfg::SB + 32 * tj + i];
-        acc[q] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[q], 0, 0, 0);
+      for (int x = 0; x < Cfg::RW; ++x) {
+        const int ra = 32 * (tr0 + x) + i;
+        av[x] = ra < WA ? la[kr * WA + ra] : 0.f;
       }
+#pragma unroll
+      for (int y = 0; y < Cfg::CW; ++y) {
+        const int rb = 32 * (tc0 + y) + i;
+        bv[y] = (tc0 + y < NT && rb < WB) ? lb[kr * WB + rb] : 0.f;
+      }
+#pragma unroll
+      for (int x = 0; x < Cfg::RW; ++x)
+#pragma unroll
+        for (int y = 0; y < Cfg::CW; ++y)
+          acc[x * Cfg::CW + y] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[x], bv[y], acc[x * Cfg::CW + y], 0, 0, 0);
     }
 #pragma unroll
     for (int q = 0; q < Cfg::TPW; ++q) asm volatile("" : "+a"(acc[q]));
@@ -141,29 +144,19 @@ __global__ __launch_bounds__(256, 1) void k_wgrad(WgradArgs a) {
   }
   // C[32ti + perm(r,hh)][32tj + i] += acc
 #pragma unroll
-  for (int q = 0; q < Cfg::TPW; ++q) {
-    const int id = w + 4 * q;
-    if (id >= Cfg::TILES) continue;
-    const int ti = id / NT, tj = id % NT;
-    const int col = 32 * tj + i;
-    if (col >= a.nb) continue;
+  for (int x = 0; x < Cfg::RW; ++x)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int row = 32 * ti + perm(r, hh);
-      if (row < a.ma) atomicAdd(a.C + (int64_t)row * a.ldc + col, acc[q][r]);
-    }
-  }
-  if (a.bias) {
+    for (int y = 0; y < Cfg::CW; ++y) {
+      const int ti = tr0 + x, tj = tc0 + y;
+      const int col = 32 * tj + i;
+      if (tj >= NT || col >= a.nb) continue;
 #pragma unroll
-    for (int r = 0; r < RA; ++r) {
-      float v = rsum[r];
-      v += __shfl_xor(v, 1);
-      v += __shfl_xor(v, 2);
-      v += __shfl_xor(v, 4);
-      const int row = r * 32 + ((int)threadIdx.x >> 3);
-      if ((threadIdx.x & 7) == 0 && row < a.ma) atomicAdd(a.bias + row, v);
+      for (int r = 0; r < 16; ++r) {
+        const int row = 32 * ti + perm(r, hh);
+        if (row < a.ma) atomicAdd(a.C + (int64_t)row * a.ldc + col, acc[x * Cfg::CW + y][r]);
+      }
     }
-  }
+  if (a.bias && (int)threadIdx.x < a.ma) atomicAdd(a.bias + threadIdx.x, csum);
 }
 
 // choose the K split so that the grid covers the chip ~2x
@@ -174,16 +167,19 @@ static int64_t pick_ks(int64_t K) {
   return ks;
 }
 
-int launch_wgrad(int MT, int NT, const float* A, int64_t lda, int ma, const float* B, int64_t ldb, int nb, int64_t K,
-                 float* C, int64_t ldc, float* bias, hipStream_t st) {
+int launch_wgrad(int kind, const float* A, int ma, const float* B, int nb, int64_t K, float* C, int64_t ldc,
+                 float* bias, hipStream_t st) {
   if (K <= 0) return 0;
-  WgradArgs a{A, lda, ma, B, ldb, nb, K, pick_ks(K), C, ldc, bias};
+  WgradArgs a{A, ma, B, nb, K, pick_ks(K), C, ldc, bias};
   const dim3 grid((unsigned)((K + a.ks - 1) / a.ks)), block(256);
-  if (MT == 8 && NT == 8) hipLaunchKernelGGL((k_wgrad<8, 8>), grid, block, 0, st, a);
-  else if (MT == 8 && NT == 3) hipLaunchKernelGGL((k_wgrad<8, 3>), grid, block, 0, st, a);
-  else if (MT == 1 && NT == 8) hipLaunchKernelGGL((k_wgrad<1, 8>), grid, block, 0, st, a);
-  else if (MT == 1 && NT == 3) hipLaunchKernelGGL((k_wgrad<1, 3>), grid, block, 0, st, a);
-  else return PNR_E_ARG;
+  TimingScope ts(kTimeWgrad, K, st);
+  switch (kind) {
+    case kWgradHidden: hipLaunchKernelGGL((k_wgrad<8, 8, 256, 256>), grid, block, 0, st, a); break;
+    case kWgradFirst: hipLaunchKernelGGL((k_wgrad<8, 3, 256, 96>), grid, block, 0, st, a); break;
+    case kWgradOut: hipLaunchKernelGGL((k_wgrad<1, 8, 4, 256>), grid, block, 0, st, a); break;
+    case kWgradFourier: hipLaunchKernelGGL((k_wgrad<1, 3, 4, 96>), grid, block, 0, st, a); break;
+    default: return PNR_E_ARG;
+  }
   return hip_status(hipGetLastError());
 }
 

@@ -1,0 +1,69 @@
+"""Kernel microbenchmarks for the MLP kernels (device time via pnr_timing_* hipEvents).
+
+  python tools/kbench.py [--points P] [--reps R]
+
+Prints one line per case: launches, mean ms, achieved TFLOP/s (443,438 FLOP/point fwd,
+442,880 FLOP/point delta chain) and the fraction of the 157.3 TF fp32 MFMA peak."""
+import argparse
+import os
+import sys
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, 'pointnerf-slam_amd'))
+sys.path.insert(0, REPO)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--points', type=int, default=4 * 1024 * 1024)
+    ap.add_argument('--reps', type=int, default=5)
+    args = ap.parse_args()
+    import pnr
+    from pnr._lib import timing_read
+    dev = torch.device('cuda:0')
+    lib = pnr.library()
+    w = np.load(os.path.join(REPO, 'tests', 'golden', 'weights.npz'))
+    params = {k[len('trained/'):]: torch.from_numpy(w[k]) for k in w.files if k.startswith('trained/')}
+    dec = pnr.get_model(pnr.ROOM0_CFG, nice=False)
+    dec.load_state_dict(params)
+    dec = dec.to(dev)
+    import types
+    s = np.load(os.path.join(REPO, 'tests', 'golden', 'scene.npz'))
+    slam = types.SimpleNamespace(bound=torch.from_numpy(s['bound']), H=480, W=640, fx=577.59, fy=578.73, cx=318.91,
+                                 cy=242.68)
+    r = pnr.Renderer(pnr.ROOM0_CFG, None, slam)
+    P = args.points
+    pts = (torch.rand(P, 3, device=dev, dtype=torch.float64) * 1.2 - 0.35)
+
+    def report(name, kind, fl):
+        n, ms, u = timing_read(kind)
+        tf = fl * u / (ms * 1e-3) / 1e12 if ms > 0 else 0
+        print(f'{name:34s} launches={n:3d} mean_ms={ms / max(n, 1):9.3f} TF/s={tf:7.2f} frac={tf / 157.3:.3f}',
+              flush=True)
+
+    # forward, inference (no save)
+    r.eval_points(pts, dec)
+    torch.cuda.synchronize()
+    lib.pnr_timing_enable(1)
+    timing_read(0)
+    for _ in range(args.reps):
+        r.eval_points(pts, dec)
+    torch.cuda.synchronize()
+    report('k_mlp_fwd eval (f64 pts, no save)', 0, 443438)
+    # forward with save + backward (MLP autograd path)
+    x = pts.float().requires_grad_(False)
+    timing_read(0), timing_read(1)
+    for _ in range(args.reps):
+        out = dec(x)
+        out.sum().backward()
+    torch.cuda.synchronize()
+    report('k_mlp_fwd train (save)', 0, 443438)
+    report('k_mlp_bwd delta chain', 1, 442880)
+    lib.pnr_timing_enable(0)
+
+
+if __name__ == '__main__':
+    main()
