@@ -12,8 +12,8 @@
  *    pointers.  The library allocates no device memory and keeps no per-call state; scratch comes
  *    from the caller's workspace (size from the matching *_workspace_bytes query).
  *  - `stream` is a hipStream_t passed as void* (0 = legacy default stream).  All calls are
- *    asynchronous and stream-ordered; they are re-entrant (no global mutable state except a
- *    per-thread cache of rocBLAS handles used by pnr_render_bwd / pnr_mlp_bwd).
+ *    asynchronous and stream-ordered; they are re-entrant (the only global state is the opt-in
+ *    kernel-timing record of pnr_timing_enable).
  *  - Return value: 0 on success, a negative PNR_E* code on argument errors, or a positive
  *    hipError_t when a launch fails.  No exception ever crosses the ABI.
  *  - Dtypes follow the reference exactly: sample depths z / points / depth / variance are
@@ -38,16 +38,52 @@
 extern "C" {
 #endif
 
-#define PNR_ABI_VERSION 1
+#define PNR_ABI_VERSION 2
 #define PNR_N_PARAMS 11
 #define PNR_MAX_SAMPLES 64      /* N_samples + N_importance per ray */
+#define PNR_C_DIM 32            /* neural-point feature width (decoder.py:122-125 fc_c input) */
+#define PNR_MAX_K 8             /* neighbours per sample of the point gather */
+#define PNR_N_FC_PARAMS 8       /* fc_c.{0..3}.weight (256,32), fc_c.{0..3}.bias (256), interleaved */
 
 enum {
   PNR_OK = 0,
   PNR_E_ARG = -1,        /* bad argument (null pointer, negative size, unsupported config) */
   PNR_E_WORKSPACE = -2,  /* workspace smaller than *_workspace_bytes */
-  PNR_E_BLAS = -3,       /* rocBLAS failure */
+  PNR_E_BLAS = -3,       /* reserved (no BLAS library is used) */
 };
+
+/* ---- neural points (build-defined, no reference counterpart) --------
+ * Feature of a sample p: the (up to) k neighbours x_i with the smallest (|p-x_i|^2, i) among
+ *   PNR_GATHER_IDW:       |p - x_i| <= radius,           weight w_i = 1 / max(|p - x_i|, eps)
+ *   PNR_GATHER_TRILINEAR: |p_a - x_i,a| < spacing_a (all a), w_i = prod_a (1 - |p_a - x_i,a| / spacing_a)
+ * c(p) = sum_k (w_k / sum w) f_k, 0 without neighbours (oracle/ref_points.py is the spec).  With
+ * points on a lattice, TRILINEAR reproduces MLP.sample_grid_feature's F.grid_sample
+ * (src/conv_onet/models/decoder.py:168-175) on interior samples.  The decoder then injects c
+ * into every hidden layer: h = relu(W h + b) + fc_c[i](c) (decoder.py:196-197).
+ * Search structure: a spatial hash of cubic cells (edge `cell`, corner `origin`) into
+ * 2^table_bits buckets, bucket-sorted copies of the positions; built on the device by
+ * pnr_points_build into the caller's `index` buffer.  `cell` must be >= radius (IDW) or
+ * >= max(spacing) (TRILINEAR): the search visits the 27 cells around p. */
+enum { PNR_GATHER_IDW = 0, PNR_GATHER_TRILINEAR = 1 };
+
+typedef struct pnr_points {
+  const float* xyz;         /* (M,3) float32 point positions                                  */
+  const float* feats;       /* (M,32) float32 point features                                  */
+  int64_t n_points;         /* M                                                              */
+  int32_t mode;             /* PNR_GATHER_IDW / PNR_GATHER_TRILINEAR                          */
+  int32_t k;                /* neighbours kept, 1..PNR_MAX_K                                  */
+  float radius;             /* IDW ball radius                                                */
+  float eps;                /* IDW distance floor                                             */
+  float spacing[3];         /* TRILINEAR lattice spacing per axis                             */
+  float cell;               /* hash cell edge                                                 */
+  float origin[3];          /* hash cell origin                                               */
+  int32_t table_bits;       /* 10..24                                                         */
+  void* index;              /* device buffer of pnr_points_index_bytes() bytes                */
+  const float* fc_packed;   /* fc_c weight image (pnr_fc_pack) for the decoder; may be NULL for
+                               the standalone gather                                           */
+  float* g_feats;           /* backward: dL/dfeats (M,32) ACCUMULATED, or NULL                */
+  float* const* g_fc;       /* backward: host array of 8 device ptrs accumulating dL/dfc_c, or NULL */
+} pnr_points;
 
 /* Renderer configuration: the cfg keys Renderer.__init__ reads (src/utils/Renderer.py:6-21)
  * plus host-computed torch.linspace tables (Renderer.py:157, common.py:33). */
@@ -63,6 +99,7 @@ typedef struct pnr_render_params {
   float u_vals[PNR_MAX_SAMPLES];   /* torch.linspace(0,1,n_importance) float32        */
   int32_t save_for_backward;       /* keep MLP activations in the workspace for pnr_render_bwd */
   int32_t need_ray_grads;          /* backward also produces dL/drays_o, dL/drays_d (tracking) */
+  const pnr_points* points;        /* neural-point features, NULL = the reference decoder (c_dim=0) */
 } pnr_render_params;
 
 /* ---- library identity -------------------------------------------------------------------- */
@@ -94,6 +131,33 @@ int pnr_mlp_fwd_train(const float* packed, const float* p, int64_t P, float* raw
 size_t pnr_mlp_bwd_workspace_bytes(int64_t P);
 int pnr_mlp_bwd(const float* packed, int64_t P, const float* g_raw, float* const* grads, float* g_p, void* ws,
                 size_t ws_bytes, void* bwd_ws, size_t bwd_bytes, void* stream);
+
+/* ---- neural points ------------------------------------------------------------------------ */
+size_t pnr_points_index_bytes(int64_t n_points, int32_t table_bits);
+/* (Re)builds pts->index from pts->xyz (after any change of positions / cell / origin). */
+int pnr_points_build(const pnr_points* pts, void* stream);
+/* Standalone gather: c (P,32) float32 for float64 points p (P,3).  idx (P,k) int32 (-1 = none)
+ * and w (P,k) float32 normalised weights are written when non-NULL (needed by the backward). */
+int pnr_point_gather(const pnr_points* pts, const double* p, int64_t P, float* c, int32_t* idx, float* w,
+                     void* stream);
+/* Backward of pnr_point_gather: g_c (P,32) -> pts->g_feats (+=, when non-NULL) and g_p (P,3)
+ * (written, when non-NULL: dL/dp through the weights). */
+int pnr_point_gather_bwd(const pnr_points* pts, const double* p, int64_t P, const int32_t* idx, const float* w,
+                         const float* c, const float* g_c, float* g_p, void* stream);
+/* fc_c weight image of the decoder (MLP(c_dim=32)): fc_params = host array of the 8 tensors
+ * fc_c.0.weight, fc_c.0.bias, ..., fc_c.3.bias (contiguous float32). */
+size_t pnr_fc_packed_floats(void);
+int pnr_fc_pack(const float* const* fc_params, float* fc_packed, void* stream);
+/* MLP.forward with per-point features c (P,32): eval (bound6 may be NULL) and training
+ * variants.  pnr_mlp_bwd_c also writes g_c (P,32) and accumulates the 8 fc_c grads. */
+int pnr_eval_points_c(const float* packed, const float* fc_packed, const double* p, const float* c, int64_t P,
+                      const double* bound6, float* raw_out, void* stream);
+int pnr_mlp_fwd_train_c(const float* packed, const float* fc_packed, const float* p, const float* c, int64_t P,
+                        float* raw_out, void* ws, size_t ws_bytes, void* stream);
+size_t pnr_mlp_bwd_workspace_bytes_c(int64_t P);
+int pnr_mlp_bwd_c(const float* packed, const float* fc_packed, const float* c, int64_t P, const float* g_raw,
+                  float* const* grads, float* const* g_fc, float* g_c, float* g_p, void* ws, size_t ws_bytes,
+                  void* bwd_ws, size_t bwd_bytes, void* stream);
 
 /* ---- render_batch_ray (src/utils/Renderer.py:63-203) ------------------------------------- */
 size_t pnr_render_workspace_bytes(const pnr_render_params* prm, int64_t n_rays);

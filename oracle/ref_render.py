@@ -225,9 +225,13 @@ def near_far(rays_o, rays_d, bound: torch.Tensor, n_samples: int, gt_depth=None,
 
 def render_batch_ray(params: Params, rays_d, rays_o, bound, n_samples=32, n_importance=12,
                      gt_depth=None, perturb=0.0, lindisp=False, t_rand=None,
-                     return_extras=False, points_batch_size=500000, far_clamp=None):
+                     return_extras=False, points_batch_size=500000, far_clamp=None, eval_fn=None):
     """src/utils/Renderer.py:63-203 (N_surface=0 path; occupancy=False).
-    Returns (depth f64 (N,), uncertainty f64 (N,), color f32 (N,3)) [, extras]."""
+    Returns (depth f64 (N,), uncertainty f64 (N,), color f32 (N,3)) [, extras].
+    `eval_fn(p) -> raw` replaces the decoder query (e.g. ref_points.eval_points_c for the
+    neural-point decoder); default: the reference MLP through `eval_points`."""
+    if eval_fn is None:
+        eval_fn = lambda q: eval_points(params, q, bound, points_batch_size)  # noqa: E731
     near, far = near_far(rays_o, rays_d, bound, n_samples, gt_depth, far_clamp)
     t_vals = torch.linspace(0., 1., steps=n_samples)
     if not lindisp:
@@ -243,7 +247,7 @@ def render_batch_ray(params: Params, rays_d, rays_o, bound, n_samples=32, n_impo
         z = lower + (upper - lower) * t_rand
     N = rays_o.shape[0]
     pts = rays_o[..., None, :] + rays_d[..., None, :] * z[..., :, None]
-    raw = eval_points(params, pts.reshape(-1, 3), bound, points_batch_size).reshape(N, z.shape[1], -1)
+    raw = eval_fn(pts.reshape(-1, 3)).reshape(N, z.shape[1], -1)
     depth, var, rgb, w = composite(raw, z, rays_d)
     extras = {'near': near, 'far': far, 'z_coarse': z, 'raw_coarse': raw, 'w_coarse': w}
     if n_importance > 0:
@@ -251,7 +255,7 @@ def render_batch_ray(params: Params, rays_d, rays_o, bound, n_samples=32, n_impo
         z_s = sample_pdf(z_mid, w[..., 1:-1], n_importance, det=(perturb == 0.)).detach()
         z, _ = torch.sort(torch.cat([z, z_s], -1), -1)
         pts = rays_o[..., None, :] + rays_d[..., None, :] * z[..., :, None]
-        raw = eval_points(params, pts.reshape(-1, 3), bound, points_batch_size).reshape(N, z.shape[1], -1)
+        raw = eval_fn(pts.reshape(-1, 3)).reshape(N, z.shape[1], -1)
         depth, var, rgb, w = composite(raw, z, rays_d)
         extras.update({'z_samples': z_s, 'z_fine': z, 'raw_fine': raw, 'w_fine': w})
     if return_extras:
@@ -259,9 +263,11 @@ def render_batch_ray(params: Params, rays_d, rays_o, bound, n_samples=32, n_impo
     return depth, var, rgb
 
 
-def regulation(params: Params, rays_d, rays_o, gt_depth, bound, n_samples=32, t_rand=None):
+def regulation(params: Params, rays_d, rays_o, gt_depth, bound, n_samples=32, t_rand=None, eval_fn=None):
     """src/utils/Renderer.py:263-301: density at 32 jittered samples in [0, 0.85*gt] (f32 z).
     `t_rand` (N,n_samples) f32 replaces the reference's torch.rand draw at :293."""
+    if eval_fn is None:
+        eval_fn = lambda q: eval_points(params, q, bound)  # noqa: E731
     g = gt_depth.reshape(-1, 1).repeat(1, n_samples)
     t_vals = torch.linspace(0., 1., steps=n_samples)
     z = 0.0 * (1. - t_vals) + (g * 0.85) * t_vals
@@ -272,7 +278,7 @@ def regulation(params: Params, rays_d, rays_o, gt_depth, bound, n_samples=32, t_
         t_rand = torch.rand(z.shape)
     z = lower + (upper - lower) * t_rand
     pts = rays_o[..., None, :] + rays_d[..., None, :] * z[..., :, None]
-    return eval_points(params, pts.reshape(-1, 3), bound)[:, -1]
+    return eval_fn(pts.reshape(-1, 3))[:, -1]
 
 
 def render_img(params: Params, c2w, bound, H, W, fx, fy, cx, cy, gt_depth=None,

@@ -112,7 +112,12 @@ struct RenderWS {
   uint8_t* ord;    // [N][64]
   double* far;     // [N]
   int64_t pc_pad;  // first saved column of the importance segment (coarse points padded to 128)
+  int64_t ld;      // pc_pad + importance points padded to 128
   SaveArgs save;   // when save_for_backward; columns [0,pc_pad) coarse, [pc_pad, ld) importance
+  // neural-point features (prm->points): rows like the save columns
+  float* c;        // [ld][32]
+  int32_t* nidx;   // [ld][k]
+  float* nw;       // [ld][k]
 };
 
 SaveArgs carve_save(Carver& c, int64_t ld) {
@@ -136,7 +141,13 @@ RenderWS carve_render(const pnr_render_params* prm, int64_t n, void* ws, size_t*
   w.ord = c.take<uint8_t>(n * PNR_MAX_SAMPLES);
   w.far = c.take<double>(n);
   w.pc_pad = pad128(n * prm->n_samples);
-  if (prm->save_for_backward) w.save = carve_save(c, w.pc_pad + pad128(n * prm->n_importance));
+  w.ld = w.pc_pad + pad128(n * prm->n_importance);
+  if (prm->save_for_backward) w.save = carve_save(c, w.ld);
+  if (prm->points) {
+    w.c = c.take<float>((size_t)w.ld * kCDim);
+    w.nidx = c.take<int32_t>((size_t)w.ld * prm->points->k);
+    w.nw = c.take<float>((size_t)w.ld * prm->points->k);
+  }
   if (bytes) *bytes = c.off;
   return w;
 }
@@ -148,10 +159,12 @@ struct BwdWS {
   float* g_nrm;   // [N]
   float* dP;      // [4][C][256]
   float* gargP;   // [C][96]
+  float* gH;      // [4][C][256]  features only: dL/dh_l
+  float* g_c;     // [P][32]      features only: dL/dc
   int64_t C;
 };
 
-BwdWS carve_bwd(int64_t P, int64_t n, void* ws, size_t* bytes) {
+BwdWS carve_bwd(int64_t P, int64_t n, void* ws, size_t* bytes, bool feat = false) {
   Carver c(ws);
   BwdWS b{};
   b.C = P < kBwdChunk ? ((P + 127) / 128) * 128 : kBwdChunk;
@@ -161,9 +174,20 @@ BwdWS carve_bwd(int64_t P, int64_t n, void* ws, size_t* bytes) {
   b.g_nrm = c.take<float>(n);
   b.dP = c.take<float>((size_t)4 * kHidden * b.C);
   b.gargP = c.take<float>(kFourierPad * b.C);
+  if (feat) {
+    b.gH = c.take<float>((size_t)4 * kHidden * b.C);
+    b.g_c = c.take<float>((size_t)P * kCDim);
+  }
   if (bytes) *bytes = c.off;
   return b;
 }
+
+// fc_c side of the backward: image, per-row features and the 8 accumulated fc_c grads
+struct FeatBwd {
+  const float* fcw;
+  const float* c;        // [rows][32], same rows as the saved activations
+  float* const* g_fc;    // 8 device pointers or null
+};
 
 __global__ void k_fill(float* p, int64_t n, float v) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -172,7 +196,7 @@ __global__ void k_fill(float* p, int64_t n, float v) {
 
 // Shared backward core over P points with saved activations `sv` and dL/draw in b.g_out.
 int mlp_backward_core(const float* packed, const SaveArgs& sv, int64_t P, BwdWS& b, float* const* grads,
-                      bool want_gx, hipStream_t st) {
+                      bool want_gx, hipStream_t st, const FeatBwd* fb = nullptr) {
   for (int64_t p0 = 0; p0 < P; p0 += b.C) {
     const int64_t C = (P - p0) < b.C ? (P - p0) : b.C;
     BwdArgs a;
@@ -185,6 +209,9 @@ int mlp_backward_core(const float* packed, const SaveArgs& sv, int64_t P, BwdWS&
     a.ld = sv.ld;
     a.p0 = p0;
     a.ld_d = b.C;
+    a.fcw = fb ? fb->fcw : nullptr;
+    a.gH = b.gH;
+    a.g_c = fb ? b.g_c + p0 * kCDim : nullptr;
     int rc = launch_mlp_bwd(packed, a, C, st);
     if (rc) return rc;
     const float* hp = sv.hP + p0 * kHidden;  // h_l rows of this chunk: hp + l_idx * ld * 256
@@ -205,6 +232,12 @@ int mlp_backward_core(const float* packed, const SaveArgs& sv, int64_t P, BwdWS&
     // Fourier: dB (3x93) += x^T g_arg   (x rows are float4 (x0,x1,x2,inside): 3 of 4 used)
     rc = launch_wgrad(kWgradFourier, reinterpret_cast<const float*>(sv.xP + p0), 3, b.gargP, kFourier, C, grads[0],
                       kFourier, nullptr, st);
+    if (rc) return rc;
+    // feature branch: dWc_l (256x32) += (dL/dh_l)^T c ; dbc_l += colsum(dL/dh_l)
+    if (fb && fb->g_fc)
+      for (int l = 0; l < 4 && rc == 0; ++l)
+        rc = launch_wgrad(kWgradFc, b.gH + l * dstride, kHidden, fb->c + p0 * kCDim, kCDim, C, fb->g_fc[2 * l], kCDim,
+                          fb->g_fc[2 * l + 1], st);
     if (rc) return rc;
   }
   return hip_status(hipGetLastError());
@@ -254,7 +287,7 @@ int pnr_timing_read(int kernel, int64_t* launches, double* ms, int64_t* units) {
 
 const char* pnr_build_info(void) {
   return "libpnr gfx950: fp32 v_mfma_f32_32x32x2_f32 fused decoder, LDS-streamed weights; "
-         "thread-per-ray compositing; rocBLAS weight-gradient GEMMs";
+         "thread-per-ray compositing; split-K MFMA weight-gradient GEMMs; spatial-hash neural-point gather";
 }
 
 size_t pnr_mlp_packed_floats(void) { return (size_t)kPackedFloats; }
@@ -348,6 +381,7 @@ int pnr_render_fwd(const pnr_render_params* prm, const float* packed, const floa
   if (!valid_prm(prm) || !packed || n < 0) return PNR_E_ARG;
   if (n == 0) return PNR_OK;
   if (!rays_o || !rays_d || !depth || !var || !rgb || !workspace) return PNR_E_ARG;
+  if (prm->points && !prm->points->fc_packed) return PNR_E_ARG;
   if (prm->n_importance > 0 && prm->n_samples < 3) return PNR_E_ARG;
   size_t need = 0;
   RenderWS w = carve_render(prm, n, workspace, &need);
@@ -367,7 +401,14 @@ int pnr_render_fwd(const pnr_render_params* prm, const float* packed, const floa
   src.z = w.z;
   src.spr = S;
   const SaveArgs* sv = prm->save_for_backward ? &w.save : nullptr;
-  rc = launch_mlp_fwd(packed, src, kRaysZ64, n * S, w.raw, sv, st);
+  const pnr_points* pts = prm->points;
+  FeatArgs fa{pts ? pts->fc_packed : nullptr, w.c};
+  const int K = pts ? pts->k : 0;
+  if (pts) {
+    rc = launch_gather(*pts, src, kRaysZ64, n * S, w.pc_pad, w.c, sv ? w.nidx : nullptr, sv ? w.nw : nullptr, st);
+    if (rc) return rc;
+  }
+  rc = launch_mlp_fwd(packed, src, kRaysZ64, n * S, w.raw, sv, st, pts ? &fa : nullptr);
   if (rc) return rc;
   double* zi = w.z + n * S;
   float* rawi = w.raw + n * S * 4;
@@ -382,7 +423,14 @@ int pnr_render_fwd(const pnr_render_params* prm, const float* packed, const floa
       s2.p0 = w.pc_pad;
       sv = &s2;
     }
-    rc = launch_mlp_fwd(packed, src, kRaysZ64, n * I, rawi, sv, st);
+    if (pts) {
+      const int64_t o = w.pc_pad;
+      rc = launch_gather(*pts, src, kRaysZ64, n * I, w.ld - o, w.c + o * kCDim, sv ? w.nidx + o * K : nullptr,
+                         sv ? w.nw + o * K : nullptr, st);
+      if (rc) return rc;
+      fa.c = w.c + o * kCDim;
+    }
+    rc = launch_mlp_fwd(packed, src, kRaysZ64, n * I, rawi, sv, st, pts ? &fa : nullptr);
     if (rc) return rc;
   }
   return launch_fine(*prm, rays_d, w.z, zi, w.raw, rawi, n, depth, var, rgb, w.ord, st);
@@ -391,7 +439,8 @@ int pnr_render_fwd(const pnr_render_params* prm, const float* packed, const floa
 size_t pnr_render_bwd_workspace_bytes(const pnr_render_params* prm, int64_t n_rays) {
   if (!valid_prm(prm) || n_rays < 0) return 0;
   size_t b = 0;
-  carve_bwd(pad128(n_rays * prm->n_samples) + pad128(n_rays * prm->n_importance), n_rays, nullptr, &b);
+  carve_bwd(pad128(n_rays * prm->n_samples) + pad128(n_rays * prm->n_importance), n_rays, nullptr, &b,
+            prm->points != nullptr);
   return b;
 }
 
@@ -411,7 +460,8 @@ int pnr_render_bwd(const pnr_render_params* prm, const float* packed, const floa
   RenderWS w = carve_render(prm, n, workspace, &need);
   const int S = prm->n_samples, I = prm->n_importance;
   const int64_t ld = w.save.ld;
-  BwdWS b = carve_bwd(ld, n, bwd_ws, &bneed);
+  const pnr_points* pts = prm->points;
+  BwdWS b = carve_bwd(ld, n, bwd_ws, &bneed, pts != nullptr);
   if (ws_bytes < need || bwd_bytes < bneed) return PNR_E_WORKSPACE;
   hipStream_t st = (hipStream_t)stream;
   const double* zi = w.z + n * S;
@@ -421,8 +471,14 @@ int pnr_render_bwd(const pnr_render_params* prm, const float* packed, const floa
   int rc = launch_fine_bwd(*prm, rays_d, w.z, zi, w.raw, rawi, w.save.xP, w.save.xP + pc, w.ord, n,
                            g_depth, g_var, g_rgb, b.g_out, b.g_out + pc * 4, b.g_nrm, st);
   if (rc) return rc;
-  rc = mlp_backward_core(packed, w.save, ld, b, grads, prm->need_ray_grads != 0, st);
+  FeatBwd fb{pts ? pts->fc_packed : nullptr, w.c, pts ? pts->g_fc : nullptr};
+  rc = mlp_backward_core(packed, w.save, ld, b, grads, prm->need_ray_grads != 0, st, pts ? &fb : nullptr);
   if (rc) return rc;
+  if (pts) {  // neural-point features and dL/dp through the gather weights
+    rc = launch_gather_bwd(*pts, nullptr, kRaysZ64, w.save.xP, ld, w.nidx, w.nw, w.c, b.g_c,
+                           prm->need_ray_grads ? b.g_x : nullptr, true, st);
+    if (rc) return rc;
+  }
   if (prm->need_ray_grads)
     rc = launch_ray_grads_f64(rays_d, w.z, S, zi, I, b.g_x, b.g_x + pc * 3, b.g_nrm, n, g_rays_o, g_rays_d, st);
   return rc;
@@ -434,6 +490,9 @@ struct RegWS {
   float* z;
   float* raw;
   SaveArgs save;
+  float* c;
+  int32_t* nidx;
+  float* nw;
 };
 RegWS carve_reg(const pnr_render_params* prm, int64_t n, void* ws, size_t* bytes) {
   Carver c(ws);
@@ -442,6 +501,11 @@ RegWS carve_reg(const pnr_render_params* prm, int64_t n, void* ws, size_t* bytes
   w.z = c.take<float>(P);
   w.raw = c.take<float>(P * 4);
   if (prm->save_for_backward) w.save = carve_save(c, pad128(P));
+  if (prm->points) {
+    w.c = c.take<float>((size_t)pad128(P) * kCDim);
+    w.nidx = c.take<int32_t>((size_t)pad128(P) * prm->points->k);
+    w.nw = c.take<float>((size_t)pad128(P) * prm->points->k);
+  }
   if (bytes) *bytes = c.off;
   return w;
 }
@@ -460,6 +524,7 @@ int pnr_regulation_fwd(const pnr_render_params* prm, const float* packed, const 
   if (!valid_prm(prm) || !packed || n < 0) return PNR_E_ARG;
   if (n == 0) return PNR_OK;
   if (!rays_o || !rays_d || !gt_depth || !t_rand || !sigma || !workspace) return PNR_E_ARG;
+  if (prm->points && !prm->points->fc_packed) return PNR_E_ARG;
   size_t need = 0;
   RegWS w = carve_reg(prm, n, workspace, &need);
   if (ws_bytes < need) return PNR_E_WORKSPACE;
@@ -474,7 +539,13 @@ int pnr_regulation_fwd(const pnr_render_params* prm, const float* packed, const 
   src.z = w.z;
   src.spr = prm->n_samples;
   const int64_t P = n * prm->n_samples;
-  rc = launch_mlp_fwd(packed, src, kRaysZ32, P, w.raw, prm->save_for_backward ? &w.save : nullptr, st);
+  const bool sv = prm->save_for_backward != 0;
+  FeatArgs fa{prm->points ? prm->points->fc_packed : nullptr, w.c};
+  if (prm->points) {
+    rc = launch_gather(*prm->points, src, kRaysZ32, P, pad128(P), w.c, sv ? w.nidx : nullptr, sv ? w.nw : nullptr, st);
+    if (rc) return rc;
+  }
+  rc = launch_mlp_fwd(packed, src, kRaysZ32, P, w.raw, sv ? &w.save : nullptr, st, prm->points ? &fa : nullptr);
   if (rc) return rc;
   return launch_extract_sigma(w.raw, P, sigma, st);
 }
@@ -482,7 +553,7 @@ int pnr_regulation_fwd(const pnr_render_params* prm, const float* packed, const 
 size_t pnr_regulation_bwd_workspace_bytes(const pnr_render_params* prm, int64_t n_rays) {
   if (!valid_prm(prm) || n_rays < 0) return 0;
   size_t b = 0;
-  carve_bwd(pad128(n_rays * prm->n_samples), n_rays, nullptr, &b);
+  carve_bwd(pad128(n_rays * prm->n_samples), n_rays, nullptr, &b, prm->points != nullptr);
   return b;
 }
 
@@ -502,16 +573,123 @@ int pnr_regulation_bwd(const pnr_render_params* prm, const float* packed, const 
   RegWS w = carve_reg(prm, n, workspace, &need);
   const int64_t P = n * prm->n_samples;
   const int64_t ld = w.save.ld;
-  BwdWS b = carve_bwd(ld, n, bwd_ws, &bneed);
+  const pnr_points* pts = prm->points;
+  BwdWS b = carve_bwd(ld, n, bwd_ws, &bneed, pts != nullptr);
   if (ws_bytes < need || bwd_bytes < bneed) return PNR_E_WORKSPACE;
   hipStream_t st = (hipStream_t)stream;
   if (hipMemsetAsync(b.g_out, 0, (size_t)ld * 16, st) != hipSuccess) return (int)hipGetLastError();
   int rc = launch_gout_sigma(g_sigma, w.save.xP, P, b.g_out, st);
   if (rc) return rc;
-  rc = mlp_backward_core(packed, w.save, ld, b, grads, prm->need_ray_grads != 0, st);
+  FeatBwd fb{pts ? pts->fc_packed : nullptr, w.c, pts ? pts->g_fc : nullptr};
+  rc = mlp_backward_core(packed, w.save, ld, b, grads, prm->need_ray_grads != 0, st, pts ? &fb : nullptr);
   if (rc) return rc;
+  if (pts) {
+    rc = launch_gather_bwd(*pts, nullptr, kRaysZ32, w.save.xP, ld, w.nidx, w.nw, w.c, b.g_c,
+                           prm->need_ray_grads ? b.g_x : nullptr, true, st);
+    if (rc) return rc;
+  }
   if (prm->need_ray_grads) rc = launch_ray_grads_f32(rays_d, w.z, prm->n_samples, b.g_x, n, g_rays_o, g_rays_d, st);
   return rc;
+}
+
+// ---- neural points ---------------------------------------------------------------------------
+size_t pnr_points_index_bytes(int64_t n_points, int32_t table_bits) {
+  if (n_points < 0 || table_bits < 10 || table_bits > 24) return 0;
+  size_t b = 0;
+  index_view(nullptr, n_points, table_bits, &b);
+  return b;
+}
+
+int pnr_points_build(const pnr_points* pts, void* stream) {
+  if (!pts || pts->n_points < 0 || !pts->index || pts->table_bits < 10 || pts->table_bits > 24 || !(pts->cell > 0.f) ||
+      (pts->n_points > 0 && !pts->xyz))
+    return PNR_E_ARG;
+  return launch_points_build(*pts, (hipStream_t)stream);
+}
+
+int pnr_point_gather(const pnr_points* pts, const double* p, int64_t P, float* c, int32_t* idx, float* w,
+                     void* stream) {
+  if (!pts || P < 0 || (P > 0 && (!p || !c)) || (!idx) != (!w)) return PNR_E_ARG;
+  PointSrc s{};
+  s.pts = p;
+  return launch_gather(*pts, s, kPtsF64, P, P, c, idx, w, (hipStream_t)stream);
+}
+
+int pnr_point_gather_bwd(const pnr_points* pts, const double* p, int64_t P, const int32_t* idx, const float* w,
+                         const float* c, const float* g_c, float* g_p, void* stream) {
+  if (!pts || P < 0 || (P > 0 && !p)) return PNR_E_ARG;
+  PointSrc s{};
+  s.pts = p;
+  return launch_gather_bwd(*pts, &s, kPtsF64, nullptr, P, idx, w, c, g_c, g_p, false, (hipStream_t)stream);
+}
+
+size_t pnr_fc_packed_floats(void) { return (size_t)kFcPackedFloats; }
+
+int pnr_fc_pack(const float* const* fc_params, float* fc_packed, void* stream) {
+  if (!fc_params || !fc_packed) return PNR_E_ARG;
+  for (int i = 0; i < PNR_N_FC_PARAMS; ++i)
+    if (!fc_params[i]) return PNR_E_ARG;
+  return launch_fc_pack(fc_params, fc_packed, (hipStream_t)stream);
+}
+
+int pnr_eval_points_c(const float* packed, const float* fc_packed, const double* p, const float* c, int64_t P,
+                      const double* bound6, float* raw_out, void* stream) {
+  if (!packed || !fc_packed || P < 0 || (P > 0 && (!p || !c || !raw_out))) return PNR_E_ARG;
+  PointSrc s{};
+  s.pts = p;
+  s.use_bound = bound6 != nullptr;
+  if (bound6) memcpy(s.bound, bound6, sizeof(s.bound));
+  FeatArgs fa{fc_packed, c};
+  return launch_mlp_fwd(packed, s, kPtsF64, P, raw_out, nullptr, (hipStream_t)stream, &fa);
+}
+
+int pnr_mlp_fwd_train_c(const float* packed, const float* fc_packed, const float* p, const float* c, int64_t P,
+                        float* raw_out, void* ws, size_t ws_bytes, void* stream) {
+  if (!packed || !fc_packed || P < 0 || (P > 0 && (!p || !c || !raw_out || !ws))) return PNR_E_ARG;
+  if (P == 0) return PNR_OK;
+  Carver cv(ws);
+  SaveArgs sv = carve_save(cv, pad128(P));
+  if (ws_bytes < cv.off) return PNR_E_WORKSPACE;
+  PointSrc s{};
+  s.pts = p;
+  FeatArgs fa{fc_packed, c};
+  return launch_mlp_fwd(packed, s, kPtsF32, P, raw_out, &sv, (hipStream_t)stream, &fa);
+}
+
+size_t pnr_mlp_bwd_workspace_bytes_c(int64_t P) {
+  if (P < 0) return 0;
+  size_t b = 0;
+  carve_bwd(pad128(P), 1, nullptr, &b, true);
+  return b;
+}
+
+int pnr_mlp_bwd_c(const float* packed, const float* fc_packed, const float* c, int64_t P, const float* g_raw,
+                  float* const* grads, float* const* g_fc, float* g_c, float* g_p, void* ws, size_t ws_bytes,
+                  void* bwd_ws, size_t bwd_bytes, void* stream) {
+  if (!packed || !fc_packed || P < 0 || (P > 0 && (!c || !g_raw || !grads || !g_fc || !ws || !bwd_ws))) return PNR_E_ARG;
+  if (P == 0) return PNR_OK;
+  for (int i = 0; i < PNR_N_PARAMS; ++i)
+    if (!grads[i]) return PNR_E_ARG;
+  for (int i = 0; i < PNR_N_FC_PARAMS; ++i)
+    if (!g_fc[i]) return PNR_E_ARG;
+  Carver cv(ws);
+  SaveArgs sv = carve_save(cv, pad128(P));
+  size_t bneed = 0;
+  BwdWS b = carve_bwd(sv.ld, 1, bwd_ws, &bneed, true);
+  if (ws_bytes < cv.off || bwd_bytes < bneed) return PNR_E_WORKSPACE;
+  hipStream_t st = (hipStream_t)stream;
+  if (hipMemsetAsync(b.g_out, 0, (size_t)sv.ld * 16, st) != hipSuccess) return (int)hipGetLastError();
+  if (hipMemcpyAsync(b.g_out, g_raw, (size_t)P * 16, hipMemcpyDeviceToDevice, st) != hipSuccess)
+    return (int)hipGetLastError();
+  // the fc_c GEMMs read c rows up to the padded row count: run them over the real rows only
+  FeatBwd fb{fc_packed, c, g_fc};
+  int rc = mlp_backward_core(packed, sv, P, b, grads, g_p != nullptr, st, &fb);
+  if (rc) return rc;
+  if (g_c && hipMemcpyAsync(g_c, b.g_c, (size_t)P * kCDim * 4, hipMemcpyDeviceToDevice, st) != hipSuccess)
+    return (int)hipGetLastError();
+  if (g_p && hipMemcpyAsync(g_p, b.g_x, (size_t)P * 12, hipMemcpyDeviceToDevice, st) != hipSuccess)
+    return (int)hipGetLastError();
+  return PNR_OK;
 }
 
 // ---- rays / optimizer ------------------------------------------------------------------------

@@ -181,27 +181,42 @@ __device__ __forceinline__ void mfma_chunk(const float* chunk, const float (&b)[
   __builtin_amdgcn_sched_barrier(0);
 }
 
-// One layer: NCH input tiles streamed as NCH LDS chunks of `chf` floats from the cursor; the
-// chunk after the last one (`nxf` floats, 0 = none) is prefetched during the last compute.
-// Buffer parity START: chunk c lives in buffer (START + c) & 1.  `stores0` (runtime, wave-
-// uniform) tells the first chunk's sync that N0 stores were issued after its DMA.
-template <int NCH, int NT, int START, int N0>
-__device__ __forceinline__ void layer(float* lds, const float*& sp, int chf, int nxf, const float (&act)[8][16],
-                                      f32x16 (&acc)[NT], bool stores0) {
+// One layer: NCH input tiles streamed as NCH LDS chunks of `chf` floats from cursor `sp`; the
+// chunk after the last one (`nxf` floats from cursor `nsp`, 0 = none) is prefetched during the
+// last compute.  `buf` (wave-uniform) is the LDS buffer of the current chunk and is advanced.
+// `stores0` (wave-uniform) tells the first chunk's sync that N0 stores were issued after its DMA.
+template <int NCH, int NT, int N0>
+__device__ __forceinline__ void layer(float* lds, const float*& sp, int chf, const float*& nsp, int nxf, int& buf,
+                                      const float (&act)[8][16], f32x16 (&acc)[NT], bool stores0) {
 #pragma unroll
   for (int c = 0; c < NCH; ++c) {
     if (c == 0 && stores0) sync_chunk<N0>();
     else sync_chunk<0>();
-    float* cur = lds + ((START + c) & 1) * kChunkFloats;
-    float* oth = lds + ((START + c + 1) & 1) * kChunkFloats;
+    float* cur = lds + buf * kChunkFloats;
+    float* oth = lds + (buf ^ 1) * kChunkFloats;
     if (c + 1 < NCH) stage(sp, oth, chf);
-    else if (nxf > 0) stage(sp, oth, nxf);
+    else if (nxf > 0) stage(nsp, oth, nxf);
     mfma_chunk<NT>(cur, act[c], acc);
     // Pin the accumulators here: without it hipcc defers half of the MFMA chains past the next
     // s_barrier (MFMAs touch no memory), keeps their A fragments alive and spills ~250 VGPRs.
 #pragma unroll
     for (int t = 0; t < NT; ++t) asm volatile("" : "+a"(acc[t]));
+    buf ^= 1;
   }
+}
+
+// One LDS chunk holding 8 k-tiles of 1024 floats (W^T images of fc_c): acc += sum_kc A_kc act[kc]
+template <int N0>
+__device__ __forceinline__ void chunk8(float* lds, const float*& nsp, int nxf, int& buf, const float (&act)[8][16],
+                                       f32x16 (&acc)[1], bool stores0) {
+  if (stores0) sync_chunk<N0>();
+  else sync_chunk<0>();
+  float* cur = lds + buf * kChunkFloats;
+  if (nxf > 0) stage(nsp, lds + (buf ^ 1) * kChunkFloats, nxf);
+#pragma unroll
+  for (int kc = 0; kc < 8; ++kc) mfma_chunk<1>(cur + kc * kSmallChunkFloats, act[kc], acc);
+  asm volatile("" : "+a"(acc[0]));
+  buf ^= 1;
 }
 
 template <int NT>
@@ -228,6 +243,36 @@ __device__ __forceinline__ void bias_relu(const f32x16 (&acc)[8], const float* _
       act[t][4 * rq + 3] = v3 > 0.f ? v3 : 0.f;
     }
     __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// act += acc + bias  (feature branch fc_c[i](c) added after the ReLU, decoder.py:196-197)
+__device__ __forceinline__ void add_bias_acc(const f32x16 (&acc)[8], const float* __restrict__ img,
+                                             float (&act)[8][16]) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+#pragma unroll
+    for (int rq = 0; rq < 4; ++rq) {
+      const float4 b = *reinterpret_cast<const float4*>(img + ((t * 4 + rq) * 64 + lane) * 4);
+      act[t][4 * rq + 0] += acc[t][4 * rq + 0] + b.x;
+      act[t][4 * rq + 1] += acc[t][4 * rq + 1] + b.y;
+      act[t][4 * rq + 2] += acc[t][4 * rq + 2] + b.z;
+      act[t][4 * rq + 3] += acc[t][4 * rq + 3] + b.w;
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// B-operand tile of the 32 feature channels of this lane's point: register r = channel perm(r,hh)
+// (4 float4 loads of the point's (32,) row).  Zero for invalid points.
+__device__ __forceinline__ void load_c_tile(const float* __restrict__ c, int64_t p, bool valid, float (&ct)[8][16]) {
+  const int hh = (threadIdx.x >> 5) & 1;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (valid) v = *reinterpret_cast<const float4*>(c + p * kCDim + 8 * q + 4 * hh);
+    ct[0][4 * q + 0] = v.x; ct[0][4 * q + 1] = v.y; ct[0][4 * q + 2] = v.z; ct[0][4 * q + 3] = v.w;
   }
 }
 
@@ -266,52 +311,13 @@ struct FwdArgs {
   float* raw;
   SaveArgs save;
   int do_save;
+  FeatArgs feat;
 };
 
 // VMEM stores issued between a layer's prefetch DMA and the next layer's first sync (a lower
 // bound is safe: it only makes the wait stricter): e + x saves = 13, mask + h saves = 33,
-// delta saves = 32.
-constexpr int kStoresE = 12, kStoresH = 32, kStoresD = 31;
-
-template <int MODE>
-__device__ __forceinline__ void load_point(const PointSrc& s, int64_t p, float& x0, float& x1, float& x2,
-                                           bool& inside) {
-  PNR_FP_STRICT
-  if (MODE == kPtsF64 || MODE == kRaysZ64) {
-    double q0, q1, q2;
-    if (MODE == kPtsF64) {
-      const double* pp = reinterpret_cast<const double*>(s.pts) + p * 3;
-      q0 = pp[0]; q1 = pp[1]; q2 = pp[2];
-    } else {
-      const int64_t ray = p / s.spr;
-      const double z = reinterpret_cast<const double*>(s.z)[p];
-      // torch: rays_o[...,None,:] + rays_d[...,None,:] * z[...,:,None], promoted to float64
-      q0 = (double)s.rays_o[ray * 3 + 0] + (double)s.rays_d[ray * 3 + 0] * z;
-      q1 = (double)s.rays_o[ray * 3 + 1] + (double)s.rays_d[ray * 3 + 1] * z;
-      q2 = (double)s.rays_o[ray * 3 + 2] + (double)s.rays_d[ray * 3 + 2] * z;
-    }
-    inside = true;
-    if (s.use_bound)
-      inside = (q0 < s.bound[1]) && (q0 > s.bound[0]) && (q1 < s.bound[3]) && (q1 > s.bound[2]) &&
-               (q2 < s.bound[5]) && (q2 > s.bound[4]);
-    x0 = (float)q0; x1 = (float)q1; x2 = (float)q2;
-  } else {
-    if (MODE == kPtsF32) {
-      const float* pp = reinterpret_cast<const float*>(s.pts) + p * 3;
-      x0 = pp[0]; x1 = pp[1]; x2 = pp[2];
-    } else {
-      const int64_t ray = p / s.spr;
-      const float z = reinterpret_cast<const float*>(s.z)[p];
-      x0 = s.rays_o[ray * 3 + 0] + s.rays_d[ray * 3 + 0] * z;
-      x1 = s.rays_o[ray * 3 + 1] + s.rays_d[ray * 3 + 1] * z;
-      x2 = s.rays_o[ray * 3 + 2] + s.rays_d[ray * 3 + 2] * z;
-    }
-    inside = true;
-    if (s.use_bound)  // a float32 tensor compared with a 0-dim float64 tensor compares in float32
-      inside = (x0 < (float)s.bound[1]) && (x0 > (float)s.bound[0]) && (x1 < (float)s.bound[3]) &&
-               (x1 > (float)s.bound[2]) && (x2 < (float)s.bound[5]) && (x2 > (float)s.bound[4]);
-  }
-}
+// mask only = 1, delta saves = 32, delta + dL/dh saves = 64.
+constexpr int kStoresE = 12, kStoresH = 32, kStoresM = 1, kStoresD = 31, kStoresDG = 62;
 
 // torch CPU computes the K=3 product x @ B as fma(x2,B2, fma(x1,B1, x0*B0)) (verified bitwise)
 __device__ __forceinline__ float fourier_arg(const float* __restrict__ FB, int k, float x0, float x1, float x2) {
@@ -322,15 +328,20 @@ __device__ __forceinline__ float fourier_arg(const float* __restrict__ FB, int k
   return a;
 }
 
-template <int MODE>
+// Weight streams: the main image in layer order (L0F, L1F, L2F, L3F, OF) and, with features
+// (HASC), the fc_c image (CF0..CF3); the chunk sequence is L0 [C0] L1 [C1] L2 [C2] L3 [C3] O.
+template <int MODE, bool HASC>
 __global__ __launch_bounds__(256, 1) void k_mlp_fwd(FwdArgs a) {
   __shared__ __attribute__((aligned(16))) float lds[2 * kChunkFloats];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, hh = lane >> 5, j = lane & 31;
   const int64_t p = (int64_t)blockIdx.x * 128 + wave * 32 + j;
   const bool valid = p < a.P;
   const float* __restrict__ W = a.packed;
+  const int lane_off = wave_id() * 256 + lane * 4;
 
-  const float* sp = W + kOffL0F + wave_id() * 256 + lane * 4;  // weight stream cursor
+  const float* sp = W + kOffL0F + lane_off;  // weight stream cursors
+  const float* spc = HASC ? a.feat.fcw + kOffCF + lane_off : sp;
+  int buf = 0;
   stage(sp, lds, kChunkFloats);  // chunk 0 of layer 0 -> buffer 0
 
   float x0 = 0.f, x1 = 0.f, x2 = 0.f;
@@ -358,29 +369,33 @@ __global__ __launch_bounds__(256, 1) void k_mlp_fwd(FwdArgs a) {
   }
 
   f32x16 acc[8];
-  zero_acc<8>(acc);
-  layer<3, 8, 0, kStoresE>(lds, sp, kChunkFloats, kChunkFloats, act, acc, save);
-  bias_relu(acc, W + kOffB0, act);
-  if (a.do_save) {
-    save_mask(a.save.masks + mask_word0, act);
-    save_tiles<8, kHidden>(a.save.hP + col * kHidden, act);
-  }
-
-  // hidden layers 1..3 (pts_linears.1..3); each starts in buffer 1 (layer 0 used 3 chunks)
-  for (int L = 1; L <= 3; ++L) {
-    const int nxf = L < 3 ? kChunkFloats : kSmallChunkFloats;
-    zero_acc<8>(acc);
-    layer<8, 8, 1, kStoresH>(lds, sp, kChunkFloats, nxf, act, acc, a.do_save);
+  // epilogue of hidden layer L: ReLU (+ mask save), feature branch, activation save
+  auto finish = [&](int L) {
     bias_relu(acc, W + kOffB0 + (int64_t)L * kBiasFloats, act);
-    if (a.do_save) {
-      save_mask(a.save.masks + (int64_t)L * (a.save.ld / 32) * 64 + mask_word0, act);
-      save_tiles<8, kHidden>(a.save.hP + ((int64_t)L * a.save.ld + col) * kHidden, act);
+    if (save) save_mask(a.save.masks + (int64_t)L * (a.save.ld / 32) * 64 + mask_word0, act);
+    if (HASC) {  // h += fc_c[L](c): one chunk, K = 32 channels
+      float ct[8][16];
+      load_c_tile(a.feat.c, p, valid, ct);
+      zero_acc<8>(acc);
+      layer<1, 8, kStoresM>(lds, spc, kChunkFloats, sp, L < 3 ? kChunkFloats : kSmallChunkFloats, buf, ct, acc, save);
+      add_bias_acc(acc, a.feat.fcw + kOffCB + (int64_t)L * kBiasFloats, act);
     }
+    if (save) save_tiles<8, kHidden>(a.save.hP + ((int64_t)L * a.save.ld + col) * kHidden, act);
+  };
+  zero_acc<8>(acc);
+  layer<3, 8, kStoresE>(lds, sp, kChunkFloats, HASC ? spc : sp, kChunkFloats, buf, act, acc, save);
+  finish(0);
+  // hidden layers 1..3 (pts_linears.1..3)
+  for (int L = 1; L <= 3; ++L) {
+    const int nxf = HASC ? kChunkFloats : (L < 3 ? kChunkFloats : kSmallChunkFloats);
+    zero_acc<8>(acc);
+    layer<8, 8, kStoresH>(lds, sp, kChunkFloats, HASC ? spc : sp, nxf, buf, act, acc, save);
+    finish(L);
   }
 
   f32x16 out[1];
   zero_acc<1>(out);
-  layer<8, 1, 1, kStoresH>(lds, sp, kSmallChunkFloats, 0, act, out, a.do_save);
+  layer<8, 1, kStoresH>(lds, sp, kSmallChunkFloats, sp, 0, buf, act, out, save);
   // rows 0..3 of the output tile live in lanes 0..31, registers 0..3
   if (valid && hh == 0) {
     const float4 bo = *reinterpret_cast<const float4*>(W + kOffBO + lane * 4);
@@ -389,9 +404,20 @@ __global__ __launch_bounds__(256, 1) void k_mlp_fwd(FwdArgs a) {
   }
 }
 
+template <bool HASC>
+static void launch_fwd_mode(int mode, dim3 grid, dim3 block, hipStream_t st, const FwdArgs& a) {
+  switch (mode) {
+    case kPtsF64: hipLaunchKernelGGL((k_mlp_fwd<kPtsF64, HASC>), grid, block, 0, st, a); break;
+    case kPtsF32: hipLaunchKernelGGL((k_mlp_fwd<kPtsF32, HASC>), grid, block, 0, st, a); break;
+    case kRaysZ64: hipLaunchKernelGGL((k_mlp_fwd<kRaysZ64, HASC>), grid, block, 0, st, a); break;
+    default: hipLaunchKernelGGL((k_mlp_fwd<kRaysZ32, HASC>), grid, block, 0, st, a); break;
+  }
+}
+
 int launch_mlp_fwd(const float* packed, const PointSrc& src, int mode, int64_t P, float* raw,
-                   const SaveArgs* save, hipStream_t st) {
+                   const SaveArgs* save, hipStream_t st, const FeatArgs* feat) {
   if (P <= 0) return 0;
+  if (mode < kPtsF64 || mode > kRaysZ32) return PNR_E_ARG;
   FwdArgs a;
   a.packed = packed;
   a.src = src;
@@ -400,15 +426,11 @@ int launch_mlp_fwd(const float* packed, const PointSrc& src, int mode, int64_t P
   a.do_save = save != nullptr;
   if (save) a.save = *save;
   else a.save = SaveArgs{nullptr, nullptr, nullptr, nullptr, 0, 0};
+  a.feat = feat ? *feat : FeatArgs{nullptr, nullptr};
   const dim3 grid((unsigned)((P + 127) / 128)), block(256);
   TimingScope ts(kTimeMlpFwd, P, st);
-  switch (mode) {
-    case kPtsF64: hipLaunchKernelGGL(k_mlp_fwd<kPtsF64>, grid, block, 0, st, a); break;
-    case kPtsF32: hipLaunchKernelGGL(k_mlp_fwd<kPtsF32>, grid, block, 0, st, a); break;
-    case kRaysZ64: hipLaunchKernelGGL(k_mlp_fwd<kRaysZ64>, grid, block, 0, st, a); break;
-    case kRaysZ32: hipLaunchKernelGGL(k_mlp_fwd<kRaysZ32>, grid, block, 0, st, a); break;
-    default: return PNR_E_ARG;
-  }
+  if (a.feat.fcw) launch_fwd_mode<true>(mode, grid, block, st, a);
+  else launch_fwd_mode<false>(mode, grid, block, st, a);
   return hip_status(hipGetLastError());
 }
 
@@ -426,6 +448,26 @@ __device__ __forceinline__ void relu_grad(const f32x16 (&acc)[8], const uint4* _
     for (int r = 0; r < 16; ++r) act[t][r] = ((w[t >> 1] >> ((t & 1) * 16 + r)) & 1u) ? acc[t][r] : 0.f;
 }
 
+// act *= [h > 0] in place
+__device__ __forceinline__ void relu_mask(const uint4* __restrict__ words, float (&act)[8][16]) {
+  const uint4 m = words[threadIdx.x & 63];
+  const uint32_t w[4] = {m.x, m.y, m.z, m.w};
+#pragma unroll
+  for (int t = 0; t < 8; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) act[t][r] = ((w[t >> 1] >> ((t & 1) * 16 + r)) & 1u) ? act[t][r] : 0.f;
+}
+
+__device__ __forceinline__ void acc_to_act(const f32x16 (&acc)[8], float (&act)[8][16]) {
+#pragma unroll
+  for (int t = 0; t < 8; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) act[t][r] = acc[t][r];
+}
+
+// Weight streams: transposed images W3^T, W2^T, W1^T (8 chunks each), W0^T (8 chunks of 3072);
+// with features (HASC) the fc_c^T images CT3..CT0 (one chunk each) precede W3^T .. W0^T.
+template <bool HASC>
 __global__ __launch_bounds__(256, 1) void k_mlp_bwd(const float* __restrict__ W, BwdArgs a, int64_t P) {
   __shared__ __attribute__((aligned(16))) float lds[2 * kChunkFloats];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, hh = lane >> 5, j = lane & 31;
@@ -438,9 +480,13 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd(const float* __restrict__ W,
   // instruction at all, so the relaxed first-chunk wait is used only when some lane is valid
   const bool valid_any = __builtin_amdgcn_readfirstlane((int)((int64_t)blockIdx.x * 128 + wave_id() * 32 < P));
   const uint4* mk = a.masks + ((a.p0 + (int64_t)blockIdx.x * 128) / 32 + wave_id()) * 64;
+  const int lane_off = wave_id() * 256 + lane * 4;
 
-  const float* sp = W + kOffL3T + wave_id() * 256 + lane * 4;  // weight stream cursor
-  stage(sp, lds, kChunkFloats);  // W3^T chunk 0 -> buffer 0 (lands during the Wo^T step)
+  const float* sp = W + kOffL3T + lane_off;  // weight stream cursors
+  const float* spc = HASC ? a.fcw + kOffCT + lane_off : sp;
+  int buf = 0;
+  if (HASC) stage(spc, lds, kChunkFloats);  // CT3 -> buffer 0
+  else stage(sp, lds, kChunkFloats);        // W3^T chunk 0 -> buffer 0 (lands during the Wo^T step)
 
   // g_h4 = Wo^T g_out  (K = 4: k-steps r = 0..3, lane half 0 carries o = r)
   float g[4] = {0.f, 0.f, 0.f, 0.f};
@@ -461,25 +507,37 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd(const float* __restrict__ W,
       acc[t] = mfma(w4.w, g[3], acc[t]);
     }
   }
+  f32x16 gc[1];  // dL/dc = sum_l Wc_l^T dL/dh_l  (32 channels x 32 points)
+  zero_acc<1>(gc);
   float act[8][16];
-  relu_grad(acc, mk + 3 * mstride, act);   // delta4
-  if (valid) save_tiles<8, kHidden>(a.dP + (3 * a.ld_d + dcol) * kHidden, act);
+  // acc = dL/dh_l (hl = mask index) -> act = delta_l; with features, dL/dh_l also feeds Wc_l^T
+  // and is saved for dWc_l; `nxf` = size of the chunk after CT_l (the next W^T chunk)
+  auto to_delta = [&](int hl, int nxf) {
+    if (HASC) {
+      acc_to_act(acc, act);
+      chunk8<0>(lds, sp, nxf, buf, act, gc, false);
+      if (valid) save_tiles<8, kHidden>(a.gH + ((int64_t)hl * a.ld_d + dcol) * kHidden, act);
+      relu_mask(mk + hl * mstride, act);
+    } else {
+      relu_grad(acc, mk + hl * mstride, act);
+    }
+    if (valid) save_tiles<8, kHidden>(a.dP + ((int64_t)hl * a.ld_d + dcol) * kHidden, act);
+  };
+  to_delta(3, kChunkFloats);  // delta4
 
   // delta3 = W3^T delta4 * [h3>0]; delta2; delta1  (images L3T, L2T, L1T; 8 chunks each)
-  // chunk parity: L3T starts in buffer 0, 8 chunks -> every image starts in buffer 0
+  constexpr int NS = HASC ? kStoresDG : kStoresD;
   for (int s = 0; s < 3; ++s) {  // s=0: W3^T -> delta3 (uses h3), s=1: W2^T -> delta2, s=2: W1^T -> delta1
-    const int nxf = s < 2 ? kChunkFloats : (int)kL0TChunkFloats;
+    const int nxw = s < 2 ? kChunkFloats : (int)kL0TChunkFloats;  // next W^T chunk
     zero_acc<8>(acc);
-    layer<8, 8, 0, kStoresD>(lds, sp, kChunkFloats, nxf, act, acc, valid_any);
-    const int hl = 2 - s;  // h3 -> index 2, h2 -> 1, h1 -> 0
-    relu_grad(acc, mk + hl * mstride, act);
-    if (valid) save_tiles<8, kHidden>(a.dP + ((int64_t)hl * a.ld_d + dcol) * kHidden, act);
+    layer<8, 8, NS>(lds, sp, kChunkFloats, HASC ? spc : sp, HASC ? kChunkFloats : nxw, buf, act, acc, valid_any);
+    to_delta(2 - s, nxw);  // h3 -> index 2, h2 -> 1, h1 -> 0
   }
 
   // g_e = W0^T delta1 : 3 output tiles (96 rows, 93 valid)
   f32x16 ge[3];
   zero_acc<3>(ge);
-  layer<8, 3, 0, kStoresD>(lds, sp, (int)kL0TChunkFloats, 0, act, ge, valid_any);
+  layer<8, 3, NS>(lds, sp, (int)kL0TChunkFloats, sp, 0, buf, act, ge, valid_any);
 
   // g_arg = g_e * cos(x@B); g_x = B g_arg
   float x0 = 0.f, x1 = 0.f, x2 = 0.f;
@@ -505,6 +563,11 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd(const float* __restrict__ W,
       garg[t][r] = gv;
     }
   if (valid) save_tiles<3, kFourierPad>(a.gargP + dcol * kFourierPad, garg);
+  if (HASC && valid) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) garg[0][r] = gc[0][r];
+    save_tiles<1, kCDim>(a.g_c + dcol * kCDim, garg);
+  }
   if (a.g_x != nullptr) {
     s0 += __shfl_xor(s0, 32);
     s1 += __shfl_xor(s1, 32);
@@ -521,7 +584,44 @@ int launch_mlp_bwd(const float* packed, const BwdArgs& a, int64_t P, hipStream_t
   if (P <= 0) return 0;
   const dim3 grid((unsigned)((P + 127) / 128)), block(256);
   TimingScope ts(kTimeMlpBwd, P, st);
-  hipLaunchKernelGGL(k_mlp_bwd, grid, block, 0, st, packed, a, P);
+  if (a.fcw) hipLaunchKernelGGL(k_mlp_bwd<true>, grid, block, 0, st, packed, a, P);
+  else hipLaunchKernelGGL(k_mlp_bwd<false>, grid, block, 0, st, packed, a, P);
+  return hip_status(hipGetLastError());
+}
+
+// ---------------------------------------------------------------------------------------------
+// fc_c image (pnr_internal.h "fc_c image"): fc[2l] = fc_c.l.weight (256,32), fc[2l+1] = bias
+// ---------------------------------------------------------------------------------------------
+struct FcRaw {
+  const float* p[PNR_N_FC_PARAMS];
+};
+
+__global__ void k_fc_pack(FcRaw fc, float* __restrict__ out) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= kFcPackedFloats) return;
+  const int seg = (int)(idx / kChunkFloats);  // 0..3 CF_l, 4..7 CB_l, 8..11 CT (reversed)
+  const int i = (int)(idx % kChunkFloats);
+  const int blk = i / 1024, rem = i % 1024;   // blk = tile t (CF, CB) or k-chunk kc (CT)
+  const int rq = rem / 256, lane = (rem % 256) / 4, r = rq * 4 + rem % 4;
+  const int hh = lane >> 5, i32 = lane & 31;
+  float v;
+  if (seg < 4) {
+    v = fc.p[2 * seg][(32 * blk + i32) * kCDim + perm(r, hh)];
+  } else if (seg < 8) {
+    v = fc.p[2 * (seg - 4) + 1][32 * blk + perm(r, hh)];
+  } else {
+    const int l = 3 - (seg - 8);  // the backward visits l = 3, 2, 1, 0
+    v = fc.p[2 * l][(32 * blk + perm(r, hh)) * kCDim + i32];
+  }
+  out[idx] = v;
+}
+
+int launch_fc_pack(const float* const* fc, float* out, hipStream_t st) {
+  FcRaw r;
+  for (int i = 0; i < PNR_N_FC_PARAMS; ++i) r.p[i] = fc[i];
+  const int threads = 256;
+  hipLaunchKernelGGL(k_fc_pack, dim3((unsigned)((kFcPackedFloats + threads - 1) / threads)), dim3(threads), 0, st,
+                     r, out);
   return hip_status(hipGetLastError());
 }
 

@@ -52,6 +52,16 @@ constexpr int64_t kL0TChunkFloats = 3 * 4 * 64 * 4;              // 3 out tiles:
 constexpr int64_t kOffL0T = kOffL1T + 8 * kChunkFloats;          // W0^T: 8 chunks of 3072
 constexpr int64_t kPackedFloats = kOffL0T + 8 * kL0TChunkFloats;
 
+// ---- fc_c image (neural-point feature injection, decoder.py:122-125,196-197), separate buffer --
+// forward  CF_l: [t][rq][lane][4], 8 out tiles x one 32-channel input tile (one LDS chunk)
+// bias     CB_l: [t][rq][lane][4] (like the hidden bias images)
+// backward CT_l: [kc][rq][lane][4], Wc_l^T: one 32-channel out tile x 8 unit tiles (one LDS chunk)
+constexpr int kCDim = PNR_C_DIM;
+constexpr int64_t kOffCF = 0;
+constexpr int64_t kOffCB = 4 * kChunkFloats;
+constexpr int64_t kOffCT = 8 * kChunkFloats;
+constexpr int64_t kFcPackedFloats = 12 * kChunkFloats;
+
 __host__ __device__ inline int perm(int r, int hh) { return (r & 3) + 8 * (r >> 2) + 4 * hh; }
 
 // Device views of the 11 reference tensors (src/conv_onet/models/decoder.py state_dict order).
@@ -77,6 +87,49 @@ struct PointSrc {
   double bound[6];
 };
 
+// Point p of a launch as the float32 MLP input (x0,x1,x2) plus the bound test.  Reference:
+// pts = o + d * z in float64 (Renderer.py:177-179) or float32 (regulation, :296-298); strict
+// bound mask (Renderer.py:43-46) in the points' dtype; MLP input p.float() (decoder.py:189).
+template <int MODE>
+__device__ __forceinline__ void load_point(const PointSrc& s, int64_t p, float& x0, float& x1, float& x2,
+                                           bool& inside) {
+#pragma clang fp contract(off)
+  if (MODE == kPtsF64 || MODE == kRaysZ64) {
+    double q0, q1, q2;
+    if (MODE == kPtsF64) {
+      const double* pp = reinterpret_cast<const double*>(s.pts) + p * 3;
+      q0 = pp[0]; q1 = pp[1]; q2 = pp[2];
+    } else {
+      const int64_t ray = p / s.spr;
+      const double z = reinterpret_cast<const double*>(s.z)[p];
+      // torch: rays_o[...,None,:] + rays_d[...,None,:] * z[...,:,None], promoted to float64
+      q0 = (double)s.rays_o[ray * 3 + 0] + (double)s.rays_d[ray * 3 + 0] * z;
+      q1 = (double)s.rays_o[ray * 3 + 1] + (double)s.rays_d[ray * 3 + 1] * z;
+      q2 = (double)s.rays_o[ray * 3 + 2] + (double)s.rays_d[ray * 3 + 2] * z;
+    }
+    inside = true;
+    if (s.use_bound)
+      inside = (q0 < s.bound[1]) && (q0 > s.bound[0]) && (q1 < s.bound[3]) && (q1 > s.bound[2]) &&
+               (q2 < s.bound[5]) && (q2 > s.bound[4]);
+    x0 = (float)q0; x1 = (float)q1; x2 = (float)q2;
+  } else {
+    if (MODE == kPtsF32) {
+      const float* pp = reinterpret_cast<const float*>(s.pts) + p * 3;
+      x0 = pp[0]; x1 = pp[1]; x2 = pp[2];
+    } else {
+      const int64_t ray = p / s.spr;
+      const float z = reinterpret_cast<const float*>(s.z)[p];
+      x0 = s.rays_o[ray * 3 + 0] + s.rays_d[ray * 3 + 0] * z;
+      x1 = s.rays_o[ray * 3 + 1] + s.rays_d[ray * 3 + 1] * z;
+      x2 = s.rays_o[ray * 3 + 2] + s.rays_d[ray * 3 + 2] * z;
+    }
+    inside = true;
+    if (s.use_bound)  // a float32 tensor compared with a 0-dim float64 tensor compares in float32
+      inside = (x0 < (float)s.bound[1]) && (x0 > (float)s.bound[0]) && (x1 < (float)s.bound[3]) &&
+               (x1 > (float)s.bound[2]) && (x2 < (float)s.bound[5]) && (x2 > (float)s.bound[4]);
+  }
+}
+
 // Activation save area for training, POINT-major (row p = one point), ld = total points
 // (multiple of 128; padded points hold finite activations of x = 0 and get zero gradient).
 struct SaveArgs {
@@ -88,8 +141,13 @@ struct SaveArgs {
   int64_t p0;      // first point (row) of this launch (multiple of 128)
 };
 
+// Neural-point feature injection for the MLP kernels (nullptr fcw = reference decoder).
+struct FeatArgs {
+  const float* fcw;  // fc_c image (kFcPackedFloats)
+  const float* c;    // forward: (rows,32) features, row p of the launch = point p
+};
 int launch_mlp_fwd(const float* packed, const PointSrc& src, int mode, int64_t P, float* raw,
-                   const SaveArgs* save, hipStream_t st);
+                   const SaveArgs* save, hipStream_t st, const FeatArgs* feat = nullptr);
 
 struct BwdArgs {
   const float* g_out;  // (P,4) dL/draw, sigma channel already zeroed where masked
@@ -101,20 +159,52 @@ struct BwdArgs {
   int64_t ld;          // rows of the saved activations
   int64_t p0;          // first saved row handled by this launch
   int64_t ld_d;        // rows of the delta buffers (chunk size)
+  // feature injection (fcw != nullptr): dL/dh_l before the ReLU mask (for dWc_l = gH_l^T c) and
+  // dL/dc = sum_l Wc_l^T dL/dh_l
+  const float* fcw;
+  float* gH;           // [4][ld_d][256]
+  float* g_c;          // [C][32] chunk-local rows
 };
 int launch_mlp_bwd(const float* packed, const BwdArgs& a, int64_t P, hipStream_t st);
 
 int launch_pack(const RawParams& rp, float* packed, hipStream_t st);
+int launch_fc_pack(const float* const* fc, float* out, hipStream_t st);
+
+// ---- neural-point gather (points.hip) --------------------------------------------------------
+// index buffer layout (pnr_points_index_bytes): cell_start[T+1] | count[T] | bucket[M] | slot[M]
+// | scan partials | sorted float4[M] (x, y, z, original index bits)
+struct IndexView {
+  int32_t* start;
+  int32_t* count;
+  int32_t* bucket;
+  int32_t* slot;
+  int32_t* partial;
+  float4* sorted;
+  int64_t T;
+};
+IndexView index_view(void* base, int64_t M, int32_t bits, size_t* bytes);
+int launch_points_build(const pnr_points& pts, hipStream_t st);
+// c rows [0, rows): points [0, P) gathered, rows [P, rows) zeroed
+int launch_gather(const pnr_points& pts, const PointSrc& src, int mode, int64_t P, int64_t rows, float* c,
+                  int32_t* idx, float* w, hipStream_t st);
+// g_c (P,32) -> g_feats (+=), g_p (P,3): `gp_accum` adds into g_p instead of writing it;
+// positions come from xP (float4 rows, MLP inputs) when non-null, else from src
+int launch_gather_bwd(const pnr_points& pts, const PointSrc* src, int mode, const float4* xP, int64_t P,
+                      const int32_t* idx, const float* w, const float* c, const float* g_c, float* g_p,
+                      bool gp_accum, hipStream_t st);
 
 // weight-gradient GEMM shapes (wgrad.hip): C[MA][NB] += A[K][WA]^T B[K][WB]
-enum WgradKind : int { kWgradHidden = 0, kWgradFirst = 1, kWgradOut = 2, kWgradFourier = 3 };
+enum WgradKind : int { kWgradHidden = 0, kWgradFirst = 1, kWgradOut = 2, kWgradFourier = 3, kWgradFc = 4 };
 int launch_wgrad(int kind, const float* A, int ma, const float* B, int nb, int64_t K, float* C, int64_t ldc,
                  float* bias, hipStream_t st);
 
 inline int hip_status(hipError_t e) { return e == hipSuccess ? 0 : (int)e; }
 
 // Diagnostics: bracket a launch with hipEvents when pnr_timing_enable(1) (capi.cpp).
-enum TimedKernel : int { kTimeMlpFwd = 0, kTimeMlpBwd = 1, kTimeRay = 2, kTimeWgrad = 3, kTimeKinds = 4 };
+enum TimedKernel : int {
+  kTimeMlpFwd = 0, kTimeMlpBwd = 1, kTimeRay = 2, kTimeWgrad = 3, kTimeGather = 4, kTimeGatherBwd = 5,
+  kTimeKinds = 6
+};
 struct TimingScope {
   hipEvent_t a = nullptr, b = nullptr;
   hipStream_t st;

@@ -16,6 +16,7 @@
 //   dW0 = delta1^T e                                            MA = 256, NB = 96 (93 used)
 //   dWo = g_out^T h4                                            MA = 4,   NB = 256
 //   dB  = x^T g_arg                                             MA = 4 (3 used), NB = 96 (93 used)
+//   dWc_l = (dL/dh_l)^T c  (fc_c, neural-point features)        MA = 256, NB = 32
 #include "pnr_internal.h"
 
 namespace pnr {
@@ -178,6 +179,7 @@ int launch_wgrad(int kind, const float* A, int ma, const float* B, int nb, int64
     case kWgradFirst: hipLaunchKernelGGL((k_wgrad<8, 3, 256, 96>), grid, block, 0, st, a); break;
     case kWgradOut: hipLaunchKernelGGL((k_wgrad<1, 8, 4, 256>), grid, block, 0, st, a); break;
     case kWgradFourier: hipLaunchKernelGGL((k_wgrad<1, 3, 4, 96>), grid, block, 0, st, a); break;
+    case kWgradFc: hipLaunchKernelGGL((k_wgrad<8, 1, 256, 32>), grid, block, 0, st, a); break;
     default: return PNR_E_ARG;
   }
   return hip_status(hipGetLastError());

@@ -5,11 +5,12 @@ src/config.py) over the C ABI of libpnr.so (include/pnr.h).  See DESIGN.md.
 """
 from . import _lib
 from .config import load_config, get_model, ROOM0_CFG
-from .decoder import MLP, PARAM_ORDER
+from .decoder import MLP, PARAM_ORDER, FC_ORDER
+from .points import NeuralPoints
 from .renderer import Renderer, get_rays, get_rays_from_uv
 from .common import scaled_bound, get_camera_from_tensor, get_tensor_from_camera, quad2rotation
 
-__all__ = ['Renderer', 'MLP', 'PARAM_ORDER', 'get_model', 'load_config', 'ROOM0_CFG', 'get_rays',
+__all__ = ['Renderer', 'MLP', 'PARAM_ORDER', 'FC_ORDER', 'NeuralPoints', 'get_model', 'load_config', 'ROOM0_CFG', 'get_rays',
            'get_rays_from_uv', 'scaled_bound', 'get_camera_from_tensor', 'get_tensor_from_camera',
            'quad2rotation']
 

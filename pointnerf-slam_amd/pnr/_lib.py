@@ -15,12 +15,26 @@ import torch
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'libpnr.so')
 MAX_SAMPLES = 64
 N_PARAMS = 11
+N_FC_PARAMS = 8
+C_DIM = 32
+MAX_K = 8
+GATHER_IDW, GATHER_TRILINEAR = 0, 1
 
 c_void_p = ctypes.c_void_p
 c_int64 = ctypes.c_int64
 c_int32 = ctypes.c_int32
 c_size_t = ctypes.c_size_t
 c_float = ctypes.c_float
+
+
+class Points(ctypes.Structure):
+    """Mirror of `pnr_points` (include/pnr.h)."""
+    _fields_ = [
+        ('xyz', c_void_p), ('feats', c_void_p), ('n_points', c_int64), ('mode', c_int32), ('k', c_int32),
+        ('radius', c_float), ('eps', c_float), ('spacing', c_float * 3), ('cell', c_float),
+        ('origin', c_float * 3), ('table_bits', c_int32), ('index', c_void_p), ('fc_packed', c_void_p),
+        ('g_feats', c_void_p), ('g_fc', c_void_p),
+    ]
 
 
 class RenderParams(ctypes.Structure):
@@ -30,10 +44,13 @@ class RenderParams(ctypes.Structure):
         ('bound', ctypes.c_double * 6), ('far_clamp', ctypes.c_double),
         ('t_vals', c_float * MAX_SAMPLES), ('u_vals', c_float * MAX_SAMPLES),
         ('save_for_backward', c_int32), ('need_ray_grads', c_int32),
+        ('points', ctypes.POINTER(Points)),
     ]
 
 
 PtrArray = c_void_p * N_PARAMS
+FcPtrArray = c_void_p * N_FC_PARAMS
+PPoints = ctypes.POINTER(Points)
 
 # name -> (restype, argtypes)
 _SIGS = {
@@ -68,6 +85,20 @@ _SIGS = {
                                         c_void_p, c_void_p, c_void_p]),
     'pnr_adam_step': (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_float, c_float, c_float,
                                      c_float, c_int64, c_void_p]),
+    'pnr_points_index_bytes': (c_size_t, [c_int64, c_int32]),
+    'pnr_points_build': (ctypes.c_int, [PPoints, c_void_p]),
+    'pnr_point_gather': (ctypes.c_int, [PPoints, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p]),
+    'pnr_point_gather_bwd': (ctypes.c_int, [PPoints, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p,
+                                            c_void_p, c_void_p]),
+    'pnr_fc_packed_floats': (c_size_t, []),
+    'pnr_fc_pack': (ctypes.c_int, [FcPtrArray, c_void_p, c_void_p]),
+    'pnr_eval_points_c': (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p,
+                                         c_void_p]),
+    'pnr_mlp_fwd_train_c': (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p,
+                                           c_size_t, c_void_p]),
+    'pnr_mlp_bwd_workspace_bytes_c': (c_size_t, [c_int64]),
+    'pnr_mlp_bwd_c': (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p, PtrArray, FcPtrArray,
+                                     c_void_p, c_void_p, c_void_p, c_size_t, c_void_p, c_size_t, c_void_p]),
     'pnr_timing_enable': (ctypes.c_int, [ctypes.c_int]),
     'pnr_timing_read': (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(c_int64), ctypes.POINTER(ctypes.c_double),
                                        ctypes.POINTER(c_int64)]),
@@ -105,7 +136,7 @@ def load(path: str = LIB_PATH):
 
 def check(rc: int, what: str):
     if rc != 0:
-        kind = {-1: 'bad argument', -2: 'workspace too small', -3: 'rocBLAS failure'}.get(rc, f'hipError {rc}')
+        kind = {-1: 'bad argument', -2: 'workspace too small'}.get(rc, f'hipError {rc}')
         raise RuntimeError(f'pnr: {what} failed ({kind})')
 
 

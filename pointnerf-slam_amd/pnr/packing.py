@@ -12,6 +12,11 @@ from . import _lib
 
 
 class PackedMLP:
+    """Image of the 11 reference tensors (pnr_mlp_pack)."""
+    _floats = 'pnr_mlp_packed_floats'
+    _pack = 'pnr_mlp_pack'
+    _arr = 'PtrArray'
+
     def __init__(self):
         self._key = None
         self._img = None
@@ -28,10 +33,17 @@ class PackedMLP:
         lib = _lib.load()
         dev = params[0].device
         if self._img is None or self._img.device != dev:
-            self._img = torch.empty(lib.pnr_mlp_packed_floats(), device=dev, dtype=torch.float32)
+            self._img = torch.empty(getattr(lib, self._floats)(), device=dev, dtype=torch.float32)
         srcs = [t.detach().float().contiguous() for t in params]
-        arr = _lib.PtrArray(*[t.data_ptr() for t in srcs])
-        _lib.check(lib.pnr_mlp_pack(arr, _lib.ptr(self._img), _lib.stream_of(dev)), 'mlp_pack')
+        arr = getattr(_lib, self._arr)(*[t.data_ptr() for t in srcs])
+        _lib.check(getattr(lib, self._pack)(arr, _lib.ptr(self._img), _lib.stream_of(dev)), self._pack)
         self._srcs = srcs  # keep converted copies alive until the pack kernel ran
         self._key = key
         return self._img
+
+
+class PackedFC(PackedMLP):
+    """Image of the 8 fc_c tensors of MLP(c_dim=32) (pnr_fc_pack)."""
+    _floats = 'pnr_fc_packed_floats'
+    _pack = 'pnr_fc_pack'
+    _arr = 'FcPtrArray'

@@ -14,10 +14,13 @@ restatement in oracle/ is test infrastructure only).
 """
 from __future__ import annotations
 
+import ctypes
+
 import torch
 
 from . import _lib
-from .packing import PackedMLP
+from .packing import PackedFC, PackedMLP
+from .points import find_points
 
 _GRAD_SHAPES = ((3, 93), (256, 93), (256,), (256, 256), (256,), (256, 256), (256,), (256, 256), (256,), (4, 256),
                 (4,))
@@ -40,28 +43,63 @@ def _decoder_params(decoders):
     return [sd[k] for k in PARAM_ORDER]
 
 
-def _packer(decoders):
-    pk = getattr(decoders, '_packed', None)
+def _packer(decoders, attr='_packed', cls=PackedMLP):
+    pk = getattr(decoders, attr, None)
     if pk is None:
-        pk = PackedMLP()
+        pk = cls()
         try:
-            decoders._packed = pk
+            setattr(decoders, attr, pk)
         except AttributeError:
             pass
     return pk
 
 
+def _feature_inputs(c, decoders):
+    """(NeuralPoints or None, fc packer, extra autograd tensors [8 fc_c tensors, feats])."""
+    pts = find_points(c, decoders)
+    if pts is None:
+        return None, None, []
+    return pts, _packer(decoders, '_packed_fc', PackedFC), [*decoders.ordered_fc_params(), pts.feats]
+
+
+class _Feat:
+    """Per-call neural-point plumbing shared by the render / regulation Functions."""
+
+    def __init__(self, pts, fc_owner, tensors):
+        self.pts = pts
+        self.fc_owner = fc_owner
+        self.params = tensors[:_lib.N_PARAMS]
+        self.fc = tensors[_lib.N_PARAMS:_lib.N_PARAMS + _lib.N_FC_PARAMS] if pts is not None else ()
+        self.keep = []
+
+    def attach(self, prm, g_feats=None, g_fc=None):
+        if self.pts is None:
+            return
+        s, keep = self.pts.descriptor(self.fc_owner.image(self.fc), g_feats, g_fc)
+        self.keep = [s, keep]
+        prm.points = ctypes.pointer(s)
+
+    def grads(self, dev, needs):
+        """Zeroed fc_c / feature grad buffers (or Nones) matching the extra autograd inputs."""
+        if self.pts is None:
+            return None, None, []
+        g_fc = [torch.zeros(t.shape, device=dev, dtype=torch.float32) for t in self.fc]
+        g_feats = torch.zeros_like(self.pts.feats)
+        return g_feats, g_fc, [*g_fc, g_feats]
+
+
 class _RenderFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, prm_bytes, packer, rays_o, rays_d, gt_depth, far_clamp, *params):
+    def forward(ctx, prm_bytes, packer, feat, rays_o, rays_d, gt_depth, far_clamp, *tensors):
         lib = _lib.load()
         prm = _lib.RenderParams.from_buffer_copy(prm_bytes)
         n = rays_o.shape[0]
         dev = rays_o.device
-        packed = packer.image(params)
+        packed = packer.image(feat.params)
+        feat.attach(prm)
         need = any(ctx.needs_input_grad)  # (inside forward grad mode is off; ask autograd)
         prm.save_for_backward = 1 if need else 0
-        prm.need_ray_grads = 1 if (ctx.needs_input_grad[2] or ctx.needs_input_grad[3]) else 0
+        prm.need_ray_grads = 1 if (ctx.needs_input_grad[3] or ctx.needs_input_grad[4]) else 0
         if far_clamp is not None:
             prm.far_mode = 1
             prm.far_clamp = float(far_clamp)
@@ -73,7 +111,9 @@ class _RenderFn(torch.autograd.Function):
                                       _lib.ptr(gt_depth), n, _lib.ptr(depth), _lib.ptr(var), _lib.ptr(rgb),
                                       _lib.ptr(ws), ws.numel(), _lib.stream_of(dev)), 'render_fwd')
         if need:
+            prm.points = None
             ctx.prm = bytes(prm)
+            ctx.feat = feat
             ctx.save_for_backward(ws, packed, rays_o, rays_d)
         return depth, var, rgb
 
@@ -85,6 +125,8 @@ class _RenderFn(torch.autograd.Function):
         n = rays_o.shape[0]
         dev = rays_o.device
         grads = [torch.zeros(s, device=dev, dtype=torch.float32) for s in _GRAD_SHAPES]
+        g_feats, g_fc, extra = ctx.feat.grads(dev, ctx.needs_input_grad)
+        ctx.feat.attach(prm, g_feats, g_fc)
         g_o = g_d = None
         if prm.need_ray_grads:
             g_o = torch.empty((n, 3), device=dev, dtype=torch.float32)
@@ -98,27 +140,30 @@ class _RenderFn(torch.autograd.Function):
                                       n, _lib.ptr(gd), _lib.ptr(gv), _lib.ptr(gc), arr, _lib.ptr(g_o),
                                       _lib.ptr(g_d), _lib.ptr(ws), ws.numel(), _lib.ptr(bws), bws.numel(),
                                       _lib.stream_of(dev)), 'render_bwd')
-        return (None, None, g_o, g_d, None, None, *grads)
+        return (None, None, None, g_o, g_d, None, None, *grads, *extra)
 
 
 class _RegulationFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, prm_bytes, packer, rays_o, rays_d, gt_depth, t_rand, *params):
+    def forward(ctx, prm_bytes, packer, feat, rays_o, rays_d, gt_depth, t_rand, *tensors):
         lib = _lib.load()
         prm = _lib.RenderParams.from_buffer_copy(prm_bytes)
         n = rays_o.shape[0]
         dev = rays_o.device
-        packed = packer.image(params)
+        packed = packer.image(feat.params)
+        feat.attach(prm)
         need = any(ctx.needs_input_grad)  # (inside forward grad mode is off; ask autograd)
         prm.save_for_backward = 1 if need else 0
-        prm.need_ray_grads = 1 if (ctx.needs_input_grad[2] or ctx.needs_input_grad[3]) else 0
+        prm.need_ray_grads = 1 if (ctx.needs_input_grad[3] or ctx.needs_input_grad[4]) else 0
         ws = torch.empty(lib.pnr_regulation_workspace_bytes(ctypes_ref(prm), n), dtype=torch.uint8, device=dev)
         sigma = torch.empty(n * prm.n_samples, dtype=torch.float32, device=dev)
         _lib.check(lib.pnr_regulation_fwd(ctypes_ref(prm), _lib.ptr(packed), _lib.ptr(rays_o), _lib.ptr(rays_d),
                                           _lib.ptr(gt_depth), _lib.ptr(t_rand), n, _lib.ptr(sigma), _lib.ptr(ws),
                                           ws.numel(), _lib.stream_of(dev)), 'regulation_fwd')
         if need:
+            prm.points = None
             ctx.prm = bytes(prm)
+            ctx.feat = feat
             ctx.save_for_backward(ws, packed, rays_o, rays_d)
         return sigma
 
@@ -130,6 +175,8 @@ class _RegulationFn(torch.autograd.Function):
         n = rays_o.shape[0]
         dev = rays_o.device
         grads = [torch.zeros(s, device=dev, dtype=torch.float32) for s in _GRAD_SHAPES]
+        g_feats, g_fc, extra = ctx.feat.grads(dev, ctx.needs_input_grad)
+        ctx.feat.attach(prm, g_feats, g_fc)
         g_o = g_d = None
         if prm.need_ray_grads:
             g_o = torch.empty((n, 3), device=dev, dtype=torch.float32)
@@ -140,11 +187,10 @@ class _RegulationFn(torch.autograd.Function):
                                           _lib.ptr(rays_d), n, _lib.ptr(g_sigma.contiguous()), arr, _lib.ptr(g_o),
                                           _lib.ptr(g_d), _lib.ptr(ws), ws.numel(), _lib.ptr(bws), bws.numel(),
                                           _lib.stream_of(dev)), 'regulation_bwd')
-        return (None, None, g_o, g_d, None, None, *grads)
+        return (None, None, None, g_o, g_d, None, None, *grads, *extra)
 
 
 def ctypes_ref(prm):
-    import ctypes
     return ctypes.byref(prm)
 
 
@@ -198,8 +244,16 @@ class Renderer(object):
         packed = _packer(decoders).image(_decoder_params(decoders))
         P = p.shape[0]
         raw = torch.empty((P, 4), dtype=torch.float32, device=p.device)
-        import ctypes
         bound = (ctypes.c_double * 6)(*self._bound6())
+        pts, fc_owner, _ = _feature_inputs(c, decoders)
+        if pts is not None:  # features: gather, then the MLP with fc_c injection (no autograd here)
+            with torch.no_grad():
+                dp = p.double().contiguous()
+                cf = pts.gather(dp)
+                fcp = fc_owner.image(decoders.ordered_fc_params())
+                _lib.check(lib.pnr_eval_points_c(_lib.ptr(packed), _lib.ptr(fcp), _lib.ptr(dp), _lib.ptr(cf), P, bound,
+                                                 _lib.ptr(raw), _lib.stream_of(p.device)), 'eval_points_c')
+            return raw
         if p.dtype == torch.float64:
             fn = lib.pnr_eval_points
         else:
@@ -220,7 +274,9 @@ class Renderer(object):
         gt = None if gt_depth is None else gt_depth.reshape(-1).float().contiguous()
         prm = self.params()
         params = _decoder_params(decoders)
-        return _RenderFn.apply(bytes(prm), _packer(decoders), rays_o, rays_d, gt, far_clamp, *params)
+        pts, fc_owner, extra = _feature_inputs(c, decoders)
+        feat = _Feat(pts, fc_owner, [*params, *extra])
+        return _RenderFn.apply(bytes(prm), _packer(decoders), feat, rays_o, rays_d, gt, far_clamp, *params, *extra)
 
     def render_img(self, c, decoders, c2w, device, stage, gt_depth=None):
         """Renderer.py:205-260: full frame in ray_batch_size chunks, float64 depth/uncertainty."""
@@ -251,7 +307,9 @@ class Renderer(object):
         t_rand = t_rand.float().contiguous()
         prm = self.params(n_importance=0)
         params = _decoder_params(decoders)
-        return _RegulationFn.apply(bytes(prm), _packer(decoders), rays_o, rays_d, gt, t_rand, *params)
+        pts, fc_owner, extra = _feature_inputs(c, decoders)
+        feat = _Feat(pts, fc_owner, [*params, *extra])
+        return _RegulationFn.apply(bytes(prm), _packer(decoders), feat, rays_o, rays_d, gt, t_rand, *params, *extra)
 
 
 def get_rays(H, W, fx, fy, cx, cy, c2w, device):

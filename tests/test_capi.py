@@ -43,7 +43,7 @@ def test_python_binding_covers_header():
 
 def test_host_only_calls(lib):
     lib.pnr_abi_version.restype = ctypes.c_int
-    assert lib.pnr_abi_version() == 1
+    assert lib.pnr_abi_version() == 2
     lib.pnr_mlp_packed_floats.restype = ctypes.c_size_t
     assert lib.pnr_mlp_packed_floats() == 486688
     lib.pnr_build_info.restype = ctypes.c_char_p
@@ -54,9 +54,14 @@ def test_params_struct_layout():
     import sys
     sys.path.insert(0, os.path.join(REPO, 'pointnerf-slam_amd'))
     from pnr import _lib
-    # int32 x4, double[6], double, float[64] x2, int32 x2 -> 592 bytes with natural alignment
-    assert ctypes.sizeof(_lib.RenderParams) == 592
+    # int32 x4, double[6], double, float[64] x2, int32 x2, pointer -> 600 bytes with natural alignment
+    assert ctypes.sizeof(_lib.RenderParams) == 600
     assert _lib.RenderParams.bound.offset == 16 and _lib.RenderParams.t_vals.offset == 72
+    assert _lib.RenderParams.points.offset == 592
+    # pnr_points: 2 ptr, int64, 2 int32, 2 float, float[3], float, float[3], int32, 4 ptr
+    assert _lib.Points.n_points.offset == 16 and _lib.Points.spacing.offset == 40
+    assert _lib.Points.table_bits.offset == 68 and _lib.Points.index.offset == 72
+    assert ctypes.sizeof(_lib.Points) == 104
 
 
 def test_workspace_queries_and_arg_errors(lib):
@@ -80,3 +85,19 @@ def test_workspace_queries_and_arg_errors(lib):
     assert L.pnr_adam_step(None, None, None, None, 5, 1e-3, 0.9, 0.999, 1e-8, 0, None) == -1
     # zero-sized calls are no-ops
     assert L.pnr_eval_points(ctypes.c_void_p(1), None, 0, None, None, None) == 0
+
+
+def test_point_queries_and_arg_errors(lib):
+    import sys
+    sys.path.insert(0, os.path.join(REPO, 'pointnerf-slam_amd'))
+    from pnr import _lib
+    L = _lib.load()
+    assert L.pnr_fc_packed_floats() == 12 * 8192
+    b20 = L.pnr_points_index_bytes(100000, 20)
+    assert b20 >= (2 * (1 << 20) + 2 * 100000) * 4 + 100000 * 16
+    assert L.pnr_points_index_bytes(100000, 9) == 0 and L.pnr_points_index_bytes(-1, 12) == 0
+    pts = _lib.Points()
+    pts.k, pts.table_bits, pts.cell = 9, 12, 0.1           # k > PNR_MAX_K
+    assert L.pnr_point_gather(ctypes.byref(pts), None, 0, None, None, None, None) == -1
+    assert L.pnr_points_build(None, None) == -1
+    assert L.pnr_eval_points_c(None, None, None, None, 3, None, None, None) == -1

@@ -1,0 +1,226 @@
+"""Parity of the neural-point stage on the GPU: spatial-hash gather,
+decoder with fc_c feature injection, and render_batch_ray / regulation with features, against
+the CPU oracle (oracle/ref_points.py) and the reference's grid_sample decoder fixtures
+(tests/golden/points_c32.npz).
+
+Tolerances: gather idx exact; c / weights 1e-5 * max; raw 2e-5 * max; depth / colour 1e-4 rel
+(north_star); grads 2e-3 * max per tensor (float32 sums in a different order).
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import load_golden, golden_params
+from oracle import ref_points as RP
+from oracle import ref_render as RR
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope='module')
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip('no GPU')
+    return torch.device('cuda:0')
+
+
+@pytest.fixture(scope='module')
+def pnr_mod():
+    import pnr
+    pnr.library()
+    return pnr
+
+
+def close(a, b, atol, what, rtol=0.0):
+    a = a.detach().cpu().numpy() if isinstance(a, torch.Tensor) else np.asarray(a)
+    b = b.detach().cpu().numpy() if isinstance(b, torch.Tensor) else np.asarray(b)
+    np.testing.assert_allclose(a, b, rtol=rtol, atol=atol, err_msg=what)
+
+
+def grid_setup(pnr, dev):
+    g = load_golden('points_c32.npz')
+    bound = torch.from_numpy(g['bound'])
+    pts = pnr.NeuralPoints.from_grid(torch.from_numpy(g['grid']).to(dev), bound).to(dev)
+    dec = pnr.MLP(name='color', dim=3, c_dim=32, color=True, skips=[], n_blocks=4, hidden_size=256)
+    dec.load_state_dict({k[2:]: torch.from_numpy(g[k]) for k in g if k.startswith('w/')})
+    return g, pts, dec.to(dev)
+
+
+def random_cloud(n=3000, seed=3):
+    gen = torch.Generator().manual_seed(seed)
+    lo = torch.tensor([-0.29, -0.32, -0.35])
+    hi = torch.tensor([0.99, 0.64, 0.61])
+    xyz = lo + (hi - lo) * torch.rand((n, 3), generator=gen)
+    feats = torch.randn((n, 32), generator=gen) * 0.5
+    q = xyz[torch.randint(0, n, (4096,), generator=gen)] + 0.03 * torch.randn((4096, 3), generator=gen)
+    return xyz, feats, q.double()
+
+
+def test_gather_trilinear_equals_grid_sample(pnr_mod, dev):
+    g, pts, _ = grid_setup(pnr_mod, dev)
+    c = pts.gather(torch.from_numpy(g['p']).to(dev))
+    close(c, g['c'], 1e-5 * np.abs(g['c']).max(), 'c vs F.grid_sample')
+
+
+@pytest.mark.parametrize('k', [8, 3])
+def test_gather_idw_matches_oracle(pnr_mod, dev, k):
+    import ctypes
+    lib = pnr_mod.library()
+    xyz, feats, q = random_cloud()
+    pts = pnr_mod.NeuralPoints(xyz.to(dev), feats.to(dev), mode='idw', radius=0.06, k=k).to(dev)
+    P = q.shape[0]
+    c = torch.empty((P, 32), device=dev)
+    idx = torch.empty((P, k), device=dev, dtype=torch.int32)
+    w = torch.empty((P, k), device=dev)
+    qd = q.to(dev)
+    s, _ = pts.descriptor()
+    assert lib.pnr_point_gather(ctypes.byref(s), qd.data_ptr(), P, c.data_ptr(), idx.data_ptr(), w.data_ptr(),
+                                None) == 0
+    torch.cuda.synchronize()
+    c_ref, idx_ref, w_ref = RP.point_gather(q, xyz, feats, 'idw', radius=0.06, k=k, return_idx=True)
+    assert (idx_ref >= 0).sum() > P, 'test cloud must give neighbours'
+    assert (idx_ref < 0).any(), 'and some samples without a full neighbourhood'
+    assert np.array_equal(idx.cpu().numpy(), idx_ref.numpy().astype(np.int32))
+    close(w, w_ref, 1e-6, 'weights')
+    close(c, c_ref, 1e-5 * c_ref.abs().max().item(), 'c')
+
+
+def test_gather_backward_matches_oracle(pnr_mod, dev):
+    xyz, feats, q = random_cloud(seed=5)
+    pts = pnr_mod.NeuralPoints(xyz.to(dev), feats.to(dev), mode='idw', radius=0.06, k=8).to(dev)
+    gen = torch.Generator().manual_seed(9)
+    gc = torch.randn((q.shape[0], 32), generator=gen)
+    qd = q.to(dev).requires_grad_(True)
+    c = pts.gather(qd)
+    (c * gc.to(dev)).sum().backward()
+    fr = feats.clone().requires_grad_(True)
+    qr = q.clone().requires_grad_(True)
+    (RP.point_gather(qr, xyz, fr, 'idw', radius=0.06, k=8) * gc).sum().backward()
+    close(pts.feats.grad, fr.grad, 2e-5 * fr.grad.abs().max().item(), 'dL/dfeats')
+    close(qd.grad, qr.grad, 2e-3 * qr.grad.abs().max().item(), 'dL/dp')
+
+
+def test_decoder_c32_matches_reference(pnr_mod, dev):
+    """pnr.MLP(c_dim=32) on lattice points == the reference MLP(c_dim=32) with F.grid_sample."""
+    g, pts, dec = grid_setup(pnr_mod, dev)
+    p = torch.from_numpy(g['p']).to(dev).requires_grad_(True)
+    raw = dec(p, c_grid={'points_color': pts})
+    close(raw, g['raw'], 2e-5 * np.abs(g['raw']).max(), 'raw')
+    (raw * torch.from_numpy(g['g_raw']).to(dev)).sum().backward()
+    for k, t in dec.named_parameters():
+        ref = g['grad/' + k]
+        close(t.grad, ref, 2e-3 * max(np.abs(ref).max(), 1e-12), k)
+    ref = RP.grid_features(torch.from_numpy(g['grad_grid'])).numpy()
+    close(pts.feats.grad, ref, 2e-3 * np.abs(ref).max(), 'dL/dgrid')
+    close(p.grad, g['grad_p'], 2e-3 * np.abs(g['grad_p']).max(), 'dL/dp')
+
+
+def surface_cloud(dev, seed=4):
+    """Neural points scattered around the golden pose-1000 surface (gt = rendered depth)."""
+    r = load_golden('render.npz')
+    ro = torch.from_numpy(r['p2_gt/rays_o'])
+    rd = torch.from_numpy(r['p2_gt/rays_d'])
+    gt = torch.from_numpy(r['p2_gt/gt_depth'])
+    gen = torch.Generator().manual_seed(seed)
+    surf = ro + rd * gt[:, None]
+    xyz = (surf.repeat(4, 1) + 0.01 * torch.randn((4 * surf.shape[0], 3), generator=gen)).float()
+    feats = torch.randn((xyz.shape[0], 32), generator=gen) * 0.5
+    return ro, rd, gt, xyz, feats
+
+
+def make_renderer(pnr, scene_bound):
+    import types
+    slam = types.SimpleNamespace(bound=scene_bound, H=680, W=1200, fx=600., fy=600., cx=599.5, cy=339.5)
+    return pnr.Renderer(pnr.ROOM0_CFG, None, slam)
+
+
+@pytest.mark.parametrize('mode', ['idw', 'trilinear'])
+def test_render_with_points_matches_oracle(pnr_mod, dev, mode):
+    scene = load_golden('scene.npz')
+    bound = torch.from_numpy(scene['bound'])
+    ro, rd, gt, xyz, feats = surface_cloud(dev)
+    n = 256
+    ro, rd, gt = ro[:n], rd[:n], gt[:n]
+    base = golden_params('trained')
+    params = RP.init_fc_c(base, seed=1)
+    kw = dict(mode=mode, k=8, radius=0.04, eps=1e-6, spacing=[0.03, 0.03, 0.03])
+    pts = pnr_mod.NeuralPoints(xyz.to(dev), feats.to(dev), **kw).to(dev)
+    dec = pnr_mod.MLP(name='color', dim=3, c_dim=32, color=True, skips=[], n_blocks=4, hidden_size=256)
+    dec.load_state_dict({k: v.clone() for k, v in params.items()})
+    dec = dec.to(dev)
+    r = make_renderer(pnr_mod, bound)
+    c = {'points_color': pts}
+    d, v, col = r.render_batch_ray(c, dec, rd.to(dev), ro.to(dev), dev, 'color', gt_depth=gt.to(dev))
+    gc_ = torch.randn_like(col)
+    loss = (d - gt.to(dev).double()).abs().sum() + 0.05 * (col * gc_).sum() + 1e-3 * v.sum()
+    loss.backward()
+
+    ref_p = {k: t.clone().requires_grad_(True) for k, t in params.items()}
+    fr = feats.clone().requires_grad_(True)
+    pdict = dict(xyz=xyz, feats=fr, mode=mode, radius=0.04, spacing=[0.03] * 3, k=8, eps=1e-6)
+    ev = lambda q: RP.eval_points_c(ref_p, q, bound, pdict)  # noqa: E731
+    dr, vr, cr = RR.render_batch_ray(ref_p, rd, ro, bound, gt_depth=gt, eval_fn=ev)
+    lr = (dr - gt.double()).abs().sum() + 0.05 * (cr * gc_.cpu()).sum() + 1e-3 * vr.sum()
+    lr.backward()
+    close(d, dr, 0, 'depth', rtol=1e-4)
+    close(col, cr, 2e-5, 'rgb', rtol=1e-4)
+    close(v, vr, 1e-8, 'var', rtol=2e-3)
+    for k, t in dec.named_parameters():
+        ref = ref_p[k].grad
+        close(t.grad, ref, 2e-3 * max(ref.abs().max().item(), 1e-12), k)
+    close(pts.feats.grad, fr.grad, 2e-3 * fr.grad.abs().max().item(), 'dL/dfeats')
+
+
+def test_tracking_ray_grads_with_points(pnr_mod, dev):
+    scene = load_golden('scene.npz')
+    bound = torch.from_numpy(scene['bound'])
+    ro, rd, gt, xyz, feats = surface_cloud(dev, seed=6)
+    n = 128
+    ro, rd, gt = ro[:n], rd[:n], gt[:n]
+    params = RP.init_fc_c(golden_params('trained'), seed=2)
+    pts = pnr_mod.NeuralPoints(xyz.to(dev), feats.to(dev), mode='idw', radius=0.04, k=8).to(dev)
+    dec = pnr_mod.MLP(name='color', dim=3, c_dim=32, color=True, skips=[], n_blocks=4, hidden_size=256)
+    dec.load_state_dict({k: v.clone() for k, v in params.items()})
+    dec = dec.to(dev).requires_grad_(False)
+    pts.feats.requires_grad_(False)
+    r = make_renderer(pnr_mod, bound)
+    rod = ro.to(dev).requires_grad_(True)
+    rdd = rd.to(dev).requires_grad_(True)
+    d, v, col = r.render_batch_ray({'points_color': pts}, dec, rdd, rod, dev, 'color', gt_depth=gt.to(dev))
+    ((d - gt.to(dev).double()).abs() / torch.sqrt(v.detach() + 1e-10)).sum().backward()
+    ror = ro.clone().requires_grad_(True)
+    rdr = rd.clone().requires_grad_(True)
+    pdict = dict(xyz=xyz, feats=feats, mode='idw', radius=0.04, k=8, eps=1e-6)
+    ev = lambda q: RP.eval_points_c(params, q, bound, pdict)  # noqa: E731
+    dr, vr, _ = RR.render_batch_ray(params, rdr, ror, bound, gt_depth=gt, eval_fn=ev)
+    ((dr - gt.double()).abs() / torch.sqrt(vr.detach() + 1e-10)).sum().backward()
+    close(rod.grad, ror.grad, 2e-3 * ror.grad.abs().max().item(), 'dL/drays_o')
+    close(rdd.grad, rdr.grad, 2e-3 * rdr.grad.abs().max().item(), 'dL/drays_d')
+
+
+def test_regulation_with_points(pnr_mod, dev):
+    scene = load_golden('scene.npz')
+    bound = torch.from_numpy(scene['bound'])
+    ro, rd, gt, xyz, feats = surface_cloud(dev, seed=8)
+    n = 128
+    ro, rd, gt = ro[:n], rd[:n], gt[:n]
+    params = RP.init_fc_c(golden_params('trained'), seed=3)
+    pts = pnr_mod.NeuralPoints(xyz.to(dev), feats.to(dev), mode='idw', radius=0.05, k=8).to(dev)
+    dec = pnr_mod.MLP(name='color', dim=3, c_dim=32, color=True, skips=[], n_blocks=4, hidden_size=256)
+    dec.load_state_dict({k: v.clone() for k, v in params.items()})
+    dec = dec.to(dev)
+    t_rand = torch.rand((n, 32), generator=torch.Generator().manual_seed(1))
+    r = make_renderer(pnr_mod, bound)
+    s = r.regulation({'points_color': pts}, dec, rd.to(dev), ro.to(dev), gt.to(dev), dev, t_rand=t_rand.to(dev))
+    s.abs().sum().backward()
+    ref_p = {k: t.clone().requires_grad_(True) for k, t in params.items()}
+    fr = feats.clone().requires_grad_(True)
+    pdict = dict(xyz=xyz, feats=fr, mode='idw', radius=0.05, k=8, eps=1e-6)
+    sr = RR.regulation(ref_p, rd, ro, gt, bound, t_rand=t_rand,
+                       eval_fn=lambda q: RP.eval_points_c(ref_p, q, bound, pdict))
+    sr.abs().sum().backward()
+    close(s, sr, 2e-5 * sr.abs().max().item(), 'sigma')
+    close(pts.feats.grad, fr.grad, 2e-3 * fr.grad.abs().max().item(), 'dL/dfeats')
+    for k in ('fc_c.0.weight', 'fc_c.3.bias', 'pts_linears.2.weight'):
+        ref = ref_p[k].grad
+        close(dict(dec.named_parameters())[k].grad, ref, 2e-3 * ref.abs().max().item(), k)

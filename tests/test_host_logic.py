@@ -48,7 +48,36 @@ def test_decoder_state_dict_compat():
     assert all(torch.equal(a, b) for a, b in zip(dec.parameters(), dec2.parameters()))
     dec.share_memory()
     with pytest.raises(NotImplementedError):
-        pnr.MLP(c_dim=32, color=True, skips=[], n_blocks=4, hidden_size=256)
+        pnr.MLP(c_dim=64, color=True, skips=[], n_blocks=4, hidden_size=256)
+    with pytest.raises(NotImplementedError):
+        pnr.MLP(c_dim=32, color=True, skips=[2], n_blocks=4, hidden_size=256)
+    # the neural-point decoder: 8 extra fc_c tensors, deepcopy drops the device caches
+    d32 = pnr.MLP(c_dim=32, color=True, skips=[], n_blocks=4, hidden_size=256)
+    assert sum(p.numel() for p in d32.parameters()) == 222747 + 4 * (32 * 256 + 256)
+    assert [k for k in d32.state_dict() if k.startswith('fc_c')] == list(pnr.FC_ORDER)
+    copy.deepcopy(d32)
+
+
+def test_neural_points_host_config():
+    xyz = torch.rand(100, 3)
+    p = pnr.NeuralPoints(xyz, mode='idw', radius=0.05, k=4)
+    assert p.feats.shape == (100, 32) and p.cell >= 0.05 and p.table_bits == 10
+    assert all(o < float(xyz[:, i].min()) for i, o in enumerate(p.origin))
+    with pytest.raises(ValueError):
+        pnr.NeuralPoints(xyz, k=9)
+    with pytest.raises(ValueError):
+        pnr.NeuralPoints(xyz, radius=0.05, cell=0.01)
+    grid = torch.randn(1, 32, 3, 4, 5)
+    q = pnr.NeuralPoints.from_grid(grid, torch.tensor([[0., 1.], [0., 1.5], [0., 1.]]))
+    assert q.mode == 'trilinear' and q.xyz.shape == (60, 3)
+    np.testing.assert_allclose(q.spacing, [0.25, 0.5, 0.5], rtol=1e-6)
+    # row (d,h,w) = (2,3,4) is the far corner and carries grid[0,:,2,3,4]
+    assert torch.equal(q.feats[59], grid[0, :, 2, 3, 4]) and torch.allclose(q.xyz[59], torch.tensor([1., 1.5, 1.]))
+    dec = pnr.MLP(name='color', c_dim=32, color=True, skips=[], n_blocks=4, hidden_size=256)
+    from pnr.points import find_points
+    assert find_points({'points_color': q}, dec) is q and find_points({}, pnr.get_model(pnr.ROOM0_CFG, nice=False)) is None
+    with pytest.raises(ValueError):
+        find_points({}, dec)
 
 
 def test_get_model_from_cfg():
