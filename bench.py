@@ -66,6 +66,94 @@ def synth_batch(n, rank, pose, dev, seed=0):
     return (ro.contiguous().to(dev), rd.contiguous().to(dev), gt.to(dev), col.to(dev))
 
 
+def neural_point_scene(dev, voxel=0.001, n_rays=W * H, seed=0):
+    """Neural points on the trained decoder's own rendered surface at room0 pose 1000 (640x480,
+    ScanNet intrinsics), voxel-downsampled like Point-NeRF's point initialisation (at most one
+    point per `voxel` cube), features N(0, 0.1); plus the sample positions of one mapping
+    iteration over `n_rays` random pixels (32 stratified in [0.01 d, 1.2 d] + 12 around the
+    surface, sigma 5 mm) as float64 points.  Returns xyz, feats, p, (rays_o, rays_d, depth) of
+    those pixels."""
+    import types
+    import pnr
+    bound, pose, params = load_scene()
+    slam = types.SimpleNamespace(bound=bound, H=H, W=W, fx=FX, fy=FY, cx=CX, cy=CY)
+    r = pnr.Renderer(pnr.ROOM0_CFG, None, slam)
+    dec = pnr.get_model(pnr.ROOM0_CFG, nice=False)
+    dec.load_state_dict(params)
+    dec = dec.to(dev)
+    with torch.no_grad():
+        depth, _, _ = r.render_img({}, dec, pose, dev, 'color')
+    ro, rd = pnr.get_rays(H, W, FX, FY, CX, CY, pose, dev)
+    depth = depth.reshape(-1).float()
+    surf = ro.reshape(-1, 3) + rd.reshape(-1, 3) * depth[:, None]
+    g = torch.Generator(device=dev).manual_seed(seed)
+    valid = surf[depth > 0]
+    key = torch.floor(valid / voxel).long()
+    key = (key[:, 0] + 4096) * (8192 * 8192) + (key[:, 1] + 4096) * 8192 + (key[:, 2] + 4096)
+    uniq, inv = torch.unique(key, return_inverse=True)
+    first = torch.full((uniq.shape[0],), valid.shape[0], device=dev, dtype=torch.long)
+    first.scatter_reduce_(0, inv, torch.arange(valid.shape[0], device=dev), reduce='amin')
+    xyz = valid[first].contiguous()
+    feats = (0.1 * torch.randn((xyz.shape[0], 32), device=dev, generator=g)).contiguous()
+    rays = torch.randint(0, surf.shape[0], (n_rays,), device=dev, generator=g)
+    o = ro.reshape(-1, 3)[rays].double()
+    d = rd.reshape(-1, 3)[rays].double()
+    gt = depth[rays].double()
+    t = torch.linspace(0, 1, 32, device=dev, dtype=torch.float64)
+    z = (0.01 * gt)[:, None] * (1 - t) + (1.2 * gt)[:, None] * t
+    zi = gt[:, None] + 0.005 * torch.randn((n_rays, 12), device=dev, dtype=torch.float64, generator=g)
+    z = torch.sort(torch.cat([z, zi], 1), 1).values
+    p = (o[:, None, :] + d[:, None, :] * z[:, :, None]).reshape(-1, 3).contiguous()
+    return xyz, feats, p, (o.float().contiguous(), d.float().contiguous(), gt.float().contiguous())
+
+
+def gather_bytes(n_samples, n_nb_total, k, save=True):
+    """Algorithmic bytes of one pnr_point_gather (with the 8 probes made): per
+    sample 24 B point + 8 x 8 B bucket headers + 128 B c (+ k x 8 B idx/weight saves), per
+    neighbour 4 B idx + 12 B xyz + 128 B features."""
+    return n_samples * (24 + 8 * 8 + 128 + (k * 8 if save else 0)) + n_nb_total * (4 + 12 + 128)
+
+
+def gather_roofline(dev, voxel=0.001, k=8, reps=5):
+    """Time the point-gather kernels (k_gather_probe + k_gather_search, hipEvents on their
+    stream) on the neural-point scene; roofline against the HBM peak."""
+    import ctypes
+    import pnr
+    from pnr._lib import timing_read
+    lib = pnr.library()
+    xyz, feats, p, _ = neural_point_scene(dev, voxel)
+    pts = pnr.NeuralPoints(xyz, feats, mode='idw', radius=2 * voxel, k=k).to(dev)
+    P = p.shape[0]
+    c = torch.empty((P, 32), device=dev)
+    idx = torch.empty((P, k), device=dev, dtype=torch.int32)
+    w = torch.empty((P, k), device=dev)
+    ws = torch.empty(lib.pnr_point_gather_workspace_bytes(P), dtype=torch.uint8, device=dev)
+    s, _ = pts.descriptor()
+    st = pnr._lib.stream_of(dev)
+
+    def run():
+        pnr._lib.check(lib.pnr_point_gather(ctypes.byref(s), p.data_ptr(), P, c.data_ptr(), idx.data_ptr(),
+                                            w.data_ptr(), ws.data_ptr(), ws.numel(), st), 'point_gather')
+    run()
+    torch.cuda.synchronize()
+    nb = int((idx >= 0).sum().item())
+    lib.pnr_timing_enable(1)
+    timing_read(4)
+    for _ in range(reps):
+        run()
+    torch.cuda.synchronize()
+    lib.pnr_timing_enable(0)
+    launches, ms, _ = timing_read(4)
+    avg = ms / launches
+    byt = gather_bytes(P, nb, k)
+    gbs = byt / (avg * 1e-3) / 1e9
+    return {'bound': 'hbm', 'achieved': round(gbs, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+            'frac': round(gbs / HBM_PEAK_GBS, 4), 'traffic': None, 'kernel': 'k_gather_probe+k_gather_search',
+            'avg_launch_ms': round(avg, 3), 'launches': launches, 'samples': P, 'points': int(xyz.shape[0]),
+            'neighbours_per_sample': round(nb / P, 3), 'radius': 2 * voxel, 'k': k,
+            'bytes_per_launch': byt}
+
+
 def cpu_baseline(bound, pose, params, workload, n_rays=2048, reps=3):
     """The oracle (oracle/ref_render.py, a bit-exact restatement of the reference CPU path pinned
     by tests/test_oracle_golden.py) timed on this host: bounded sample, median of `reps`."""
@@ -103,9 +191,10 @@ def main():
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=5)
     ap.add_argument('--warmup', type=int, default=2)
-    ap.add_argument('--workload', choices=['map', 'fwd'], default='map')
+    ap.add_argument('--workload', choices=['map', 'fwd', 'map-points'], default='map')
     ap.add_argument('--rays', type=int, default=W * H, help='rays per GPU per step')
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--no-gather', action='store_true', help='skip the point-gather roofline line')
     args = ap.parse_args()
 
     import pnr
@@ -126,17 +215,31 @@ def main():
         cfg = copy.deepcopy(cfg)
         cfg['rendering']['N_samples'], cfg['rendering']['N_importance'] = 64, 0
     renderer = pnr.Renderer(cfg, None, slam)
-    dec = pnr.get_model(cfg, nice=False)
-    if params is not None:
-        dec.load_state_dict(params)
-    dec = dec.to(dev)
+    points = None
+    if args.workload == 'map-points':
+        # the neural-point decoder: trained base weights + fresh fc_c, points on
+        # the rendered surface, the same pixels' rendered depth as gt
+        dec = pnr.MLP(name='color', dim=3, c_dim=32, color=True, skips=[], n_blocks=4, hidden_size=256)
+        sd = dec.state_dict()
+        sd.update(params)
+        dec.load_state_dict(sd)
+        dec = dec.to(dev)
+        xyz, feats, _, (ro, rd, gt) = neural_point_scene(dev, n_rays=args.rays, seed=rank)
+        points = pnr.NeuralPoints(xyz, feats, mode='idw', radius=0.002, k=8).to(dev)
+        col = torch.rand((args.rays, 3), device=dev, generator=torch.Generator(device=dev).manual_seed(rank))
+    else:
+        dec = pnr.get_model(cfg, nice=False)
+        if params is not None:
+            dec.load_state_dict(params)
+        dec = dec.to(dev)
+        ro, rd, gt, col = synth_batch(args.rays, rank, pose, dev)
     ddp = pdist.DataParallel()
-    ro, rd, gt, col = synth_batch(args.rays, rank, pose, dev)
     n = args.rays
 
-    if args.workload == 'map':
+    if args.workload in ('map', 'map-points'):
         mstep = MapStep(renderer, dec, lr=cfg['mapping']['imap_decoders_lr'],
-                        w_color_loss=cfg['mapping']['w_color_loss'], ddp=ddp if world > 1 else None)
+                        w_color_loss=cfg['mapping']['w_color_loss'], ddp=ddp if world > 1 else None,
+                        points=points)
 
         def step():
             t_rand = torch.rand((n, cfg['rendering']['N_samples']), device=dev)
@@ -151,7 +254,8 @@ def main():
     ddp.barrier()
     torch.cuda.synchronize()
     lib.pnr_timing_enable(1)
-    timing_read(0), timing_read(1), timing_read(3)
+    for kind in range(6):
+        timing_read(kind)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
@@ -160,6 +264,8 @@ def main():
     el = time.perf_counter() - t0
     lib.pnr_timing_enable(0)
     kt = {'mlp_fwd': timing_read(0), 'mlp_bwd': timing_read(1), 'wgrad': timing_read(3)}
+    if points is not None:
+        kt.update({'gather': timing_read(4), 'gather_bwd': timing_read(5)})
     t = torch.tensor([el], device=dev, dtype=torch.float64)
     if world > 1:
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
@@ -170,7 +276,7 @@ def main():
     # roofline of the dominant hand-written kernel (fused MLP fwd or delta chain), per launch
     best = None
     for name, (launches, ms, units) in kt.items():
-        if launches == 0 or name == 'wgrad':
+        if launches == 0 or name not in ('mlp_fwd', 'mlp_bwd'):
             continue
         fl = FLOP_PER_POINT_FWD if name == 'mlp_fwd' else FLOP_PER_POINT_BWD
         cand = {'kernel': 'k_mlp_fwd' if name == 'mlp_fwd' else 'k_mlp_bwd', 'launches': launches,
@@ -187,17 +293,20 @@ def main():
 
     if rank == 0:
         cpu = None
-        if world == 1 and not args.no_cpu_baseline and params is not None:
+        if world == 1 and not args.no_cpu_baseline and params is not None and args.workload != 'map-points':
             cpu = cpu_baseline(bound, pose, params, args.workload)
-        samples = '32+12 (+32 regulation)' if args.workload == 'map' else '64'
+        samples = '64' if args.workload == 'fwd' else '32+12 (+32 regulation)'
+        wl_name = {'map': 'S-map: full mapping iteration (render+regulation+L1 losses+backward+Adam)',
+                   'fwd': 'S-fwd: render_batch_ray forward',
+                   'map-points': 'S-map with neural points (A15): c_dim=32 decoder, IDW k=8 r=2 mm gather, '
+                                 'fc_c injection, feature + decoder Adam'}[args.workload]
         out = {
             'metric': METRIC, 'value': round(value, 1), 'unit': 'rays/s', 'n_gpus': world, 'steps': args.steps,
             'warmup': args.warmup, 'ms_per_step': round(ms_per_step, 3), 'higher_is_better': True, 'scaling': 'weak',
             'vs_baseline': None, 'dtype': 'fp32',
             'data': 'synthetic (640x480 ScanNet-intrinsics rays at room0 pose 1000, U[0.05,0.6] gt depth, trained '
                     'room0 decoder fixture)',
-            'config': {'workload': ('S-map: full mapping iteration (render+regulation+L1 losses+backward+Adam)'
-                                    if args.workload == 'map' else 'S-fwd: render_batch_ray forward'),
+            'config': {'workload': wl_name,
                        'rays_per_gpu': n, 'global_batch': n * world, 'samples_per_ray': samples,
                        'parallelism': f'dp{world}'},
             'roofline': roofline, 'cpu_baseline': cpu,
@@ -205,6 +314,9 @@ def main():
         }
         if cpu is not None:
             out['speedup_vs_cpu'] = round(value / cpu['value'], 1)
+        if world == 1 and not args.no_gather and params is not None and args.workload != 'fwd':
+            # the neural-point gather on its own roofline, after the timed region
+            out['gather_roofline'] = gather_roofline(dev)
         print(json.dumps(out), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()

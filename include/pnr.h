@@ -62,8 +62,9 @@ enum {
  * into every hidden layer: h = relu(W h + b) + fc_c[i](c) (decoder.py:196-197).
  * Search structure: a spatial hash of cubic cells (edge `cell`, corner `origin`) into
  * 2^table_bits buckets, bucket-sorted copies of the positions; built on the device by
- * pnr_points_build into the caller's `index` buffer.  `cell` must be >= radius (IDW) or
- * >= max(spacing) (TRILINEAR): the search visits the 27 cells around p. */
+ * pnr_points_build into the caller's `index` buffer.  `cell` must be >= 2 * radius (IDW) or
+ * >= 2 * max(spacing) (TRILINEAR): the search visits the 2x2x2 cells covering [p - reach, p + reach]
+ * (a margin of ~1e-3 relative absorbs float rounding). */
 enum { PNR_GATHER_IDW = 0, PNR_GATHER_TRILINEAR = 1 };
 
 typedef struct pnr_points {
@@ -137,13 +138,15 @@ size_t pnr_points_index_bytes(int64_t n_points, int32_t table_bits);
 /* (Re)builds pts->index from pts->xyz (after any change of positions / cell / origin). */
 int pnr_points_build(const pnr_points* pts, void* stream);
 /* Standalone gather: c (P,32) float32 for float64 points p (P,3).  idx (P,k) int32 (-1 = none)
- * and w (P,k) float32 normalised weights are written when non-NULL (needed by the backward). */
+ * and w (P,k) float32 normalised weights are written when non-NULL (needed by the backward).
+ * ws: pnr_point_gather_workspace_bytes(P) bytes (work list of samples with candidates). */
+size_t pnr_point_gather_workspace_bytes(int64_t P);
 int pnr_point_gather(const pnr_points* pts, const double* p, int64_t P, float* c, int32_t* idx, float* w,
-                     void* stream);
+                     void* ws, size_t ws_bytes, void* stream);
 /* Backward of pnr_point_gather: g_c (P,32) -> pts->g_feats (+=, when non-NULL) and g_p (P,3)
- * (written, when non-NULL: dL/dp through the weights). */
+ * (written, when non-NULL: dL/dp through the weights).  ws as for pnr_point_gather. */
 int pnr_point_gather_bwd(const pnr_points* pts, const double* p, int64_t P, const int32_t* idx, const float* w,
-                         const float* c, const float* g_c, float* g_p, void* stream);
+                         const float* c, const float* g_c, float* g_p, void* ws, size_t ws_bytes, void* stream);
 /* fc_c weight image of the decoder (MLP(c_dim=32)): fc_params = host array of the 8 tensors
  * fc_c.0.weight, fc_c.0.bias, ..., fc_c.3.bias (contiguous float32). */
 size_t pnr_fc_packed_floats(void);

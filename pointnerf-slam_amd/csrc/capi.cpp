@@ -118,6 +118,8 @@ struct RenderWS {
   float* c;        // [ld][32]
   int32_t* nidx;   // [ld][k]
   float* nw;       // [ld][k]
+  void* gws;       // gather work list (coarse and importance passes reuse it)
+  size_t gws_bytes;
 };
 
 SaveArgs carve_save(Carver& c, int64_t ld) {
@@ -147,6 +149,9 @@ RenderWS carve_render(const pnr_render_params* prm, int64_t n, void* ws, size_t*
     w.c = c.take<float>((size_t)w.ld * kCDim);
     w.nidx = c.take<int32_t>((size_t)w.ld * prm->points->k);
     w.nw = c.take<float>((size_t)w.ld * prm->points->k);
+    const int64_t pmax = n * (prm->n_samples > prm->n_importance ? prm->n_samples : prm->n_importance);
+    w.gws_bytes = gather_workspace_bytes(pmax);
+    w.gws = c.take<char>(w.gws_bytes);
   }
   if (bytes) *bytes = c.off;
   return w;
@@ -161,6 +166,8 @@ struct BwdWS {
   float* gargP;   // [C][96]
   float* gH;      // [4][C][256]  features only: dL/dh_l
   float* g_c;     // [P][32]      features only: dL/dc
+  void* gws;      // features only: gather-backward work list
+  size_t gws_bytes;
   int64_t C;
 };
 
@@ -177,6 +184,8 @@ BwdWS carve_bwd(int64_t P, int64_t n, void* ws, size_t* bytes, bool feat = false
   if (feat) {
     b.gH = c.take<float>((size_t)4 * kHidden * b.C);
     b.g_c = c.take<float>((size_t)P * kCDim);
+    b.gws_bytes = gather_workspace_bytes(P);
+    b.gws = c.take<char>(b.gws_bytes);
   }
   if (bytes) *bytes = c.off;
   return b;
@@ -405,7 +414,8 @@ int pnr_render_fwd(const pnr_render_params* prm, const float* packed, const floa
   FeatArgs fa{pts ? pts->fc_packed : nullptr, w.c};
   const int K = pts ? pts->k : 0;
   if (pts) {
-    rc = launch_gather(*pts, src, kRaysZ64, n * S, w.pc_pad, w.c, sv ? w.nidx : nullptr, sv ? w.nw : nullptr, st);
+    rc = launch_gather(*pts, src, kRaysZ64, n * S, w.pc_pad, w.c, sv ? w.nidx : nullptr, sv ? w.nw : nullptr, w.gws,
+                       w.gws_bytes, st);
     if (rc) return rc;
   }
   rc = launch_mlp_fwd(packed, src, kRaysZ64, n * S, w.raw, sv, st, pts ? &fa : nullptr);
@@ -426,7 +436,7 @@ int pnr_render_fwd(const pnr_render_params* prm, const float* packed, const floa
     if (pts) {
       const int64_t o = w.pc_pad;
       rc = launch_gather(*pts, src, kRaysZ64, n * I, w.ld - o, w.c + o * kCDim, sv ? w.nidx + o * K : nullptr,
-                         sv ? w.nw + o * K : nullptr, st);
+                         sv ? w.nw + o * K : nullptr, w.gws, w.gws_bytes, st);
       if (rc) return rc;
       fa.c = w.c + o * kCDim;
     }
@@ -476,7 +486,7 @@ int pnr_render_bwd(const pnr_render_params* prm, const float* packed, const floa
   if (rc) return rc;
   if (pts) {  // neural-point features and dL/dp through the gather weights
     rc = launch_gather_bwd(*pts, nullptr, kRaysZ64, w.save.xP, ld, w.nidx, w.nw, w.c, b.g_c,
-                           prm->need_ray_grads ? b.g_x : nullptr, true, st);
+                           prm->need_ray_grads ? b.g_x : nullptr, true, b.gws, b.gws_bytes, st);
     if (rc) return rc;
   }
   if (prm->need_ray_grads)
@@ -493,6 +503,8 @@ struct RegWS {
   float* c;
   int32_t* nidx;
   float* nw;
+  void* gws;
+  size_t gws_bytes;
 };
 RegWS carve_reg(const pnr_render_params* prm, int64_t n, void* ws, size_t* bytes) {
   Carver c(ws);
@@ -505,6 +517,8 @@ RegWS carve_reg(const pnr_render_params* prm, int64_t n, void* ws, size_t* bytes
     w.c = c.take<float>((size_t)pad128(P) * kCDim);
     w.nidx = c.take<int32_t>((size_t)pad128(P) * prm->points->k);
     w.nw = c.take<float>((size_t)pad128(P) * prm->points->k);
+    w.gws_bytes = gather_workspace_bytes(P);
+    w.gws = c.take<char>(w.gws_bytes);
   }
   if (bytes) *bytes = c.off;
   return w;
@@ -542,7 +556,8 @@ int pnr_regulation_fwd(const pnr_render_params* prm, const float* packed, const 
   const bool sv = prm->save_for_backward != 0;
   FeatArgs fa{prm->points ? prm->points->fc_packed : nullptr, w.c};
   if (prm->points) {
-    rc = launch_gather(*prm->points, src, kRaysZ32, P, pad128(P), w.c, sv ? w.nidx : nullptr, sv ? w.nw : nullptr, st);
+    rc = launch_gather(*prm->points, src, kRaysZ32, P, pad128(P), w.c, sv ? w.nidx : nullptr, sv ? w.nw : nullptr,
+                       w.gws, w.gws_bytes, st);
     if (rc) return rc;
   }
   rc = launch_mlp_fwd(packed, src, kRaysZ32, P, w.raw, sv ? &w.save : nullptr, st, prm->points ? &fa : nullptr);
@@ -585,7 +600,7 @@ int pnr_regulation_bwd(const pnr_render_params* prm, const float* packed, const 
   if (rc) return rc;
   if (pts) {
     rc = launch_gather_bwd(*pts, nullptr, kRaysZ32, w.save.xP, ld, w.nidx, w.nw, w.c, b.g_c,
-                           prm->need_ray_grads ? b.g_x : nullptr, true, st);
+                           prm->need_ray_grads ? b.g_x : nullptr, true, b.gws, b.gws_bytes, st);
     if (rc) return rc;
   }
   if (prm->need_ray_grads) rc = launch_ray_grads_f32(rays_d, w.z, prm->n_samples, b.g_x, n, g_rays_o, g_rays_d, st);
@@ -607,20 +622,23 @@ int pnr_points_build(const pnr_points* pts, void* stream) {
   return launch_points_build(*pts, (hipStream_t)stream);
 }
 
-int pnr_point_gather(const pnr_points* pts, const double* p, int64_t P, float* c, int32_t* idx, float* w,
-                     void* stream) {
+size_t pnr_point_gather_workspace_bytes(int64_t P) { return P < 0 ? 0 : gather_workspace_bytes(P); }
+
+int pnr_point_gather(const pnr_points* pts, const double* p, int64_t P, float* c, int32_t* idx, float* w, void* ws,
+                     size_t ws_bytes, void* stream) {
   if (!pts || P < 0 || (P > 0 && (!p || !c)) || (!idx) != (!w)) return PNR_E_ARG;
   PointSrc s{};
   s.pts = p;
-  return launch_gather(*pts, s, kPtsF64, P, P, c, idx, w, (hipStream_t)stream);
+  return launch_gather(*pts, s, kPtsF64, P, P, c, idx, w, ws, ws_bytes, (hipStream_t)stream);
 }
 
 int pnr_point_gather_bwd(const pnr_points* pts, const double* p, int64_t P, const int32_t* idx, const float* w,
-                         const float* c, const float* g_c, float* g_p, void* stream) {
+                         const float* c, const float* g_c, float* g_p, void* ws, size_t ws_bytes, void* stream) {
   if (!pts || P < 0 || (P > 0 && !p)) return PNR_E_ARG;
   PointSrc s{};
   s.pts = p;
-  return launch_gather_bwd(*pts, &s, kPtsF64, nullptr, P, idx, w, c, g_c, g_p, false, (hipStream_t)stream);
+  return launch_gather_bwd(*pts, &s, kPtsF64, nullptr, P, idx, w, c, g_c, g_p, false, ws, ws_bytes,
+                           (hipStream_t)stream);
 }
 
 size_t pnr_fc_packed_floats(void) { return (size_t)kFcPackedFloats; }

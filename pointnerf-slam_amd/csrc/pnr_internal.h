@@ -172,7 +172,7 @@ int launch_fc_pack(const float* const* fc, float* out, hipStream_t st);
 
 // ---- neural-point gather (points.hip) --------------------------------------------------------
 // index buffer layout (pnr_points_index_bytes): cell_start[T+1] | count[T] | bucket[M] | slot[M]
-// | scan partials | sorted float4[M] (x, y, z, original index bits)
+// | scan partials | sorted float4[M] (x, y, z, original index bits) | hdr int4[T] | occupancy bits
 struct IndexView {
   int32_t* start;
   int32_t* count;
@@ -180,18 +180,23 @@ struct IndexView {
   int32_t* slot;
   int32_t* partial;
   float4* sorted;
+  int4* hdr;       // [T] {start, end, cell key lo, key hi | collision bit}
+  uint32_t* occ;   // occupancy filter (points.hip k_occ_mark)
+  int64_t occ_words;
   int64_t T;
 };
 IndexView index_view(void* base, int64_t M, int32_t bits, size_t* bytes);
 int launch_points_build(const pnr_points& pts, hipStream_t st);
 // c rows [0, rows): points [0, P) gathered, rows [P, rows) zeroed
+// ws: gather_workspace_bytes(P) (work list of the two-pass gather)
+size_t gather_workspace_bytes(int64_t P);
 int launch_gather(const pnr_points& pts, const PointSrc& src, int mode, int64_t P, int64_t rows, float* c,
-                  int32_t* idx, float* w, hipStream_t st);
+                  int32_t* idx, float* w, void* ws, size_t ws_bytes, hipStream_t st);
 // g_c (P,32) -> g_feats (+=), g_p (P,3): `gp_accum` adds into g_p instead of writing it;
 // positions come from xP (float4 rows, MLP inputs) when non-null, else from src
 int launch_gather_bwd(const pnr_points& pts, const PointSrc* src, int mode, const float4* xP, int64_t P,
                       const int32_t* idx, const float* w, const float* c, const float* g_c, float* g_p,
-                      bool gp_accum, hipStream_t st);
+                      bool gp_accum, void* ws, size_t ws_bytes, hipStream_t st);
 
 // weight-gradient GEMM shapes (wgrad.hip): C[MA][NB] += A[K][WA]^T B[K][WB]
 enum WgradKind : int { kWgradHidden = 0, kWgradFirst = 1, kWgradOut = 2, kWgradFourier = 3, kWgradFc = 4 };

@@ -2,18 +2,24 @@
 //
 // The reference has no neural-point stage; its nearest analogue is MLP.sample_grid_feature
 // (src/conv_onet/models/decoder.py:168-175, trilinear F.grid_sample on a dense grid).  The stage
-// is specified by oracle/ref_points.py and include/pnr.h (pnr_points):
+// is specified by oracle/ref_points.py and include/pnr.h (pnr_points).
 //
-//   k_hash_count / scan / k_hash_scatter : spatial hash of the points (cell edge `cell`) into
-//        2^bits buckets -> cell_start[T+1] + bucket-sorted float4 (x, y, z, index bits)
-//   k_gather   : per sample, probe the 27 cells around it, keep the k nearest (d2, index)
-//        inside the neighbourhood (IDW ball / trilinear box), normalised weights, then the
-//        feature sum  c = sum_k w_k f_k  with 8 lanes per sample reading 128-B feature rows
-//   k_gather_bwd : dL/df_i += w_k dL/dc (float atomics, 8 lanes per sample) and dL/dp through
-//        the weights (8-lane dot products g.f_k, g.c)
+// Index (pnr_points_build): points hashed by cell (edge `cell` >= 2 x reach) into T = 2^bits
+// buckets, bucket-sorted float4 (x, y, z, index bits), one 16-B header per bucket
+// {start, end, packed cell key | collision flag}, and an occupancy filter (one bit per hashed
+// probe-block base cell).
 //
-// The search is thread-per-sample: the samples of one wave are consecutive points of the same
-// two rays, so they probe the same few buckets and the bucket data stays in L1/L2.
+// Gather, two passes:
+//   k_gather_probe  one thread per sample row: coalesced zero fill of the block's output rows,
+//                   occupancy-filter test of the sample's 2x2x2 probe block; samples that may have
+//                   neighbours go to a work list (one atomic per wave, 64 sub-lists).  Free space -- most of a
+//                   ray -- costs one L2-resident bit load.
+//   k_gather_search persistent blocks over the work list, one thread per sample: 8 bucket headers
+//                   (foreign buckets of a hash collision are skipped by their key), one flattened
+//                   candidate loop, and a branch-free top-k insertion network on packed
+//                   (d2, index) keys compared as float64 (2 VALU per stage); normalised weights,
+//                   then the feature sum with 8 lanes per sample (16-B loads of 128-B rows).
+//   k_gather_bwd    dL/df_i += w_k dL/dc (float atomics) and dL/dp through the weights.
 #include "pnr_internal.h"
 
 namespace pnr {
@@ -24,9 +30,12 @@ namespace {
 
 struct HashGrid {
   float o0, o1, o2;
-  float inv;      // 1 / cell
-  uint32_t mask;  // T - 1
+  float inv;       // 1 / cell
+  uint32_t mask;   // T - 1
+  uint32_t omask;  // occupancy bits - 1
 };
+
+int occ_bits_log2(int32_t bits) { return bits + 6 < 26 ? bits + 6 : 26; }
 
 HashGrid make_grid(const pnr_points& p) {
   HashGrid g;
@@ -35,6 +44,7 @@ HashGrid make_grid(const pnr_points& p) {
   g.o2 = p.origin[2];
   g.inv = 1.0f / p.cell;
   g.mask = (uint32_t)((1ll << p.table_bits) - 1);
+  g.omask = (uint32_t)((1ll << occ_bits_log2(p.table_bits)) - 1);
   return g;
 }
 
@@ -45,9 +55,36 @@ __device__ __forceinline__ int cell_coord(float x, float o, float inv) {
   return (int)f;
 }
 
+// lower of the two cells per axis that cover [x - reach, x + reach] when cell >= 2 reach
+__device__ __forceinline__ void base_cell(float x, float o, float inv, int& b) {
+  PNR_FP_STRICT
+  float t = (x - o) * inv;
+  t = fminf(fmaxf(t, -1.0e9f), 1.0e9f);
+  const float f = floorf(t);
+  b = (int)f - (t - f < 0.5f ? 1 : 0);
+}
+
 __device__ __forceinline__ uint32_t cell_hash(int cx, int cy, int cz, uint32_t mask) {
   return (((uint32_t)cx * 73856093u) ^ ((uint32_t)cy * 19349663u) ^ ((uint32_t)cz * 83492791u)) & mask;
 }
+
+// exact cell identity: 3 x 21-bit two's complement (scenes stay far below 2^20 cells per axis)
+__device__ __forceinline__ uint64_t cell_key(int cx, int cy, int cz) {
+  return (uint64_t)((uint32_t)cx & 0x1FFFFFu) | ((uint64_t)((uint32_t)cy & 0x1FFFFFu) << 21) |
+         ((uint64_t)((uint32_t)cz & 0x1FFFFFu) << 42);
+}
+constexpr uint64_t kCollision = 1ull << 63;
+
+// (d2, index) as one float64 whose order is the lexicographic order: d2 >= 0 has monotone float
+// bits; +2^20 on the high word keeps every key a normal double (no denormal flushing)
+__device__ __forceinline__ double pack_key(float d2, int id) {
+  const uint64_t k = ((uint64_t)((uint32_t)__float_as_int(d2) + 0x00100000u) << 32) | (uint32_t)id;
+  return __longlong_as_double((long long)k);
+}
+__device__ __forceinline__ float key_d2(double k) {
+  return __int_as_float((int)((uint32_t)((uint64_t)__double_as_longlong(k) >> 32) - 0x00100000u));
+}
+__device__ __forceinline__ int key_id(double k) { return (int)(uint32_t)(uint64_t)__double_as_longlong(k); }
 
 }  // namespace
 
@@ -83,6 +120,9 @@ IndexView index_view(void* base, int64_t M, int32_t bits, size_t* bytes) {
   v.slot = reinterpret_cast<int32_t*>(take((size_t)M * 4));
   v.partial = reinterpret_cast<int32_t*>(take((size_t)scan_scratch_ints(v.T) * 4));
   v.sorted = reinterpret_cast<float4*>(take((size_t)M * 16));
+  v.hdr = reinterpret_cast<int4*>(take((size_t)v.T * 16));
+  v.occ_words = (1ll << occ_bits_log2(bits)) / 32;
+  v.occ = reinterpret_cast<uint32_t*>(take((size_t)v.occ_words * 4));
   if (bytes) *bytes = off;
   return v;
 }
@@ -111,8 +151,7 @@ __global__ void k_scan_tile(const int32_t* __restrict__ in, int32_t* __restrict_
 #pragma unroll
   for (int e = 0; e < 4; ++e) v[e] = base + e < n ? in[base + e] : 0;
   const int t = v[0] + v[1] + v[2] + v[3];
-  // inclusive wave scan of t
-  int incl = t;
+  int incl = t;  // inclusive wave scan of t
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
@@ -165,152 +204,301 @@ __global__ void k_hash_scatter(const float* __restrict__ xyz, int64_t M, const i
   sorted[pos] = make_float4(xyz[i * 3 + 0], xyz[i * 3 + 1], xyz[i * 3 + 2], __int_as_float((int)i));
 }
 
+// bucket header {start, end, key lo, key hi}: the cell of the bucket's first point, plus the
+// collision flag when the bucket also holds points of other cells
+__global__ void k_bucket_hdr(const int32_t* __restrict__ start, const float4* __restrict__ sorted, int64_t T,
+                             HashGrid g, int4* __restrict__ hdr) {
+  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= T) return;
+  const int s = start[b], e = start[b + 1];
+  uint64_t key = 0;
+  if (e > s) {
+    const float4 q = sorted[s];
+    key = cell_key(cell_coord(q.x, g.o0, g.inv), cell_coord(q.y, g.o1, g.inv), cell_coord(q.z, g.o2, g.inv));
+    for (int j = s + 1; j < e; ++j) {
+      const float4 r = sorted[j];
+      if (cell_key(cell_coord(r.x, g.o0, g.inv), cell_coord(r.y, g.o1, g.inv), cell_coord(r.z, g.o2, g.inv)) != key) {
+        key |= kCollision;
+        break;
+      }
+    }
+  }
+  hdr[b] = make_int4(s, e, (int)(uint32_t)key, (int)(uint32_t)(key >> 32));
+}
+
+// Occupancy filter: bit hash(b) is set when the probe block with base cell b (cells b..b+1 per
+// axis) holds a point.  A clear bit proves a sample has no candidate (hash collisions only set
+// extra bits), so free-space samples skip the bucket headers.
+__global__ void k_occ_mark(const float* __restrict__ xyz, int64_t M, HashGrid g, uint32_t* __restrict__ occ) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= M) return;
+  const int cx = cell_coord(xyz[i * 3 + 0], g.o0, g.inv), cy = cell_coord(xyz[i * 3 + 1], g.o1, g.inv),
+            cz = cell_coord(xyz[i * 3 + 2], g.o2, g.inv);
+#pragma unroll
+  for (int n = 0; n < 8; ++n) {
+    const uint32_t bit = cell_hash(cx - (n & 1), cy - ((n >> 1) & 1), cz - (n >> 2), g.omask);
+    atomicOr(occ + (bit >> 5), 1u << (bit & 31u));
+  }
+}
+
 int launch_points_build(const pnr_points& pts, hipStream_t st) {
   const int64_t M = pts.n_points;
   IndexView v = index_view(pts.index, M, pts.table_bits, nullptr);
   if (hipMemsetAsync(v.count, 0, (size_t)v.T * 4, st) != hipSuccess) return (int)hipGetLastError();
+  if (hipMemsetAsync(v.occ, 0, (size_t)v.occ_words * 4, st) != hipSuccess) return (int)hipGetLastError();
   const HashGrid g = make_grid(pts);
   const unsigned nbm = (unsigned)((M + 255) / 256);
   if (M > 0)
     hipLaunchKernelGGL(k_hash_count, dim3(nbm), dim3(256), 0, st, pts.xyz, M, g, v.count, v.bucket, v.slot);
   int rc = scan_exclusive(v.count, v.start, v.T, v.partial, st);
   if (rc) return rc;
-  if (M > 0)
+  if (M > 0) {
     hipLaunchKernelGGL(k_hash_scatter, dim3(nbm), dim3(256), 0, st, pts.xyz, M, v.start, v.bucket, v.slot, v.sorted);
+    hipLaunchKernelGGL(k_occ_mark, dim3(nbm), dim3(256), 0, st, pts.xyz, M, g, v.occ);
+  }
+  hipLaunchKernelGGL(k_bucket_hdr, dim3((unsigned)((v.T + 255) / 256)), dim3(256), 0, st, v.start, v.sorted, v.T, g,
+                     v.hdr);
   return hip_status(hipGetLastError());
 }
 
 // ---------------------------------------------------------------------------------------------
 // Gather
 // ---------------------------------------------------------------------------------------------
+// Work lists: samples are appended by wave (one atomic per wave) to one of kLists sub-lists, each
+// with its own counter on its own 128-B line, dealt round-robin by wave -- a single counter would
+// serialise ~10^5 same-address atomics.  Consumers walk (sub-list, 256-item chunk) tasks.
+constexpr int kLists = 64;
+struct WorkList {
+  uint32_t* cnt;   // [kLists * 32], counter r at cnt[32 r]
+  float4* items;   // [kLists][cap]
+  int64_t cap;     // per sub-list capacity
+};
+
+static int64_t wl_cap(int64_t rows) {
+  const int64_t waves = (rows + 63) / 64;
+  return (waves + kLists - 1) / kLists * 64;
+}
+static size_t wl_bytes(int64_t rows) { return (size_t)kLists * 32 * 4 + (size_t)kLists * wl_cap(rows) * 16; }
+static WorkList wl_view(void* ws, int64_t rows) {
+  WorkList w;
+  w.cnt = static_cast<uint32_t*>(ws);
+  w.items = reinterpret_cast<float4*>(static_cast<char*>(ws) + kLists * 32 * 4);
+  w.cap = wl_cap(rows);
+  return w;
+}
+
+__device__ __forceinline__ void wl_append(const WorkList& wl, bool has, const float4& item) {
+  const uint64_t m = __ballot(has);
+  if (m == 0) return;
+  const int lane = threadIdx.x & 63;
+  const int r = (int)(((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) & (kLists - 1));
+  const int leader = __ffsll((unsigned long long)m) - 1;
+  uint32_t base = 0;
+  if (lane == leader) base = atomicAdd(wl.cnt + r * 32, (uint32_t)__popcll(m));
+  base = __shfl(base, leader);
+  if (has) wl.items[(int64_t)r * wl.cap + base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = item;
+}
+
 struct GatherArgs {
   PointSrc src;
   int64_t P, rows;
   HashGrid g;
-  const int32_t* start;
+  const int4* hdr;
   const float4* sorted;
   const float4* feats4;  // (M, 8) float4
   const float* xyz;      // (M, 3)
+  const uint32_t* occ;   // occupancy filter
   int k;
   float r2, eps;
   float h0, h1, h2;      // trilinear spacing
   float* c;              // (rows, 32)
   int32_t* idx;          // (rows, k) or null
   float* w;              // (rows, k) or null
+  WorkList wl;           // (x, y, z, sample row bits) of the samples that may have neighbours
 };
 
-__device__ __forceinline__ bool key_less(float da, int ia, float db, int ib) {
-  return da < db || (da == db && ia < ib);
-}
-
-template <int SRC, int KER>
-__global__ __launch_bounds__(256) void k_gather(GatherArgs a) {
+// Pass 1, one thread per sample row: the occupancy bit of each sample's probe block; the hits go
+// to the work list, the block zero-fills the other rows of its 256 with coalesced stores.
+template <int SRC>
+__global__ __launch_bounds__(256) void k_gather_probe(GatherArgs a) {
   PNR_FP_STRICT
-  __shared__ int32_t s_idx[256 * PNR_MAX_K];
-  __shared__ float s_w[256 * PNR_MAX_K];
-  const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
-
-  float kd[PNR_MAX_K];
-  int ki[PNR_MAX_K];
-#pragma unroll
-  for (int s = 0; s < PNR_MAX_K; ++s) {
-    kd[s] = __builtin_inff();
-    ki[s] = 0x7fffffff;
-  }
+  __shared__ uint8_t s_has[256];
+  const int64_t r0 = (int64_t)blockIdx.x * 256;
+  const int64_t nrow = a.rows - r0 < 256 ? a.rows - r0 : 256;
+  const int64_t p = r0 + threadIdx.x;
   float x0 = 0.f, x1 = 0.f, x2 = 0.f;
+  bool has = false;
   if (p < a.P) {
     bool inside;
     load_point<SRC>(a.src, p, x0, x1, x2, inside);
-    const int cx = cell_coord(x0, a.g.o0, a.g.inv), cy = cell_coord(x1, a.g.o1, a.g.inv),
-              cz = cell_coord(x2, a.g.o2, a.g.inv);
-#pragma unroll 1
-    for (int n = 0; n < 27; ++n) {
-      const int qx = cx + n % 3 - 1, qy = cy + (n / 3) % 3 - 1, qz = cz + n / 9 - 1;
-      const uint32_t b = cell_hash(qx, qy, qz, a.g.mask);
-      const int e = a.start[b + 1];
-#pragma unroll 1
-      for (int jj = a.start[b]; jj < e; ++jj) {
-        const float4 q = a.sorted[jj];
-        const float d0 = x0 - q.x, d1 = x1 - q.y, d2 = x2 - q.z;
+    int bx, by, bz;
+    base_cell(x0, a.g.o0, a.g.inv, bx);
+    base_cell(x1, a.g.o1, a.g.inv, by);
+    base_cell(x2, a.g.o2, a.g.inv, bz);
+    const uint32_t bit = cell_hash(bx, by, bz, a.g.omask);
+    has = (a.occ[bit >> 5] >> (bit & 31u)) & 1u;
+  }
+  s_has[threadIdx.x] = has ? 1 : 0;
+  __syncthreads();
+  // coalesced zero fill of the rows the search pass will not write
+  {
+    float4* c4 = reinterpret_cast<float4*>(a.c) + r0 * 8;
+    for (int e = threadIdx.x; e < nrow * 8; e += 256)
+      if (!s_has[e >> 3]) c4[e] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (a.idx) {
+      for (int e = threadIdx.x; e < nrow * a.k; e += 256) {
+        if (s_has[e / a.k]) continue;
+        a.idx[r0 * a.k + e] = -1;
+        a.w[r0 * a.k + e] = 0.f;
+      }
+    }
+  }
+  wl_append(a.wl, has, make_float4(x0, x1, x2, __int_as_float((int)p)));
+}
+
+// Pass 2, persistent blocks over the work list, one thread per sample.
+template <int KER>
+__global__ __launch_bounds__(256) void k_gather_search(GatherArgs a) {
+  PNR_FP_STRICT
+  __shared__ int32_t s_idx[256 * PNR_MAX_K];
+  __shared__ float s_w[256 * PNR_MAX_K];
+  __shared__ int32_t s_row[256];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, gq = lane >> 3, q = lane & 7;
+  const double kInf = __longlong_as_double(0x7FF0000000000000ll);
+  const int64_t nchunk = (a.wl.cap + 255) / 256;
+  for (int64_t task = blockIdx.x; task < kLists * nchunk; task += gridDim.x) {
+    const int r = (int)(task % kLists);
+    const int64_t j0 = task / kLists * 256;
+    const int64_t n_work = (int64_t)a.wl.cnt[r * 32];
+    if (j0 >= n_work) continue;  // uniform over the block
+    const int64_t i = j0 + threadIdx.x;
+    double key[PNR_MAX_K];
+#pragma unroll
+    for (int t = 0; t < PNR_MAX_K; ++t) key[t] = kInf;
+    float x0 = 0.f, x1 = 0.f, x2 = 0.f;
+    int row = -1;
+    if (i < n_work) {
+      const float4 wk = a.wl.items[r * a.wl.cap + i];
+      x0 = wk.x; x1 = wk.y; x2 = wk.z;
+      row = __float_as_int(wk.w);
+      int bx, by, bz;
+      base_cell(x0, a.g.o0, a.g.inv, bx);
+      base_cell(x1, a.g.o1, a.g.inv, by);
+      base_cell(x2, a.g.o2, a.g.inv, bz);
+      int4 h[8];
+#pragma unroll
+      for (int n = 0; n < 8; ++n)  // the 8 bucket headers in flight at once
+        h[n] = a.hdr[cell_hash(bx + (n & 1), by + ((n >> 1) & 1), bz + (n >> 2), a.g.mask)];
+      // ranges to scan: own buckets whole, colliding buckets with a per-point cell test (cf bit 8),
+      // foreign buckets not at all.  A bucket reached from two probe cells is scanned once per
+      // cell that it actually holds, so every point is seen exactly once.
+      int rs[8], re[8], rf[8];
+#pragma unroll
+      for (int n = 0; n < 8; ++n) {
+        const int cx = bx + (n & 1), cy = by + ((n >> 1) & 1), cz = bz + (n >> 2);
+        const uint64_t hk = (uint64_t)(uint32_t)h[n].z | ((uint64_t)(uint32_t)h[n].w << 32);
+        const bool coll = (hk & kCollision) != 0;
+        const bool own = (hk & ~kCollision) == cell_key(cx, cy, cz);
+        rs[n] = h[n].x;
+        re[n] = (coll || own) ? h[n].y : h[n].x;
+        rf[n] = n | (coll ? 8 : 0);
+      }
+      int jj = rs[0], je = re[0], jf = rf[0], left = 7;
+      while (true) {
+        if (jj >= je) {  // this range is done: shift the next one in
+          if (left == 0) break;
+#pragma unroll
+          for (int t = 0; t < 7; ++t) {
+            rs[t] = rs[t + 1];
+            re[t] = re[t + 1];
+            rf[t] = rf[t + 1];
+          }
+          jj = rs[0];
+          je = re[0];
+          jf = rf[0];
+          --left;
+          continue;
+        }
+        const float4 qv = a.sorted[jj++];
+        const float d0 = x0 - qv.x, d1 = x1 - qv.y, d2 = x2 - qv.z;
         const float dd = (d0 * d0 + d1 * d1) + d2 * d2;
         bool ok;
         if (KER == PNR_GATHER_IDW) ok = dd <= a.r2;
         else ok = fabsf(d0) < a.h0 && fabsf(d1) < a.h1 && fabsf(d2) < a.h2;
-        if (!ok) continue;
-        // a colliding bucket holds points of other cells: count each point only in its own cell
-        if (cell_coord(q.x, a.g.o0, a.g.inv) != qx || cell_coord(q.y, a.g.o1, a.g.inv) != qy ||
-            cell_coord(q.z, a.g.o2, a.g.inv) != qz)
-          continue;
-        const int id = __float_as_int(q.w);
-        if (!key_less(dd, id, kd[PNR_MAX_K - 1], ki[PNR_MAX_K - 1])) continue;
-        kd[PNR_MAX_K - 1] = dd;
-        ki[PNR_MAX_K - 1] = id;
+        if (jf & 8) {  // colliding bucket: the point must lie in this probe cell
+          ok = ok && cell_coord(qv.x, a.g.o0, a.g.inv) == bx + (jf & 1) &&
+               cell_coord(qv.y, a.g.o1, a.g.inv) == by + ((jf >> 1) & 1) &&
+               cell_coord(qv.z, a.g.o2, a.g.inv) == bz + ((jf >> 2) & 1);
+        }
+        // branch-free insertion into the sorted top-k list (min/max of float64 keys)
+        double kn = ok ? pack_key(dd, __float_as_int(qv.w)) : kInf;
 #pragma unroll
-        for (int s = PNR_MAX_K - 1; s > 0; --s) {
-          if (key_less(kd[s], ki[s], kd[s - 1], ki[s - 1])) {
-            const float tdd = kd[s]; kd[s] = kd[s - 1]; kd[s - 1] = tdd;
-            const int tid = ki[s]; ki[s] = ki[s - 1]; ki[s - 1] = tid;
-          }
+        for (int t = 0; t < PNR_MAX_K; ++t) {
+          const double lo = fmin(key[t], kn);
+          kn = fmax(key[t], kn);
+          key[t] = lo;
         }
       }
     }
-  }
-  // weights of the first k, normalised by their sequential sum (ascending distance)
-  float wv[PNR_MAX_K];
-  float W = 0.f;
+    // weights of the first k, normalised by their sequential sum (ascending distance)
+    float wv_[PNR_MAX_K];
+    int ki[PNR_MAX_K];
+    float W = 0.f;
 #pragma unroll
-  for (int s = 0; s < PNR_MAX_K; ++s) {
-    float w = 0.f;
-    if (s < a.k && ki[s] != 0x7fffffff) {
-      if (KER == PNR_GATHER_IDW) {
-        w = 1.0f / fmaxf(sqrtf(kd[s]), a.eps);
-      } else {  // per-axis offsets of the kept point (same f32 arithmetic as the search)
-        const float* xi = a.xyz + (int64_t)ki[s] * 3;
-        const float t0 = 1.0f - fabsf(x0 - xi[0]) / a.h0;
-        const float t1 = 1.0f - fabsf(x1 - xi[1]) / a.h1;
-        const float t2 = 1.0f - fabsf(x2 - xi[2]) / a.h2;
-        w = (t0 * t1) * t2;
+    for (int t = 0; t < PNR_MAX_K; ++t) {
+      float w = 0.f;
+      const bool v = t < a.k && key[t] != kInf;
+      ki[t] = v ? key_id(key[t]) : -1;
+      if (v) {
+        if (KER == PNR_GATHER_IDW) {
+          w = 1.0f / fmaxf(sqrtf(key_d2(key[t])), a.eps);
+        } else {  // per-axis offsets of the kept point (same f32 arithmetic as the search)
+          const float* xi = a.xyz + (int64_t)ki[t] * 3;
+          const float t0 = 1.0f - fabsf(x0 - xi[0]) / a.h0;
+          const float t1 = 1.0f - fabsf(x1 - xi[1]) / a.h1;
+          const float t2 = 1.0f - fabsf(x2 - xi[2]) / a.h2;
+          w = (t0 * t1) * t2;
+        }
+      }
+      wv_[t] = w;
+      W = W + w;
+    }
+    const float Wd = W > 0.f ? W : 1.0f;
+    __syncthreads();  // the previous iteration's readers are done with the LDS lists
+    s_row[threadIdx.x] = row;
+#pragma unroll
+    for (int t = 0; t < PNR_MAX_K; ++t) {
+      const float wn = ki[t] >= 0 ? wv_[t] / Wd : 0.f;
+      s_idx[threadIdx.x * PNR_MAX_K + t] = ki[t];
+      s_w[threadIdx.x * PNR_MAX_K + t] = wn;
+      if (row >= 0 && t < a.k && a.idx) {
+        a.idx[(int64_t)row * a.k + t] = ki[t];
+        a.w[(int64_t)row * a.k + t] = wn;
       }
     }
-    wv[s] = w;
-    W = W + w;
-  }
-  const float Wd = W > 0.f ? W : 1.0f;
-#pragma unroll
-  for (int s = 0; s < PNR_MAX_K; ++s) {
-    const bool v = s < a.k && ki[s] != 0x7fffffff;
-    const float wn = v ? wv[s] / Wd : 0.f;
-    s_idx[threadIdx.x * PNR_MAX_K + s] = v ? ki[s] : -1;
-    s_w[threadIdx.x * PNR_MAX_K + s] = wn;
-    if (p < a.rows && s < a.k) {
-      if (a.idx) a.idx[p * a.k + s] = v ? ki[s] : -1;
-      if (a.w) a.w[p * a.k + s] = wn;
-    }
-  }
-  __syncthreads();
-  // feature sum: 8 lanes per sample, lane q owns channels 4q..4q+3 (one 16-B load per neighbour)
-  const int lane = threadIdx.x & 63, wv_ = threadIdx.x >> 6, gq = lane >> 3, q = lane & 7;
+    __syncthreads();
+    // feature sum: 8 lanes per sample, lane q owns channels 4q..4q+3
 #pragma unroll 1
-  for (int rr = 0; rr < 8; ++rr) {
-    const int s = wv_ * 64 + rr * 8 + gq;
-    const int64_t ps = (int64_t)blockIdx.x * 256 + s;
-    if (ps >= a.rows) continue;
-    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int rr = 0; rr < 8; ++rr) {
+      const int sl = wv * 64 + rr * 8 + gq;
+      const int r = s_row[sl];
+      if (r < 0) continue;
+      float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-    for (int kk = 0; kk < PNR_MAX_K; ++kk) {
-      const int id = s_idx[s * PNR_MAX_K + kk];
-      if (id < 0) continue;
-      const float wn = s_w[s * PNR_MAX_K + kk];
-      const float4 f = a.feats4[(int64_t)id * 8 + q];
-      acc.x = acc.x + wn * f.x;
-      acc.y = acc.y + wn * f.y;
-      acc.z = acc.z + wn * f.z;
-      acc.w = acc.w + wn * f.w;
+      for (int kk = 0; kk < PNR_MAX_K; ++kk) {
+        const int id = s_idx[sl * PNR_MAX_K + kk];
+        if (id < 0) continue;
+        const float wn = s_w[sl * PNR_MAX_K + kk];
+        const float4 f = a.feats4[(int64_t)id * 8 + q];
+        acc.x = acc.x + wn * f.x;
+        acc.y = acc.y + wn * f.y;
+        acc.z = acc.z + wn * f.z;
+        acc.w = acc.w + wn * f.w;
+      }
+      reinterpret_cast<float4*>(a.c)[(int64_t)r * 8 + q] = acc;
     }
-    reinterpret_cast<float4*>(a.c)[ps * 8 + q] = acc;
   }
 }
-
 
 // ---------------------------------------------------------------------------------------------
 // Backward
@@ -330,90 +518,95 @@ struct GatherBwdArgs {
   float* g_feats;        // (M,32) += or null
   float* g_p;            // (P,3) or null
   int gp_accum;
+  WorkList wl;           // rows with at least one neighbour
 };
 
+// rows with a neighbour (idx[row][0] >= 0: neighbours are stored nearest first) -> work list
+__global__ __launch_bounds__(256) void k_gather_bwd_probe(GatherBwdArgs a) {
+  const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const bool has = p < a.P && a.idx[p * a.k] >= 0;
+  wl_append(a.wl, has, make_float4(0.f, 0.f, 0.f, __int_as_float((int)p)));
+}
+
+// Half a wave per row: lane c owns channel c, so the feature-gradient atomics of one neighbour
+// are ONE instruction per two rows, each row a whole 128-B line (2 full 64-B atomic requests).
 template <int SRC, int KER>
 __global__ __launch_bounds__(256) void k_gather_bwd(GatherBwdArgs a) {
   PNR_FP_STRICT
-  const int lane = threadIdx.x & 63, wv_ = threadIdx.x >> 6, gq = lane >> 3, q = lane & 7;
+  const int ch = threadIdx.x & 31, half = threadIdx.x >> 5;  // 8 half-waves per block
+  const int64_t nchunk = (a.wl.cap + 255) / 256;
+  for (int64_t task = blockIdx.x; task < kLists * nchunk; task += gridDim.x) {
+    const int rl = (int)(task % kLists);
+    const int64_t j0 = task / kLists * 256;
+    const int64_t n_work = (int64_t)a.wl.cnt[rl * 32];
+    if (j0 >= n_work) continue;  // uniform over the block
+    const int64_t jn = n_work - j0 < 256 ? n_work - j0 : 256;
 #pragma unroll 1
-  for (int rr = 0; rr < 8; ++rr) {
-    const int64_t p = (int64_t)blockIdx.x * 256 + wv_ * 64 + rr * 8 + gq;
-    if (p >= a.P) continue;  // groups of 8 lanes share p: the shuffles below stay inside a group
-    const float4 g = reinterpret_cast<const float4*>(a.g_c)[p * 8 + q];
-    float dots[PNR_MAX_K];
-    float gcd = 0.f;
-    if (a.g_p) {
-      const float4 cv = reinterpret_cast<const float4*>(a.c)[p * 8 + q];
-      gcd = g.x * cv.x + g.y * cv.y + g.z * cv.z + g.w * cv.w;
-    }
+    for (int64_t t = half; t < jn; t += 8) {  // uniform over each half-wave
+      const int64_t p = __float_as_int(a.wl.items[rl * a.wl.cap + j0 + t].w);
+      const float g = a.g_c[p * 32 + ch];
+      float dots[PNR_MAX_K];
+      float gcd = 0.f;
+      if (a.g_p) gcd = g * a.c[p * 32 + ch];
 #pragma unroll
-    for (int kk = 0; kk < PNR_MAX_K; ++kk) {
-      dots[kk] = 0.f;
-      if (kk >= a.k) continue;
-      const int id = a.idx[p * a.k + kk];
-      if (id < 0) continue;
-      const float wn = a.w[p * a.k + kk];
-      if (a.g_feats) {
-        float* gf = a.g_feats + (int64_t)id * 32 + 4 * q;
-        unsafeAtomicAdd(gf + 0, wn * g.x);
-        unsafeAtomicAdd(gf + 1, wn * g.y);
-        unsafeAtomicAdd(gf + 2, wn * g.z);
-        unsafeAtomicAdd(gf + 3, wn * g.w);
+      for (int kk = 0; kk < PNR_MAX_K; ++kk) {
+        dots[kk] = 0.f;
+        if (kk >= a.k) continue;
+        const int id = a.idx[p * a.k + kk];
+        if (id < 0) continue;
+        const float wn = a.w[p * a.k + kk];
+        if (a.g_feats) unsafeAtomicAdd(a.g_feats + (int64_t)id * 32 + ch, wn * g);
+        if (a.g_p) dots[kk] = g * reinterpret_cast<const float*>(a.feats4)[(int64_t)id * 32 + ch];
       }
-      if (a.g_p) {
-        const float4 f = a.feats4[(int64_t)id * 8 + q];
-        dots[kk] = g.x * f.x + g.y * f.y + g.z * f.z + g.w * f.w;
+      if (!a.g_p) continue;
+#pragma unroll
+      for (int m = 1; m < 32; m <<= 1) {  // sums over the 32 channels (xor stays inside the half-wave)
+        gcd += __shfl_xor(gcd, m);
+#pragma unroll
+        for (int kk = 0; kk < PNR_MAX_K; ++kk) dots[kk] += __shfl_xor(dots[kk], m);
       }
-    }
-    if (!a.g_p) continue;
+      if (ch != 0) continue;
+      float x0, x1, x2;
+      if (a.xP) {
+        const float4 xv = a.xP[p];
+        x0 = xv.x; x1 = xv.y; x2 = xv.z;
+      } else {
+        bool inside;
+        load_point<SRC>(a.src, p, x0, x1, x2, inside);
+      }
+      // dL/dp = sum_k wn_k (g.f_k - g.c) (1/w_k) dw_k/dp
+      float gp0 = 0.f, gp1 = 0.f, gp2 = 0.f;
 #pragma unroll
-    for (int m = 1; m < 8; m <<= 1) {
-      gcd += __shfl_xor(gcd, m);
-#pragma unroll
-      for (int kk = 0; kk < PNR_MAX_K; ++kk) dots[kk] += __shfl_xor(dots[kk], m);
-    }
-    if (q != 0) continue;
-    float x0, x1, x2;
-    if (a.xP) {
-      const float4 xv = a.xP[p];
-      x0 = xv.x; x1 = xv.y; x2 = xv.z;
-    } else {
-      bool inside;
-      load_point<SRC>(a.src, p, x0, x1, x2, inside);
-    }
-    // dL/dp = sum_k wn_k (g.f_k - g.c) (1/w_k) dw_k/dp
-    float gp0 = 0.f, gp1 = 0.f, gp2 = 0.f;
-#pragma unroll
-    for (int kk = 0; kk < PNR_MAX_K; ++kk) {
-      if (kk >= a.k) continue;
-      const int id = a.idx[p * a.k + kk];
-      if (id < 0) continue;
-      const float wn = a.w[p * a.k + kk];
-      const float* xi = a.xyz + (int64_t)id * 3;
-      const float d0 = x0 - xi[0], d1 = x1 - xi[1], d2 = x2 - xi[2];
-      const float coef = wn * (dots[kk] - gcd);
-      if (KER == PNR_GATHER_IDW) {
-        const float dd = (d0 * d0 + d1 * d1) + d2 * d2;
-        if (sqrtf(dd) > a.eps) {  // w = 1/|d|: (1/w) dw/dp = -d / |d|^2
-          const float f = -coef / dd;
-          gp0 += f * d0; gp1 += f * d1; gp2 += f * d2;
+      for (int kk = 0; kk < PNR_MAX_K; ++kk) {
+        if (kk >= a.k) continue;
+        const int id = a.idx[p * a.k + kk];
+        if (id < 0) continue;
+        const float wn = a.w[p * a.k + kk];
+        const float* xi = a.xyz + (int64_t)id * 3;
+        const float d0 = x0 - xi[0], d1 = x1 - xi[1], d2 = x2 - xi[2];
+        const float coef = wn * (dots[kk] - gcd);
+        if (KER == PNR_GATHER_IDW) {
+          const float dd = (d0 * d0 + d1 * d1) + d2 * d2;
+          if (sqrtf(dd) > a.eps) {  // w = 1/|d|: (1/w) dw/dp = -d / |d|^2
+            const float f = -coef / dd;
+            gp0 += f * d0; gp1 += f * d1; gp2 += f * d2;
+          }
+        } else {  // w = prod (1 - |d_a|/h_a): (1/w) dw/dp_a = -sign(d_a) / (h_a t_a)
+          const float t0 = 1.0f - fabsf(d0) / a.h0, t1 = 1.0f - fabsf(d1) / a.h1, t2 = 1.0f - fabsf(d2) / a.h2;
+          const float s0 = d0 > 0.f ? 1.f : (d0 < 0.f ? -1.f : 0.f);
+          const float s1 = d1 > 0.f ? 1.f : (d1 < 0.f ? -1.f : 0.f);
+          const float s2 = d2 > 0.f ? 1.f : (d2 < 0.f ? -1.f : 0.f);
+          gp0 -= coef * s0 / (a.h0 * t0);
+          gp1 -= coef * s1 / (a.h1 * t1);
+          gp2 -= coef * s2 / (a.h2 * t2);
         }
-      } else {  // w = prod (1 - |d_a|/h_a): (1/w) dw/dp_a = -sign(d_a) / (h_a t_a)
-        const float t0 = 1.0f - fabsf(d0) / a.h0, t1 = 1.0f - fabsf(d1) / a.h1, t2 = 1.0f - fabsf(d2) / a.h2;
-        const float s0 = d0 > 0.f ? 1.f : (d0 < 0.f ? -1.f : 0.f);
-        const float s1 = d1 > 0.f ? 1.f : (d1 < 0.f ? -1.f : 0.f);
-        const float s2 = d2 > 0.f ? 1.f : (d2 < 0.f ? -1.f : 0.f);
-        gp0 -= coef * s0 / (a.h0 * t0);
-        gp1 -= coef * s1 / (a.h1 * t1);
-        gp2 -= coef * s2 / (a.h2 * t2);
       }
-    }
-    float* o = a.g_p + p * 3;
-    if (a.gp_accum) {
-      o[0] += gp0; o[1] += gp1; o[2] += gp2;
-    } else {
-      o[0] = gp0; o[1] = gp1; o[2] = gp2;
+      float* o = a.g_p + p * 3;
+      if (a.gp_accum) {
+        o[0] += gp0; o[1] += gp1; o[2] += gp2;
+      } else {
+        o[0] = gp0; o[1] = gp1; o[2] = gp2;
+      }
     }
   }
 }
@@ -422,35 +615,41 @@ __global__ __launch_bounds__(256) void k_gather_bwd(GatherBwdArgs a) {
 // Launchers
 // ---------------------------------------------------------------------------------------------
 static bool points_ok(const pnr_points& pts) {
+  const float reach = pts.mode == PNR_GATHER_IDW
+                          ? pts.radius
+                          : fmaxf(pts.spacing[0], fmaxf(pts.spacing[1], pts.spacing[2]));
   return pts.n_points >= 0 && pts.k >= 1 && pts.k <= PNR_MAX_K && pts.table_bits >= 10 && pts.table_bits <= 24 &&
-         pts.index && (pts.mode == PNR_GATHER_IDW || pts.mode == PNR_GATHER_TRILINEAR) && pts.cell > 0.f &&
-         (pts.n_points == 0 || (pts.xyz && pts.feats));
+         pts.index && (pts.mode == PNR_GATHER_IDW || pts.mode == PNR_GATHER_TRILINEAR) && reach > 0.f &&
+         pts.cell >= 2.0f * reach && (pts.n_points == 0 || (pts.xyz && pts.feats));
 }
 
-template <int KER>
-static void gather_mode(int mode, dim3 grid, hipStream_t st, const GatherArgs& a) {
+static void gather_probe(int mode, dim3 grid, hipStream_t st, const GatherArgs& a) {
   switch (mode) {
-    case kPtsF64: hipLaunchKernelGGL((k_gather<kPtsF64, KER>), grid, dim3(256), 0, st, a); break;
-    case kPtsF32: hipLaunchKernelGGL((k_gather<kPtsF32, KER>), grid, dim3(256), 0, st, a); break;
-    case kRaysZ64: hipLaunchKernelGGL((k_gather<kRaysZ64, KER>), grid, dim3(256), 0, st, a); break;
-    default: hipLaunchKernelGGL((k_gather<kRaysZ32, KER>), grid, dim3(256), 0, st, a); break;
+    case kPtsF64: hipLaunchKernelGGL((k_gather_probe<kPtsF64>), grid, dim3(256), 0, st, a); break;
+    case kPtsF32: hipLaunchKernelGGL((k_gather_probe<kPtsF32>), grid, dim3(256), 0, st, a); break;
+    case kRaysZ64: hipLaunchKernelGGL((k_gather_probe<kRaysZ64>), grid, dim3(256), 0, st, a); break;
+    default: hipLaunchKernelGGL((k_gather_probe<kRaysZ32>), grid, dim3(256), 0, st, a); break;
   }
 }
 
+size_t gather_workspace_bytes(int64_t P) { return wl_bytes(P > 0 ? P : 0); }
+
 int launch_gather(const pnr_points& pts, const PointSrc& src, int mode, int64_t P, int64_t rows, float* c,
-                  int32_t* idx, float* w, hipStream_t st) {
-  if (!points_ok(pts) || mode < kPtsF64 || mode > kRaysZ32 || P < 0 || rows < P) return PNR_E_ARG;
+                  int32_t* idx, float* w, void* ws, size_t ws_bytes, hipStream_t st) {
+  if (!points_ok(pts) || mode < kPtsF64 || mode > kRaysZ32 || P < 0 || rows < P || P >= (1ll << 31)) return PNR_E_ARG;
   if (rows == 0) return PNR_OK;
+  if (!ws || ws_bytes < gather_workspace_bytes(P)) return PNR_E_WORKSPACE;
   IndexView v = index_view(pts.index, pts.n_points, pts.table_bits, nullptr);
   GatherArgs a{};
   a.src = src;
   a.P = P;
   a.rows = rows;
   a.g = make_grid(pts);
-  a.start = v.start;
+  a.hdr = v.hdr;
   a.sorted = v.sorted;
   a.feats4 = reinterpret_cast<const float4*>(pts.feats);
   a.xyz = pts.xyz;
+  a.occ = v.occ;
   a.k = pts.k;
   a.r2 = pts.radius * pts.radius;
   a.eps = pts.eps;
@@ -460,10 +659,14 @@ int launch_gather(const pnr_points& pts, const PointSrc& src, int mode, int64_t 
   a.c = c;
   a.idx = idx;
   a.w = w;
-  const dim3 grid((unsigned)((rows + 255) / 256));
+  a.wl = wl_view(ws, P);
+  if (hipMemsetAsync(a.wl.cnt, 0, kLists * 32 * 4, st) != hipSuccess) return (int)hipGetLastError();
   TimingScope ts(kTimeGather, P, st);
-  if (pts.mode == PNR_GATHER_IDW) gather_mode<PNR_GATHER_IDW>(mode, grid, st, a);
-  else gather_mode<PNR_GATHER_TRILINEAR>(mode, grid, st, a);
+  gather_probe(mode, dim3((unsigned)((rows + 255) / 256)), st, a);
+  const int64_t tasks = kLists * ((a.wl.cap + 255) / 256);
+  const dim3 grid((unsigned)(tasks < 2048 ? tasks : 2048));
+  if (pts.mode == PNR_GATHER_IDW) hipLaunchKernelGGL((k_gather_search<PNR_GATHER_IDW>), grid, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((k_gather_search<PNR_GATHER_TRILINEAR>), grid, dim3(256), 0, st, a);
   return hip_status(hipGetLastError());
 }
 
@@ -479,10 +682,12 @@ static void gather_bwd_mode(int mode, dim3 grid, hipStream_t st, const GatherBwd
 
 int launch_gather_bwd(const pnr_points& pts, const PointSrc* src, int mode, const float4* xP, int64_t P,
                       const int32_t* idx, const float* w, const float* c, const float* g_c, float* g_p,
-                      bool gp_accum, hipStream_t st) {
-  if (!points_ok(pts) || P < 0 || (!src && !xP) || mode < kPtsF64 || mode > kRaysZ32) return PNR_E_ARG;
+                      bool gp_accum, void* ws, size_t ws_bytes, hipStream_t st) {
+  if (!points_ok(pts) || P < 0 || (!src && !xP) || mode < kPtsF64 || mode > kRaysZ32 || P >= (1ll << 31))
+    return PNR_E_ARG;
   if (P == 0 || (!pts.g_feats && !g_p)) return PNR_OK;
   if (!idx || !w || !g_c || (g_p && !c)) return PNR_E_ARG;
+  if (!ws || ws_bytes < gather_workspace_bytes(P)) return PNR_E_WORKSPACE;
   GatherBwdArgs a{};
   if (src) a.src = *src;
   a.xP = xP;
@@ -501,8 +706,13 @@ int launch_gather_bwd(const pnr_points& pts, const PointSrc* src, int mode, cons
   a.g_feats = pts.g_feats;
   a.g_p = g_p;
   a.gp_accum = gp_accum ? 1 : 0;
-  const dim3 grid((unsigned)((P + 255) / 256));
+  a.wl = wl_view(ws, P);
+  if (hipMemsetAsync(a.wl.cnt, 0, kLists * 32 * 4, st) != hipSuccess) return (int)hipGetLastError();
+  if (g_p && !gp_accum && hipMemsetAsync(g_p, 0, (size_t)P * 12, st) != hipSuccess) return (int)hipGetLastError();
   TimingScope ts(kTimeGatherBwd, P, st);
+  hipLaunchKernelGGL(k_gather_bwd_probe, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, st, a);
+  const int64_t tasks = kLists * ((a.wl.cap + 255) / 256);
+  const dim3 grid((unsigned)(tasks < 2048 ? tasks : 2048));
   if (pts.mode == PNR_GATHER_IDW) gather_bwd_mode<PNR_GATHER_IDW>(mode, grid, st, a);
   else gather_bwd_mode<PNR_GATHER_TRILINEAR>(mode, grid, st, a);
   return hip_status(hipGetLastError());

@@ -87,9 +87,11 @@ _SIGS = {
                                      c_float, c_int64, c_void_p]),
     'pnr_points_index_bytes': (c_size_t, [c_int64, c_int32]),
     'pnr_points_build': (ctypes.c_int, [PPoints, c_void_p]),
-    'pnr_point_gather': (ctypes.c_int, [PPoints, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p]),
+    'pnr_point_gather_workspace_bytes': (c_size_t, [c_int64]),
+    'pnr_point_gather': (ctypes.c_int, [PPoints, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t,
+                                        c_void_p]),
     'pnr_point_gather_bwd': (ctypes.c_int, [PPoints, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p,
-                                            c_void_p, c_void_p]),
+                                            c_void_p, c_void_p, c_size_t, c_void_p]),
     'pnr_fc_packed_floats': (c_size_t, []),
     'pnr_fc_pack': (ctypes.c_int, [FcPtrArray, c_void_p, c_void_p]),
     'pnr_eval_points_c': (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p,

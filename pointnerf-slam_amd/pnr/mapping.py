@@ -7,7 +7,9 @@ regulation query (:650-655), backward, Adam step with lr = imap_decoders_lr (:54
 
 The decoder parameters live in ONE flat float32 buffer (and so do their grads), so a data-
 parallel caller reduces a single 891 KB buffer per step and Adam is one kernel
-(pnr_adam_step).  `ddp` (pnr.dist.DataParallel) adds the cross-GPU gradient all-reduce and the
+(pnr_adam_step).  With neural points the fc_c tensors and the point features
+join the same buffer (features last, with their own learning rate: a second Adam launch over the
+tail of the buffer), still one all-reduce per step.  `ddp` (pnr.dist.DataParallel) adds the cross-GPU gradient all-reduce and the
 global far clamp; without it the step is single-GPU and bit-identical to the reference order of
 operations of a 1-process Mapper.
 """
@@ -41,12 +43,14 @@ class FlatParams:
 
 
 class Adam:
-    """torch.optim.Adam(lr, betas=(0.9, 0.999), eps=1e-8) over a FlatParams buffer, one launch."""
+    """torch.optim.Adam(lr, betas=(0.9, 0.999), eps=1e-8) over a FlatParams buffer, one launch per
+    learning-rate segment.  `segments` = [(first word, words, lr)], default the whole buffer."""
 
-    def __init__(self, flat: FlatParams, lr: float, betas=(0.9, 0.999), eps=1e-8, on_update=None):
+    def __init__(self, flat: FlatParams, lr: float, betas=(0.9, 0.999), eps=1e-8, on_update=None, segments=None):
         self.flat = flat
         self.on_update = on_update
         self.lr = lr
+        self.segments = segments if segments is not None else [(0, flat.numel, lr)]
         self.b1, self.b2 = betas
         self.eps = eps
         self.m = torch.zeros_like(flat.data)
@@ -57,31 +61,50 @@ class Adam:
         self.step_count += 1
         lib = _lib.load()
         f = self.flat
-        _lib.check(lib.pnr_adam_step(_lib.ptr(f.data), _lib.ptr(f.grad), _lib.ptr(self.m), _lib.ptr(self.v), f.numel,
-                                     self.lr, self.b1, self.b2, self.eps, self.step_count,
-                                     _lib.stream_of(f.data.device)), 'adam_step')
+        st = _lib.stream_of(f.data.device)
+        for a, n, lr in self.segments:
+            _lib.check(lib.pnr_adam_step(_lib.ptr(f.data[a:]), _lib.ptr(f.grad[a:]), _lib.ptr(self.m[a:]),
+                                         _lib.ptr(self.v[a:]), n, lr, self.b1, self.b2, self.eps, self.step_count,
+                                         st), 'adam_step')
         if self.on_update is not None:  # weights changed behind autograd: drop the packed image
             self.on_update()
 
 
 class MapStep:
-    def __init__(self, renderer, decoder, lr=2e-4, w_color_loss=0.05, w_reg=0.0005, ddp=None):
+    def __init__(self, renderer, decoder, lr=2e-4, w_color_loss=0.05, w_reg=0.0005, ddp=None, points=None,
+                 feat_lr=None):
         self.renderer = renderer
         self.decoder = decoder
-        self.flat = FlatParams(decoder.ordered_params())
-        self.opt = Adam(self.flat, lr, on_update=decoder._packed.invalidate)
+        self.points = points
+        params = list(decoder.ordered_params())
+        if points is not None:
+            params += list(decoder.ordered_fc_params())
+        n_dec = sum(p.numel() for p in params)
+        if points is not None:
+            params.append(points.feats)
+        self.flat = FlatParams(params)
+        segs = [(0, n_dec, lr)]
+        if points is not None:
+            segs.append((n_dec, points.feats.numel(), lr if feat_lr is None else feat_lr))
+        self.opt = Adam(self.flat, lr, on_update=self._invalidate, segments=segs)
+        self.c = {} if points is None else {'points_' + getattr(decoder, 'name', ''): points}
         self.w_color = w_color_loss
         self.w_reg = w_reg
         self.ddp = ddp
 
+    def _invalidate(self):
+        self.decoder._packed.invalidate()
+        if self.points is not None:
+            self.decoder._packed_fc.invalidate()
+
     def loss(self, rays_o, rays_d, gt_depth, gt_color, t_rand=None, far_clamp=None):
         r, dec = self.renderer, self.decoder
         dev = rays_o.device
-        d, _, c = r.render_batch_ray({}, dec, rays_d, rays_o, dev, 'color', gt_depth, far_clamp=far_clamp)
+        d, _, c = r.render_batch_ray(self.c, dec, rays_d, rays_o, dev, 'color', gt_depth, far_clamp=far_clamp)
         m = gt_depth > 0
         loss = torch.abs(gt_depth[m] - d[m]).sum()
         loss = loss + self.w_color * torch.abs(gt_color - c).sum()
-        sigma = r.regulation({}, dec, rays_d, rays_o, gt_depth, dev, 'color', t_rand=t_rand)
+        sigma = r.regulation(self.c, dec, rays_d, rays_o, gt_depth, dev, 'color', t_rand=t_rand)
         return loss + self.w_reg * torch.abs(sigma).sum()
 
     def __call__(self, rays_o, rays_d, gt_depth, gt_color, t_rand=None):

@@ -50,15 +50,16 @@ class NeuralPoints(nn.Module):
         self.eps = float(eps)
         self.spacing = [float(v) for v in (spacing if spacing is not None else (radius, radius, radius))]
         reach = self.radius if mode == 'idw' else max(self.spacing)
-        # a cell a hair larger than the reach: float rounding can never put a neighbour 2 cells away
-        self.cell = float(cell) if cell is not None else reach * (1.0 + 1e-4)
-        if self.cell < reach:
-            raise ValueError('pnr.NeuralPoints: cell must be >= the neighbourhood reach')
+        # the search probes the 2x2x2 cells covering [p - reach, p + reach]: cell >= 2 reach, with a
+        # margin so that float rounding of the cell coordinates never misses a neighbour
+        self.cell = float(cell) if cell is not None else 2.0 * reach * (1.0 + 1e-3)
+        if self.cell < 2.0 * reach * (1.0 + 1e-4):
+            raise ValueError('pnr.NeuralPoints: cell must be >= 2 x the neighbourhood reach (+1e-4)')
         if origin is None:
             origin = (xyz.min(0).values - self.cell).tolist() if M > 0 else [0.0, 0.0, 0.0]
         self.origin = [float(v) for v in origin]
-        if table_bits is None:
-            table_bits = min(24, max(10, int(math.ceil(math.log2(max(2 * M, 1))))))
+        if table_bits is None:  # ~2 buckets per occupied cell (a surface cell holds ~4-16 points)
+            table_bits = min(24, max(10, int(math.ceil(math.log2(max(M // 2, 1))))))
         self.table_bits = int(table_bits)
         self._index = None
         self._index_key = None
@@ -149,8 +150,9 @@ class _GatherFn(torch.autograd.Function):
         idx = torch.empty((P, pts.k), device=dev, dtype=torch.int32) if need else None
         w = torch.empty((P, pts.k), device=dev, dtype=torch.float32) if need else None
         s, keep = pts.descriptor()
+        ws = torch.empty(lib.pnr_point_gather_workspace_bytes(P), dtype=torch.uint8, device=dev)
         _lib.check(lib.pnr_point_gather(ctypes.byref(s), _lib.ptr(p), P, _lib.ptr(c), _lib.ptr(idx), _lib.ptr(w),
-                                        _lib.stream_of(dev)), 'point_gather')
+                                        _lib.ptr(ws), ws.numel(), _lib.stream_of(dev)), 'point_gather')
         if need:
             ctx.pts = pts
             ctx.save_for_backward(p, idx, w, c)
@@ -166,9 +168,10 @@ class _GatherFn(torch.autograd.Function):
         g_feats = torch.zeros_like(pts.feats) if ctx.needs_input_grad[2] else None
         g_p = torch.empty((P, 3), device=dev, dtype=torch.float32) if ctx.needs_input_grad[0] else None
         s, keep = pts.descriptor(g_feats=g_feats)
+        ws = torch.empty(lib.pnr_point_gather_workspace_bytes(P), dtype=torch.uint8, device=dev)
         _lib.check(lib.pnr_point_gather_bwd(ctypes.byref(s), _lib.ptr(p), P, _lib.ptr(idx), _lib.ptr(w), _lib.ptr(c),
-                                            _lib.ptr(g_c.contiguous()), _lib.ptr(g_p), _lib.stream_of(dev)),
-                   'point_gather_bwd')
+                                            _lib.ptr(g_c.contiguous()), _lib.ptr(g_p), _lib.ptr(ws), ws.numel(),
+                                            _lib.stream_of(dev)), 'point_gather_bwd')
         return (None if g_p is None else g_p.double(), None, g_feats)
 
 

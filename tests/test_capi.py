@@ -98,6 +98,7 @@ def test_point_queries_and_arg_errors(lib):
     assert L.pnr_points_index_bytes(100000, 9) == 0 and L.pnr_points_index_bytes(-1, 12) == 0
     pts = _lib.Points()
     pts.k, pts.table_bits, pts.cell = 9, 12, 0.1           # k > PNR_MAX_K
-    assert L.pnr_point_gather(ctypes.byref(pts), None, 0, None, None, None, None) == -1
+    assert L.pnr_point_gather(ctypes.byref(pts), None, 0, None, None, None, None, 0, None) == -1
+    assert L.pnr_point_gather_workspace_bytes(1000) >= 16000
     assert L.pnr_points_build(None, None) == -1
     assert L.pnr_eval_points_c(None, None, None, None, 3, None, None, None) == -1

@@ -74,8 +74,9 @@ def test_gather_idw_matches_oracle(pnr_mod, dev, k):
     w = torch.empty((P, k), device=dev)
     qd = q.to(dev)
     s, _ = pts.descriptor()
+    ws = torch.empty(lib.pnr_point_gather_workspace_bytes(P), dtype=torch.uint8, device=dev)
     assert lib.pnr_point_gather(ctypes.byref(s), qd.data_ptr(), P, c.data_ptr(), idx.data_ptr(), w.data_ptr(),
-                                None) == 0
+                                ws.data_ptr(), ws.numel(), None) == 0
     torch.cuda.synchronize()
     c_ref, idx_ref, w_ref = RP.point_gather(q, xyz, feats, 'idw', radius=0.06, k=k, return_idx=True)
     assert (idx_ref >= 0).sum() > P, 'test cloud must give neighbours'

@@ -1,0 +1,107 @@
+"""Point-gather microbenchmark on a neural-point scene.
+
+  python tools/gather_bench.py [--points M] [--rays N] [--radius R] [--reps K] [--mode idw|trilinear]
+
+Scene: neural points on the trained room0 decoder's own rendered surface (640x480 frame at room0
+pose 1000, ScanNet-style intrinsics), voxel-downsampled like Point-NeRF's point initialisation: at
+most one point per voxel of edge `--voxel` (the first pixel landing in it), features N(0, 0.1).
+The gather radius defaults to 2 voxels (~12 points inside it on a surface, k = 8 kept).
+Samples: for N random pixels, 32 stratified depths in [0.01 d, 1.2 d] + 12 around the surface
+(sigma 5 mm), as float64 points -- the sample distribution of one mapping iteration.
+
+Prints per-launch device time of k_gather (hipEvents through pnr_timing_*), the neighbour
+statistics and the algorithmic HBM bytes (SURVEY.md 8(d) with the 8 probes made: per sample 24 B point + 8 x 8 B bucket
+headers + n_nb x (4 B idx + 12 B xyz + 128 B features) + 128 B c + k x 8 B idx/weight saves).
+"""
+import argparse
+import ctypes
+import os
+import sys
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, 'pointnerf-slam_amd'))
+sys.path.insert(0, REPO)
+
+HBM_PEAK_GBS = 8000.0
+
+
+from bench import gather_bytes, neural_point_scene  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--voxel', type=float, default=0.001)
+    ap.add_argument('--rays', type=int, default=640 * 480)
+    ap.add_argument('--radius', type=float, default=None, help='default: 2 voxels')
+    ap.add_argument('--k', type=int, default=8)
+    ap.add_argument('--mode', default='idw')
+    ap.add_argument('--reps', type=int, default=5)
+    args = ap.parse_args()
+    import pnr
+    from pnr._lib import timing_read
+    dev = torch.device('cuda:0')
+    lib = pnr.library()
+    xyz, feats, p, _ = neural_point_scene(dev, args.voxel, args.rays)
+    args.points = xyz.shape[0]
+    if args.radius is None:
+        args.radius = 2 * args.voxel
+    pts = pnr.NeuralPoints(xyz, feats, mode=args.mode, radius=args.radius, k=args.k,
+                           spacing=[args.radius] * 3).to(dev)
+    P = p.shape[0]
+    c = torch.empty((P, 32), device=dev)
+    idx = torch.empty((P, args.k), device=dev, dtype=torch.int32)
+    w = torch.empty((P, args.k), device=dev)
+    s, _ = pts.descriptor()
+    st = pnr._lib.stream_of(dev)
+    ws = torch.empty(lib.pnr_point_gather_workspace_bytes(P), dtype=torch.uint8, device=dev)
+
+    def run():
+        pnr._lib.check(lib.pnr_point_gather(ctypes.byref(s), p.data_ptr(), P, c.data_ptr(), idx.data_ptr(),
+                                            w.data_ptr(), ws.data_ptr(), ws.numel(), st), 'gather')
+
+    run()
+    torch.cuda.synchronize()
+    nb = int((idx >= 0).sum().item())
+    n_work = int(ws[:64 * 32 * 4].view(torch.int32)[::32].sum().item())
+    hist = torch.bincount((idx >= 0).sum(1), minlength=args.k + 1).tolist()
+    lib.pnr_timing_enable(1)
+    timing_read(4)
+    for _ in range(args.reps):
+        run()
+    torch.cuda.synchronize()
+    lib.pnr_timing_enable(0)
+    launches, ms, _ = timing_read(4)
+    avg = ms / launches
+    byt = gather_bytes(P, nb, args.k)
+    gbs = byt / (avg * 1e-3) / 1e9
+    # backward (feature grads + position grads)
+    gf = torch.zeros_like(feats)
+    gc = torch.randn_like(c)
+    gp = torch.empty((P, 3), device=dev)
+    sb, _ = pts.descriptor(g_feats=gf)
+    lib.pnr_timing_enable(1)
+    timing_read(5)
+    for _ in range(args.reps):
+        pnr._lib.check(lib.pnr_point_gather_bwd(ctypes.byref(sb), p.data_ptr(), P, idx.data_ptr(), w.data_ptr(),
+                                                c.data_ptr(), gc.data_ptr(), gp.data_ptr(), ws.data_ptr(), ws.numel(),
+                                                st), 'gather_bwd')
+    torch.cuda.synchronize()
+    lib.pnr_timing_enable(0)
+    bl, bms, _ = timing_read(5)
+    bavg = bms / bl
+    # bwd algorithmic bytes: 24 B point + 128 g_c + 128 c + k*8 idx/w + per neighbour (128 feats + 12 xyz
+    # + 128 B feature-grad atomics) + 12 B g_p
+    bbyt = P * (24 + 128 + 128 + args.k * 8 + 12) + nb * (128 + 12 + 128)
+    print(f'voxel {args.voxel} points {args.points} samples {P} ({args.rays} rays x 44) mode {args.mode} r {args.radius} k {args.k}')
+    print(f'neighbours: mean {nb / P:.2f}/sample, histogram {hist}; samples with candidates {n_work} '
+          f'({100 * n_work / P:.1f}%)')
+    print(f'k_gather     {avg:.3f} ms/launch  {P / avg / 1e6:.1f} Msamples/ms... algorithmic {byt / 1e9:.2f} GB '
+          f'-> {gbs:.0f} GB/s = {gbs / HBM_PEAK_GBS:.3f} of HBM peak')
+    print(f'k_gather_bwd {bavg:.3f} ms/launch  algorithmic {bbyt / 1e9:.2f} GB -> {bbyt / (bavg * 1e-3) / 1e9:.0f} GB/s')
+
+
+if __name__ == '__main__':
+    main()
