@@ -66,6 +66,20 @@ def synth_batch(n, rank, pose, dev, seed=0):
     return (ro.contiguous().to(dev), rd.contiguous().to(dev), gt.to(dev), col.to(dev))
 
 
+def pmc_traffic(kernel, units_per_launch):
+    """HBM bytes per launch of `kernel` from the newest committed PMC measurement
+    (profiles/r*_traffic.json, written from tools/prof_bench.sh's FETCH_SIZE/WRITE_SIZE passes):
+    measured bytes per unit x units per launch, or None."""
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, 'profiles', 'r*_traffic.json')))
+    if not files:
+        return None
+    t = json.load(open(files[-1])).get(kernel)
+    if not t:
+        return None
+    return round((t['fetch_B'] + t['write_B']) * units_per_launch)
+
+
 def neural_point_scene(dev, voxel=0.001, n_rays=W * H, seed=0):
     """Neural points on the trained decoder's own rendered surface at room0 pose 1000 (640x480,
     ScanNet intrinsics), voxel-downsampled like Point-NeRF's point initialisation (at most one
@@ -148,7 +162,8 @@ def gather_roofline(dev, voxel=0.001, k=8, reps=5):
     byt = gather_bytes(P, nb, k)
     gbs = byt / (avg * 1e-3) / 1e9
     return {'bound': 'hbm', 'achieved': round(gbs, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
-            'frac': round(gbs / HBM_PEAK_GBS, 4), 'traffic': None, 'kernel': 'k_gather_probe+k_gather_search',
+            'frac': round(gbs / HBM_PEAK_GBS, 4), 'traffic': pmc_traffic('k_gather', P),
+            'kernel': 'k_gather_probe+k_gather_search',
             'avg_launch_ms': round(avg, 3), 'launches': launches, 'samples': P, 'points': int(xyz.shape[0]),
             'neighbours_per_sample': round(nb / P, 3), 'radius': 2 * voxel, 'k': k,
             'bytes_per_launch': byt}
@@ -280,14 +295,16 @@ def main():
             continue
         fl = FLOP_PER_POINT_FWD if name == 'mlp_fwd' else FLOP_PER_POINT_BWD
         cand = {'kernel': 'k_mlp_fwd' if name == 'mlp_fwd' else 'k_mlp_bwd', 'launches': launches,
-                'avg_ms': ms / launches, 'share_of_step': ms / (el * 1e3),
+                'avg_ms': ms / launches, 'share_of_step': ms / (el * 1e3), 'units': units / launches,
                 'achieved': fl * units / launches / (ms / launches * 1e-3) / 1e12}
         if best is None or ms > best['_ms']:
             best = dict(cand, _ms=ms)
     roofline = None
     if best is not None:
+        traffic = pmc_traffic('k_mlp_fwd_train', best['units']) if best['kernel'] == 'k_mlp_fwd' and \
+            args.workload == 'map' else None
         roofline = {'bound': 'mfma', 'achieved': round(best['achieved'], 2), 'peak': FP32_MFMA_PEAK_TF,
-                    'unit': 'TFLOP/s', 'frac': round(best['achieved'] / FP32_MFMA_PEAK_TF, 4), 'traffic': None,
+                    'unit': 'TFLOP/s', 'frac': round(best['achieved'] / FP32_MFMA_PEAK_TF, 4), 'traffic': traffic,
                     'kernel': best['kernel'], 'avg_launch_ms': round(best['avg_ms'], 3),
                     'launches': best['launches'], 'kernel_share_of_step': round(best['share_of_step'], 3)}
 
