@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define PNR_ABI_VERSION 2
+#define PNR_ABI_VERSION 3
 #define PNR_N_PARAMS 11
 #define PNR_MAX_SAMPLES 64      /* N_samples + N_importance per ray */
 #define PNR_C_DIM 32            /* neural-point feature width (decoder.py:122-125 fc_c input) */
@@ -66,6 +66,21 @@ enum {
  * >= 2 * max(spacing) (TRILINEAR): the search visits the 2x2x2 cells covering [p - reach, p + reach]
  * (a margin of ~1e-3 relative absorbs float rounding). */
 enum { PNR_GATHER_IDW = 0, PNR_GATHER_TRILINEAR = 1 };
+
+/* Arithmetic of the decoder matmuls (build-defined; the reference runs torch fp32 matmuls).
+ *   PNR_PREC_FP32:   v_mfma_f32_32x32x2_f32, an exact fp32 fma chain (bitwise the CPU order per
+ *                    product; only the summation order differs from torch CPU).
+ *   PNR_PREC_BF16X3: every fp32 operand split x = hi + lo into two bf16 parts, W x computed as
+ *                    Wh xh + Wh xl + Wl xh on v_mfma_f32_32x32x16_bf16 with fp32 accumulation:
+ *                    ~2^-16 relative per product (fp32-class), 5.3x the fp32 MFMA rate.
+ *   PNR_PREC_BF16:   plain bf16 operands, fp32 accumulation (BASELINE config C3).
+ *   PNR_PREC_F16X3:  the split of BF16X3 in f16 (22 significant bits, ~2^-21 per product) on
+ *                    v_mfma_f32_32x32x16_f16; the packer scales each weight tensor by a power of
+ *                    two (max |W| s <= 2^14) and the kernel scales the accumulator back exactly.
+ *                    Needs |activations| < 65504 (f16 range).
+ * Fourier features, bias, ReLU, compositing and all float64 work stay fp32 / fp64 in every mode.
+ * The backward (delta chain, weight gradients) runs in fp32 in every mode. */
+enum { PNR_PREC_FP32 = 0, PNR_PREC_BF16X3 = 1, PNR_PREC_BF16 = 2, PNR_PREC_F16X3 = 3 };
 
 typedef struct pnr_points {
   const float* xyz;         /* (M,3) float32 point positions                                  */
@@ -101,6 +116,7 @@ typedef struct pnr_render_params {
   int32_t save_for_backward;       /* keep MLP activations in the workspace for pnr_render_bwd */
   int32_t need_ray_grads;          /* backward also produces dL/drays_o, dL/drays_d (tracking) */
   const pnr_points* points;        /* neural-point features, NULL = the reference decoder (c_dim=0) */
+  int32_t precision;               /* PNR_PREC_* of the decoder matmuls                           */
 } pnr_render_params;
 
 /* ---- library identity -------------------------------------------------------------------- */
@@ -108,27 +124,28 @@ int pnr_abi_version(void);
 const char* pnr_build_info(void);
 
 /* ---- decoder: MLP.forward / eval_points -------------------------------------------------- */
-/* Number of float32 words of the packed (MFMA-fragment-ordered) weight image. */
+/* Number of float32 words of the packed (MFMA-fragment-ordered) weight image: the fp32 fragment
+ * images plus the bf16 split images of the PNR_PREC_BF16X3 / PNR_PREC_BF16 kernels. */
 size_t pnr_mlp_packed_floats(void);
 /* Builds the packed image from the 11 reference tensors (params: host array of device ptrs).
  * Must be re-run after every optimizer step (the image is a pure function of the weights). */
 int pnr_mlp_pack(const float* const* params, float* packed, void* stream);
 
 /* Renderer.eval_points (src/utils/Renderer.py:23-61): raw[P,4] = MLP(p) with raw[:,3] := 100
- * where p is not strictly inside `bound6`.  p float64 (P,3). */
+ * where p is not strictly inside `bound6`.  p float64 (P,3).  `precision`: PNR_PREC_*. */
 int pnr_eval_points(const float* packed, const double* p, int64_t P, const double* bound6,
-                    float* raw_out, void* stream);
+                    float* raw_out, int32_t precision, void* stream);
 /* Same for float32 points (MLP.forward on f32 input, decoder.py:177-203); bound6 may be NULL
  * (then no masking).  The mask comparison is done in float32 as torch does for f32 points. */
 int pnr_eval_points_f32(const float* packed, const float* p, int64_t P, const double* bound6,
-                        float* raw_out, void* stream);
+                        float* raw_out, int32_t precision, void* stream);
 
 /* MLP.forward with autograd (decoder.py:177-203 on float32 points, no bound mask): the forward
  * keeps activations in `ws` (size pnr_mlp_train_workspace_bytes(P)); pnr_mlp_bwd consumes them.
  * g_raw (P,4) float32; grads accumulated (+=); g_p (P,3) written when non-NULL. */
 size_t pnr_mlp_train_workspace_bytes(int64_t P);
 int pnr_mlp_fwd_train(const float* packed, const float* p, int64_t P, float* raw_out, void* ws, size_t ws_bytes,
-                      void* stream);
+                      int32_t precision, void* stream);
 size_t pnr_mlp_bwd_workspace_bytes(int64_t P);
 int pnr_mlp_bwd(const float* packed, int64_t P, const float* g_raw, float* const* grads, float* g_p, void* ws,
                 size_t ws_bytes, void* bwd_ws, size_t bwd_bytes, void* stream);
@@ -154,9 +171,9 @@ int pnr_fc_pack(const float* const* fc_params, float* fc_packed, void* stream);
 /* MLP.forward with per-point features c (P,32): eval (bound6 may be NULL) and training
  * variants.  pnr_mlp_bwd_c also writes g_c (P,32) and accumulates the 8 fc_c grads. */
 int pnr_eval_points_c(const float* packed, const float* fc_packed, const double* p, const float* c, int64_t P,
-                      const double* bound6, float* raw_out, void* stream);
+                      const double* bound6, float* raw_out, int32_t precision, void* stream);
 int pnr_mlp_fwd_train_c(const float* packed, const float* fc_packed, const float* p, const float* c, int64_t P,
-                        float* raw_out, void* ws, size_t ws_bytes, void* stream);
+                        float* raw_out, void* ws, size_t ws_bytes, int32_t precision, void* stream);
 size_t pnr_mlp_bwd_workspace_bytes_c(int64_t P);
 int pnr_mlp_bwd_c(const float* packed, const float* fc_packed, const float* c, int64_t P, const float* g_raw,
                   float* const* grads, float* const* g_fc, float* g_c, float* g_p, void* ws, size_t ws_bytes,

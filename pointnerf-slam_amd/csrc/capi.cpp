@@ -295,37 +295,39 @@ int pnr_timing_read(int kernel, int64_t* launches, double* ms, int64_t* units) {
 }
 
 const char* pnr_build_info(void) {
-  return "libpnr gfx950: fp32 v_mfma_f32_32x32x2_f32 fused decoder, LDS-streamed weights; "
+  return "libpnr gfx950: fused decoder on fp32 v_mfma_f32_32x32x2_f32 or bf16x3 / bf16 v_mfma_f32_32x32x16_bf16, "
+         "LDS-DMA-streamed weights; "
          "thread-per-ray compositing; split-K MFMA weight-gradient GEMMs; spatial-hash neural-point gather";
 }
 
-size_t pnr_mlp_packed_floats(void) { return (size_t)kPackedFloats; }
+size_t pnr_mlp_packed_floats(void) { return (size_t)packed_floats_all(); }
 
 int pnr_mlp_pack(const float* const* params, float* packed, void* stream) {
   if (!check_params(params) || !packed) return PNR_E_ARG;
   RawParams rp;
   for (int i = 0; i < PNR_N_PARAMS; ++i) rp.p[i] = params[i];
-  return launch_pack(rp, packed, (hipStream_t)stream);
+  const int rc = launch_pack(rp, packed, (hipStream_t)stream);
+  return rc ? rc : launch_pack_bf(rp, packed, (hipStream_t)stream);
 }
 
 int pnr_eval_points(const float* packed, const double* p, int64_t P, const double* bound6, float* raw_out,
-                    void* stream) {
+                    int32_t precision, void* stream) {
   if (!packed || P < 0 || (P > 0 && (!p || !raw_out))) return PNR_E_ARG;
   PointSrc s{};
   s.pts = p;
   s.use_bound = bound6 != nullptr;
   if (bound6) memcpy(s.bound, bound6, sizeof(s.bound));
-  return launch_mlp_fwd(packed, s, kPtsF64, P, raw_out, nullptr, (hipStream_t)stream);
+  return mlp_fwd(precision, packed, s, kPtsF64, P, raw_out, nullptr, (hipStream_t)stream);
 }
 
 int pnr_eval_points_f32(const float* packed, const float* p, int64_t P, const double* bound6, float* raw_out,
-                        void* stream) {
+                        int32_t precision, void* stream) {
   if (!packed || P < 0 || (P > 0 && (!p || !raw_out))) return PNR_E_ARG;
   PointSrc s{};
   s.pts = p;
   s.use_bound = bound6 != nullptr;
   if (bound6) memcpy(s.bound, bound6, sizeof(s.bound));
-  return launch_mlp_fwd(packed, s, kPtsF32, P, raw_out, nullptr, (hipStream_t)stream);
+  return mlp_fwd(precision, packed, s, kPtsF32, P, raw_out, nullptr, (hipStream_t)stream);
 }
 
 size_t pnr_mlp_train_workspace_bytes(int64_t P) {
@@ -336,7 +338,7 @@ size_t pnr_mlp_train_workspace_bytes(int64_t P) {
 }
 
 int pnr_mlp_fwd_train(const float* packed, const float* p, int64_t P, float* raw_out, void* ws, size_t ws_bytes,
-                      void* stream) {
+                      int32_t precision, void* stream) {
   if (!packed || P < 0 || (P > 0 && (!p || !raw_out || !ws))) return PNR_E_ARG;
   if (P == 0) return PNR_OK;
   Carver c(ws);
@@ -345,7 +347,7 @@ int pnr_mlp_fwd_train(const float* packed, const float* p, int64_t P, float* raw
   PointSrc s{};
   s.pts = p;
   s.use_bound = 0;
-  return launch_mlp_fwd(packed, s, kPtsF32, P, raw_out, &sv, (hipStream_t)stream);
+  return mlp_fwd(precision, packed, s, kPtsF32, P, raw_out, &sv, (hipStream_t)stream);
 }
 
 size_t pnr_mlp_bwd_workspace_bytes(int64_t P) {
@@ -418,7 +420,7 @@ int pnr_render_fwd(const pnr_render_params* prm, const float* packed, const floa
                        w.gws_bytes, st);
     if (rc) return rc;
   }
-  rc = launch_mlp_fwd(packed, src, kRaysZ64, n * S, w.raw, sv, st, pts ? &fa : nullptr);
+  rc = mlp_fwd(prm->precision, packed, src, kRaysZ64, n * S, w.raw, sv, st, pts ? &fa : nullptr);
   if (rc) return rc;
   double* zi = w.z + n * S;
   float* rawi = w.raw + n * S * 4;
@@ -440,7 +442,7 @@ int pnr_render_fwd(const pnr_render_params* prm, const float* packed, const floa
       if (rc) return rc;
       fa.c = w.c + o * kCDim;
     }
-    rc = launch_mlp_fwd(packed, src, kRaysZ64, n * I, rawi, sv, st, pts ? &fa : nullptr);
+    rc = mlp_fwd(prm->precision, packed, src, kRaysZ64, n * I, rawi, sv, st, pts ? &fa : nullptr);
     if (rc) return rc;
   }
   return launch_fine(*prm, rays_d, w.z, zi, w.raw, rawi, n, depth, var, rgb, w.ord, st);
@@ -560,7 +562,8 @@ int pnr_regulation_fwd(const pnr_render_params* prm, const float* packed, const 
                        w.gws, w.gws_bytes, st);
     if (rc) return rc;
   }
-  rc = launch_mlp_fwd(packed, src, kRaysZ32, P, w.raw, sv ? &w.save : nullptr, st, prm->points ? &fa : nullptr);
+  rc = mlp_fwd(prm->precision, packed, src, kRaysZ32, P, w.raw, sv ? &w.save : nullptr, st,
+               prm->points ? &fa : nullptr);
   if (rc) return rc;
   return launch_extract_sigma(w.raw, P, sigma, st);
 }
@@ -641,28 +644,29 @@ int pnr_point_gather_bwd(const pnr_points* pts, const double* p, int64_t P, cons
                            (hipStream_t)stream);
 }
 
-size_t pnr_fc_packed_floats(void) { return (size_t)kFcPackedFloats; }
+size_t pnr_fc_packed_floats(void) { return (size_t)fc_packed_floats_all(); }
 
 int pnr_fc_pack(const float* const* fc_params, float* fc_packed, void* stream) {
   if (!fc_params || !fc_packed) return PNR_E_ARG;
   for (int i = 0; i < PNR_N_FC_PARAMS; ++i)
     if (!fc_params[i]) return PNR_E_ARG;
-  return launch_fc_pack(fc_params, fc_packed, (hipStream_t)stream);
+  const int rc = launch_fc_pack(fc_params, fc_packed, (hipStream_t)stream);
+  return rc ? rc : launch_fc_pack_bf(fc_params, fc_packed, (hipStream_t)stream);
 }
 
 int pnr_eval_points_c(const float* packed, const float* fc_packed, const double* p, const float* c, int64_t P,
-                      const double* bound6, float* raw_out, void* stream) {
+                      const double* bound6, float* raw_out, int32_t precision, void* stream) {
   if (!packed || !fc_packed || P < 0 || (P > 0 && (!p || !c || !raw_out))) return PNR_E_ARG;
   PointSrc s{};
   s.pts = p;
   s.use_bound = bound6 != nullptr;
   if (bound6) memcpy(s.bound, bound6, sizeof(s.bound));
   FeatArgs fa{fc_packed, c};
-  return launch_mlp_fwd(packed, s, kPtsF64, P, raw_out, nullptr, (hipStream_t)stream, &fa);
+  return mlp_fwd(precision, packed, s, kPtsF64, P, raw_out, nullptr, (hipStream_t)stream, &fa);
 }
 
 int pnr_mlp_fwd_train_c(const float* packed, const float* fc_packed, const float* p, const float* c, int64_t P,
-                        float* raw_out, void* ws, size_t ws_bytes, void* stream) {
+                        float* raw_out, void* ws, size_t ws_bytes, int32_t precision, void* stream) {
   if (!packed || !fc_packed || P < 0 || (P > 0 && (!p || !c || !raw_out || !ws))) return PNR_E_ARG;
   if (P == 0) return PNR_OK;
   Carver cv(ws);
@@ -671,7 +675,7 @@ int pnr_mlp_fwd_train_c(const float* packed, const float* fc_packed, const float
   PointSrc s{};
   s.pts = p;
   FeatArgs fa{fc_packed, c};
-  return launch_mlp_fwd(packed, s, kPtsF32, P, raw_out, &sv, (hipStream_t)stream, &fa);
+  return mlp_fwd(precision, packed, s, kPtsF32, P, raw_out, &sv, (hipStream_t)stream, &fa);
 }
 
 size_t pnr_mlp_bwd_workspace_bytes_c(int64_t P) {

@@ -170,6 +170,21 @@ int launch_mlp_bwd(const float* packed, const BwdArgs& a, int64_t P, hipStream_t
 int launch_pack(const RawParams& rp, float* packed, hipStream_t st);
 int launch_fc_pack(const float* const* fc, float* out, hipStream_t st);
 
+// bf16 split forward (mlp_bf.hip): images appended to the fp32 images in the same buffers
+int64_t packed_floats_all();
+int64_t fc_packed_floats_all();
+int launch_pack_bf(const RawParams& rp, float* packed, hipStream_t st);
+int launch_fc_pack_bf(const float* const* fc, float* out, hipStream_t st);
+// prec = PNR_PREC_BF16X3 / PNR_PREC_BF16 / PNR_PREC_F16X3
+int launch_mlp_fwd_bf(int prec, const float* packed, const PointSrc& src, int mode, int64_t P, float* raw,
+                      const SaveArgs* save, hipStream_t st, const FeatArgs* feat = nullptr);
+// forward dispatch on PNR_PREC_*
+inline int mlp_fwd(int prec, const float* packed, const PointSrc& src, int mode, int64_t P, float* raw,
+                   const SaveArgs* save, hipStream_t st, const FeatArgs* feat = nullptr) {
+  if (prec == PNR_PREC_FP32) return launch_mlp_fwd(packed, src, mode, P, raw, save, st, feat);
+  return launch_mlp_fwd_bf(prec, packed, src, mode, P, raw, save, st, feat);
+}
+
 // ---- neural-point gather (points.hip) --------------------------------------------------------
 // index buffer layout (pnr_points_index_bytes): cell_start[T+1] | count[T] | bucket[M] | slot[M]
 // | scan partials | sorted float4[M] (x, y, z, original index bits) | hdr int4[T] | occupancy bits

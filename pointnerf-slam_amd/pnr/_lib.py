@@ -19,6 +19,18 @@ N_FC_PARAMS = 8
 C_DIM = 32
 MAX_K = 8
 GATHER_IDW, GATHER_TRILINEAR = 0, 1
+# decoder matmul arithmetic (include/pnr.h PNR_PREC_*)
+PRECISIONS = {'fp32': 0, 'bf16x3': 1, 'bf16': 2, 'f16x3': 3}
+# f16x3: fp32-class results (tests/test_gpu_parity.py runs every case under fp32 and f16x3 at the
+# same tolerances) at 2.9x the fp32 MFMA kernel's speed
+DEFAULT_PRECISION = os.environ.get('PNR_PRECISION', 'f16x3')
+
+
+def precision_code(name) -> int:
+    """PNR_PREC_* code of a precision name ('fp32' | 'bf16x3' | 'bf16')."""
+    if name not in PRECISIONS:
+        raise ValueError(f'pnr: unknown decoder precision {name!r} (one of {sorted(PRECISIONS)})')
+    return PRECISIONS[name]
 
 c_void_p = ctypes.c_void_p
 c_int64 = ctypes.c_int64
@@ -44,7 +56,7 @@ class RenderParams(ctypes.Structure):
         ('bound', ctypes.c_double * 6), ('far_clamp', ctypes.c_double),
         ('t_vals', c_float * MAX_SAMPLES), ('u_vals', c_float * MAX_SAMPLES),
         ('save_for_backward', c_int32), ('need_ray_grads', c_int32),
-        ('points', ctypes.POINTER(Points)),
+        ('points', ctypes.POINTER(Points)), ('precision', c_int32),
     ]
 
 
@@ -58,10 +70,11 @@ _SIGS = {
     'pnr_build_info': (ctypes.c_char_p, []),
     'pnr_mlp_packed_floats': (c_size_t, []),
     'pnr_mlp_pack': (ctypes.c_int, [PtrArray, c_void_p, c_void_p]),
-    'pnr_eval_points': (ctypes.c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p]),
-    'pnr_eval_points_f32': (ctypes.c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p]),
+    'pnr_eval_points': (ctypes.c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_int32, c_void_p]),
+    'pnr_eval_points_f32': (ctypes.c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_int32, c_void_p]),
     'pnr_mlp_train_workspace_bytes': (c_size_t, [c_int64]),
-    'pnr_mlp_fwd_train': (ctypes.c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_size_t, c_void_p]),
+    'pnr_mlp_fwd_train': (ctypes.c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_size_t, c_int32,
+                                         c_void_p]),
     'pnr_mlp_bwd_workspace_bytes': (c_size_t, [c_int64]),
     'pnr_mlp_bwd': (ctypes.c_int, [c_void_p, c_int64, c_void_p, PtrArray, c_void_p, c_void_p, c_size_t,
                                    c_void_p, c_size_t, c_void_p]),
@@ -95,9 +108,9 @@ _SIGS = {
     'pnr_fc_packed_floats': (c_size_t, []),
     'pnr_fc_pack': (ctypes.c_int, [FcPtrArray, c_void_p, c_void_p]),
     'pnr_eval_points_c': (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p,
-                                         c_void_p]),
+                                         c_int32, c_void_p]),
     'pnr_mlp_fwd_train_c': (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p,
-                                           c_size_t, c_void_p]),
+                                           c_size_t, c_int32, c_void_p]),
     'pnr_mlp_bwd_workspace_bytes_c': (c_size_t, [c_int64]),
     'pnr_mlp_bwd_c': (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p, PtrArray, FcPtrArray,
                                      c_void_p, c_void_p, c_void_p, c_size_t, c_void_p, c_size_t, c_void_p]),

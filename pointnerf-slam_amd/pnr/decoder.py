@@ -54,7 +54,7 @@ class _MLPFn(torch.autograd.Function):
     """raw = MLP(p) on the HIP path with the fused backward (pnr_mlp_fwd_train / pnr_mlp_bwd)."""
 
     @staticmethod
-    def forward(ctx, p, packed_owner, *params):
+    def forward(ctx, p, packed_owner, prec, *params):
         lib = _lib.load()
         P = p.shape[0]
         packed = packed_owner.image(params)
@@ -64,12 +64,13 @@ class _MLPFn(torch.autograd.Function):
         if need:
             ws = torch.empty(lib.pnr_mlp_train_workspace_bytes(P), dtype=torch.uint8, device=p.device)
             _lib.check(lib.pnr_mlp_fwd_train(_lib.ptr(packed), _lib.ptr(p), P, _lib.ptr(raw), _lib.ptr(ws),
-                                             ws.numel(), st), 'mlp_fwd_train')
+                                             ws.numel(), prec, st), 'mlp_fwd_train')
             ctx.save_for_backward(ws, packed)
             ctx.P = P
             ctx.p_grad = ctx.needs_input_grad[0]
         else:
-            _lib.check(lib.pnr_eval_points_f32(_lib.ptr(packed), _lib.ptr(p), P, None, _lib.ptr(raw), st), 'mlp_fwd')
+            _lib.check(lib.pnr_eval_points_f32(_lib.ptr(packed), _lib.ptr(p), P, None, _lib.ptr(raw), prec, st),
+                       'mlp_fwd')
         return raw
 
     @staticmethod
@@ -85,7 +86,7 @@ class _MLPFn(torch.autograd.Function):
         _lib.check(lib.pnr_mlp_bwd(_lib.ptr(packed), P, _lib.ptr(g_raw.contiguous()), arr, _lib.ptr(gp),
                                    _lib.ptr(ws), ws.numel(), _lib.ptr(bws), bws.numel(), _lib.stream_of(dev)),
                    'mlp_bwd')
-        return (gp, None, *grads)
+        return (gp, None, None, *grads)
 
     shapes = ((3, 93), (256, 93), (256,), (256, 256), (256,), (256, 256), (256,), (256, 256), (256,), (4, 256), (4,))
 
@@ -98,7 +99,7 @@ class _MLPFnC(torch.autograd.Function):
     """raw = MLP(p, c) with per-point features c (P,32) (pnr_mlp_fwd_train_c / pnr_mlp_bwd_c)."""
 
     @staticmethod
-    def forward(ctx, p, c, packed_owner, fc_owner, *tensors):
+    def forward(ctx, p, c, packed_owner, fc_owner, prec, *tensors):
         lib = _lib.load()
         P = p.shape[0]
         params, fc = tensors[:_lib.N_PARAMS], tensors[_lib.N_PARAMS:]
@@ -109,13 +110,13 @@ class _MLPFnC(torch.autograd.Function):
         if any(ctx.needs_input_grad):
             ws = torch.empty(lib.pnr_mlp_train_workspace_bytes(P), dtype=torch.uint8, device=p.device)
             _lib.check(lib.pnr_mlp_fwd_train_c(_lib.ptr(packed), _lib.ptr(fcp), _lib.ptr(p), _lib.ptr(c), P,
-                                               _lib.ptr(raw), _lib.ptr(ws), ws.numel(), st), 'mlp_fwd_train_c')
+                                               _lib.ptr(raw), _lib.ptr(ws), ws.numel(), prec, st), 'mlp_fwd_train_c')
             ctx.save_for_backward(ws, packed, fcp, c)
             ctx.P = P
         else:
             dp = p.double().contiguous()
             _lib.check(lib.pnr_eval_points_c(_lib.ptr(packed), _lib.ptr(fcp), _lib.ptr(dp), _lib.ptr(c), P, None,
-                                             _lib.ptr(raw), st), 'eval_points_c')
+                                             _lib.ptr(raw), prec, st), 'eval_points_c')
         return raw
 
     @staticmethod
@@ -134,7 +135,7 @@ class _MLPFnC(torch.autograd.Function):
         _lib.check(lib.pnr_mlp_bwd_c(_lib.ptr(packed), _lib.ptr(fcp), _lib.ptr(c), P, _lib.ptr(g_raw.contiguous()),
                                      arr, farr, _lib.ptr(gc), _lib.ptr(gp), _lib.ptr(ws), ws.numel(), _lib.ptr(bws),
                                      bws.numel(), _lib.stream_of(dev)), 'mlp_bwd_c')
-        return (gp, gc, None, None, *grads, *g_fc)
+        return (gp, gc, None, None, None, *grads, *g_fc)
 
 
 class MLP(nn.Module):
@@ -165,6 +166,8 @@ class MLP(nn.Module):
                                           for _ in range(n_blocks - 1)])
         self.output_linear = DenseLayer(hidden_size, 4, activation='linear')
         self._packed = PackedMLP()
+        # decoder matmul arithmetic of forward() (pnr extension, not a parameter): 'fp32' | 'bf16x3' | 'bf16'
+        self.precision = _lib.DEFAULT_PRECISION
 
     def ordered_params(self):
         sd = dict(self.named_parameters())
@@ -189,9 +192,10 @@ class MLP(nn.Module):
         if self.c_dim != 0:  # decoder.py:178-181: features first (here: neural-point gather)
             c = find_points(c_grid, self).gather(x)
             xf = x.float().contiguous()
-            return _MLPFnC.apply(xf, c, self._packed, self._packed_fc, *params, *self.ordered_fc_params())
+            return _MLPFnC.apply(xf, c, self._packed, self._packed_fc, _lib.precision_code(self.precision), *params,
+                                 *self.ordered_fc_params())
         x = x.float().contiguous()
-        return _MLPFn.apply(x, self._packed, *params)
+        return _MLPFn.apply(x, self._packed, _lib.precision_code(self.precision), *params)
 
     def __getstate__(self):
         st = self.__dict__.copy()

@@ -210,6 +210,9 @@ class Renderer(object):
         self.nice = False
         self.bound = slam.bound
         self.H, self.W, self.fx, self.fy, self.cx, self.cy = slam.H, slam.W, slam.fx, slam.fy, slam.cx, slam.cy
+        # decoder matmul arithmetic (pnr extension; cfg['pnr']['precision'], default _lib.DEFAULT_PRECISION)
+        self.precision = (cfg.get('pnr') or {}).get('precision', _lib.DEFAULT_PRECISION)
+        _lib.precision_code(self.precision)
         if self.N_surface > 0 or self.occupancy or self.perturb > 0.:
             raise NotImplementedError('pnr.Renderer: N_surface>0 / occupancy / perturb>0 are not on the '
                                       'configs/pointNeRF_slam.yaml path (SURVEY.md section 8)')
@@ -234,6 +237,7 @@ class Renderer(object):
             prm.t_vals[i] = v
         for i, v in enumerate(_linspace_table(prm.n_importance)):
             prm.u_vals[i] = v
+        prm.precision = _lib.precision_code(self.precision)
         return prm
 
     # -- reference API ------------------------------------------------------------------------------
@@ -252,15 +256,16 @@ class Renderer(object):
                 cf = pts.gather(dp)
                 fcp = fc_owner.image(decoders.ordered_fc_params())
                 _lib.check(lib.pnr_eval_points_c(_lib.ptr(packed), _lib.ptr(fcp), _lib.ptr(dp), _lib.ptr(cf), P, bound,
-                                                 _lib.ptr(raw), _lib.stream_of(p.device)), 'eval_points_c')
+                                                 _lib.ptr(raw), _lib.precision_code(self.precision),
+                                                 _lib.stream_of(p.device)), 'eval_points_c')
             return raw
         if p.dtype == torch.float64:
             fn = lib.pnr_eval_points
         else:
             fn = lib.pnr_eval_points_f32
             p = p.float()
-        _lib.check(fn(_lib.ptr(packed), _lib.ptr(p.contiguous()), P, bound, _lib.ptr(raw), _lib.stream_of(p.device)),
-                   'eval_points')
+        _lib.check(fn(_lib.ptr(packed), _lib.ptr(p.contiguous()), P, bound, _lib.ptr(raw),
+                      _lib.precision_code(self.precision), _lib.stream_of(p.device)), 'eval_points')
         return raw
 
     def render_batch_ray(self, c, decoders, rays_d, rays_o, device, stage, gt_depth=None, far_clamp=None):

@@ -43,9 +43,10 @@ def test_python_binding_covers_header():
 
 def test_host_only_calls(lib):
     lib.pnr_abi_version.restype = ctypes.c_int
-    assert lib.pnr_abi_version() == 2
+    assert lib.pnr_abi_version() == 3
     lib.pnr_mlp_packed_floats.restype = ctypes.c_size_t
-    assert lib.pnr_mlp_packed_floats() == 486688
+    # fp32 images 486,688 + bf16x3 / bf16 / f16x3 streams 229,376 / 118,784 / 229,376 + raw table 2,048
+    assert lib.pnr_mlp_packed_floats() == 486688 + 229376 + 118784 + 229376 + 2048
     lib.pnr_build_info.restype = ctypes.c_char_p
     assert b'gfx950' in lib.pnr_build_info()
 
@@ -55,7 +56,8 @@ def test_params_struct_layout():
     sys.path.insert(0, os.path.join(REPO, 'pointnerf-slam_amd'))
     from pnr import _lib
     # int32 x4, double[6], double, float[64] x2, int32 x2, pointer -> 600 bytes with natural alignment
-    assert ctypes.sizeof(_lib.RenderParams) == 600
+    assert ctypes.sizeof(_lib.RenderParams) == 608
+    assert _lib.RenderParams.precision.offset == 600
     assert _lib.RenderParams.bound.offset == 16 and _lib.RenderParams.t_vals.offset == 72
     assert _lib.RenderParams.points.offset == 592
     # pnr_points: 2 ptr, int64, 2 int32, 2 float, float[3], float, float[3], int32, 4 ptr
@@ -81,10 +83,10 @@ def test_workspace_queries_and_arg_errors(lib):
     assert L.pnr_render_workspace_bytes(ctypes.byref(bad), 10) == 0
     # argument errors are reported without touching the device
     assert L.pnr_render_fwd(ctypes.byref(bad), None, None, None, None, 10, None, None, None, None, 0, None) == -1
-    assert L.pnr_eval_points(None, None, 5, None, None, None) == -1
+    assert L.pnr_eval_points(None, None, 5, None, None, 0, None) == -1
     assert L.pnr_adam_step(None, None, None, None, 5, 1e-3, 0.9, 0.999, 1e-8, 0, None) == -1
     # zero-sized calls are no-ops
-    assert L.pnr_eval_points(ctypes.c_void_p(1), None, 0, None, None, None) == 0
+    assert L.pnr_eval_points(ctypes.c_void_p(1), None, 0, None, None, 0, None) == 0
 
 
 def test_point_queries_and_arg_errors(lib):
@@ -92,7 +94,7 @@ def test_point_queries_and_arg_errors(lib):
     sys.path.insert(0, os.path.join(REPO, 'pointnerf-slam_amd'))
     from pnr import _lib
     L = _lib.load()
-    assert L.pnr_fc_packed_floats() == 12 * 8192
+    assert L.pnr_fc_packed_floats() == 12 * 8192 + 3 * 32768 + 2048  # fp32 + three 16-bit images + raw
     b20 = L.pnr_points_index_bytes(100000, 20)
     assert b20 >= (2 * (1 << 20) + 2 * 100000) * 4 + 100000 * 16
     assert L.pnr_points_index_bytes(100000, 9) == 0 and L.pnr_points_index_bytes(-1, 12) == 0
@@ -101,4 +103,4 @@ def test_point_queries_and_arg_errors(lib):
     assert L.pnr_point_gather(ctypes.byref(pts), None, 0, None, None, None, None, 0, None) == -1
     assert L.pnr_point_gather_workspace_bytes(1000) >= 16000
     assert L.pnr_points_build(None, None) == -1
-    assert L.pnr_eval_points_c(None, None, None, None, 3, None, None, None) == -1
+    assert L.pnr_eval_points_c(None, None, None, None, 3, None, None, 0, None) == -1

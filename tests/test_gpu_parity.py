@@ -18,6 +18,15 @@ from conftest import load_golden, golden_params
 
 pytestmark = pytest.mark.gpu
 
+
+@pytest.fixture(autouse=True, params=['fp32', 'f16x3'])
+def precision(request, monkeypatch):
+    """Every GPU test runs under both decoder precisions (include/pnr.h PNR_PREC_*): the exact
+    fp32 MFMA path and the f16x3 split path (the default), against the same tolerances."""
+    from pnr import _lib
+    monkeypatch.setattr(_lib, 'DEFAULT_PRECISION', request.param)
+    return request.param
+
 CASES = [f'p{i}_{c}' for i in range(4) for c in ('none', 'gt', 'gtzero')] + ['rand_none', 'edge_none']
 
 
@@ -55,7 +64,7 @@ def close(a, b, rtol, atol, what):
 
 def test_library_info(pnr_mod):
     lib = pnr_mod.library()
-    assert lib.pnr_abi_version() == 2
+    assert lib.pnr_abi_version() == 3
     assert lib.pnr_mlp_packed_floats() > 0
 
 
@@ -223,18 +232,43 @@ def test_batch_invariance_with_global_far(pnr_mod, dev, scene):
     assert torch.isfinite(d).all() and torch.isfinite(c).all()
 
 
-def test_psnr_vs_oracle_frame(pnr_mod, dev, scene):
-    """PSNR(HIP render, oracle render) on a strided 170x300 sub-frame of room0 pose 1000: far
-    above the 39 dB margin that bounds the PSNR delta vs ground truth by 0.1 dB (SURVEY 8d)."""
+@pytest.fixture(scope='module')
+def oracle_frame(scene):
+    """Oracle render of a strided 170x300 sub-frame of room0 pose 1000 (trained decoder)."""
     from oracle import ref_render as ref
     params = golden_params('trained')
-    dec = make_decoder(pnr_mod, params, dev)
-    r = make_renderer(pnr_mod, scene)
     c2w = torch.from_numpy(scene['poses'][2])
     ro, rd = ref.full_frame_rays(680, 1200, 600., 600., 599.5, 339.5, c2w)
     ro, rd = ro[::4, ::4].reshape(-1, 3).contiguous(), rd[::4, ::4].reshape(-1, 3).contiguous()
     torch.set_num_threads(max(1, min(16, torch.get_num_threads())))
     dr, vr, cr = ref.render_batch_ray(params, rd, ro, scene['bound_t'])
+    return params, ro, rd, dr, vr, cr
+
+
+def test_psnr_bf16_frame(pnr_mod, dev, scene, oracle_frame):
+    """BASELINE config C3 (bf16 MLP on MFMA): PSNR(HIP bf16 render, oracle fp32 render) on the
+    same sub-frame.  bf16 operands are not fp32-faithful; the bar is the 0.1 dB PSNR budget, shown
+    here as a PSNR against the fp32 render far above the frame's own PSNR scale (> 50 dB)."""
+    from oracle import ref_render as ref
+    params, ro, rd, dr, vr, cr = oracle_frame
+    dec = make_decoder(pnr_mod, params, dev)
+    dec.precision = 'bf16'
+    r = make_renderer(pnr_mod, scene)
+    r.precision = 'bf16'
+    with torch.no_grad():
+        d, v, c = r.render_batch_ray({}, dec, rd.to(dev), ro.to(dev), dev, 'color')
+    p = ref.psnr(c.cpu().clamp(0, 1), cr.clamp(0, 1))
+    print(f'PSNR(bf16 HIP, fp32 oracle) = {p:.2f} dB')
+    assert p > 50.0, p
+
+
+def test_psnr_vs_oracle_frame(pnr_mod, dev, scene, oracle_frame):
+    """PSNR(HIP render, oracle render) on a strided 170x300 sub-frame of room0 pose 1000: far
+    above the 39 dB margin that bounds the PSNR delta vs ground truth by 0.1 dB (SURVEY 8d)."""
+    from oracle import ref_render as ref
+    params, ro, rd, dr, vr, cr = oracle_frame
+    dec = make_decoder(pnr_mod, params, dev)
+    r = make_renderer(pnr_mod, scene)
     with torch.no_grad():
         d, v, c = r.render_batch_ray({}, dec, rd.to(dev), ro.to(dev), dev, 'color')
     p = ref.psnr(c.cpu().clamp(0, 1), cr.clamp(0, 1))

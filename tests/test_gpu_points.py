@@ -17,6 +17,15 @@ from oracle import ref_render as RR
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True, params=['fp32', 'f16x3'])
+def precision(request, monkeypatch):
+    """Every GPU test runs under both decoder precisions (include/pnr.h PNR_PREC_*): the exact
+    fp32 MFMA path and the f16x3 split path (the default), against the same tolerances."""
+    from pnr import _lib
+    monkeypatch.setattr(_lib, 'DEFAULT_PRECISION', request.param)
+    return request.param
+
+
 @pytest.fixture(scope='module')
 def dev():
     if not torch.cuda.is_available():

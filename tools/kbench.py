@@ -20,6 +20,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--points', type=int, default=4 * 1024 * 1024)
     ap.add_argument('--reps', type=int, default=5)
+    ap.add_argument('--precision', default='fp32,bf16x3,bf16')
     args = ap.parse_args()
     import pnr
     from pnr._lib import timing_read
@@ -44,25 +45,34 @@ def main():
         print(f'{name:34s} launches={n:3d} mean_ms={ms / max(n, 1):9.3f} TF/s={tf:7.2f} frac={tf / 157.3:.3f}',
               flush=True)
 
-    # forward, inference (no save)
-    r.eval_points(pts, dec)
-    torch.cuda.synchronize()
-    lib.pnr_timing_enable(1)
-    timing_read(0)
-    for _ in range(args.reps):
-        r.eval_points(pts, dec)
-    torch.cuda.synchronize()
-    report('k_mlp_fwd eval (f64 pts, no save)', 0, 443438)
-    # forward with save + backward (MLP autograd path)
-    x = pts.float().requires_grad_(False)
-    timing_read(0), timing_read(1)
-    for _ in range(args.reps):
-        out = dec(x)
-        out.sum().backward()
-    torch.cuda.synchronize()
-    report('k_mlp_fwd train (save)', 0, 443438)
-    report('k_mlp_bwd delta chain', 1, 442880)
-    lib.pnr_timing_enable(0)
+    ref = None
+    for prec in args.precision.split(','):
+        r.precision = prec
+        dec.precision = prec
+        # forward, inference (no save)
+        out = r.eval_points(pts, dec)
+        torch.cuda.synchronize()
+        if ref is None:
+            ref = out.clone()
+        err = ((out - ref).abs() / (ref.abs() + 1e-3)).max().item()
+        rel = ((out - ref).abs().max() / ref.abs().max()).item()
+        print(f'[{prec}] eval vs first precision: max rel err {err:.3e}, max abs/max {rel:.3e}', flush=True)
+        lib.pnr_timing_enable(1)
+        timing_read(0)
+        for _ in range(args.reps):
+            r.eval_points(pts, dec)
+        torch.cuda.synchronize()
+        report(f'[{prec}] k_mlp_fwd eval (f64 pts)', 0, 443438)
+        # forward with save + backward (MLP autograd path)
+        x = pts.float().requires_grad_(False)
+        timing_read(0), timing_read(1)
+        for _ in range(args.reps):
+            out = dec(x)
+            out.sum().backward()
+        torch.cuda.synchronize()
+        report(f'[{prec}] k_mlp_fwd train (save)', 0, 443438)
+        report(f'[{prec}] k_mlp_bwd delta chain', 1, 442880)
+        lib.pnr_timing_enable(0)
 
 
 if __name__ == '__main__':
