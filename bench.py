@@ -34,6 +34,11 @@ sys.path.insert(0, REPO)
 
 METRIC = 'rendered rays/sec per mapping iter (Replica room0); PSNR Δ vs ref ≤0.1 dB'
 FP32_MFMA_PEAK_TF = 157.3          # MI355X_MICROARCH.md: f32 MFMA dense = f32 vector peak
+F16_MFMA_PEAK_TF = 2500.0          # MI355X_MICROARCH.md: f16/bf16 MFMA dense (~2.5 PF, no sparsity)
+# Peak of the ALGORITHMIC (fp32-equivalent) FLOP rate per decoder precision: a split form runs
+# 3 f16/bf16 MFMA products per fp32 product (include/pnr.h PNR_PREC_*)
+ALGO_PEAK_TF = {'fp32': FP32_MFMA_PEAK_TF, 'f16x3': F16_MFMA_PEAK_TF / 3, 'bf16x3': F16_MFMA_PEAK_TF / 3,
+                'bf16': F16_MFMA_PEAK_TF}
 HBM_PEAK_GBS = 8000.0
 FLOP_PER_POINT_FWD = 443438        # 2 x (279 + 23,808 + 3 x 65,536 + 1,024) MAC
 FLOP_PER_POINT_BWD = 442880        # delta chain: 2 x (1,024 + 3 x 65,536 + 23,808) MAC
@@ -210,12 +215,18 @@ def main():
     ap.add_argument('--rays', type=int, default=W * H, help='rays per GPU per step')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-gather', action='store_true', help='skip the point-gather roofline line')
+    ap.add_argument('--precision', default=None, help="decoder forward matmuls: fp32 | f16x3 (default) | bf16x3 | bf16")
     args = ap.parse_args()
 
     import pnr
+    from pnr import _lib as plib
     from pnr import dist as pdist
     from pnr._lib import timing_read
     from pnr.mapping import MapStep
+    if args.precision is not None:
+        plib.precision_code(args.precision)
+        plib.DEFAULT_PRECISION = args.precision
+    prec = plib.DEFAULT_PRECISION
 
     rank, world, local = pdist.init()
     dev = torch.device('cuda', local % torch.cuda.device_count())
@@ -294,19 +305,25 @@ def main():
         if launches == 0 or name not in ('mlp_fwd', 'mlp_bwd'):
             continue
         fl = FLOP_PER_POINT_FWD if name == 'mlp_fwd' else FLOP_PER_POINT_BWD
-        cand = {'kernel': 'k_mlp_fwd' if name == 'mlp_fwd' else 'k_mlp_bwd', 'launches': launches,
+        kprec = prec if name == 'mlp_fwd' else 'fp32'  # the delta chain is fp32 in every mode
+        cand = {'kernel': ('k_mlp_fwd16' if prec != 'fp32' else 'k_mlp_fwd') if name == 'mlp_fwd' else 'k_mlp_bwd',
+                'launches': launches, 'prec': kprec, 'peak': ALGO_PEAK_TF[kprec],
                 'avg_ms': ms / launches, 'share_of_step': ms / (el * 1e3), 'units': units / launches,
                 'achieved': fl * units / launches / (ms / launches * 1e-3) / 1e12}
         if best is None or ms > best['_ms']:
             best = dict(cand, _ms=ms)
     roofline = None
     if best is not None:
-        traffic = pmc_traffic('k_mlp_fwd_train', best['units']) if best['kernel'] == 'k_mlp_fwd' and \
-            args.workload == 'map' else None
-        roofline = {'bound': 'mfma', 'achieved': round(best['achieved'], 2), 'peak': FP32_MFMA_PEAK_TF,
-                    'unit': 'TFLOP/s', 'frac': round(best['achieved'] / FP32_MFMA_PEAK_TF, 4), 'traffic': traffic,
+        tkey = {'k_mlp_fwd': 'k_mlp_fwd_train', 'k_mlp_fwd16': 'k_mlp_fwd16_train', 'k_mlp_bwd': 'k_mlp_bwd'}
+        traffic = pmc_traffic(tkey[best['kernel']], best['units']) if args.workload == 'map' else None
+        roofline = {'bound': 'mfma', 'achieved': round(best['achieved'], 2), 'peak': round(best['peak'], 1),
+                    'unit': 'TFLOP/s', 'frac': round(best['achieved'] / best['peak'], 4), 'traffic': traffic,
                     'kernel': best['kernel'], 'avg_launch_ms': round(best['avg_ms'], 3),
-                    'launches': best['launches'], 'kernel_share_of_step': round(best['share_of_step'], 3)}
+                    'launches': best['launches'], 'kernel_share_of_step': round(best['share_of_step'], 3),
+                    'flop_basis': 'algorithmic fp32-equivalent FLOP (443,438 fwd / 442,880 bwd per point); peak = '
+                                  + ('fp32 MFMA 157.3 TF' if best['prec'] == 'fp32' else
+                                     'f16/bf16 MFMA 2.5 PF dense / 3 products per fp32 product'
+                                     if best['prec'] != 'bf16' else 'bf16 MFMA 2.5 PF dense')}
 
     if rank == 0:
         cpu = None
@@ -320,12 +337,15 @@ def main():
         out = {
             'metric': METRIC, 'value': round(value, 1), 'unit': 'rays/s', 'n_gpus': world, 'steps': args.steps,
             'warmup': args.warmup, 'ms_per_step': round(ms_per_step, 3), 'higher_is_better': True, 'scaling': 'weak',
-            'vs_baseline': None, 'dtype': 'fp32',
+            'vs_baseline': None,
+            'dtype': {'fp32': 'fp32', 'f16x3': 'fp32-class: f16x3 split MFMA forward (fp32 accumulate) + fp32 backward',
+                      'bf16x3': 'bf16x3 split MFMA forward (fp32 accumulate) + fp32 backward',
+                      'bf16': 'bf16 MFMA forward (fp32 accumulate) + fp32 backward'}[prec],
             'data': 'synthetic (640x480 ScanNet-intrinsics rays at room0 pose 1000, U[0.05,0.6] gt depth, trained '
                     'room0 decoder fixture)',
             'config': {'workload': wl_name,
                        'rays_per_gpu': n, 'global_batch': n * world, 'samples_per_ray': samples,
-                       'parallelism': f'dp{world}'},
+                       'parallelism': f'dp{world}', 'decoder_precision': prec},
             'roofline': roofline, 'cpu_baseline': cpu,
             'kernels': {k: {'launches': v[0], 'ms': round(v[1], 3), 'units': v[2]} for k, v in kt.items()},
         }

@@ -79,7 +79,8 @@ enum { PNR_GATHER_IDW = 0, PNR_GATHER_TRILINEAR = 1 };
  *                    two (max |W| s <= 2^14) and the kernel scales the accumulator back exactly.
  *                    Needs |activations| < 65504 (f16 range).
  * Fourier features, bias, ReLU, compositing and all float64 work stay fp32 / fp64 in every mode.
- * The backward (delta chain, weight gradients) runs in fp32 in every mode. */
+ * Backward: PNR_PREC_FP32 runs the delta chain on fp32 MFMA; every other mode runs it as bf16x3
+ * (bf16 parts keep the fp32 exponent range of tiny gradients).  Weight-gradient GEMMs are fp32. */
 enum { PNR_PREC_FP32 = 0, PNR_PREC_BF16X3 = 1, PNR_PREC_BF16 = 2, PNR_PREC_F16X3 = 3 };
 
 typedef struct pnr_points {
@@ -148,7 +149,7 @@ int pnr_mlp_fwd_train(const float* packed, const float* p, int64_t P, float* raw
                       int32_t precision, void* stream);
 size_t pnr_mlp_bwd_workspace_bytes(int64_t P);
 int pnr_mlp_bwd(const float* packed, int64_t P, const float* g_raw, float* const* grads, float* g_p, void* ws,
-                size_t ws_bytes, void* bwd_ws, size_t bwd_bytes, void* stream);
+                size_t ws_bytes, void* bwd_ws, size_t bwd_bytes, int32_t precision, void* stream);
 
 /* ---- neural points ------------------------------------------------------------------------ */
 size_t pnr_points_index_bytes(int64_t n_points, int32_t table_bits);
@@ -177,7 +178,7 @@ int pnr_mlp_fwd_train_c(const float* packed, const float* fc_packed, const float
 size_t pnr_mlp_bwd_workspace_bytes_c(int64_t P);
 int pnr_mlp_bwd_c(const float* packed, const float* fc_packed, const float* c, int64_t P, const float* g_raw,
                   float* const* grads, float* const* g_fc, float* g_c, float* g_p, void* ws, size_t ws_bytes,
-                  void* bwd_ws, size_t bwd_bytes, void* stream);
+                  void* bwd_ws, size_t bwd_bytes, int32_t precision, void* stream);
 
 /* ---- render_batch_ray (src/utils/Renderer.py:63-203) ------------------------------------- */
 size_t pnr_render_workspace_bytes(const pnr_render_params* prm, int64_t n_rays);

@@ -204,7 +204,7 @@ __global__ void k_fill(float* p, int64_t n, float v) {
 }
 
 // Shared backward core over P points with saved activations `sv` and dL/draw in b.g_out.
-int mlp_backward_core(const float* packed, const SaveArgs& sv, int64_t P, BwdWS& b, float* const* grads,
+int mlp_backward_core(int prec, const float* packed, const SaveArgs& sv, int64_t P, BwdWS& b, float* const* grads,
                       bool want_gx, hipStream_t st, const FeatBwd* fb = nullptr) {
   for (int64_t p0 = 0; p0 < P; p0 += b.C) {
     const int64_t C = (P - p0) < b.C ? (P - p0) : b.C;
@@ -221,7 +221,8 @@ int mlp_backward_core(const float* packed, const SaveArgs& sv, int64_t P, BwdWS&
     a.fcw = fb ? fb->fcw : nullptr;
     a.gH = b.gH;
     a.g_c = fb ? b.g_c + p0 * kCDim : nullptr;
-    int rc = launch_mlp_bwd(packed, a, C, st);
+    // the delta chain: exact fp32 MFMA for PNR_PREC_FP32, bf16x3 split MFMA otherwise
+    int rc = prec == PNR_PREC_FP32 ? launch_mlp_bwd(packed, a, C, st) : launch_mlp_bwd_bf(packed, a, C, st);
     if (rc) return rc;
     const float* hp = sv.hP + p0 * kHidden;  // h_l rows of this chunk: hp + l_idx * ld * 256
     const int64_t hstride = sv.ld * kHidden;
@@ -358,7 +359,7 @@ size_t pnr_mlp_bwd_workspace_bytes(int64_t P) {
 }
 
 int pnr_mlp_bwd(const float* packed, int64_t P, const float* g_raw, float* const* grads, float* g_p, void* ws,
-                size_t ws_bytes, void* bwd_ws, size_t bwd_bytes, void* stream) {
+                size_t ws_bytes, void* bwd_ws, size_t bwd_bytes, int32_t precision, void* stream) {
   if (!packed || P < 0 || (P > 0 && (!g_raw || !grads || !ws || !bwd_ws))) return PNR_E_ARG;
   if (P == 0) return PNR_OK;
   for (int i = 0; i < PNR_N_PARAMS; ++i)
@@ -372,7 +373,7 @@ int pnr_mlp_bwd(const float* packed, int64_t P, const float* g_raw, float* const
   if (hipMemsetAsync(b.g_out, 0, (size_t)sv.ld * 16, st) != hipSuccess) return (int)hipGetLastError();
   if (hipMemcpyAsync(b.g_out, g_raw, (size_t)P * 16, hipMemcpyDeviceToDevice, st) != hipSuccess)
     return (int)hipGetLastError();
-  int rc = mlp_backward_core(packed, sv, sv.ld, b, grads, g_p != nullptr, st);
+  int rc = mlp_backward_core(precision, packed, sv, sv.ld, b, grads, g_p != nullptr, st);
   if (rc) return rc;
   if (g_p && hipMemcpyAsync(g_p, b.g_x, (size_t)P * 12, hipMemcpyDeviceToDevice, st) != hipSuccess)
     return (int)hipGetLastError();
@@ -484,7 +485,8 @@ int pnr_render_bwd(const pnr_render_params* prm, const float* packed, const floa
                            g_depth, g_var, g_rgb, b.g_out, b.g_out + pc * 4, b.g_nrm, st);
   if (rc) return rc;
   FeatBwd fb{pts ? pts->fc_packed : nullptr, w.c, pts ? pts->g_fc : nullptr};
-  rc = mlp_backward_core(packed, w.save, ld, b, grads, prm->need_ray_grads != 0, st, pts ? &fb : nullptr);
+  rc = mlp_backward_core(prm->precision, packed, w.save, ld, b, grads, prm->need_ray_grads != 0, st,
+                         pts ? &fb : nullptr);
   if (rc) return rc;
   if (pts) {  // neural-point features and dL/dp through the gather weights
     rc = launch_gather_bwd(*pts, nullptr, kRaysZ64, w.save.xP, ld, w.nidx, w.nw, w.c, b.g_c,
@@ -599,7 +601,8 @@ int pnr_regulation_bwd(const pnr_render_params* prm, const float* packed, const 
   int rc = launch_gout_sigma(g_sigma, w.save.xP, P, b.g_out, st);
   if (rc) return rc;
   FeatBwd fb{pts ? pts->fc_packed : nullptr, w.c, pts ? pts->g_fc : nullptr};
-  rc = mlp_backward_core(packed, w.save, ld, b, grads, prm->need_ray_grads != 0, st, pts ? &fb : nullptr);
+  rc = mlp_backward_core(prm->precision, packed, w.save, ld, b, grads, prm->need_ray_grads != 0, st,
+                         pts ? &fb : nullptr);
   if (rc) return rc;
   if (pts) {
     rc = launch_gather_bwd(*pts, nullptr, kRaysZ32, w.save.xP, ld, w.nidx, w.nw, w.c, b.g_c,
@@ -687,7 +690,7 @@ size_t pnr_mlp_bwd_workspace_bytes_c(int64_t P) {
 
 int pnr_mlp_bwd_c(const float* packed, const float* fc_packed, const float* c, int64_t P, const float* g_raw,
                   float* const* grads, float* const* g_fc, float* g_c, float* g_p, void* ws, size_t ws_bytes,
-                  void* bwd_ws, size_t bwd_bytes, void* stream) {
+                  void* bwd_ws, size_t bwd_bytes, int32_t precision, void* stream) {
   if (!packed || !fc_packed || P < 0 || (P > 0 && (!c || !g_raw || !grads || !g_fc || !ws || !bwd_ws))) return PNR_E_ARG;
   if (P == 0) return PNR_OK;
   for (int i = 0; i < PNR_N_PARAMS; ++i)
@@ -705,7 +708,7 @@ int pnr_mlp_bwd_c(const float* packed, const float* fc_packed, const float* c, i
     return (int)hipGetLastError();
   // the fc_c GEMMs read c rows up to the padded row count: run them over the real rows only
   FeatBwd fb{fc_packed, c, g_fc};
-  int rc = mlp_backward_core(packed, sv, P, b, grads, g_p != nullptr, st, &fb);
+  int rc = mlp_backward_core(precision, packed, sv, P, b, grads, g_p != nullptr, st, &fb);
   if (rc) return rc;
   if (g_c && hipMemcpyAsync(g_c, b.g_c, (size_t)P * kCDim * 4, hipMemcpyDeviceToDevice, st) != hipSuccess)
     return (int)hipGetLastError();

@@ -1,4 +1,4 @@
-// mlp_bf.hip -- decoder forward on the 16-bit matrix cores (v_mfma_f32_32x32x16_{f16,bf16}).
+// mlp16.h -- decoder forward on the 16-bit matrix cores (v_mfma_f32_32x32x16_{f16,bf16}).
 //
 // Same math as k_mlp_fwd (mlp.hip; src/conv_onet/models/decoder.py:177-203 plus the bound mask of
 // src/utils/Renderer.py:43-57 and the fc_c feature branch of decoder.py:196-197), three precisions
@@ -28,6 +28,7 @@
 //  - Feature branch h_L += Wc_L c + bc_L (decoder.py:196-197): c (32 channels) is one B tile kept
 //    in registers; each converted tile adds one 32x32 product (6 MFMAs) whose A fragments ride in
 //    a 4 KiB tail of the step's slot (the fc stream is laid out in conversion order).
+#pragma once
 #include <type_traits>
 
 #include "dev_common.h"
@@ -65,22 +66,32 @@ constexpr int64_t kRawBytes = 8192;   // padded to 2 x 4 KiB (two DMA pieces)
 constexpr int kFcRawInv = 1024, kFcRawScl = 1028;
 constexpr int64_t kFcRawBytes = 8192;
 
-// Packed buffer (floats): [fp32 image][BF16X3 main][BF16 main][F16X3 main][raw]
+// Backward (delta chain) image, bf16x3: steps g = 0: Wo^T (K = 4: one k-step) [T 8][part 2][lane][8];
+// 1..24: W3^T, W2^T, W1^T input tiles [T 8][s 2][part 2][lane][8]; 25..32: W0^T (96 output rows)
+// [T 3][s 2][part 2][lane][8].  fc backward image: 32 entries of 4 KiB, entry e = 8(3 - l) + t
+// holds Wc_l^T over unit tile t as [s 2][part 2][lane][8].
+constexpr int kBwdSteps = 33;
+__host__ __device__ constexpr int64_t bwd_main_off(int g) {
+  return g == 0 ? 0 : (g <= 25 ? 16384LL + (g - 1) * 32768LL : 16384LL + 24 * 32768LL + (g - 25) * 12288LL);
+}
+constexpr int64_t kBwdBytes = bwd_main_off(kBwdSteps);
+
+// Packed buffer (floats): [fp32 image][BF16X3 main][BF16 main][F16X3 main][BF16X3 bwd][raw]
 constexpr int64_t kOffBf2 = kPackedFloats;
 constexpr int64_t kOffBf1 = kOffBf2 + bf_main_bytes(2) / 4;
 constexpr int64_t kOffH2 = kOffBf1 + bf_main_bytes(1) / 4;
-constexpr int64_t kOffRaw = kOffH2 + bf_main_bytes(2) / 4;
+constexpr int64_t kOffBwd = kOffH2 + bf_main_bytes(2) / 4;
+constexpr int64_t kOffRaw = kOffBwd + kBwdBytes / 4;
 constexpr int64_t kPackedFloatsAll = kOffRaw + kRawBytes / 4;
-// fc buffer (floats): [fp32 fc image][BF16X3 fc][BF16 fc][F16X3 fc][raw]
+// fc buffer (floats): [fp32 fc image][BF16X3 fc][BF16 fc][F16X3 fc][BF16X3 fc bwd][raw]
 constexpr int64_t kOffFcBf2 = kFcPackedFloats;
 constexpr int64_t kOffFcBf1 = kOffFcBf2 + kBfFcBytes / 4;
 constexpr int64_t kOffFcH2 = kOffFcBf1 + kBfFcBytes / 4;
-constexpr int64_t kOffFcRaw = kOffFcH2 + kBfFcBytes / 4;
+constexpr int64_t kOffFcBwd = kOffFcH2 + kBfFcBytes / 4;
+constexpr int64_t kOffFcRaw = kOffFcBwd + kBfFcBytes / 4;
 constexpr int64_t kFcPackedFloatsAll = kOffFcRaw + kFcRawBytes / 4;
 
 static_assert(kOffBf2 % 4 == 0 && kOffFcBf2 % 4 == 0, "16-B aligned images");
-int64_t packed_floats_all() { return kPackedFloatsAll; }
-int64_t fc_packed_floats_all() { return kFcPackedFloatsAll; }
 
 constexpr int64_t main_off_floats(int pr) {
   return pr == PNR_PREC_BF16X3 ? kOffBf2 : pr == PNR_PREC_BF16 ? kOffBf1 : kOffH2;
@@ -90,188 +101,23 @@ constexpr int64_t fc_off_floats(int pr) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// Packing
-// ---------------------------------------------------------------------------------------------
-// Per-tensor power-of-two scale of the f16 images: s = 2^e, e = floor(log2(2^14 / max|W|)),
-// clamped to [-20, 20]; scl[i] = s, inv[i] = 1/s (both exact).  One block per tensor.
-struct ScaleArgs {
-  const float* w[5];
-  int n[5];
-  float* inv;
-  float* scl;
-};
-__global__ void k_wscale(ScaleArgs a) {
-  __shared__ float red[256];
-  const float* w = a.w[blockIdx.x];
-  const int n = a.n[blockIdx.x];
-  float m = 0.f;
-  for (int i = threadIdx.x; i < n; i += 256) m = fmaxf(m, fabsf(w[i]));
-  red[threadIdx.x] = m;
-  __syncthreads();
-  for (int s = 128; s > 0; s >>= 1) {
-    if ((int)threadIdx.x < s) red[threadIdx.x] = fmaxf(red[threadIdx.x], red[threadIdx.x + s]);
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) {
-    int e = 20;
-    if (red[0] > 0.f) {
-      int ex;
-      frexpf(16384.f / red[0], &ex);  // 16384/max = f 2^ex, f in [0.5,1)
-      e = ex - 1;                     // 2^e <= 16384/max
-      e = e < -20 ? -20 : (e > 20 ? 20 : e);
-    }
-    a.scl[blockIdx.x] = ldexpf(1.f, e);
-    a.inv[blockIdx.x] = ldexpf(1.f, -e);
-  }
-}
-
-template <typename E>
-__device__ __forceinline__ uint16_t part_bits(float x, int part) {
-  const E h = (E)x;
-  const E v = part == 0 ? h : (E)(x - (float)h);
-  return __builtin_bit_cast(uint16_t, v);
-}
-
-// element (T, s, part, lane, j) of a weight fragment image for a layer with A[row][k]:
-// row = 32T + (lane&31), k = 32kc + perm(8s+j, lane>>5).  img 0: BF16X3, 1: BF16, 2: F16X3.
-__global__ void k_pack16(RawParams rp, uint16_t* __restrict__ bf2, uint16_t* __restrict__ bf1,
-                         uint16_t* __restrict__ h2, float* __restrict__ raw) {
-  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t n2 = bf_main_bytes(2) / 2, n1 = bf_main_bytes(1) / 2;
-  if (idx < 2 * n2 + n1) {
-    const int img = idx < n2 ? 0 : (idx < n2 + n1 ? 1 : 2);
-    const int np = img == 1 ? 1 : 2;
-    const int64_t e0 = img == 0 ? idx : (img == 1 ? idx - n2 : idx - n2 - n1);
-    int64_t e = e0;
-    const int64_t hstep = (int64_t)np * 8192;  // 16-bit elements per hidden step
-    float v = 0.f;
-    int part = 0, tensor = 4;
-    if (e < 27 * hstep) {
-      const int g = (int)(e / hstep);
-      int64_t r = e % hstep;
-      const int j = (int)(r % 8); r /= 8;
-      const int lane = (int)(r % 64); r /= 64;
-      part = (int)(r % np); r /= np;
-      const int s = (int)(r % 2);
-      const int T = (int)(r / 2);
-      const int layer = g < 3 ? 0 : 1 + (g - 3) / 8;
-      const int kc = g < 3 ? g : (g - 3) % 8;
-      const int row = 32 * T + (lane & 31);
-      const int k = 32 * kc + perm(8 * s + j, lane >> 5);
-      const float* W = rp.p[1 + 2 * layer];
-      tensor = layer;
-      if (layer == 0) v = k < kFourier ? W[row * kFourier + k] : 0.f;
-      else v = W[row * kHidden + k];
-    } else {
-      e -= 27 * hstep;
-      const int kc = (int)(e / 2048);
-      int64_t r = e % 2048;  // 4 KiB piece = 2048 elements
-      if (r < (int64_t)np * 1024) {
-        const int j = (int)(r % 8); r /= 8;
-        const int lane = (int)(r % 64); r /= 64;
-        part = (int)(r % np);
-        const int s = (int)(r / np);
-        const int row = lane & 31;
-        const int k = 32 * kc + perm(8 * s + j, lane >> 5);
-        v = row < 4 ? rp.p[9][row * kHidden + k] : 0.f;
-      }
-    }
-    if (img == 2) h2[e0] = part_bits<_Float16>(v * raw[kRawScl + tensor], part);
-    else (img == 0 ? bf2 : bf1)[e0] = part_bits<__bf16>(v, part);
-    return;
-  }
-  const int64_t ri = idx - 2 * n2 - n1;
-  if (ri < kRawInv) {
-    float v = 0.f;
-    const int i = (int)ri;
-    if (i < kRawBo) v = rp.p[2 + 2 * (i / 256)][i % 256];
-    else if (i < kRawFB) v = (i - kRawBo) < 4 ? rp.p[10][i - kRawBo] : 0.f;
-    else {
-      const int c = (i - kRawFB) / kFourierPad, k = (i - kRawFB) % kFourierPad;
-      v = k < kFourier ? rp.p[0][c * kFourier + k] : 0.f;
-    }
-    raw[i] = v;
-  }
-}
-
-int launch_pack_bf(const RawParams& rp, float* packed, hipStream_t st) {
-  float* raw = packed + kOffRaw;
-  ScaleArgs sa;
-  const int nw[5] = {kHidden * kFourier, kHidden * kHidden, kHidden * kHidden, kHidden * kHidden, 4 * kHidden};
-  for (int i = 0; i < 5; ++i) {
-    sa.w[i] = rp.p[i < 4 ? 1 + 2 * i : 9];
-    sa.n[i] = nw[i];
-  }
-  sa.inv = raw + kRawInv;
-  sa.scl = raw + kRawScl;
-  hipLaunchKernelGGL(k_wscale, dim3(5), dim3(256), 0, st, sa);
-  const int64_t n = 2 * (bf_main_bytes(2) / 2) + bf_main_bytes(1) / 2 + kRawInv;
-  const int threads = 256;
-  hipLaunchKernelGGL(k_pack16, dim3((unsigned)((n + threads - 1) / threads)), dim3(threads), 0, st, rp,
-                     reinterpret_cast<uint16_t*>(packed + kOffBf2), reinterpret_cast<uint16_t*>(packed + kOffBf1),
-                     reinterpret_cast<uint16_t*>(packed + kOffH2), raw);
-  return hip_status(hipGetLastError());
-}
-
-struct FcRaw16 {
-  const float* p[PNR_N_FC_PARAMS];
-};
-
-// fc entry e = 8L + t: A[row = unit 32t + (lane&31)][k = channel perm(8s+j, lane>>5)] of Wc_L
-__global__ void k_fc_pack16(FcRaw16 fc, uint16_t* __restrict__ bf2, uint16_t* __restrict__ bf1,
-                            uint16_t* __restrict__ h2, float* __restrict__ raw) {
-  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t n = kBfFcBytes / 2;  // elements per image
-  if (idx < 3 * n) {
-    const int img = (int)(idx / n);
-    const int np = img == 1 ? 1 : 2;
-    const int64_t e = idx % n;
-    const int ent = (int)(e / 2048);
-    int64_t r = e % 2048;
-    float v = 0.f;
-    int part = 0;
-    const int L = ent / 8, t = ent % 8;
-    if (r < (int64_t)np * 1024) {
-      const int j = (int)(r % 8); r /= 8;
-      const int lane = (int)(r % 64); r /= 64;
-      part = (int)(r % np);
-      const int s = (int)(r / np);
-      const int unit = 32 * t + (lane & 31);
-      const int ch = perm(8 * s + j, lane >> 5);
-      v = fc.p[2 * L][unit * kCDim + ch];
-    }
-    if (img == 2) h2[e] = part_bits<_Float16>(v * raw[kFcRawScl + L], part);
-    else (img == 0 ? bf2 : bf1)[e] = part_bits<__bf16>(v, part);
-    return;
-  }
-  const int64_t ri = idx - 3 * n;
-  if (ri < kFcRawInv) raw[ri] = fc.p[2 * (int)(ri / 256) + 1][ri % 256];
-}
-
-int launch_fc_pack_bf(const float* const* fcp, float* out, hipStream_t st) {
-  FcRaw16 r;
-  for (int i = 0; i < PNR_N_FC_PARAMS; ++i) r.p[i] = fcp[i];
-  float* raw = out + kOffFcRaw;
-  ScaleArgs sa{};
-  for (int i = 0; i < 4; ++i) {
-    sa.w[i] = fcp[2 * i];
-    sa.n[i] = kHidden * kCDim;
-  }
-  sa.inv = raw + kFcRawInv;
-  sa.scl = raw + kFcRawScl;
-  hipLaunchKernelGGL(k_wscale, dim3(4), dim3(256), 0, st, sa);
-  const int64_t n = 3 * (kBfFcBytes / 2) + kFcRawInv;
-  const int threads = 256;
-  hipLaunchKernelGGL(k_fc_pack16, dim3((unsigned)((n + threads - 1) / threads)), dim3(threads), 0, st, r,
-                     reinterpret_cast<uint16_t*>(out + kOffFcBf2), reinterpret_cast<uint16_t*>(out + kOffFcBf1),
-                     reinterpret_cast<uint16_t*>(out + kOffFcH2), raw);
-  return hip_status(hipGetLastError());
-}
-
-// ---------------------------------------------------------------------------------------------
 // Forward kernel
 // ---------------------------------------------------------------------------------------------
-template <int NP, bool HASC>
+// Forward step program: layer and input tile of step g, and the epilogue job placed in it
+// (h_CL tile CT; tile 0 of a layer is built in that layer's last step).
+__host__ __device__ constexpr int fwd_layer(int g) { return g < 3 ? 0 : (g < 27 ? 1 + (g - 3) / 8 : 4); }
+__host__ __device__ constexpr int fwd_kc(int g) { return g < 3 ? g : (g - 3) % 8; }
+__host__ __device__ constexpr bool fwd_conv(int g) {
+  return !(fwd_layer(g) == 0 && fwd_kc(g) < 2) && !(fwd_layer(g) == 4 && fwd_kc(g) == 7);
+}
+__host__ __device__ constexpr int fwd_ct(int g) {
+  return (fwd_layer(g) == 0 || (fwd_layer(g) <= 3 && fwd_kc(g) == 7)) ? 0 : fwd_kc(g) + 1;
+}
+// activation-save stores one wave issues in step g (SAVE): 4 h quads + the mask words after tile 7
+__host__ __device__ constexpr int fwd_stores(int g) { return fwd_conv(g) ? 4 + (fwd_ct(g) == 7 ? 1 : 0) : 0; }
+constexpr int kFwdPrologueStores = 13;  // e tiles (3 x 4 quads) + x
+
+template <int NP, bool HASC, bool SAVE = false>
 struct BfGeo {
   static constexpr int kMainH = NP * 16384;                  // bytes of a hidden main piece
   static constexpr int kSlot = kMainH + (HASC ? 4096 : 0);   // LDS slot bytes
@@ -282,10 +128,17 @@ struct BfGeo {
   __host__ __device__ static constexpr int main_n(int g) { return g < 27 ? kMainH / 4096 : 1; }
   __host__ __device__ static constexpr int fc_n(int g) { return (HASC && g >= 2 && g <= 33) ? 1 : 0; }
   __host__ __device__ static constexpr int n_glds(int g) { return g < kBfSteps ? main_n(g) + fc_n(g) : 0; }
-  // DMA instructions of this wave issued after step g's (the steps still allowed in flight)
+  // VMEM instructions of this wave issued after step g's DMA (at the top of step g - kDist): the
+  // DMAs of the steps still allowed in flight plus, when saving, the activation stores of steps
+  // g - kDist .. g - 1 (and the prologue's e / x stores while g < kDist).  Exact, so the wait at
+  // the top of step g never drains a store.
   __host__ __device__ static constexpr int younger(int g) {
     int s = 0;
     for (int i = g + 1; i < g + kDist && i < kBfSteps; ++i) s += n_glds(i);
+    if (SAVE) {
+      for (int i = g - kDist < 0 ? 0 : g - kDist; i < g; ++i) s += fwd_stores(i);
+      if (g < kDist) s += kFwdPrologueStores;
+    }
     return s;
   }
   __host__ __device__ static constexpr int64_t main_off(int g) {
@@ -295,6 +148,7 @@ struct BfGeo {
 static_assert(BfGeo<2, true>::kLds <= 160 * 1024, "LDS budget");
 static_assert(BfGeo<1, true>::kLds <= 160 * 1024, "LDS budget");
 static_assert(BfGeo<2, true>::younger(0) + BfGeo<2, true>::n_glds(0) < 64, "vmcnt range");
+static_assert(BfGeo<2, true, true>::younger(2) < 64 && BfGeo<2, true, true>::younger(3) < 64, "vmcnt range");
 
 struct BfFwdArgs {
   const char* wmain;   // main 16-bit image of the precision
@@ -305,7 +159,6 @@ struct BfFwdArgs {
   int64_t P;
   float* raw_out;
   SaveArgs save;
-  int do_save;
   const float* c;      // (rows, 32) features of the launch's points
 };
 
@@ -352,20 +205,20 @@ struct Frag {
   typename Prec<PR>::V8 a[Prec<PR>::NP][2];
 };
 
-template <int PR>
+template <int PR, int NS = 2>
 __device__ __forceinline__ void load_frag(const char* base, Frag<PR>& f) {
   using V8 = typename Prec<PR>::V8;
   constexpr int NP = Prec<PR>::NP;
   const int lane = threadIdx.x & 63;
 #pragma unroll
-  for (int s = 0; s < 2; ++s)
+  for (int s = 0; s < NS; ++s)
 #pragma unroll
     for (int pt = 0; pt < NP; ++pt) f.a[pt][s] = *reinterpret_cast<const V8*>(base + (s * NP + pt) * 1024 + lane * 16);
 }
 
 // acc (+)= A . act over one 32-deep input tile: per k-step Al.xh + Ah.xl + Ah.xh (split) or Ah.xh.
 // ZERO: the accumulator starts at 0 (first input tile of a layer)
-template <int PR, bool ZERO, typename T>
+template <int PR, bool ZERO, typename T, int NS = 2>
 __device__ __forceinline__ void mfma_frag(const Frag<PR>& F, const T (&act)[Prec<PR>::NP][2], f32x16& acc) {
   f32x16 c = acc;
   if (ZERO) {
@@ -373,7 +226,7 @@ __device__ __forceinline__ void mfma_frag(const Frag<PR>& F, const T (&act)[Prec
     for (int r = 0; r < 16; ++r) c[r] = 0.f;
   }
 #pragma unroll
-  for (int s = 0; s < 2; ++s) {
+  for (int s = 0; s < NS; ++s) {
     if (Prec<PR>::NP == 2) {
       c = Prec<PR>::mfma(F.a[1][s], act[0][s], c);
       c = Prec<PR>::mfma(F.a[0][s], act[1][s], c);
@@ -383,11 +236,11 @@ __device__ __forceinline__ void mfma_frag(const Frag<PR>& F, const T (&act)[Prec
   acc = c;
 }
 
-template <int PR, bool HASC>
+template <int PR, bool HASC, bool SAVE>
 struct BfFwd {
   static constexpr int NP = Prec<PR>::NP;
   static constexpr bool F16 = Prec<PR>::F16;
-  using G = BfGeo<NP, HASC>;
+  using G = BfGeo<NP, HASC, SAVE>;
   using V8 = typename Prec<PR>::V8;
   using St = BfState<PR>;
 
@@ -426,7 +279,7 @@ struct BfFwd {
       const float x = (F16 ? src[4 * q + i] * inv : src[4 * q + i]) + b4[i];
       S.v[4 * q + i] = x > 0.f ? x : 0.f;
     }
-    if (a.do_save) {
+    if constexpr (SAVE) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) S.mw[t >> 1] |= (S.v[4 * q + i] > 0.f ? 1u : 0u) << ((t & 1) * 16 + 4 * q + i);
       if (t == 7 && q == 3) {
@@ -447,7 +300,7 @@ struct BfFwd {
 #pragma unroll
       for (int i = 0; i < 4; ++i) S.v[4 * q + i] += (F16 ? S.f[4 * q + i] * inv : S.f[4 * q + i]) + b4[i];
     }
-    if (a.do_save)
+    if constexpr (SAVE)
       *reinterpret_cast<float4*>(a.save.hP + ((int64_t)L * a.save.ld + S.col) * kHidden + 32 * t + 8 * q + 4 * hh) =
           make_float4(S.v[4 * q], S.v[4 * q + 1], S.v[4 * q + 2], S.v[4 * q + 3]);
     split_quad<PR>(S.v + 4 * q, q, S.nxt);
@@ -496,15 +349,15 @@ struct BfFwd {
   template <int g>
   static __device__ __forceinline__ void step(const BfFwdArgs& a, St& S, const char* lds) {
     if constexpr (g < kBfSteps) {
-      constexpr int layer = g < 3 ? 0 : (g < 27 ? 1 + (g - 3) / 8 : 4);
-      constexpr int kc = g < 3 ? g : (g - 3) % 8;
+      constexpr int layer = fwd_layer(g);
+      constexpr int kc = fwd_kc(g);
       constexpr int NT = layer == 4 ? 1 : 8;
       constexpr int OUTSET = layer & 1;                      // h_layer -> acc[layer & 1]
       constexpr bool ZERO = kc == 0 && layer <= 3;
       // epilogue job of this step: h_CL tile CT (tile 0 of a layer is built in its last step)
-      constexpr bool CONV = !(layer == 0 && kc < 2) && !(layer == 4 && kc == 7);
+      constexpr bool CONV = fwd_conv(g);
       constexpr int CL = layer == 0 ? 0 : (layer == 4 ? 3 : (kc < 7 ? layer - 1 : layer));
-      constexpr int CT = (layer == 0 || (layer <= 3 && kc == 7)) ? 0 : kc + 1;
+      constexpr int CT = fwd_ct(g);
       constexpr int SET = CL & 1;
       constexpr int SHIFT = CT == 0 ? 1 : 0;  // that tile is produced by group 0 of this step
       sync_chunk<G::younger(g)>();
@@ -536,9 +389,9 @@ struct BfFwd {
   }
 };
 
-template <int PR, bool HASC>
+template <int PR, bool HASC, bool SAVE>
 __global__ __launch_bounds__(256, 1) void k_mlp_fwd16(BfFwdArgs a, int mode) {
-  using K = BfFwd<PR, HASC>;
+  using K = BfFwd<PR, HASC, SAVE>;
   using G = typename K::G;
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, hh = lane >> 5, j = lane & 31;
@@ -611,7 +464,7 @@ __global__ __launch_bounds__(256, 1) void k_mlp_fwd16(BfFwdArgs a, int mode) {
         }
         v[r] = k < kFourier ? sinf(arg) : 0.f;
       }
-      if (a.do_save) {
+      if constexpr (SAVE) {
         float* row = a.save.eP + S.col * kFourierPad + 32 * t + 4 * hh;
 #pragma unroll
         for (int q = 0; q < 4; ++q)
@@ -619,7 +472,7 @@ __global__ __launch_bounds__(256, 1) void k_mlp_fwd16(BfFwdArgs a, int mode) {
       }
       split_tile<PR>(v, S.ft[t]);
     }
-    if (a.do_save && hh == 0) a.save.xP[S.col] = make_float4(x0, x1, x2, inside ? 1.f : 0.f);
+    if (SAVE && hh == 0) a.save.xP[S.col] = make_float4(x0, x1, x2, inside ? 1.f : 0.f);
   }
   K::template step<0>(a, S, lds);
 
@@ -634,45 +487,25 @@ __global__ __launch_bounds__(256, 1) void k_mlp_fwd16(BfFwdArgs a, int mode) {
   }
 }
 
-template <int PR, bool HASC>
-static int launch16(int mode, dim3 grid, hipStream_t st, const BfFwdArgs& a) {
+// per-precision launchers (mlp16_fwd_*.hip), dispatched by launch_mlp_fwd_bf (mlp16_pack.hip)
+int launch_fwd16_f16x3(int mode, dim3 grid, hipStream_t st, const BfFwdArgs& a, bool hasc, bool save);
+int launch_fwd16_bf16x3(int mode, dim3 grid, hipStream_t st, const BfFwdArgs& a, bool hasc, bool save);
+int launch_fwd16_bf16(int mode, dim3 grid, hipStream_t st, const BfFwdArgs& a, bool hasc, bool save);
+
+template <int PR, bool HASC, bool SAVE>
+static int launch16s(int mode, dim3 grid, hipStream_t st, const BfFwdArgs& a) {
   const size_t lds = BfGeo<Prec<PR>::NP, HASC>::kLds;
-  auto kern = k_mlp_fwd16<PR, HASC>;
+  auto kern = k_mlp_fwd16<PR, HASC, SAVE>;
   static const bool attr = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                                                (int)lds) == hipSuccess;
   if (!attr) return PNR_E_ARG;
   hipLaunchKernelGGL(kern, grid, dim3(256), lds, st, a, mode);
   return hip_status(hipGetLastError());
 }
-
-int launch_mlp_fwd_bf(int prec, const float* packed, const PointSrc& src, int mode, int64_t P, float* raw,
-                      const SaveArgs* save, hipStream_t st, const FeatArgs* feat) {
-  if (P <= 0) return 0;
-  if (mode < kPtsF64 || mode > kRaysZ32) return PNR_E_ARG;
-  if (prec != PNR_PREC_BF16X3 && prec != PNR_PREC_BF16 && prec != PNR_PREC_F16X3) return PNR_E_ARG;
-  BfFwdArgs a;
-  a.wmain = reinterpret_cast<const char*>(packed + main_off_floats(prec));
-  a.raw = reinterpret_cast<const char*>(packed + kOffRaw);
-  const bool hasc = feat && feat->fcw;
-  a.wfc = hasc ? reinterpret_cast<const char*>(feat->fcw + fc_off_floats(prec)) : nullptr;
-  a.fcraw = hasc ? reinterpret_cast<const char*>(feat->fcw + kOffFcRaw) : nullptr;
-  a.c = hasc ? feat->c : nullptr;
-  a.src = src;
-  a.P = P;
-  a.raw_out = raw;
-  a.do_save = save != nullptr;
-  if (save) a.save = *save;
-  else a.save = SaveArgs{nullptr, nullptr, nullptr, nullptr, 0, 0};
-  const dim3 grid((unsigned)((P + 127) / 128));
-  TimingScope ts(kTimeMlpFwd, P, st);
-  switch (prec) {
-    case PNR_PREC_BF16X3:
-      return hasc ? launch16<PNR_PREC_BF16X3, true>(mode, grid, st, a) : launch16<PNR_PREC_BF16X3, false>(mode, grid, st, a);
-    case PNR_PREC_BF16:
-      return hasc ? launch16<PNR_PREC_BF16, true>(mode, grid, st, a) : launch16<PNR_PREC_BF16, false>(mode, grid, st, a);
-    default:
-      return hasc ? launch16<PNR_PREC_F16X3, true>(mode, grid, st, a) : launch16<PNR_PREC_F16X3, false>(mode, grid, st, a);
-  }
+template <int PR>
+static int launch16(int mode, dim3 grid, hipStream_t st, const BfFwdArgs& a, bool hasc, bool save) {
+  if (hasc) return save ? launch16s<PR, true, true>(mode, grid, st, a) : launch16s<PR, true, false>(mode, grid, st, a);
+  return save ? launch16s<PR, false, true>(mode, grid, st, a) : launch16s<PR, false, false>(mode, grid, st, a);
 }
 
 }  // namespace pnr

@@ -1,0 +1,268 @@
+// mlp16_pack.hip -- 16-bit weight images of the split-precision decoder kernels (mlp16.h) and
+// the forward dispatch on PNR_PREC_*.
+#include "mlp16.h"
+
+namespace pnr {
+
+int64_t packed_floats_all() { return kPackedFloatsAll; }
+int64_t fc_packed_floats_all() { return kFcPackedFloatsAll; }
+// ---------------------------------------------------------------------------------------------
+// Packing
+// ---------------------------------------------------------------------------------------------
+// Per-tensor power-of-two scale of the f16 images: s = 2^e, e = floor(log2(2^14 / max|W|)),
+// clamped to [-20, 20]; scl[i] = s, inv[i] = 1/s (both exact).  One block per tensor.
+struct ScaleArgs {
+  const float* w[5];
+  int n[5];
+  float* inv;
+  float* scl;
+};
+__global__ void k_wscale(ScaleArgs a) {
+  __shared__ float red[256];
+  const float* w = a.w[blockIdx.x];
+  const int n = a.n[blockIdx.x];
+  float m = 0.f;
+  for (int i = threadIdx.x; i < n; i += 256) m = fmaxf(m, fabsf(w[i]));
+  red[threadIdx.x] = m;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) red[threadIdx.x] = fmaxf(red[threadIdx.x], red[threadIdx.x + s]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    int e = 20;
+    if (red[0] > 0.f) {
+      int ex;
+      frexpf(16384.f / red[0], &ex);  // 16384/max = f 2^ex, f in [0.5,1)
+      e = ex - 1;                     // 2^e <= 16384/max
+      e = e < -20 ? -20 : (e > 20 ? 20 : e);
+    }
+    a.scl[blockIdx.x] = ldexpf(1.f, e);
+    a.inv[blockIdx.x] = ldexpf(1.f, -e);
+  }
+}
+
+template <typename E>
+__device__ __forceinline__ uint16_t part_bits(float x, int part) {
+  const E h = (E)x;
+  const E v = part == 0 ? h : (E)(x - (float)h);
+  return __builtin_bit_cast(uint16_t, v);
+}
+
+// element (T, s, part, lane, j) of a weight fragment image for a layer with A[row][k]:
+// row = 32T + (lane&31), k = 32kc + perm(8s+j, lane>>5).  img 0: BF16X3, 1: BF16, 2: F16X3.
+__global__ void k_pack16(RawParams rp, uint16_t* __restrict__ bf2, uint16_t* __restrict__ bf1,
+                         uint16_t* __restrict__ h2, float* __restrict__ raw) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t n2 = bf_main_bytes(2) / 2, n1 = bf_main_bytes(1) / 2;
+  if (idx < 2 * n2 + n1) {
+    const int img = idx < n2 ? 0 : (idx < n2 + n1 ? 1 : 2);
+    const int np = img == 1 ? 1 : 2;
+    const int64_t e0 = img == 0 ? idx : (img == 1 ? idx - n2 : idx - n2 - n1);
+    int64_t e = e0;
+    const int64_t hstep = (int64_t)np * 8192;  // 16-bit elements per hidden step
+    float v = 0.f;
+    int part = 0, tensor = 4;
+    if (e < 27 * hstep) {
+      const int g = (int)(e / hstep);
+      int64_t r = e % hstep;
+      const int j = (int)(r % 8); r /= 8;
+      const int lane = (int)(r % 64); r /= 64;
+      part = (int)(r % np); r /= np;
+      const int s = (int)(r % 2);
+      const int T = (int)(r / 2);
+      const int layer = g < 3 ? 0 : 1 + (g - 3) / 8;
+      const int kc = g < 3 ? g : (g - 3) % 8;
+      const int row = 32 * T + (lane & 31);
+      const int k = 32 * kc + perm(8 * s + j, lane >> 5);
+      const float* W = rp.p[1 + 2 * layer];
+      tensor = layer;
+      if (layer == 0) v = k < kFourier ? W[row * kFourier + k] : 0.f;
+      else v = W[row * kHidden + k];
+    } else {
+      e -= 27 * hstep;
+      const int kc = (int)(e / 2048);
+      int64_t r = e % 2048;  // 4 KiB piece = 2048 elements
+      if (r < (int64_t)np * 1024) {
+        const int j = (int)(r % 8); r /= 8;
+        const int lane = (int)(r % 64); r /= 64;
+        part = (int)(r % np);
+        const int s = (int)(r / np);
+        const int row = lane & 31;
+        const int k = 32 * kc + perm(8 * s + j, lane >> 5);
+        v = row < 4 ? rp.p[9][row * kHidden + k] : 0.f;
+      }
+    }
+    if (img == 2) h2[e0] = part_bits<_Float16>(v * raw[kRawScl + tensor], part);
+    else (img == 0 ? bf2 : bf1)[e0] = part_bits<__bf16>(v, part);
+    return;
+  }
+  const int64_t ri = idx - 2 * n2 - n1;
+  if (ri < kRawInv) {
+    float v = 0.f;
+    const int i = (int)ri;
+    if (i < kRawBo) v = rp.p[2 + 2 * (i / 256)][i % 256];
+    else if (i < kRawFB) v = (i - kRawBo) < 4 ? rp.p[10][i - kRawBo] : 0.f;
+    else {
+      const int c = (i - kRawFB) / kFourierPad, k = (i - kRawFB) % kFourierPad;
+      v = k < kFourier ? rp.p[0][c * kFourier + k] : 0.f;
+    }
+    raw[i] = v;
+  }
+}
+
+// Transposed bf16x3 images of the delta chain (element e of the backward stream)
+__global__ void k_pack16_bwd(RawParams rp, uint16_t* __restrict__ out) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= kBwdBytes / 2) return;
+  const int64_t byte = 2 * e;
+  int g = 0;
+  while (g + 1 < kBwdSteps && bwd_main_off(g + 1) <= byte) ++g;
+  int64_t r = (byte - bwd_main_off(g)) / 2;
+  const int j = (int)(r % 8); r /= 8;
+  const int lane = (int)(r % 64); r /= 64;
+  const int part = (int)(r % 2); r /= 2;
+  float v = 0.f;
+  if (g == 0) {  // Wo^T: A[row = unit 32T + i][k = o = perm(j, hh)], k < 4
+    const int T = (int)r, row = 32 * T + (lane & 31), k = perm(j, lane >> 5);
+    v = k < 4 ? rp.p[9][k * kHidden + row] : 0.f;
+  } else {
+    const int s = (int)(r % 2), T = (int)(r / 2);
+    const int row = 32 * T + (lane & 31);
+    const int kc = g <= 24 ? (g - 1) % 8 : g - 25;
+    const int k = 32 * kc + perm(8 * s + j, lane >> 5);
+    if (g <= 24) {
+      const int l = 3 - (g - 1) / 8;  // W3, W2, W1
+      v = rp.p[1 + 2 * l][k * kHidden + row];
+    } else {
+      v = row < kFourier ? rp.p[1][k * kFourier + row] : 0.f;
+    }
+  }
+  out[e] = part_bits<__bf16>(v, part);
+}
+
+int launch_pack_bf(const RawParams& rp, float* packed, hipStream_t st) {
+  {
+    const int64_t n = kBwdBytes / 2;
+    hipLaunchKernelGGL(k_pack16_bwd, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, rp,
+                       reinterpret_cast<uint16_t*>(packed + kOffBwd));
+  }
+  float* raw = packed + kOffRaw;
+  ScaleArgs sa;
+  const int nw[5] = {kHidden * kFourier, kHidden * kHidden, kHidden * kHidden, kHidden * kHidden, 4 * kHidden};
+  for (int i = 0; i < 5; ++i) {
+    sa.w[i] = rp.p[i < 4 ? 1 + 2 * i : 9];
+    sa.n[i] = nw[i];
+  }
+  sa.inv = raw + kRawInv;
+  sa.scl = raw + kRawScl;
+  hipLaunchKernelGGL(k_wscale, dim3(5), dim3(256), 0, st, sa);
+  const int64_t n = 2 * (bf_main_bytes(2) / 2) + bf_main_bytes(1) / 2 + kRawInv;
+  const int threads = 256;
+  hipLaunchKernelGGL(k_pack16, dim3((unsigned)((n + threads - 1) / threads)), dim3(threads), 0, st, rp,
+                     reinterpret_cast<uint16_t*>(packed + kOffBf2), reinterpret_cast<uint16_t*>(packed + kOffBf1),
+                     reinterpret_cast<uint16_t*>(packed + kOffH2), raw);
+  return hip_status(hipGetLastError());
+}
+
+struct FcRaw16 {
+  const float* p[PNR_N_FC_PARAMS];
+};
+
+// fc entry e = 8L + t: A[row = unit 32t + (lane&31)][k = channel perm(8s+j, lane>>5)] of Wc_L
+__global__ void k_fc_pack16(FcRaw16 fc, uint16_t* __restrict__ bf2, uint16_t* __restrict__ bf1,
+                            uint16_t* __restrict__ h2, float* __restrict__ raw) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t n = kBfFcBytes / 2;  // elements per image
+  if (idx < 3 * n) {
+    const int img = (int)(idx / n);
+    const int np = img == 1 ? 1 : 2;
+    const int64_t e = idx % n;
+    const int ent = (int)(e / 2048);
+    int64_t r = e % 2048;
+    float v = 0.f;
+    int part = 0;
+    const int L = ent / 8, t = ent % 8;
+    if (r < (int64_t)np * 1024) {
+      const int j = (int)(r % 8); r /= 8;
+      const int lane = (int)(r % 64); r /= 64;
+      part = (int)(r % np);
+      const int s = (int)(r / np);
+      const int unit = 32 * t + (lane & 31);
+      const int ch = perm(8 * s + j, lane >> 5);
+      v = fc.p[2 * L][unit * kCDim + ch];
+    }
+    if (img == 2) h2[e] = part_bits<_Float16>(v * raw[kFcRawScl + L], part);
+    else (img == 0 ? bf2 : bf1)[e] = part_bits<__bf16>(v, part);
+    return;
+  }
+  const int64_t ri = idx - 3 * n;
+  if (ri < kFcRawInv) raw[ri] = fc.p[2 * (int)(ri / 256) + 1][ri % 256];
+}
+
+// fc backward entry e = 8(3 - l) + t: A[row = channel (lane&31)][k = unit 32t + perm(8s+j, lane>>5)]
+// = Wc_l[unit][channel], bf16x3
+__global__ void k_fc_pack16_bwd(FcRaw16 fc, uint16_t* __restrict__ out) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= kBfFcBytes / 2) return;
+  const int ent = (int)(e / 2048);
+  int64_t r = e % 2048;
+  const int j = (int)(r % 8); r /= 8;
+  const int lane = (int)(r % 64); r /= 64;
+  const int part = (int)(r % 2);
+  const int s = (int)(r / 2);
+  const int l = 3 - ent / 8, t = ent % 8;
+  const int unit = 32 * t + perm(8 * s + j, lane >> 5);
+  out[e] = part_bits<__bf16>(fc.p[2 * l][unit * kCDim + (lane & 31)], part);
+}
+
+int launch_fc_pack_bf(const float* const* fcp, float* out, hipStream_t st) {
+  FcRaw16 r;
+  for (int i = 0; i < PNR_N_FC_PARAMS; ++i) r.p[i] = fcp[i];
+  float* raw = out + kOffFcRaw;
+  ScaleArgs sa{};
+  for (int i = 0; i < 4; ++i) {
+    sa.w[i] = fcp[2 * i];
+    sa.n[i] = kHidden * kCDim;
+  }
+  sa.inv = raw + kFcRawInv;
+  sa.scl = raw + kFcRawScl;
+  hipLaunchKernelGGL(k_wscale, dim3(4), dim3(256), 0, st, sa);
+  const int64_t n = 3 * (kBfFcBytes / 2) + kFcRawInv;
+  const int threads = 256;
+  hipLaunchKernelGGL(k_fc_pack16, dim3((unsigned)((n + threads - 1) / threads)), dim3(threads), 0, st, r,
+                     reinterpret_cast<uint16_t*>(out + kOffFcBf2), reinterpret_cast<uint16_t*>(out + kOffFcBf1),
+                     reinterpret_cast<uint16_t*>(out + kOffFcH2), raw);
+  hipLaunchKernelGGL(k_fc_pack16_bwd, dim3((unsigned)((kBfFcBytes / 2 + 255) / 256)), dim3(256), 0, st, r,
+                     reinterpret_cast<uint16_t*>(out + kOffFcBwd));
+  return hip_status(hipGetLastError());
+}
+
+int launch_mlp_fwd_bf(int prec, const float* packed, const PointSrc& src, int mode, int64_t P, float* raw,
+                      const SaveArgs* save, hipStream_t st, const FeatArgs* feat) {
+  if (P <= 0) return 0;
+  if (mode < kPtsF64 || mode > kRaysZ32) return PNR_E_ARG;
+  if (prec != PNR_PREC_BF16X3 && prec != PNR_PREC_BF16 && prec != PNR_PREC_F16X3) return PNR_E_ARG;
+  BfFwdArgs a;
+  a.wmain = reinterpret_cast<const char*>(packed + main_off_floats(prec));
+  a.raw = reinterpret_cast<const char*>(packed + kOffRaw);
+  const bool hasc = feat && feat->fcw;
+  a.wfc = hasc ? reinterpret_cast<const char*>(feat->fcw + fc_off_floats(prec)) : nullptr;
+  a.fcraw = hasc ? reinterpret_cast<const char*>(feat->fcw + kOffFcRaw) : nullptr;
+  a.c = hasc ? feat->c : nullptr;
+  a.src = src;
+  a.P = P;
+  a.raw_out = raw;
+  const bool sv = save != nullptr;
+  if (save) a.save = *save;
+  else a.save = SaveArgs{nullptr, nullptr, nullptr, nullptr, 0, 0};
+  const dim3 grid((unsigned)((P + 127) / 128));
+  TimingScope ts(kTimeMlpFwd, P, st);
+  switch (prec) {
+    case PNR_PREC_BF16X3: return launch_fwd16_bf16x3(mode, grid, st, a, hasc, sv);
+    case PNR_PREC_BF16: return launch_fwd16_bf16(mode, grid, st, a, hasc, sv);
+    default: return launch_fwd16_f16x3(mode, grid, st, a, hasc, sv);
+  }
+}
+
+}  // namespace pnr

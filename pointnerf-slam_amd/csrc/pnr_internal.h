@@ -166,6 +166,8 @@ struct BwdArgs {
   float* g_c;          // [C][32] chunk-local rows
 };
 int launch_mlp_bwd(const float* packed, const BwdArgs& a, int64_t P, hipStream_t st);
+// bf16x3 delta chain (mlp_bf.hip): same arguments; used for every precision but PNR_PREC_FP32
+int launch_mlp_bwd_bf(const float* packed, const BwdArgs& a, int64_t P, hipStream_t st);
 
 int launch_pack(const RawParams& rp, float* packed, hipStream_t st);
 int launch_fc_pack(const float* const* fc, float* out, hipStream_t st);

@@ -77,7 +77,7 @@ _SIGS = {
                                          c_void_p]),
     'pnr_mlp_bwd_workspace_bytes': (c_size_t, [c_int64]),
     'pnr_mlp_bwd': (ctypes.c_int, [c_void_p, c_int64, c_void_p, PtrArray, c_void_p, c_void_p, c_size_t,
-                                   c_void_p, c_size_t, c_void_p]),
+                                   c_void_p, c_size_t, c_int32, c_void_p]),
     'pnr_render_workspace_bytes': (c_size_t, [ctypes.POINTER(RenderParams), c_int64]),
     'pnr_render_fwd': (ctypes.c_int, [ctypes.POINTER(RenderParams), c_void_p, c_void_p, c_void_p, c_void_p, c_int64,
                                       c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
@@ -113,7 +113,7 @@ _SIGS = {
                                            c_size_t, c_int32, c_void_p]),
     'pnr_mlp_bwd_workspace_bytes_c': (c_size_t, [c_int64]),
     'pnr_mlp_bwd_c': (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p, PtrArray, FcPtrArray,
-                                     c_void_p, c_void_p, c_void_p, c_size_t, c_void_p, c_size_t, c_void_p]),
+                                     c_void_p, c_void_p, c_void_p, c_size_t, c_void_p, c_size_t, c_int32, c_void_p]),
     'pnr_timing_enable': (ctypes.c_int, [ctypes.c_int]),
     'pnr_timing_read': (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(c_int64), ctypes.POINTER(ctypes.c_double),
                                        ctypes.POINTER(c_int64)]),

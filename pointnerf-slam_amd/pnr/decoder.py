@@ -67,6 +67,7 @@ class _MLPFn(torch.autograd.Function):
                                              ws.numel(), prec, st), 'mlp_fwd_train')
             ctx.save_for_backward(ws, packed)
             ctx.P = P
+            ctx.prec = prec
             ctx.p_grad = ctx.needs_input_grad[0]
         else:
             _lib.check(lib.pnr_eval_points_f32(_lib.ptr(packed), _lib.ptr(p), P, None, _lib.ptr(raw), prec, st),
@@ -84,8 +85,8 @@ class _MLPFn(torch.autograd.Function):
         bws = torch.empty(lib.pnr_mlp_bwd_workspace_bytes(P), dtype=torch.uint8, device=dev)
         arr = _lib.PtrArray(*[g.data_ptr() for g in grads])
         _lib.check(lib.pnr_mlp_bwd(_lib.ptr(packed), P, _lib.ptr(g_raw.contiguous()), arr, _lib.ptr(gp),
-                                   _lib.ptr(ws), ws.numel(), _lib.ptr(bws), bws.numel(), _lib.stream_of(dev)),
-                   'mlp_bwd')
+                                   _lib.ptr(ws), ws.numel(), _lib.ptr(bws), bws.numel(), ctx.prec,
+                                   _lib.stream_of(dev)), 'mlp_bwd')
         return (gp, None, None, *grads)
 
     shapes = ((3, 93), (256, 93), (256,), (256, 256), (256,), (256, 256), (256,), (256, 256), (256,), (4, 256), (4,))
@@ -113,6 +114,7 @@ class _MLPFnC(torch.autograd.Function):
                                                _lib.ptr(raw), _lib.ptr(ws), ws.numel(), prec, st), 'mlp_fwd_train_c')
             ctx.save_for_backward(ws, packed, fcp, c)
             ctx.P = P
+            ctx.prec = prec
         else:
             dp = p.double().contiguous()
             _lib.check(lib.pnr_eval_points_c(_lib.ptr(packed), _lib.ptr(fcp), _lib.ptr(dp), _lib.ptr(c), P, None,
@@ -134,7 +136,7 @@ class _MLPFnC(torch.autograd.Function):
         farr = _lib.FcPtrArray(*[g.data_ptr() for g in g_fc])
         _lib.check(lib.pnr_mlp_bwd_c(_lib.ptr(packed), _lib.ptr(fcp), _lib.ptr(c), P, _lib.ptr(g_raw.contiguous()),
                                      arr, farr, _lib.ptr(gc), _lib.ptr(gp), _lib.ptr(ws), ws.numel(), _lib.ptr(bws),
-                                     bws.numel(), _lib.stream_of(dev)), 'mlp_bwd_c')
+                                     bws.numel(), ctx.prec, _lib.stream_of(dev)), 'mlp_bwd_c')
         return (gp, gc, None, None, None, *grads, *g_fc)
 
 

@@ -45,8 +45,9 @@ def test_host_only_calls(lib):
     lib.pnr_abi_version.restype = ctypes.c_int
     assert lib.pnr_abi_version() == 3
     lib.pnr_mlp_packed_floats.restype = ctypes.c_size_t
-    # fp32 images 486,688 + bf16x3 / bf16 / f16x3 streams 229,376 / 118,784 / 229,376 + raw table 2,048
-    assert lib.pnr_mlp_packed_floats() == 486688 + 229376 + 118784 + 229376 + 2048
+    # fp32 images 486,688 + bf16x3 / bf16 / f16x3 forward streams 229,376 / 118,784 / 229,376
+    # + bf16x3 delta-chain stream 225,280 + raw table 2,048
+    assert lib.pnr_mlp_packed_floats() == 486688 + 229376 + 118784 + 229376 + 225280 + 2048
     lib.pnr_build_info.restype = ctypes.c_char_p
     assert b'gfx950' in lib.pnr_build_info()
 
@@ -94,7 +95,7 @@ def test_point_queries_and_arg_errors(lib):
     sys.path.insert(0, os.path.join(REPO, 'pointnerf-slam_amd'))
     from pnr import _lib
     L = _lib.load()
-    assert L.pnr_fc_packed_floats() == 12 * 8192 + 3 * 32768 + 2048  # fp32 + three 16-bit images + raw
+    assert L.pnr_fc_packed_floats() == 12 * 8192 + 4 * 32768 + 2048  # fp32 + four 16-bit images + raw
     b20 = L.pnr_points_index_bytes(100000, 20)
     assert b20 >= (2 * (1 << 20) + 2 * 100000) * 4 + 100000 * 16
     assert L.pnr_points_index_bytes(100000, 9) == 0 and L.pnr_points_index_bytes(-1, 12) == 0
