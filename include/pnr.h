@@ -80,7 +80,8 @@ enum { PNR_GATHER_IDW = 0, PNR_GATHER_TRILINEAR = 1 };
  *                    Needs |activations| < 65504 (f16 range).
  * Fourier features, bias, ReLU, compositing and all float64 work stay fp32 / fp64 in every mode.
  * Backward: PNR_PREC_FP32 runs the delta chain on fp32 MFMA; every other mode runs it as bf16x3
- * (bf16 parts keep the fp32 exponent range of tiny gradients).  Weight-gradient GEMMs are fp32. */
+ * (bf16 parts keep the fp32 exponent range of tiny gradients), and so do the 256-row weight-gradient
+ * GEMMs (dW0..dW3); the small ones (dWo, dB, dWc) stay fp32. */
 enum { PNR_PREC_FP32 = 0, PNR_PREC_BF16X3 = 1, PNR_PREC_BF16 = 2, PNR_PREC_F16X3 = 3 };
 
 typedef struct pnr_points {

@@ -231,13 +231,17 @@ int mlp_backward_core(int prec, const float* packed, const SaveArgs& sv, int64_t
     rc = launch_wgrad(kWgradOut, b.g_out + p0 * 4, 4, hp + 3 * hstride, kHidden, C, grads[9], kHidden, grads[10], st);
     if (rc) return rc;
     // hidden layers: dW_l += delta_{l+1}^T h_l  (W3: delta4.h3, W2: delta3.h2, W1: delta2.h1)
+    const bool split = prec != PNR_PREC_FP32;  // bf16x3 split MFMA (wgrad16.hip) for the large shapes
     for (int l = 3; l >= 1 && rc == 0; --l)
-      rc = launch_wgrad(kWgradHidden, b.dP + l * dstride, kHidden, hp + (l - 1) * hstride, kHidden, C,
-                        grads[1 + 2 * l], kHidden, grads[2 + 2 * l], st);
+      rc = split ? launch_wgrad16(kWgradHidden, b.dP + l * dstride, hp + (l - 1) * hstride, C, grads[1 + 2 * l],
+                                  kHidden, grads[2 + 2 * l], st)
+                 : launch_wgrad(kWgradHidden, b.dP + l * dstride, kHidden, hp + (l - 1) * hstride, kHidden, C,
+                                grads[1 + 2 * l], kHidden, grads[2 + 2 * l], st);
     if (rc) return rc;
     // first layer: dW0 (256x93) += delta1^T e ; db0
-    rc = launch_wgrad(kWgradFirst, b.dP, kHidden, sv.eP + p0 * kFourierPad, kFourier, C, grads[1], kFourier,
-                      grads[2], st);
+    rc = split ? launch_wgrad16(kWgradFirst, b.dP, sv.eP + p0 * kFourierPad, C, grads[1], kFourier, grads[2], st)
+               : launch_wgrad(kWgradFirst, b.dP, kHidden, sv.eP + p0 * kFourierPad, kFourier, C, grads[1], kFourier,
+                              grads[2], st);
     if (rc) return rc;
     // Fourier: dB (3x93) += x^T g_arg   (x rows are float4 (x0,x1,x2,inside): 3 of 4 used)
     rc = launch_wgrad(kWgradFourier, reinterpret_cast<const float*>(sv.xP + p0), 3, b.gargP, kFourier, C, grads[0],

@@ -219,6 +219,9 @@ int launch_gather_bwd(const pnr_points& pts, const PointSrc* src, int mode, cons
 enum WgradKind : int { kWgradHidden = 0, kWgradFirst = 1, kWgradOut = 2, kWgradFourier = 3, kWgradFc = 4 };
 int launch_wgrad(int kind, const float* A, int ma, const float* B, int nb, int64_t K, float* C, int64_t ldc,
                  float* bias, hipStream_t st);
+// bf16x3 split-MFMA form (wgrad16.hip) of kWgradHidden / kWgradFirst (MA = 256)
+int launch_wgrad16(int kind, const float* A, const float* B, int64_t K, float* C, int64_t ldc, float* bias,
+                   hipStream_t st);
 
 inline int hip_status(hipError_t e) { return e == hipSuccess ? 0 : (int)e; }
 
