@@ -44,4 +44,29 @@ __device__ __forceinline__ void sync_chunk() {
   asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
 }
 
+// sin / cos for the Fourier features of the split-precision kernels (decoder.py:26-30).  OCML's
+// sinf runs its Payne-Hanek large-argument path for every lane (~113 VALU per call, measured);
+// here: k = rint(x 2/pi), r = x - k pi/2 by three fma steps with pi/2 = C1 + C2 + C3 (fp32 parts),
+// minimax polynomials on [-pi/4, pi/4], quadrant select: ~20 VALU, max abs error 6.7e-8 on
+// |x| < 3000 (= the fp32 libm sinf error; checked in tests/test_host_logic.py).  The fma reduction
+// stays exact while k is an exact integer, |x| < 2^22; the Fourier arguments x @ B (scene
+// coordinates times B ~ N(0, 25^2), decoder.py:21) are orders of magnitude below.  (A sinf
+// fallback branch for large |x| is not used: hipcc if-converts it and runs Payne-Hanek always.)
+template <bool COS>
+__device__ __forceinline__ float fourier_sc(float x) {
+  const float k = __builtin_rintf(x * 0.636619772367581343f);
+  float r = __builtin_fmaf(-k, 1.5707963705062866f, x);
+  r = __builtin_fmaf(-k, -4.3711388286737929e-08f, r);
+  r = __builtin_fmaf(-k, -1.7151245100058819e-15f, r);
+  const float z = r * r;
+  const float sn = __builtin_fmaf(__builtin_fmaf(__builtin_fmaf(-1.9515295891e-4f, z, 8.3321608736e-3f), z,
+                                                 -1.6666654611e-1f), z * r, r);
+  const float cs = __builtin_fmaf(__builtin_fmaf(__builtin_fmaf(__builtin_fmaf(2.443315711809948e-5f, z,
+                                                                               -1.388731625493765e-3f), z,
+                                                                4.166664568298827e-2f), z, -0.5f), z, 1.f);
+  const int q = ((int)k + (COS ? 1 : 0)) & 3;
+  const float v = (q & 1) ? cs : sn;
+  return (q & 2) ? -v : v;
+}
+
 }  // namespace pnr

@@ -128,27 +128,12 @@ struct BfGeo {
   __host__ __device__ static constexpr int main_n(int g) { return g < 27 ? kMainH / 4096 : 1; }
   __host__ __device__ static constexpr int fc_n(int g) { return (HASC && g >= 2 && g <= 33) ? 1 : 0; }
   __host__ __device__ static constexpr int n_glds(int g) { return g < kBfSteps ? main_n(g) + fc_n(g) : 0; }
-  // VMEM instructions of this wave issued after step g's DMA (at the top of step g - kDist): the
-  // DMAs of the steps still allowed in flight plus, when saving, the activation stores of steps
-  // g - kDist .. g - 1 (and the prologue's e / x stores while g < kDist).  Exact, so the wait at
-  // the top of step g never drains a store.
-  __host__ __device__ static constexpr int younger(int g) {
-    int s = 0;
-    for (int i = g + 1; i < g + kDist && i < kBfSteps; ++i) s += n_glds(i);
-    if (SAVE) {
-      for (int i = g - kDist < 0 ? 0 : g - kDist; i < g; ++i) s += fwd_stores(i);
-      if (g < kDist) s += kFwdPrologueStores;
-    }
-    return s;
-  }
   __host__ __device__ static constexpr int64_t main_off(int g) {
     return g <= 27 ? (int64_t)g * kMainH : 27LL * kMainH + (int64_t)(g - 27) * 4096;
   }
 };
 static_assert(BfGeo<2, true>::kLds <= 160 * 1024, "LDS budget");
 static_assert(BfGeo<1, true>::kLds <= 160 * 1024, "LDS budget");
-static_assert(BfGeo<2, true>::younger(0) + BfGeo<2, true>::n_glds(0) < 64, "vmcnt range");
-static_assert(BfGeo<2, true, true>::younger(2) < 64 && BfGeo<2, true, true>::younger(3) < 64, "vmcnt range");
 
 struct BfFwdArgs {
   const char* wmain;   // main 16-bit image of the precision
@@ -160,6 +145,12 @@ struct BfFwdArgs {
   float* raw_out;
   SaveArgs save;
   const float* c;      // (rows, 32) features of the launch's points
+};
+
+// A fragments of one 32-row output tile over one 32-deep input tile: [part][k-step]
+template <int PR>
+struct Frag {
+  typename Prec<PR>::V8 a[Prec<PR>::NP][2];
 };
 
 // Per-wave register state of the forward.
@@ -175,7 +166,12 @@ struct BfState {
   V8 ct[NP][2];        // feature tile
   float v[16];         // epilogue values of the tile being converted
   f32x16 f;            // feature-branch product of that tile
+  float4 bq[4];        // bias quads of that tile (read from LDS at the top of the step)
+  float4 bcq[4];       // fc bias quads (features)
+  float inv, finv;     // f16 weight scales of the layer / fc branch
   uint32_t mw[4];      // ReLU bit words of the layer being converted
+  Frag<PR> F[3];       // fragment ring (one 32-row output tile of the current / next step each)
+  Frag<PR> FC;         // feature-branch fragments of the step's epilogue tile
   int64_t col, mask_word0;
   bool valid, inside;
 };
@@ -189,7 +185,7 @@ __device__ __forceinline__ void split_quad(const float* v4, int q, T (&t)[Prec<P
     const float x = v4[i];
     const E h = (E)x;
     t[0][q >> 1][4 * (q & 1) + i] = h;
-    if (Prec<PR>::NP == 2) t[Prec<PR>::NP - 1][q >> 1][4 * (q & 1) + i] = (E)(x - (float)h);
+    if constexpr (Prec<PR>::NP == 2) t[1][q >> 1][4 * (q & 1) + i] = (E)(x - (float)h);
   }
 }
 
@@ -199,11 +195,6 @@ __device__ __forceinline__ void split_tile(const float (&v)[16], T (&t)[Prec<PR>
   for (int q = 0; q < 4; ++q) split_quad<PR>(v + 4 * q, q, t);
 }
 
-// A fragments of one 32-row output tile over one 32-deep input tile: [part][k-step]
-template <int PR>
-struct Frag {
-  typename Prec<PR>::V8 a[Prec<PR>::NP][2];
-};
 
 template <int PR, int NS = 2>
 __device__ __forceinline__ void load_frag(const char* base, Frag<PR>& f) {
@@ -227,7 +218,7 @@ __device__ __forceinline__ void mfma_frag(const Frag<PR>& F, const T (&act)[Prec
   }
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
-    if (Prec<PR>::NP == 2) {
+    if constexpr (Prec<PR>::NP == 2) {
       c = Prec<PR>::mfma(F.a[1][s], act[0][s], c);
       c = Prec<PR>::mfma(F.a[0][s], act[1][s], c);
     }
@@ -235,6 +226,20 @@ __device__ __forceinline__ void mfma_frag(const Frag<PR>& F, const T (&act)[Prec
   }
   acc = c;
 }
+
+#if defined(PNR_EXP_TIMELINE)
+// experiment: s_memtime timeline of one steady-state workgroup (wave 0 .. 3, lane 0)
+extern __device__ unsigned long long g_pnr_dbg[4][48];
+#define PNR_TICK(i)                                                                     \
+  do {                                                                                  \
+    if (blockIdx.x == 2000 && (threadIdx.x & 63) == 0)                                  \
+      g_pnr_dbg[threadIdx.x >> 6][(i)] = __builtin_amdgcn_s_memtime();                  \
+  } while (0)
+#else
+#define PNR_TICK(i) \
+  do {              \
+  } while (0)
+#endif
 
 template <int PR, bool HASC, bool SAVE>
 struct BfFwd {
@@ -267,13 +272,33 @@ struct BfFwd {
   // Epilogue of h_L tile t (src = its accumulator), in pieces spread over a step's MFMA groups:
   //   phase 1, quad q: v = relu(acc + b) for units 4q..4q+3 of the lane (+ ReLU mask bits)
   //   phase 2, quad q: feature branch v += f + bc, activation save, 16-bit split into S.nxt
+  // Epilogue constants of h_L tile t, read at the top of the step BEFORE the fragment prefetch:
+  // LDS reads return in order, so a wait for a constant read later would drain the prefetch too.
+  template <int L, int t>
+  static __device__ __forceinline__ void preload(St& S, const char* lds) {
+    const int hh = (threadIdx.x >> 5) & 1;
+    const float* rawl = raw_lds(lds);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) S.bq[q] = *reinterpret_cast<const float4*>(rawl + kRawB + L * 256 + 32 * t + 8 * q + 4 * hh);
+    if (F16) S.inv = rawl[kRawInv + L];
+  }
+  // feature-branch bias quads of h_L tile t (read early in the step, before that group's fragment
+  // prefetch, so their wait never drains it)
+  template <int L, int t>
+  static __device__ __forceinline__ void preload_fc(St& S, const char* lds) {
+    const int hh = (threadIdx.x >> 5) & 1;
+    const float* fr = raw_lds(lds) + kRawBytes / 4;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) S.bcq[q] = *reinterpret_cast<const float4*>(fr + L * 256 + 32 * t + 8 * q + 4 * hh);
+    if (F16) S.finv = fr[kFcRawInv + L];
+  }
+
   template <int L, int t, int q>
   static __device__ __forceinline__ void conv1(const BfFwdArgs& a, St& S, const f32x16& src, const char* lds) {
-    const int lane = threadIdx.x & 63, hh = lane >> 5;
-    const float* rawl = raw_lds(lds);
-    const float4 b = *reinterpret_cast<const float4*>(rawl + kRawB + L * 256 + 32 * t + 8 * q + 4 * hh);
+    const int lane = threadIdx.x & 63;
+    const float4 b = S.bq[q];
     const float b4[4] = {b.x, b.y, b.z, b.w};
-    const float inv = F16 ? rawl[kRawInv + L] : 1.f;
+    const float inv = F16 ? S.inv : 1.f;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const float x = (F16 ? src[4 * q + i] * inv : src[4 * q + i]) + b4[i];
@@ -293,10 +318,9 @@ struct BfFwd {
   static __device__ __forceinline__ void conv2(const BfFwdArgs& a, St& S, const char* lds) {
     const int lane = threadIdx.x & 63, hh = lane >> 5;
     if constexpr (HASC) {
-      const float* fr = raw_lds(lds) + kRawBytes / 4;
-      const float4 b = *reinterpret_cast<const float4*>(fr + L * 256 + 32 * t + 8 * q + 4 * hh);
+      const float4 b = S.bcq[q];
       const float b4[4] = {b.x, b.y, b.z, b.w};
-      const float inv = F16 ? fr[kFcRawInv + L] : 1.f;
+      const float inv = F16 ? S.finv : 1.f;
 #pragma unroll
       for (int i = 0; i < 4; ++i) S.v[4 * q + i] += (F16 ? S.f[4 * q + i] * inv : S.f[4 * q + i]) + b4[i];
     }
@@ -331,68 +355,184 @@ struct BfFwd {
     }
   }
 
-  // MFMA group T of a step (prefetching the fragments of group T+2), then its epilogue pieces
-  template <int NT, int T, int OUTSET, bool ZERO, bool CONV, int CL, int CT, int SET, int SHIFT>
-  static __device__ __forceinline__ void group(const BfFwdArgs& a, St& S, const char* lds, const char* slot,
-                                               const V8 (&act)[NP][2], Frag<PR> (&F)[3], const Frag<PR>& FC) {
+  // ---- step pipeline ------------------------------------------------------------------------
+  // Step g runs NT(g) MFMA groups (one per output tile).  The wait + barrier that make step g+1's
+  // ring slot valid sit after group SYNC_T(g) of step g, followed by the DMA of step g+1+kD into the
+  // slot step g-1 used; the next step's first two fragment tiles and epilogue constants are then
+  // read during step g's last groups, so no step starts with an LDS round trip or a barrier.
+  static constexpr int kD = G::kNbuf - 2;  // DMA distance (steps)
+  __host__ __device__ static constexpr int nt(int g) { return fwd_layer(g) == 4 ? 1 : 8; }
+  __host__ __device__ static constexpr int sync_t(int g) { return nt(g) == 1 ? 0 : 5; }
+  __host__ __device__ static constexpr int ring(int g) {
+    int b = 0;
+    for (int i = 0; i < g; ++i) b += nt(i);
+    return b % 3;
+  }
+  __host__ __device__ static constexpr int shift(int g) { return fwd_ct(g) == 0 ? 1 : 0; }
+  __host__ __device__ static constexpr int clamp_t(int t, int g) { return t < nt(g) - 1 ? t : nt(g) - 1; }
+  // activation-save stores the epilogue pieces of step g issue in group T (SAVE)
+  __host__ __device__ static constexpr int stores_grp(int g, int T) {
+    if (!SAVE || !fwd_conv(g)) return 0;
+    int n = 0;
+    for (int q = 0; q < 4; ++q) n += clamp_t(4 + q, g) == T ? 1 : 0;
+    if (fwd_ct(g) == 7 && clamp_t(3 + shift(g), g) == T) ++n;
+    return n;
+  }
+  __host__ __device__ static constexpr int stores_rng(int g, int t0, int t1) {  // groups [t0, t1]
+    int n = 0;
+    for (int T = t0; T <= t1; ++T) n += stores_grp(g, T);
+    return n;
+  }
+  // VMEM ops issued after DMA(i) and before the wait of barrier B_i (i >= 1, in step i-1)
+  __host__ __device__ static constexpr int younger_b(int i) {
+    int n = 0;
+    for (int j = i + 1; j <= i + kD - 1 && j < kBfSteps; ++j) n += G::n_glds(j);
+    if (SAVE) {
+      int first = 0;  // first step whose stores all follow the DMA
+      if (i >= kD && i - kD >= 1) {
+        const int p = i - kD;  // DMA(i) issued at B_p, after group sync_t(p-1) of step p-1
+        n += stores_rng(p - 1, sync_t(p - 1) + 1, nt(p - 1) - 1);
+        first = p;
+      } else {
+        if (i < kD) n += kFwdPrologueStores;  // DMA(i) issued in the prologue, before e / x saves
+        first = 0;
+      }
+      for (int g = first; g <= i - 2; ++g) n += stores_rng(g, 0, nt(g) - 1);
+      n += stores_rng(i - 1, 0, sync_t(i - 1));
+    }
+    return n;
+  }
+  __host__ __device__ static constexpr int younger_b0() {
+    int n = 0;
+    for (int j = 1; j < kD; ++j) n += G::n_glds(j);
+    return n + (SAVE ? kFwdPrologueStores : 0);
+  }
+
+  static __device__ __forceinline__ const char* slot_of(const char* lds, int g) {
+    return lds + (g % G::kNbuf) * G::kSlot;
+  }
+
+  // next step's first fragments / constants (issued after its barrier)
+  template <int g>
+  static __device__ __forceinline__ void next_first(St& S, const char* lds) {
+    load_frag<PR>(slot_of(lds, g), S.F[ring(g) % 3]);
+  }
+  template <int g>
+  static __device__ __forceinline__ void next_rest(St& S, const char* lds) {
+    if constexpr (nt(g) > 1) load_frag<PR>(slot_of(lds, g) + 2 * NP * 1024, S.F[(ring(g) + 1) % 3]);
+    constexpr int layer = fwd_layer(g), kc = fwd_kc(g);
+    constexpr int CL = layer == 0 ? 0 : (layer == 4 ? 3 : (kc < 7 ? layer - 1 : layer));
+    if constexpr (fwd_conv(g)) preload<CL, fwd_ct(g)>(S, lds);
+    (void)CL;
+  }
+
+  // MFMA group T of step g (prefetching the fragments of group T+2), its epilogue pieces, and the
+  // next step's barrier / DMA / first loads where they fall
+  template <int g, int T>
+  static __device__ __forceinline__ void group(const BfFwdArgs& a, St& S, const char* lds, const V8 (&act)[NP][2]) {
+    constexpr int NT = nt(g);
     if constexpr (T < NT) {
-      if constexpr (T + 2 < NT) load_frag<PR>(slot + (T + 2) * 2 * NP * 1024, F[(T + 2) % 3]);
-      if constexpr (NT == 1) mfma_frag<PR, false>(F[0], act, S.out);
-      else mfma_frag<PR, ZERO>(F[T % 3], act, S.acc[OUTSET][T]);
-      if constexpr (HASC && CONV && T == 0) mfma_frag<PR, true>(FC, S.ct, S.f);
+      constexpr int layer = fwd_layer(g);
+      constexpr int kc = fwd_kc(g);
+      constexpr int OUTSET = layer & 1;                      // h_layer -> acc[layer & 1]
+      constexpr bool ZERO = kc == 0 && layer <= 3;
+#if defined(PNR_EXP_NOCONV)
+      constexpr bool CONV = false;  // experiment: no epilogue work
+#else
+      constexpr bool CONV = fwd_conv(g);
+#endif
+      // epilogue job of this step: h_CL tile CT (tile 0 of a layer is built in its last step)
+      constexpr int CL = layer == 0 ? 0 : (layer == 4 ? 3 : (kc < 7 ? layer - 1 : layer));
+      constexpr int CT = fwd_ct(g);
+      constexpr int SET = CL & 1;
+      constexpr int SHIFT = shift(g);  // that tile is produced by group 0 of this step
+      constexpr int b = ring(g);
+      const char* slot = slot_of(lds, g);
+      if constexpr (HASC && CONV && T == clamp_t(1, g)) load_frag<PR>(slot + G::kMainH, S.FC);
+      if constexpr (HASC && CONV && T == clamp_t(3, g)) preload_fc<CL, CT>(S, lds);
+      if constexpr (T + 2 < NT) load_frag<PR>(slot + (T + 2) * 2 * NP * 1024, S.F[(b + T + 2) % 3]);
+      if constexpr (NT == 1) {
+        if constexpr (kc == 0) mfma_frag<PR, true>(S.F[b], act, S.out);
+        else mfma_frag<PR, false>(S.F[b], act, S.out);
+      } else {
+        mfma_frag<PR, ZERO>(S.F[(b + T) % 3], act, S.acc[OUTSET][T]);
+        // keep the accumulator in AGPRs: otherwise hipcc shuffles whole tiles between the register
+        // files every step (measured: 114 v_accvgpr_read per step where the epilogue needs 16)
+        asm volatile("" : "+a"(S.acc[OUTSET][T]));
+      }
+      // feature-branch product, one group before its consumers (conv2 from group 4 on)
+      if constexpr (HASC && CONV && T == clamp_t(3, g)) mfma_frag<PR, true>(S.FC, S.ct, S.f);
       if constexpr (CONV) conv_pieces<CL, CT, SET, SHIFT, NT, T>(a, S, lds);
+      if constexpr (g + 1 < kBfSteps) {
+        if constexpr (T == sync_t(g)) {
+          PNR_TICK(3 + g);
+#if defined(PNR_EXP_NODMA)
+          sync_chunk<0>();
+#else
+          sync_chunk<younger_b(g + 1)>();
+          stage_step<g + 1 + kD>(a, lds);
+#endif
+        }
+        constexpr int L0 = sync_t(g) > NT - 2 ? sync_t(g) : NT - 2;
+        if constexpr (T == L0) next_first<g + 1>(S, lds);
+        if constexpr (T == NT - 1) next_rest<g + 1>(S, lds);
+      }
       __builtin_amdgcn_sched_barrier(0);
-      group<NT, T + 1, OUTSET, ZERO, CONV, CL, CT, SET, SHIFT>(a, S, lds, slot, act, F, FC);
+      group<g, T + 1>(a, S, lds, act);
     }
   }
 
   template <int g>
   static __device__ __forceinline__ void step(const BfFwdArgs& a, St& S, const char* lds) {
     if constexpr (g < kBfSteps) {
-      constexpr int layer = fwd_layer(g);
-      constexpr int kc = fwd_kc(g);
-      constexpr int NT = layer == 4 ? 1 : 8;
-      constexpr int OUTSET = layer & 1;                      // h_layer -> acc[layer & 1]
-      constexpr bool ZERO = kc == 0 && layer <= 3;
-      // epilogue job of this step: h_CL tile CT (tile 0 of a layer is built in its last step)
-      constexpr bool CONV = fwd_conv(g);
-      constexpr int CL = layer == 0 ? 0 : (layer == 4 ? 3 : (kc < 7 ? layer - 1 : layer));
-      constexpr int CT = fwd_ct(g);
-      constexpr int SET = CL & 1;
-      constexpr int SHIFT = CT == 0 ? 1 : 0;  // that tile is produced by group 0 of this step
-      sync_chunk<G::younger(g)>();
-      stage_step<g + G::kDist>(a, lds);
-      const char* slot = lds + (g % G::kNbuf) * G::kSlot;
-      Frag<PR> F[3], FC;
-      load_frag<PR>(slot, F[0]);
-      if constexpr (NT > 1) load_frag<PR>(slot + 2 * NP * 1024, F[1]);
-      if constexpr (HASC && CONV) load_frag<PR>(slot + G::kMainH, FC);
-      if constexpr (layer == 0) {
-        group<NT, 0, OUTSET, ZERO, CONV, CL, CT, SET, SHIFT>(a, S, lds, slot, S.ft[kc], F, FC);
+      // both accumulator sets live in the 256 AGPRs for the whole kernel; out / f stay in VGPRs
+#pragma unroll
+      for (int st = 0; st < 2; ++st)
+#pragma unroll
+        for (int t = 0; t < 8; ++t) asm volatile("" : "+a"(S.acc[st][t]));
+      if constexpr (fwd_layer(g) == 0) {
+        group<g, 0>(a, S, lds, S.ft[fwd_kc(g)]);
       } else {
 #pragma unroll
         for (int pt = 0; pt < NP; ++pt)
 #pragma unroll
           for (int s = 0; s < 2; ++s) S.cur[pt][s] = S.nxt[pt][s];
-        group<NT, 0, OUTSET, ZERO, CONV, CL, CT, SET, SHIFT>(a, S, lds, slot, S.cur, F, FC);
+        group<g, 0>(a, S, lds, S.cur);
       }
       step<g + 1>(a, S, lds);
     }
   }
 
+  __host__ __device__ static constexpr int prologue_glds() {
+    int n = 0;
+    for (int j = 0; j < kD; ++j) n += G::n_glds(j);
+    return n;
+  }
+  // prologue DMAs: steps 0 .. kD-1 (after the raw tables)
   template <int g>
   static __device__ __forceinline__ void prologue(const BfFwdArgs& a, const char* lds) {
-    if constexpr (g < G::kDist) {
+    if constexpr (g < kD) {
       stage_step<g>(a, lds);
       prologue<g + 1>(a, lds);
     }
+  }
+  // barrier B_0: step 0's slot is valid; DMA of step kD; step 0's first loads
+  static __device__ __forceinline__ void start(const BfFwdArgs& a, St& S, const char* lds) {
+    PNR_TICK(2);
+#if defined(PNR_EXP_NODMA)
+    sync_chunk<0>();
+#else
+    sync_chunk<younger_b0()>();
+    stage_step<kD>(a, lds);
+#endif
+    next_first<0>(S, lds);
+    next_rest<0>(S, lds);
   }
 };
 
 template <int PR, bool HASC, bool SAVE>
 __global__ __launch_bounds__(256, 1) void k_mlp_fwd16(BfFwdArgs a, int mode) {
   using K = BfFwd<PR, HASC, SAVE>;
-  using G = typename K::G;
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, hh = lane >> 5, j = lane & 31;
   const int64_t p = (int64_t)blockIdx.x * 128 + wave * 32 + j;
@@ -411,6 +551,7 @@ __global__ __launch_bounds__(256, 1) void k_mlp_fwd16(BfFwdArgs a, int mode) {
                rbase + kRawBytes + i * 4096);
     }
   }
+  PNR_TICK(0);
   K::template prologue<0>(a, lds);
 
   BfState<PR> S;
@@ -443,10 +584,14 @@ __global__ __launch_bounds__(256, 1) void k_mlp_fwd16(BfFwdArgs a, int mode) {
     split_tile<PR>(cv, S.ct);
   }
 #pragma unroll
-  for (int r = 0; r < 16; ++r) S.out[r] = 0.f;
+  for (int st = 0; st < 2; ++st)
+#pragma unroll
+    for (int t = 0; t < 8; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) S.acc[st][t][r] = 0.f;
 
   // Fourier features: the raw tables must have landed (they are older than the step DMAs)
-  sync_chunk<G::younger(0) + G::n_glds(0)>();
+  sync_chunk<K::prologue_glds()>();
   {
     const float* FB = K::raw_lds(lds) + kRawFB;
 #pragma unroll
@@ -462,7 +607,7 @@ __global__ __launch_bounds__(256, 1) void k_mlp_fwd16(BfFwdArgs a, int mode) {
           arg = __builtin_fmaf(x1, FB[kFourierPad + k], arg);
           arg = __builtin_fmaf(x2, FB[2 * kFourierPad + k], arg);
         }
-        v[r] = k < kFourier ? sinf(arg) : 0.f;
+        v[r] = k < kFourier ? fourier_sc<false>(arg) : 0.f;
       }
       if constexpr (SAVE) {
         float* row = a.save.eP + S.col * kFourierPad + 32 * t + 4 * hh;
@@ -474,7 +619,12 @@ __global__ __launch_bounds__(256, 1) void k_mlp_fwd16(BfFwdArgs a, int mode) {
     }
     if (SAVE && hh == 0) a.save.xP[S.col] = make_float4(x0, x1, x2, inside ? 1.f : 0.f);
   }
+  PNR_TICK(1);
+  static_assert(K::younger_b(1) < 64 && K::younger_b(2) < 64 && K::younger_b(3) < 64 && K::younger_b(20) < 64,
+                "vmcnt range");
+  K::start(a, S, lds);
   K::template step<0>(a, S, lds);
+  PNR_TICK(40);
 
   if (S.valid && hh == 0) {
     const float* rawl = K::raw_lds(lds);

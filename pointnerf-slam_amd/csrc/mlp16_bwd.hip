@@ -128,6 +128,7 @@ struct BfBwd {
     if constexpr (T < NT) {
       if constexpr (T + 2 < NT) load_frag<PR, NS>(slot + (T + 2) * NS * 2 * 1024, F[(T + 2) % 3]);
       mfma_frag<PR, ZERO, bf16x8, NS>(F[T % 3], act, S.acc[OUTSET][T]);
+      asm volatile("" : "+a"(S.acc[OUTSET][T]));
       if constexpr (CONV) conv_pieces<CC, CT, SHIFT, NT, T>(a, S, FC);
       __builtin_amdgcn_sched_barrier(0);
       group<NS, NT, T + 1, OUTSET, ZERO, CONV, CC, CT, SHIFT>(a, S, slot, act, F, FC);
@@ -151,10 +152,17 @@ struct BfBwd {
       sync_chunk<G::younger(g)>();
       stage_step<g + G::kDist>(a, wmain, wfc, lds);
       const char* slot = lds + (g % G::kNbuf) * G::kSlot;
+      // both accumulator sets live in the 256 AGPRs for the whole kernel (see k_mlp_fwd16)
+#pragma unroll
+      for (int st = 0; st < 2; ++st)
+#pragma unroll
+        for (int t = 0; t < 8; ++t) asm volatile("" : "+a"(S.acc[st][t]));
+      asm volatile("" : "+v"(S.gc));
       Frag<PR> F[3], FC;
       load_frag<PR, NS>(slot, F[0]);
       load_frag<PR, NS>(slot + NS * 2 * 1024, F[1]);
       if constexpr (HASC && CONV) load_frag<PR>(slot + 32768, FC);
+      __builtin_amdgcn_sched_barrier(0);
       if constexpr (g > 0) {
 #pragma unroll
         for (int pt = 0; pt < 2; ++pt)
@@ -208,6 +216,12 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd16(const float* __restrict__ 
   }
 #pragma unroll
   for (int r = 0; r < 16; ++r) S.gc[r] = 0.f;
+#pragma unroll
+  for (int st = 0; st < 2; ++st)
+#pragma unroll
+    for (int t = 0; t < 8; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) S.acc[st][t][r] = 0.f;
   K::template step<0>(a, S, wmain, wfc, lds);
 
   // g_arg = g_e * cos(x@B), g_x = B g_arg (the k_mlp_bwd epilogue on set 0, tiles 0..2)
@@ -233,7 +247,7 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd16(const float* __restrict__ 
           arg = __builtin_fmaf(x1, FB[kFourierPad + k], arg);
           arg = __builtin_fmaf(x2, FB[2 * kFourierPad + k], arg);
         }
-        g = S.acc[0][t][r] * cosf(arg);
+        g = S.acc[0][t][r] * fourier_sc<true>(arg);
         s0 = __builtin_fmaf(FB[k], g, s0);
         s1 = __builtin_fmaf(FB[kFourierPad + k], g, s1);
         s2 = __builtin_fmaf(FB[2 * kFourierPad + k], g, s2);

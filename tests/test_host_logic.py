@@ -118,3 +118,40 @@ def test_renderer_rejects_out_of_scope_cfg():
     cfg['rendering']['N_surface'] = 4
     with pytest.raises(NotImplementedError):
         pnr.Renderer(cfg, None, slam)
+
+
+def test_fourier_sincos_reduction_matches_libm():
+    """The sin / cos of the split-precision kernels (csrc/dev_common.h fourier_sc): k = rint(2x/pi),
+    r = x - k pi/2 by three fma steps with pi/2 = C1 + C2 + C3 (fp32 parts), minimax polynomials on
+    [-pi/4, pi/4].  Emulated here in exact rational arithmetic per fp32 operation; the max abs error
+    over the Fourier argument range must stay at the fp32 libm level (~1 ulp of 1)."""
+    from fractions import Fraction
+    f32 = np.float32
+
+    def fma(a, b, c):
+        return f32(float(Fraction(float(a)) * Fraction(float(b)) + Fraction(float(c))))
+
+    C1, C2, C3 = f32(1.5707963705062866), f32(-4.3711388286737929e-08), f32(-1.7151245100058819e-15)
+    # C1 + C2 + C3 is pi/2 to ~1e-22
+    assert abs(float(C1) + float(C2) + float(C3) - np.pi / 2) < 1e-15
+
+    def sc(x, cos):
+        x = f32(x)
+        k = f32(np.rint(f32(x * f32(0.636619772367581343))))
+        r = fma(-k, C1, x)
+        r = fma(-k, C2, r)
+        r = fma(-k, C3, r)
+        z = f32(r * r)
+        sn = fma(fma(fma(f32(-1.9515295891e-4), z, f32(8.3321608736e-3)), z, f32(-1.6666654611e-1)), f32(z * r), r)
+        cs = fma(fma(fma(fma(f32(2.443315711809948e-5), z, f32(-1.388731625493765e-3)), z,
+                         f32(4.166664568298827e-2)), z, f32(-0.5)), z, f32(1.0))
+        q = (int(k) + (1 if cos else 0)) & 3
+        v = cs if q & 1 else sn
+        return -v if q & 2 else v
+
+    rng = np.random.default_rng(0)
+    xs = np.concatenate([rng.uniform(-300, 300, 3000), rng.uniform(-3000, 3000, 500),
+                         rng.uniform(-1, 1, 300)]).astype(np.float32)
+    es = max(abs(float(sc(x, False)) - np.sin(np.float64(x))) for x in xs)
+    ec = max(abs(float(sc(x, True)) - np.cos(np.float64(x))) for x in xs)
+    assert es < 1e-7 and ec < 1e-7, (es, ec)

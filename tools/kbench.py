@@ -21,8 +21,12 @@ def main():
     ap.add_argument('--points', type=int, default=4 * 1024 * 1024)
     ap.add_argument('--reps', type=int, default=5)
     ap.add_argument('--precision', default='fp32,bf16x3,bf16')
+    ap.add_argument('--lib', default=None, help='load this libpnr.so build instead (experiments)')
+    ap.add_argument('--eval-only', action='store_true')
     args = ap.parse_args()
     import pnr
+    if args.lib:
+        pnr._lib.load(os.path.abspath(args.lib))
     from pnr._lib import timing_read
     dev = torch.device('cuda:0')
     lib = pnr.library()
@@ -63,6 +67,17 @@ def main():
             r.eval_points(pts, dec)
         torch.cuda.synchronize()
         report(f'[{prec}] k_mlp_fwd eval (f64 pts)', 0, 443438)
+        if hasattr(lib, 'pnr_dbg_read'):  # experiment build: s_memtime timeline of one workgroup
+            import ctypes
+            buf = (ctypes.c_ulonglong * (4 * 48))()
+            lib.pnr_dbg_read(buf)
+            for w in range(4):
+                t = [buf[w * 48 + i] for i in range(48)]
+                d = [t[i + 1] - t[i] for i in range(0, 39)] + [t[40] - t[36]]
+                print(f'wave {w}: start->prologue {d[0]}, steps:', ' '.join(str(x) for x in d[1:]), flush=True)
+        if args.eval_only:
+            lib.pnr_timing_enable(0)
+            continue
         # forward with save + backward (MLP autograd path)
         x = pts.float().requires_grad_(False)
         timing_read(0), timing_read(1), timing_read(3)
