@@ -153,8 +153,12 @@ struct Frag {
   typename Prec<PR>::V8 a[Prec<PR>::NP][2];
 };
 
+// Fragment ring of the split kernels: R tiles, prefetched R-1 MFMA groups ahead (LDS read latency
+// under four streaming waves is ~300 cycles: 2 groups of lead left MFMAs waiting).  The feature
+// + save variant keeps R = 3 (R = 4 spills there).
+
 // Per-wave register state of the forward.
-template <int PR>
+template <int PR, int R>
 struct BfState {
   using V8 = typename Prec<PR>::V8;
   static constexpr int NP = Prec<PR>::NP;
@@ -170,7 +174,7 @@ struct BfState {
   float4 bcq[4];       // fc bias quads (features)
   float inv, finv;     // f16 weight scales of the layer / fc branch
   uint32_t mw[4];      // ReLU bit words of the layer being converted
-  Frag<PR> F[3];       // fragment ring (one 32-row output tile of the current / next step each)
+  Frag<PR> F[R];       // fragment ring (one 32-row output tile of the current / next step each)
   Frag<PR> FC;         // feature-branch fragments of the step's epilogue tile
   int64_t col, mask_word0;
   bool valid, inside;
@@ -247,7 +251,8 @@ struct BfFwd {
   static constexpr bool F16 = Prec<PR>::F16;
   using G = BfGeo<NP, HASC, SAVE>;
   using V8 = typename Prec<PR>::V8;
-  using St = BfState<PR>;
+  static constexpr int kRing = (HASC && SAVE) ? 3 : 4, kPf = kRing - 1;
+  using St = BfState<PR, kRing>;
 
   // issue the DMA of step g into its ring slot (wave-uniform, lane-linear 4 KiB pieces)
   template <int g>
@@ -366,7 +371,13 @@ struct BfFwd {
   __host__ __device__ static constexpr int ring(int g) {
     int b = 0;
     for (int i = 0; i < g; ++i) b += nt(i);
-    return b % 3;
+    return b % kRing;
+  }
+  // group of step g that issues the read of the next step's fragment tile k (after the barrier)
+  __host__ __device__ static constexpr int next_grp(int g, int k) {
+    const int t = nt(g) - kPf + k;
+    const int u = t > sync_t(g) ? t : sync_t(g);
+    return u < nt(g) - 1 ? u : nt(g) - 1;
   }
   __host__ __device__ static constexpr int shift(int g) { return fwd_ct(g) == 0 ? 1 : 0; }
   __host__ __device__ static constexpr int clamp_t(int t, int g) { return t < nt(g) - 1 ? t : nt(g) - 1; }
@@ -412,14 +423,14 @@ struct BfFwd {
     return lds + (g % G::kNbuf) * G::kSlot;
   }
 
-  // next step's first fragments / constants (issued after its barrier)
-  template <int g>
-  static __device__ __forceinline__ void next_first(St& S, const char* lds) {
-    load_frag<PR>(slot_of(lds, g), S.F[ring(g) % 3]);
+  // next step's fragment tile k (issued after its barrier)
+  template <int g, int k>
+  static __device__ __forceinline__ void next_frag(St& S, const char* lds) {
+    if constexpr (k < nt(g)) load_frag<PR>(slot_of(lds, g) + k * 2 * NP * 1024, S.F[(ring(g) + k) % kRing]);
   }
+  // next step's epilogue constants
   template <int g>
-  static __device__ __forceinline__ void next_rest(St& S, const char* lds) {
-    if constexpr (nt(g) > 1) load_frag<PR>(slot_of(lds, g) + 2 * NP * 1024, S.F[(ring(g) + 1) % 3]);
+  static __device__ __forceinline__ void next_consts(St& S, const char* lds) {
     constexpr int layer = fwd_layer(g), kc = fwd_kc(g);
     constexpr int CL = layer == 0 ? 0 : (layer == 4 ? 3 : (kc < 7 ? layer - 1 : layer));
     if constexpr (fwd_conv(g)) preload<CL, fwd_ct(g)>(S, lds);
@@ -450,12 +461,13 @@ struct BfFwd {
       const char* slot = slot_of(lds, g);
       if constexpr (HASC && CONV && T == clamp_t(1, g)) load_frag<PR>(slot + G::kMainH, S.FC);
       if constexpr (HASC && CONV && T == clamp_t(3, g)) preload_fc<CL, CT>(S, lds);
-      if constexpr (T + 2 < NT) load_frag<PR>(slot + (T + 2) * 2 * NP * 1024, S.F[(b + T + 2) % 3]);
+      if constexpr (T + kPf < NT) load_frag<PR>(slot + (T + kPf) * 2 * NP * 1024, S.F[(b + T + kPf) % kRing]);
+      __builtin_amdgcn_sched_barrier(0);  // prefetch first, then the group's MFMAs
       if constexpr (NT == 1) {
         if constexpr (kc == 0) mfma_frag<PR, true>(S.F[b], act, S.out);
         else mfma_frag<PR, false>(S.F[b], act, S.out);
       } else {
-        mfma_frag<PR, ZERO>(S.F[(b + T) % 3], act, S.acc[OUTSET][T]);
+        mfma_frag<PR, ZERO>(S.F[(b + T) % kRing], act, S.acc[OUTSET][T]);
         // keep the accumulator in AGPRs: otherwise hipcc shuffles whole tiles between the register
         // files every step (measured: 114 v_accvgpr_read per step where the epilogue needs 16)
         asm volatile("" : "+a"(S.acc[OUTSET][T]));
@@ -473,9 +485,10 @@ struct BfFwd {
           stage_step<g + 1 + kD>(a, lds);
 #endif
         }
-        constexpr int L0 = sync_t(g) > NT - 2 ? sync_t(g) : NT - 2;
-        if constexpr (T == L0) next_first<g + 1>(S, lds);
-        if constexpr (T == NT - 1) next_rest<g + 1>(S, lds);
+        if constexpr (T == next_grp(g, 0)) next_frag<g + 1, 0>(S, lds);
+        if constexpr (T == next_grp(g, 1)) next_frag<g + 1, 1>(S, lds);
+        if constexpr (T == next_grp(g, 2)) next_frag<g + 1, 2>(S, lds);
+        if constexpr (T == NT - 1) next_consts<g + 1>(S, lds);
       }
       __builtin_amdgcn_sched_barrier(0);
       group<g, T + 1>(a, S, lds, act);
@@ -525,8 +538,10 @@ struct BfFwd {
     sync_chunk<younger_b0()>();
     stage_step<kD>(a, lds);
 #endif
-    next_first<0>(S, lds);
-    next_rest<0>(S, lds);
+    next_frag<0, 0>(S, lds);
+    next_frag<0, 1>(S, lds);
+    next_frag<0, 2>(S, lds);
+    next_consts<0>(S, lds);
   }
 };
 
@@ -554,7 +569,7 @@ __global__ __launch_bounds__(256, 1) void k_mlp_fwd16(BfFwdArgs a, int mode) {
   PNR_TICK(0);
   K::template prologue<0>(a, lds);
 
-  BfState<PR> S;
+  typename K::St S;
   S.valid = p < a.P;
   float x0 = 0.f, x1 = 0.f, x2 = 0.f;
   bool inside = false;
