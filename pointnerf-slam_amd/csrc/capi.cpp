@@ -168,6 +168,7 @@ struct BwdWS {
   float* g_c;     // [P][32]      features only: dL/dc
   void* gws;      // features only: gather-backward work list
   size_t gws_bytes;
+  uint32_t* gmax; // split precisions: max |g_out| (float bits) -> scale of the f16 deltas
   int64_t C;
 };
 
@@ -179,6 +180,7 @@ BwdWS carve_bwd(int64_t P, int64_t n, void* ws, size_t* bytes, bool feat = false
   b.g_out = c.take<float>(P * 4);
   b.g_x = c.take<float>(P * 3);
   b.g_nrm = c.take<float>(n);
+  b.gmax = c.take<uint32_t>(64);
   b.dP = c.take<float>((size_t)4 * kHidden * b.C);
   b.gargP = c.take<float>(kFourierPad * b.C);
   if (feat) {
@@ -206,6 +208,12 @@ __global__ void k_fill(float* p, int64_t n, float v) {
 // Shared backward core over P points with saved activations `sv` and dL/draw in b.g_out.
 int mlp_backward_core(int prec, const float* packed, const SaveArgs& sv, int64_t P, BwdWS& b, float* const* grads,
                       bool want_gx, hipStream_t st, const FeatBwd* fb = nullptr) {
+  const bool split = prec != PNR_PREC_FP32;  // split MFMA delta chain + f16 operands (wgrad16.hip)
+  if (split) {  // one delta scale for the whole call, from max |g_out| over every saved row
+    if (hipMemsetAsync(b.gmax, 0, 4, st) != hipSuccess) return (int)hipGetLastError();
+    const int rc = launch_gmax(b.g_out, sv.ld * 4, b.gmax, st);
+    if (rc) return rc;
+  }
   for (int64_t p0 = 0; p0 < P; p0 += b.C) {
     const int64_t C = (P - p0) < b.C ? (P - p0) : b.C;
     BwdArgs a;
@@ -221,27 +229,35 @@ int mlp_backward_core(int prec, const float* packed, const SaveArgs& sv, int64_t
     a.fcw = fb ? fb->fcw : nullptr;
     a.gH = b.gH;
     a.g_c = fb ? b.g_c + p0 * kCDim : nullptr;
+    a.gmax = b.gmax;
     // the delta chain: exact fp32 MFMA for PNR_PREC_FP32, bf16x3 split MFMA otherwise
     int rc = prec == PNR_PREC_FP32 ? launch_mlp_bwd(packed, a, C, st) : launch_mlp_bwd_bf(packed, a, C, st);
     if (rc) return rc;
-    const float* hp = sv.hP + p0 * kHidden;  // h_l rows of this chunk: hp + l_idx * ld * 256
-    const int64_t hstride = sv.ld * kHidden;
+    const int64_t hstride = sv.ld * kHidden;  // h_l rows of this chunk: h + l_idx * ld * 256 + p0 * 256
     const int64_t dstride = b.C * kHidden;
-    // output layer: dWo (4x256) += g_out^T h4 ; dbo += colsum(g_out)
-    rc = launch_wgrad(kWgradOut, b.g_out + p0 * 4, 4, hp + 3 * hstride, kHidden, C, grads[9], kHidden, grads[10], st);
-    if (rc) return rc;
-    // hidden layers: dW_l += delta_{l+1}^T h_l  (W3: delta4.h3, W2: delta3.h2, W1: delta2.h1)
-    const bool split = prec != PNR_PREC_FP32;  // bf16x3 split MFMA (wgrad16.hip) for the large shapes
-    for (int l = 3; l >= 1 && rc == 0; --l)
-      rc = split ? launch_wgrad16(kWgradHidden, b.dP + l * dstride, hp + (l - 1) * hstride, C, grads[1 + 2 * l],
-                                  kHidden, grads[2 + 2 * l], st)
-                 : launch_wgrad(kWgradHidden, b.dP + l * dstride, kHidden, hp + (l - 1) * hstride, kHidden, C,
-                                grads[1 + 2 * l], kHidden, grads[2 + 2 * l], st);
-    if (rc) return rc;
-    // first layer: dW0 (256x93) += delta1^T e ; db0
-    rc = split ? launch_wgrad16(kWgradFirst, b.dP, sv.eP + p0 * kFourierPad, C, grads[1], kFourier, grads[2], st)
-               : launch_wgrad(kWgradFirst, b.dP, kHidden, sv.eP + p0 * kFourierPad, kFourier, C, grads[1], kFourier,
-                              grads[2], st);
+    if (split) {  // f16 operands: h / e saved by k_mlp_fwd16, scaled deltas by k_mlp_bwd16
+      const _Float16* h16 = reinterpret_cast<const _Float16*>(sv.hP) + p0 * kHidden;
+      const _Float16* d16 = reinterpret_cast<const _Float16*>(b.dP);
+      const _Float16* e16 = reinterpret_cast<const _Float16*>(sv.eP) + p0 * kFourierPad;
+      // output layer: dWo (4x256) += g_out^T h4 ; dbo += colsum(g_out)
+      rc = launch_wgrad_out16(b.g_out + p0 * 4, h16 + 3 * hstride, C, grads[9], grads[10], st);
+      // hidden layers: dW_l += delta_{l+1}^T h_l  (W3: delta4.h3, W2: delta3.h2, W1: delta2.h1)
+      for (int l = 3; l >= 1 && rc == 0; --l)
+        rc = launch_wgrad16(kWgradHidden, d16 + l * dstride, h16 + (l - 1) * hstride, C, grads[1 + 2 * l], kHidden,
+                            grads[2 + 2 * l], b.gmax, st);
+      // first layer: dW0 (256x93) += delta1^T e ; db0
+      if (rc == 0) rc = launch_wgrad16(kWgradFirst, d16, e16, C, grads[1], kFourier, grads[2], b.gmax, st);
+    } else {
+      const float* hp = sv.hP + p0 * kHidden;
+      rc = launch_wgrad(kWgradOut, b.g_out + p0 * 4, 4, hp + 3 * hstride, kHidden, C, grads[9], kHidden, grads[10],
+                        st);
+      for (int l = 3; l >= 1 && rc == 0; --l)
+        rc = launch_wgrad(kWgradHidden, b.dP + l * dstride, kHidden, hp + (l - 1) * hstride, kHidden, C,
+                          grads[1 + 2 * l], kHidden, grads[2 + 2 * l], st);
+      if (rc == 0)
+        rc = launch_wgrad(kWgradFirst, b.dP, kHidden, sv.eP + p0 * kFourierPad, kFourier, C, grads[1], kFourier,
+                          grads[2], st);
+    }
     if (rc) return rc;
     // Fourier: dB (3x93) += x^T g_arg   (x rows are float4 (x0,x1,x2,inside): 3 of 4 used)
     rc = launch_wgrad(kWgradFourier, reinterpret_cast<const float*>(sv.xP + p0), 3, b.gargP, kFourier, C, grads[0],

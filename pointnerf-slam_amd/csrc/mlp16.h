@@ -37,6 +37,7 @@ namespace pnr {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 
 template <int PR>
 struct Prec {
@@ -329,9 +330,11 @@ struct BfFwd {
 #pragma unroll
       for (int i = 0; i < 4; ++i) S.v[4 * q + i] += (F16 ? S.f[4 * q + i] * inv : S.f[4 * q + i]) + b4[i];
     }
-    if constexpr (SAVE)
-      *reinterpret_cast<float4*>(a.save.hP + ((int64_t)L * a.save.ld + S.col) * kHidden + 32 * t + 8 * q + 4 * hh) =
-          make_float4(S.v[4 * q], S.v[4 * q + 1], S.v[4 * q + 2], S.v[4 * q + 3]);
+    if constexpr (SAVE) {  // f16 activation save (pnr_internal.h SaveArgs)
+      f16x4 hv = {(_Float16)S.v[4 * q], (_Float16)S.v[4 * q + 1], (_Float16)S.v[4 * q + 2], (_Float16)S.v[4 * q + 3]};
+      *reinterpret_cast<f16x4*>(reinterpret_cast<_Float16*>(a.save.hP) +
+                                ((int64_t)L * a.save.ld + S.col) * kHidden + 32 * t + 8 * q + 4 * hh) = hv;
+    }
     split_quad<PR>(S.v + 4 * q, q, S.nxt);
   }
 
@@ -625,10 +628,12 @@ __global__ __launch_bounds__(256, 1) void k_mlp_fwd16(BfFwdArgs a, int mode) {
         v[r] = k < kFourier ? fourier_sc<false>(arg) : 0.f;
       }
       if constexpr (SAVE) {
-        float* row = a.save.eP + S.col * kFourierPad + 32 * t + 4 * hh;
+        _Float16* row = reinterpret_cast<_Float16*>(a.save.eP) + S.col * kFourierPad + 32 * t + 4 * hh;
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
-          *reinterpret_cast<float4*>(row + 8 * q) = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+        for (int q = 0; q < 4; ++q) {
+          f16x4 ev = {(_Float16)v[4 * q], (_Float16)v[4 * q + 1], (_Float16)v[4 * q + 2], (_Float16)v[4 * q + 3]};
+          *reinterpret_cast<f16x4*>(row + 8 * q) = ev;
+        }
       }
       split_tile<PR>(v, S.ft[t]);
     }

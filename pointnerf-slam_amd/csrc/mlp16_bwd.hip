@@ -48,6 +48,7 @@ struct BwdState {
   bf16x8 tmp[2][2];     // split dL/dh tile (feature branch operand)
   float v[16];
   uint4 m[4];           // ReLU bit words of h1..h4 (this lane)
+  float dscale;         // 2^e of the f16 delta saves
   int64_t dcol;
 };
 
@@ -92,8 +93,11 @@ struct BfBwd {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
       if (!((wd >> ((t & 1) * 16 + 4 * q + i)) & 1u)) S.v[4 * q + i] = 0.f;
-    *reinterpret_cast<float4*>(a.dP + ((int64_t)li * a.ld_d + S.dcol) * kHidden + 32 * t + 8 * q + 4 * hh) =
-        make_float4(S.v[4 * q], S.v[4 * q + 1], S.v[4 * q + 2], S.v[4 * q + 3]);
+    // f16 delta * 2^e for the weight-gradient GEMMs (wgrad16.hip undoes the scale)
+    f16x4 dv = {(_Float16)(S.v[4 * q] * S.dscale), (_Float16)(S.v[4 * q + 1] * S.dscale),
+                (_Float16)(S.v[4 * q + 2] * S.dscale), (_Float16)(S.v[4 * q + 3] * S.dscale)};
+    *reinterpret_cast<f16x4*>(reinterpret_cast<_Float16*>(a.dP) + ((int64_t)li * a.ld_d + S.dcol) * kHidden + 32 * t +
+                              8 * q + 4 * hh) = dv;
     split_quad<PR>(S.v + 4 * q, q, S.nxt);
   }
 
@@ -197,6 +201,7 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd16(const float* __restrict__ 
 
   BwdState S;
   S.dcol = p;
+  S.dscale = delta_scale(*a.gmax);
   const int64_t col = a.p0 + p;
   const int64_t mstride = (a.ld / 32) * 64;
   const uint4* mk = a.masks + ((a.p0 + (int64_t)blockIdx.x * 128) / 32 + wave_id()) * 64;
@@ -285,6 +290,23 @@ static int launch_bwd16(const float* packed, const BwdArgs& a, int64_t P, hipStr
                                                (int)lds) == hipSuccess;
   if (!attr) return PNR_E_ARG;
   hipLaunchKernelGGL(kern, dim3((unsigned)((P + 127) / 128)), dim3(256), lds, st, packed, a, P);
+  return hip_status(hipGetLastError());
+}
+
+__global__ void k_gmax(const float* __restrict__ g, int64_t n, uint32_t* __restrict__ out) {
+  float m = 0.f;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    m = fmaxf(m, fabsf(g[i]));
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  if ((threadIdx.x & 63) == 0 && m > 0.f) atomicMax(out, __float_as_uint(m));  // non-negative floats order as uints
+}
+
+int launch_gmax(const float* g, int64_t n, uint32_t* out, hipStream_t st) {
+  if (n <= 0) return 0;
+  int64_t blocks = (n + 255) / 256;
+  if (blocks > 2048) blocks = 2048;
+  hipLaunchKernelGGL(k_gmax, dim3((unsigned)blocks), dim3(256), 0, st, g, n, out);
   return hip_status(hipGetLastError());
 }
 

@@ -1,22 +1,26 @@
-// wgrad16.hip -- weight-gradient GEMMs of the decoder backward on bf16x3 split MFMA.
+// wgrad16.hip -- weight-gradient GEMMs of the decoder backward for the split precisions.
 //
-//   C[256][NB] += A[K][256]^T B[K][WB]        (A, B point-major fp32: row k = one point)
-//   bias[256]  += sum_k A[k][:]               (optional)
+//   C[256][NB] += s^-1 * A[K][256]^T B[K][WB]     (A, B point-major f16: row k = one point)
+//   bias[256]  += s^-1 * sum_k A[k][:]            (optional)
 //
-// Used for every precision but PNR_PREC_FP32 (wgrad.hip keeps the fp32 MFMA form) on the two large
-// shapes of src/conv_onet/models/decoder.py:149-159:
+// Used for every precision but PNR_PREC_FP32 (wgrad.hip keeps the fp32 form) on the two large shapes
+// of src/conv_onet/models/decoder.py:149-159:
 //   dW3 = delta4^T h3, dW2 = delta3^T h2, dW1 = delta2^T h1     WB = 256 (8 column tiles)
 //   dW0 = delta1^T e                                            WB = 96 (3 column tiles, 93 used)
+// A = deltas stored by k_mlp_bwd16 as f16 * s (s = 2^e from max |g_out|, delta_scale), B = f16
+// activations stored by k_mlp_fwd16.  The products of f16 values are exact in fp32, so the only
+// error is the one storage rounding of each operand (<= 2^-12 relative).
 //
-// K (points, millions) is split over workgroups.  A workgroup streams 32-point tiles: every thread
-// loads its float4s of the next tile into registers while the current tile computes, then splits
-// them into bf16 hi / lo parts and writes them to a double-buffered LDS image [part][128-column
-// half][32 rows][256 B] whose 16-B chunks are XOR-swizzled by row.  The MFMA operands need 8
-// consecutive points of one column per lane: ds_read_b64_tr_b16 reads them transposed out of that
-// image (conflict-free with the swizzle; cdna_hip_programming.md T10).  Wave w owns output rows
-// [64w, 64w + 64) x all NB columns: 2 x NTB accumulator tiles stay in AGPRs for the whole K range
-// and are added into C with one float atomic per element at the end.
-// Per product Al.Bh + Ah.Bl + Ah.Bh: ~2^-16 relative, exponent range of fp32.
+// The training step is HBM-bound on these operands: the kernel only moves them.  K (points) is
+// split over workgroups of 8 waves (2 per SIMD).  Each 32-point tile of A and B goes straight from
+// HBM into LDS by global_load_lds (16-B pieces: the LDS side is lane-linear, the source address is
+// free, so the DMA itself lays the tile out as [32-column block T][32 points][64 B]); a 4-slot ring
+// keeps 3 tiles (~100 KB) in flight per CU.  The MFMA operands need 8 consecutive points of one
+// column per lane: ds_read_b64_tr_b16 reads them transposed out of the image (a 16-lane group
+// covers 4 rows x 32 B = 64 distinct banks; cdna_hip_programming.md T10).  Wave w owns output rows
+// [32w, 32w + 32) x all NB columns in NTB accumulator tiles for the whole K range, added into C with
+// one float atomic per element at the end.  The bias row sums come from the A fragments.
+// K must be a multiple of 32 and rows in [real K, K) zero in A (padded points: delta = 0).
 #include "mlp16.h"
 
 namespace pnr {
@@ -24,186 +28,194 @@ namespace pnr {
 typedef short v4i16 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
 
+constexpr int kTileB = 2112;  // bytes of one [32 points][64 B] block, +64 B pad (store banks)
+
 template <int NTB, int WB>
 struct Wg16 {
-  static constexpr int kHalvesA = 2;
-  static constexpr int kHalvesB = (WB + 127) / 128;
-  static constexpr int kImgA = 2 * kHalvesA * 32 * 256;  // bytes
-  static constexpr int kImgB = 2 * kHalvesB * 32 * 256;
-  static constexpr int kBuf = kImgA + kImgB;
-  static constexpr int kAV4 = 32 * 256 / 4 / 256;          // float4 of A per thread per tile (8)
-  static constexpr int kBV4 = (32 * WB / 4 + 255) / 256;   // float4 of B per thread per tile (8 or 3)
+  static constexpr int kThreads = 512;                     // 8 waves, 2 per SIMD
+  static constexpr int kTB = NTB == 3 ? 4 : NTB;           // B blocks staged (dW0: 4, one duplicate)
+  static constexpr int kImgA = 8 * kTileB;
+  static constexpr int kSlot = kImgA + kTB * kTileB;
+  static constexpr int kNbuf = 4, kDist = kNbuf - 1;
+  static constexpr int kLds = kNbuf * kSlot;
+  // DMA pieces (1 KiB = 16 points x 64 B of one block) per wave per tile: A 16 / 8 waves, B 2 kTB / 8
+  static constexpr int kPA = 2, kPB = 2 * kTB / 8;
+  static constexpr int kPieces = kPA + kPB;
 };
 
 struct Wg16Args {
-  const float* A;   // [K][256]
-  const float* B;   // [K][WB]
-  int nb;           // valid columns of B (columns of C)
-  int64_t K;
-  int64_t ks;       // points per workgroup (multiple of 32)
+  const _Float16* A;   // [K][256]
+  const _Float16* B;   // [K][WB]
+  int nb;              // valid columns of B (columns of C)
+  int64_t K;           // multiple of 32
+  int64_t ks;          // points per workgroup (multiple of 32)
   float* C;
   int64_t ldc;
   float* bias;
+  const uint32_t* gmax;  // scale of A: delta_scale(*gmax)
 };
 
-__device__ __forceinline__ int swz(int row) { return ((row & 3) << 2) | ((row >> 2) & 3); }
-
-// byte offset of 16-bit element (row, col) block start: col multiple of 4, within a [half][32][256 B] image
-__device__ __forceinline__ int img_off(int row, int col) {
-  const int half = col >> 7, cc = col & 127;
-  return (half * 32 + row) * 256 + 16 * ((cc >> 3) ^ swz(row)) + 8 * ((cc >> 2) & 1);
+__device__ __forceinline__ void glds16b(const void* gsrc, uint32_t lds_byte) {
+  glds16(reinterpret_cast<const float*>(gsrc), lds_byte);
 }
 
-// split one float4 (row, cols c..c+3) into the hi / lo images
-__device__ __forceinline__ void put4(char* img, int part_bytes, int row, int col, const float4& v) {
-  const float x[4] = {v.x, v.y, v.z, v.w};
-  v4i16 h, l;
+// stage 32-point tile k0 into `slot`: piece pc of an operand = (block T = pc >> 1, half h = pc & 1),
+// lane L -> point 16h + (L >> 2), 16-B chunk (L & 3) of the block's 64 B
+template <int NTB, int WB>
+__device__ __forceinline__ void stage_tile(const Wg16Args& a, int64_t k0, uint32_t slot) {
+  using Cfg = Wg16<NTB, WB>;
+  const int w = wave_id(), L = threadIdx.x & 63;
+  const int row = L >> 2, c16 = L & 3;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const __bf16 hb = (__bf16)x[i];
-    const __bf16 lb = (__bf16)(x[i] - (float)hb);
-    h[i] = __builtin_bit_cast(short, hb);
-    l[i] = __builtin_bit_cast(short, lb);
+  for (int i = 0; i < Cfg::kPA; ++i) {
+    const int pc = w + 8 * i, T = pc >> 1, h = pc & 1;
+    const char* src = reinterpret_cast<const char*>(a.A + (k0 + 16 * h + row) * 256) + T * 64 + c16 * 16;
+    glds16b(src, slot + T * kTileB + h * 1024);
   }
-  const int o = img_off(row, col);
-  *reinterpret_cast<v4i16*>(img + o) = h;
-  *reinterpret_cast<v4i16*>(img + part_bytes + o) = l;
+#pragma unroll
+  for (int i = 0; i < Cfg::kPB; ++i) {
+    const int pc = w + 8 * i, T = pc >> 1, h = pc & 1;
+    const int Ts = T < NTB ? T : 0;  // dW0: the 4th block duplicates block 0 (never read)
+    const char* src = reinterpret_cast<const char*>(a.B + (k0 + 16 * h + row) * WB) + Ts * 64 + c16 * 16;
+    glds16b(src, slot + Cfg::kImgA + T * kTileB + h * 1024);
+  }
 }
 
-// MFMA operand of column tile T (32 columns), k-step s of the tile, part image `img`:
-// lane l holds column 32T + (l&31), rows 16s + 8(l>>5) + j, j = 0..7 (two transposed reads)
-__device__ __forceinline__ bf16x8 tr_frag(const char* img, int T, int s) {
-  const int l = threadIdx.x & 63, g = l >> 4, i = l & 15, q = i >> 2, p = i & 3;
-  const int col = 32 * T + 16 * (g & 1) + 4 * p;
-  const int row0 = 16 * s + 8 * (g >> 1) + q;
-  const v4i16 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(img + img_off(row0, col)));
-  const v4i16 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(img + img_off(row0 + 4, col)));
-  const short e[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
-  bf16x8 r;
+// MFMA operand of 32-column block T, k-step s: lane l holds column 32T + (l&31), points
+// 16s + 8(l>>5) + j, j = 0..7 (two transposed reads; lane 4q+p of 16-lane group g supplies point
+// 16s + 8(g>>1) + q (+4), columns 16(g&1) + 4p .. +3)
+__device__ __forceinline__ f16x8 tr_frag(const char* img, int T, int s) {
+  const int l = threadIdx.x & 63, g = l >> 4, q = (l >> 2) & 3, p = l & 3;
+  const char* base = img + T * kTileB + (16 * s + 8 * (g >> 1) + q) * 64 + 32 * (g & 1) + 8 * p;
+  const v4i16 x = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)base);
+  const v4i16 y = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(base + 4 * 64));
+  const short e[8] = {x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]};
+  f16x8 r;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) r[j] = __builtin_bit_cast(__bf16, e[j]);
+  for (int j = 0; j < 8; ++j) r[j] = __builtin_bit_cast(_Float16, e[j]);
   return r;
 }
 
-__device__ __forceinline__ f32x16 mfma3(const bf16x8& ah, const bf16x8& al, const bf16x8& bh, const bf16x8& bl,
-                                        f32x16 c) {
-  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, c, 0, 0, 0);
-  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, c, 0, 0, 0);
-}
-
 template <int NTB, int WB>
-__global__ __launch_bounds__(256, 1) void k_wgrad16(Wg16Args a) {
+__global__ __launch_bounds__(512, 1) void k_wgrad16(Wg16Args a) {
   using Cfg = Wg16<NTB, WB>;
   extern __shared__ __attribute__((aligned(16))) char lds[];
-  const int tid = threadIdx.x, lane = tid & 63, hh = lane >> 5;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lane = threadIdx.x & 63, hh = lane >> 5;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // output row block of this wave
   const int64_t kb = (int64_t)blockIdx.x * a.ks;
   const int64_t ke = kb + a.ks < a.K ? kb + a.ks : a.K;
+  const int64_t ntile = (ke - kb) / 32;
+  const uint32_t lbase = lds_addr(reinterpret_cast<const float*>(lds));
 
-  f32x16 acc[2][NTB];
+  f32x16 acc[NTB];
 #pragma unroll
-  for (int x = 0; x < 2; ++x)
+  for (int y = 0; y < NTB; ++y)
 #pragma unroll
-    for (int y = 0; y < NTB; ++y)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[x][y][r] = 0.f;
-  float cs[4] = {0.f, 0.f, 0.f, 0.f};  // column sums of A (bias): columns 4 (tid & 63) .. +3
+    for (int r = 0; r < 16; ++r) acc[y][r] = 0.f;
+  float cs = 0.f;  // row sums of A (bias) for column 32w + (lane & 31), this lane half's points
 
-  float4 va[Cfg::kAV4], vb[Cfg::kBV4];
-  auto load = [&](int64_t k0) {
+  // the ring always issues exactly kDist tiles ahead (the tail re-stages the last tile into the
+  // free slot) so that every wait below has the same constant count
 #pragma unroll
-    for (int i = 0; i < Cfg::kAV4; ++i) {
-      const int f = tid + 256 * i, row = f >> 6;
-      va[i] = k0 + row < ke ? reinterpret_cast<const float4*>(a.A + (k0 + row) * 256)[f & 63]
-                            : make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int t = 0; t < Cfg::kDist; ++t)
+    stage_tile<NTB, WB>(a, kb + 32 * (t < ntile ? t : ntile - 1), lbase + t * Cfg::kSlot);
+  for (int64_t t = 0; t < ntile; ++t) {
+    sync_chunk<(Cfg::kDist - 1) * Cfg::kPieces>();  // this wave's pieces of tile t landed; all waves met
+    {
+      const int64_t tn = t + Cfg::kDist < ntile ? t + Cfg::kDist : ntile - 1;
+      stage_tile<NTB, WB>(a, kb + 32 * tn, lbase + (uint32_t)(((t + Cfg::kDist) % Cfg::kNbuf) * Cfg::kSlot));
     }
-#pragma unroll
-    for (int i = 0; i < Cfg::kBV4; ++i) {
-      const int f = tid + 256 * i, row = f / (WB / 4), c4 = f % (WB / 4);
-      vb[i] = (f < 32 * WB / 4 && k0 + row < ke) ? reinterpret_cast<const float4*>(a.B + (k0 + row) * WB)[c4]
-                                                 : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-  };
-  load(kb);
-  int buf = 0;
-  for (int64_t k0 = kb; k0 < ke; k0 += 32) {
-    char* ia = lds + buf * Cfg::kBuf;
-    char* ib = ia + Cfg::kImgA;
-#pragma unroll
-    for (int i = 0; i < Cfg::kAV4; ++i) {
-      const int f = tid + 256 * i;
-      put4(ia, Cfg::kImgA / 2, f >> 6, 4 * (f & 63), va[i]);
-      cs[0] += va[i].x; cs[1] += va[i].y; cs[2] += va[i].z; cs[3] += va[i].w;
-    }
-#pragma unroll
-    for (int i = 0; i < Cfg::kBV4; ++i) {
-      const int f = tid + 256 * i;
-      if (f < 32 * WB / 4) put4(ib, Cfg::kImgB / 2, f / (WB / 4), 4 * (f % (WB / 4)), vb[i]);
-    }
-    __syncthreads();
-    if (k0 + 32 < ke) load(k0 + 32);  // next tile in flight during the MFMAs
+    const char* ia = lds + (t % Cfg::kNbuf) * Cfg::kSlot;
+    const char* ib = ia + Cfg::kImgA;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      bf16x8 ah[2], al[2];
+      const f16x8 af = tr_frag(ia, w, s);
 #pragma unroll
-      for (int x = 0; x < 2; ++x) {
-        ah[x] = tr_frag(ia, 2 * w + x, s);
-        al[x] = tr_frag(ia + Cfg::kImgA / 2, 2 * w + x, s);
-      }
+      for (int j = 0; j < 8; ++j) cs += (float)af[j];
 #pragma unroll
-      for (int y = 0; y < NTB; ++y) {
-        const bf16x8 bh = tr_frag(ib, y, s), bl = tr_frag(ib + Cfg::kImgB / 2, y, s);
-#pragma unroll
-        for (int x = 0; x < 2; ++x) acc[x][y] = mfma3(ah[x], al[x], bh, bl, acc[x][y]);
-      }
+      for (int y = 0; y < NTB; ++y)
+        acc[y] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af, tr_frag(ib, y, s), acc[y], 0, 0, 0);
     }
-#pragma unroll
-    for (int x = 0; x < 2; ++x)
-#pragma unroll
-      for (int y = 0; y < NTB; ++y) asm volatile("" : "+a"(acc[x][y]));
-    buf ^= 1;
   }
-  // C[32(2w+x) + perm(r,hh)][32y + (lane&31)] += acc
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the re-staged tail DMAs
+  const float inv = 1.f / delta_scale(*a.gmax);
+  // C[32w + perm(r,hh)][32y + (lane&31)] += acc / s
 #pragma unroll
-  for (int x = 0; x < 2; ++x)
+  for (int y = 0; y < NTB; ++y) {
+    const int col = 32 * y + (lane & 31);
+    if (col >= a.nb) continue;
 #pragma unroll
-    for (int y = 0; y < NTB; ++y) {
-      const int col = 32 * y + (lane & 31);
-      if (col >= a.nb) continue;
-#pragma unroll
-      for (int r = 0; r < 16; ++r)
-        atomicAdd(a.C + (int64_t)(32 * (2 * w + x) + perm(r, hh)) * a.ldc + col, acc[x][y][r]);
-    }
-  if (a.bias) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) atomicAdd(a.bias + 4 * (tid & 63) + j, cs[j]);
+    for (int r = 0; r < 16; ++r) atomicAdd(a.C + (int64_t)(32 * w + perm(r, hh)) * a.ldc + col, acc[y][r] * inv);
   }
+  cs += __shfl_xor(cs, 32);
+  if (a.bias && hh == 0) atomicAdd(a.bias + 32 * w + lane, cs * inv);
 }
 
 template <int NTB, int WB>
 static int launch_k(const Wg16Args& a, hipStream_t st) {
   using Cfg = Wg16<NTB, WB>;
-  const size_t lds = 2 * Cfg::kBuf;
   auto kern = k_wgrad16<NTB, WB>;
   static const bool attr = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                               (int)lds) == hipSuccess;
+                                               Cfg::kLds) == hipSuccess;
   if (!attr) return PNR_E_ARG;
-  hipLaunchKernelGGL(kern, dim3((unsigned)((a.K + a.ks - 1) / a.ks)), dim3(256), lds, st, a);
+  hipLaunchKernelGGL(kern, dim3((unsigned)((a.K + a.ks - 1) / a.ks)), dim3(Cfg::kThreads), Cfg::kLds, st, a);
   return hip_status(hipGetLastError());
 }
 
-// kind: kWgradHidden (B [K][256]) or kWgradFirst (B [K][96], 93 columns)
-int launch_wgrad16(int kind, const float* A, const float* B, int64_t K, float* C, int64_t ldc, float* bias,
-                   hipStream_t st) {
+// kind: kWgradHidden (B [K][256]) or kWgradFirst (B [K][96], 93 columns); K is rounded up to 32
+// (the rows up to it exist and carry zero deltas)
+int launch_wgrad16(int kind, const void* A, const void* B, int64_t K, float* C, int64_t ldc, float* bias,
+                   const uint32_t* gmax, hipStream_t st) {
   if (K <= 0) return 0;
-  int64_t ks = (K + 511) / 512;  // ~2 workgroups per CU
+  K = (K + 31) / 32 * 32;
+  int64_t ks = (K + 255) / 256;  // one workgroup per CU
   ks = (ks + 31) / 32 * 32;
-  if (ks < 256) ks = 256;
+  if (ks < 128) ks = 128;
+  Wg16Args a{static_cast<const _Float16*>(A), static_cast<const _Float16*>(B), 256, K, ks, C, ldc, bias, gmax};
   TimingScope ts(kTimeWgrad, K, st);
-  if (kind == kWgradHidden) return launch_k<8, 256>(Wg16Args{A, B, 256, K, ks, C, ldc, bias}, st);
-  if (kind == kWgradFirst) return launch_k<3, 96>(Wg16Args{A, B, kFourier, K, ks, C, ldc, bias}, st);
+  if (kind == kWgradHidden) return launch_k<8, 256>(a, st);
+  if (kind == kWgradFirst) {
+    a.nb = kFourier;
+    return launch_k<3, 96>(a, st);
+  }
   return PNR_E_ARG;
+}
+
+// dWo (4 x 256) += g_out^T h4, dbo += colsum(g_out): g_out fp32 [K][4], h4 f16 [K][256].  Thread u
+// of a block owns column u; the block streams its K range (bandwidth-bound on h4).
+__global__ __launch_bounds__(256) void k_wgrad_out16(const float4* __restrict__ g, const _Float16* __restrict__ h,
+                                                     int64_t K, int64_t ks, float* __restrict__ C,
+                                                     float* __restrict__ bias) {
+  const int u = threadIdx.x;
+  const int64_t kb = (int64_t)blockIdx.x * ks;
+  const int64_t ke = kb + ks < K ? kb + ks : K;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f, b0 = 0.f, b1 = 0.f, b2 = 0.f, b3 = 0.f;
+  for (int64_t k = kb; k < ke; ++k) {
+    const float4 gv = g[k];
+    const float x = (float)h[k * 256 + u];
+    s0 = __builtin_fmaf(gv.x, x, s0);
+    s1 = __builtin_fmaf(gv.y, x, s1);
+    s2 = __builtin_fmaf(gv.z, x, s2);
+    s3 = __builtin_fmaf(gv.w, x, s3);
+    if (u == 0) { b0 += gv.x; b1 += gv.y; b2 += gv.z; b3 += gv.w; }
+  }
+  atomicAdd(C + u, s0);
+  atomicAdd(C + 256 + u, s1);
+  atomicAdd(C + 512 + u, s2);
+  atomicAdd(C + 768 + u, s3);
+  if (u == 0 && bias) {
+    atomicAdd(bias + 0, b0); atomicAdd(bias + 1, b1); atomicAdd(bias + 2, b2); atomicAdd(bias + 3, b3);
+  }
+}
+
+int launch_wgrad_out16(const float* g_out, const void* h4, int64_t K, float* C, float* bias, hipStream_t st) {
+  if (K <= 0) return 0;
+  int64_t ks = (K + 2047) / 2048;
+  if (ks < 64) ks = 64;
+  TimingScope ts(kTimeWgrad, K, st);
+  hipLaunchKernelGGL(k_wgrad_out16, dim3((unsigned)((K + ks - 1) / ks)), dim3(256), 0, st,
+                     reinterpret_cast<const float4*>(g_out), static_cast<const _Float16*>(h4), K, ks, C, bias);
+  return hip_status(hipGetLastError());
 }
 
 }  // namespace pnr
