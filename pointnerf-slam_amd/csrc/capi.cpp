@@ -260,8 +260,9 @@ int mlp_backward_core(int prec, const float* packed, const SaveArgs& sv, int64_t
     }
     if (rc) return rc;
     // Fourier: dB (3x93) += x^T g_arg   (x rows are float4 (x0,x1,x2,inside): 3 of 4 used)
-    rc = launch_wgrad(kWgradFourier, reinterpret_cast<const float*>(sv.xP + p0), 3, b.gargP, kFourier, C, grads[0],
-                      kFourier, nullptr, st);
+    rc = split ? launch_wgrad_fourier16(sv.xP + p0, b.gargP, C, grads[0], b.gmax, st)
+               : launch_wgrad(kWgradFourier, reinterpret_cast<const float*>(sv.xP + p0), 3, b.gargP, kFourier, C,
+                              grads[0], kFourier, nullptr, st);
     if (rc) return rc;
     // feature branch: dWc_l (256x32) += (dL/dh_l)^T c ; dbc_l += colsum(dL/dh_l)
     if (fb && fb->g_fc)

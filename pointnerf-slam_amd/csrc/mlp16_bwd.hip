@@ -259,10 +259,14 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd16(const float* __restrict__ 
       }
       gv[r] = g;
     }
-    float* row = a.gargP + p * kFourierPad + 32 * t + 4 * hh;
+    // f16 g_arg * 2^e (same scale as the deltas) for the dB GEMM (wgrad16.hip k_wgrad_skinny16)
+    _Float16* row = reinterpret_cast<_Float16*>(a.gargP) + p * kFourierPad + 32 * t + 4 * hh;
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
-      *reinterpret_cast<float4*>(row + 8 * q) = make_float4(gv[4 * q], gv[4 * q + 1], gv[4 * q + 2], gv[4 * q + 3]);
+    for (int q = 0; q < 4; ++q) {
+      f16x4 gq = {(_Float16)(gv[4 * q] * S.dscale), (_Float16)(gv[4 * q + 1] * S.dscale),
+                  (_Float16)(gv[4 * q + 2] * S.dscale), (_Float16)(gv[4 * q + 3] * S.dscale)};
+      *reinterpret_cast<f16x4*>(row + 8 * q) = gq;
+    }
   }
   if (HASC && valid) {
     float* row = a.g_c + p * kCDim + 4 * hh;

@@ -230,6 +230,8 @@ int launch_wgrad(int kind, const float* A, int ma, const float* B, int nb, int64
 int launch_wgrad16(int kind, const void* A, const void* B, int64_t K, float* C, int64_t ldc, float* bias,
                    const uint32_t* gmax, hipStream_t st);
 int launch_wgrad_out16(const float* g_out, const void* h4, int64_t K, float* C, float* bias, hipStream_t st);
+int launch_wgrad_fourier16(const float4* xP, const void* garg, int64_t K, float* C, const uint32_t* gmax,
+                           hipStream_t st);
 
 inline int hip_status(hipError_t e) { return e == hipSuccess ? 0 : (int)e; }
 

@@ -181,40 +181,101 @@ int launch_wgrad16(int kind, const void* A, const void* B, int64_t K, float* C, 
   return PNR_E_ARG;
 }
 
-// dWo (4 x 256) += g_out^T h4, dbo += colsum(g_out): g_out fp32 [K][4], h4 f16 [K][256].  Thread u
-// of a block owns column u; the block streams its K range (bandwidth-bound on h4).
-__global__ __launch_bounds__(256) void k_wgrad_out16(const float4* __restrict__ g, const _Float16* __restrict__ h,
-                                                     int64_t K, int64_t ks, float* __restrict__ C,
-                                                     float* __restrict__ bias) {
-  const int u = threadIdx.x;
+// Skinny weight-gradient GEMMs, bandwidth-bound on B:
+//   C[m][n] += inv * sum_k A[k][m] B[k][n]   m < M (<= 4), n < N      (bias[m] += sum_k A[k][m])
+// A fp32 rows of 4 (float4: g_out, or x = (x0, x1, x2, inside) with M = 3), B f16 rows of WB.
+//   dWo (4 x 256) = g_out^T h4 (+ dbo)       dB (3 x 93) = x^T (g_arg * s)  (inv = 1/s)
+// A block streams its K range 16 rows at a time: thread (r, c) = (tid / CPR, tid % CPR) loads 16 B
+// (8 columns) of row r and the row's float4 of A, keeping 4 x 8 partial sums; the rows are then
+// reduced through LDS and flushed with one atomic per output element per block.
+template <int WB>
+__global__ __launch_bounds__(256) void k_wgrad_skinny16(const float4* __restrict__ A, const _Float16* __restrict__ B,
+                                                        int64_t K, int64_t ks, int M, int N, float* __restrict__ C,
+                                                        int64_t ldc, float* __restrict__ bias,
+                                                        const uint32_t* __restrict__ gmax) {
+  typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+  constexpr int CPR = WB / 8;          // threads per row (32 for 256, 12 for 96)
+  constexpr int RPI = 256 / CPR;       // rows per iteration (8 or 21)
+  __shared__ float red[4][256 + 8];
+  const int tid = threadIdx.x;
+  const int r = tid / CPR, c = tid % CPR;
+  const bool act = r < RPI;
   const int64_t kb = (int64_t)blockIdx.x * ks;
   const int64_t ke = kb + ks < K ? kb + ks : K;
-  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f, b0 = 0.f, b1 = 0.f, b2 = 0.f, b3 = 0.f;
-  for (int64_t k = kb; k < ke; ++k) {
-    const float4 gv = g[k];
-    const float x = (float)h[k * 256 + u];
-    s0 = __builtin_fmaf(gv.x, x, s0);
-    s1 = __builtin_fmaf(gv.y, x, s1);
-    s2 = __builtin_fmaf(gv.z, x, s2);
-    s3 = __builtin_fmaf(gv.w, x, s3);
-    if (u == 0) { b0 += gv.x; b1 += gv.y; b2 += gv.z; b3 += gv.w; }
+  float acc[4][8];
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[m][j] = 0.f;
+  float bs[4] = {0.f, 0.f, 0.f, 0.f};
+  if (act) {
+    for (int64_t k = kb + r; k < ke; k += 2 * RPI) {
+      const bool two = k + RPI < ke;
+      const float4 a0 = A[k];
+      const h8 b0 = *reinterpret_cast<const h8*>(B + k * WB + 8 * c);
+      float4 a1 = make_float4(0.f, 0.f, 0.f, 0.f);
+      h8 b1 = b0;
+      if (two) {
+        a1 = A[k + RPI];
+        b1 = *reinterpret_cast<const h8*>(B + (k + RPI) * WB + 8 * c);
+      }
+      const float av0[4] = {a0.x, a0.y, a0.z, a0.w}, av1[4] = {a1.x, a1.y, a1.z, a1.w};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float x0 = (float)b0[j], x1 = two ? (float)b1[j] : 0.f;
+#pragma unroll
+        for (int m = 0; m < 4; ++m) acc[m][j] = __builtin_fmaf(av1[m], x1, __builtin_fmaf(av0[m], x0, acc[m][j]));
+      }
+      if (c == 0) {
+#pragma unroll
+        for (int m = 0; m < 4; ++m) bs[m] += av0[m] + av1[m];
+      }
+    }
   }
-  atomicAdd(C + u, s0);
-  atomicAdd(C + 256 + u, s1);
-  atomicAdd(C + 512 + u, s2);
-  atomicAdd(C + 768 + u, s3);
-  if (u == 0 && bias) {
-    atomicAdd(bias + 0, b0); atomicAdd(bias + 1, b1); atomicAdd(bias + 2, b2); atomicAdd(bias + 3, b3);
+  const float inv = gmax ? 1.f / delta_scale(*gmax) : 1.f;
+  // reduce the RPI row groups: column n = 8c + j
+  for (int m = 0; m < 4; ++m) {
+    for (int i = tid; i < 256 + 8; i += 256) red[m][i] = 0.f;
   }
+  __syncthreads();
+  if (act) {
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) atomicAdd(&red[m][8 * c + j], acc[m][j]);  // LDS atomics
+    if (c == 0)
+#pragma unroll
+      for (int m = 0; m < 4; ++m) atomicAdd(&red[m][256 + 4], bs[m]);
+  }
+  __syncthreads();
+  for (int i = tid; i < 4 * N; i += 256) {
+    const int m = i / N, n = i % N;
+    if (m < M) atomicAdd(C + (int64_t)m * ldc + n, red[m][n] * inv);
+  }
+  if (bias && tid < M) atomicAdd(bias + tid, red[tid][256 + 4]);
 }
 
+// dWo (4 x 256) += g_out^T h4 (f16), dbo += colsum(g_out)
 int launch_wgrad_out16(const float* g_out, const void* h4, int64_t K, float* C, float* bias, hipStream_t st) {
   if (K <= 0) return 0;
-  int64_t ks = (K + 2047) / 2048;
-  if (ks < 64) ks = 64;
+  int64_t ks = (K + 1023) / 1024;
+  if (ks < 256) ks = 256;
   TimingScope ts(kTimeWgrad, K, st);
-  hipLaunchKernelGGL(k_wgrad_out16, dim3((unsigned)((K + ks - 1) / ks)), dim3(256), 0, st,
-                     reinterpret_cast<const float4*>(g_out), static_cast<const _Float16*>(h4), K, ks, C, bias);
+  hipLaunchKernelGGL(k_wgrad_skinny16<256>, dim3((unsigned)((K + ks - 1) / ks)), dim3(256), 0, st,
+                     reinterpret_cast<const float4*>(g_out), static_cast<const _Float16*>(h4), K, ks, 4, kHidden, C,
+                     (int64_t)kHidden, bias, nullptr);
+  return hip_status(hipGetLastError());
+}
+
+// dB (3 x 93) += x^T g_arg: x rows float4 (x0, x1, x2, inside), g_arg f16 * s [K][96]
+int launch_wgrad_fourier16(const float4* xP, const void* garg, int64_t K, float* C, const uint32_t* gmax,
+                           hipStream_t st) {
+  if (K <= 0) return 0;
+  int64_t ks = (K + 1023) / 1024;
+  if (ks < 256) ks = 256;
+  TimingScope ts(kTimeWgrad, K, st);
+  hipLaunchKernelGGL(k_wgrad_skinny16<96>, dim3((unsigned)((K + ks - 1) / ks)), dim3(256), 0, st, xP,
+                     static_cast<const _Float16*>(garg), K, ks, 3, kFourier, C, (int64_t)kFourier, nullptr, gmax);
   return hip_status(hipGetLastError());
 }
 
