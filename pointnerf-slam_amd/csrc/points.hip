@@ -14,11 +14,12 @@
 //                   occupancy-filter test of the sample's 2x2x2 probe block; samples that may have
 //                   neighbours go to a work list (one atomic per wave, 64 sub-lists).  Free space -- most of a
 //                   ray -- costs one L2-resident bit load.
-//   k_gather_search persistent blocks over the work list, one thread per sample: 8 bucket headers
-//                   (foreign buckets of a hash collision are skipped by their key), one flattened
-//                   candidate loop, and a branch-free top-k insertion network on packed
-//                   (d2, index) keys compared as float64 (2 VALU per stage); normalised weights,
-//                   then the feature sum with 8 lanes per sample (16-B loads of 128-B rows).
+//   k_gather_search persistent blocks over the work list, 8 lanes per sample: lane q loads probe
+//                   cell q's bucket header (foreign buckets of a hash collision are skipped by their
+//                   key); each range is scanned 8 candidates per trip with one coalesced 128-B load;
+//                   hits go one by one into a top-k list held one key per lane (packed (d2, index)
+//                   keys as u64, insertion = DPP shift + 64-bit compares); lane q then computes the
+//                   q-th weight and sums channels 4q..4q+3 of the features.
 //   k_gather_bwd    dL/df_i += w_k dL/dc (float atomics) and dL/dp through the weights.
 #include "pnr_internal.h"
 
@@ -356,146 +357,144 @@ __global__ __launch_bounds__(256) void k_gather_probe(GatherArgs a) {
   wl_append(a.wl, has, make_float4(x0, x1, x2, __int_as_float((int)p)));
 }
 
-// Pass 2, persistent blocks over the work list, one thread per sample.
+// Pass 2 helpers.  A sample's top-k list lives across the 8 lanes of its group: lane q holds the
+// q-th smallest (d2, index) key, as the unsigned 64-bit pattern of pack_key (positive doubles order
+// like their bit patterns, +inf last).
+__device__ __forceinline__ uint64_t lane_shr1(uint64_t v) {  // lane l-1's value (row_shr:1)
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)v, 0x111, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(v >> 32), 0x111, 0xF, 0xF, false);
+  return (uint64_t)(uint32_t)lo | ((uint64_t)(uint32_t)hi << 32);
+}
+__device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
+  const int lo = __shfl((int)(uint32_t)v, src), hi = __shfl((int)(uint32_t)(v >> 32), src);
+  return (uint64_t)(uint32_t)lo | ((uint64_t)(uint32_t)hi << 32);
+}
+// insert the group-uniform key kn into the group's sorted list (kn = +inf leaves it unchanged)
+__device__ __forceinline__ uint64_t group_insert(uint64_t key, uint64_t kn, int q) {
+  uint64_t prev = lane_shr1(key);
+  if (q == 0) prev = 0;
+  const uint64_t up = prev > kn ? prev : kn;
+  return key <= kn ? key : up;
+}
+
+// Pass 2, persistent blocks over the work list.  8 lanes per sample, 8 samples per wave and round:
+// lane q loads the bucket header of probe cell q; each of the 8 ranges is scanned 8 candidates per
+// trip (one coalesced 128-B load per group); candidates inside the reach are inserted one by one
+// into the group's distributed top-k list (a DPP shift and three 64-bit compares per insertion);
+// then lane q computes the weight of the q-th neighbour, the sequential weight sum is gathered in
+// order over the group, and lane q sums channels 4q..4q+3 of the features.
 template <int KER>
 __global__ __launch_bounds__(256) void k_gather_search(GatherArgs a) {
   PNR_FP_STRICT
-  __shared__ int32_t s_idx[256 * PNR_MAX_K];
-  __shared__ float s_w[256 * PNR_MAX_K];
-  __shared__ int32_t s_row[256];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, gq = lane >> 3, q = lane & 7;
-  const double kInf = __longlong_as_double(0x7FF0000000000000ll);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, g = lane >> 3, q = lane & 7, gb = lane & ~7;
+  constexpr uint64_t kInfKey = 0x7FF0000000000000ull;
   const int64_t nchunk = (a.wl.cap + 255) / 256;
   for (int64_t task = blockIdx.x; task < kLists * nchunk; task += gridDim.x) {
     const int r = (int)(task % kLists);
     const int64_t j0 = task / kLists * 256;
     const int64_t n_work = (int64_t)a.wl.cnt[r * 32];
     if (j0 >= n_work) continue;  // uniform over the block
-    const int64_t i = j0 + threadIdx.x;
-    double key[PNR_MAX_K];
-#pragma unroll
-    for (int t = 0; t < PNR_MAX_K; ++t) key[t] = kInf;
-    float x0 = 0.f, x1 = 0.f, x2 = 0.f;
-    int row = -1;
-    if (i < n_work) {
-      const float4 wk = a.wl.items[r * a.wl.cap + i];
-      x0 = wk.x; x1 = wk.y; x2 = wk.z;
-      row = __float_as_int(wk.w);
+    const float4* items = a.wl.items + r * a.wl.cap;
+#pragma unroll 1
+    for (int rd = 0; rd < 8; ++rd) {
+      const int64_t i = j0 + wv * 64 + rd * 8 + g;
+      if (j0 + wv * 64 + rd * 8 >= n_work) break;  // uniform over the wave
+      const bool live = i < n_work;                  // uniform over the group
+      float x0 = 0.f, x1 = 0.f, x2 = 0.f;
+      int row = -1;
+      if (live) {
+        const float4 wk = items[i];
+        x0 = wk.x; x1 = wk.y; x2 = wk.z;
+        row = __float_as_int(wk.w);
+      }
       int bx, by, bz;
       base_cell(x0, a.g.o0, a.g.inv, bx);
       base_cell(x1, a.g.o1, a.g.inv, by);
       base_cell(x2, a.g.o2, a.g.inv, bz);
-      int4 h[8];
-#pragma unroll
-      for (int n = 0; n < 8; ++n)  // the 8 bucket headers in flight at once
-        h[n] = a.hdr[cell_hash(bx + (n & 1), by + ((n >> 1) & 1), bz + (n >> 2), a.g.mask)];
-      // ranges to scan: own buckets whole, colliding buckets with a per-point cell test (cf bit 8),
-      // foreign buckets not at all.  A bucket reached from two probe cells is scanned once per
-      // cell that it actually holds, so every point is seen exactly once.
-      int rs[8], re[8], rf[8];
-#pragma unroll
-      for (int n = 0; n < 8; ++n) {
-        const int cx = bx + (n & 1), cy = by + ((n >> 1) & 1), cz = bz + (n >> 2);
-        const uint64_t hk = (uint64_t)(uint32_t)h[n].z | ((uint64_t)(uint32_t)h[n].w << 32);
+      // lane q: probe cell q's range -- own bucket whole, colliding bucket with the per-point cell
+      // test (end bit 31), foreign bucket empty; every point is seen exactly once
+      int rs = 0, re = 0;
+      if (live) {
+        const int cx = bx + (q & 1), cy = by + ((q >> 1) & 1), cz = bz + (q >> 2);
+        const int4 h = a.hdr[cell_hash(cx, cy, cz, a.g.mask)];
+        const uint64_t hk = (uint64_t)(uint32_t)h.z | ((uint64_t)(uint32_t)h.w << 32);
         const bool coll = (hk & kCollision) != 0;
         const bool own = (hk & ~kCollision) == cell_key(cx, cy, cz);
-        rs[n] = h[n].x;
-        re[n] = (coll || own) ? h[n].y : h[n].x;
-        rf[n] = n | (coll ? 8 : 0);
+        rs = h.x;
+        re = (coll || own) ? (h.y | (coll ? (int)0x80000000u : 0)) : h.x;
       }
-      int jj = rs[0], je = re[0], jf = rf[0], left = 7;
-      while (true) {
-        if (jj >= je) {  // this range is done: shift the next one in
-          if (left == 0) break;
-#pragma unroll
-          for (int t = 0; t < 7; ++t) {
-            rs[t] = rs[t + 1];
-            re[t] = re[t + 1];
-            rf[t] = rf[t + 1];
+      uint64_t key = kInfKey;
+#pragma unroll 1
+      for (int n = 0; n < 8; ++n) {
+        const int s = __shfl(rs, gb + n);
+        const int ef = __shfl(re, gb + n);
+        const int e = ef & 0x7FFFFFFF;
+        const bool cf = ef < 0;
+#pragma unroll 1
+        for (int j = s + q; __ballot(j - q < e) != 0; j += 8) {
+          bool ok = false;
+          uint64_t cand = kInfKey;
+          if (j < e) {
+            const float4 qv = a.sorted[j];
+            const float d0 = x0 - qv.x, d1 = x1 - qv.y, d2 = x2 - qv.z;
+            const float dd = (d0 * d0 + d1 * d1) + d2 * d2;
+            if (KER == PNR_GATHER_IDW) ok = dd <= a.r2;
+            else ok = fabsf(d0) < a.h0 && fabsf(d1) < a.h1 && fabsf(d2) < a.h2;
+            if (cf) {  // colliding bucket: the point must lie in this probe cell
+              ok = ok && cell_coord(qv.x, a.g.o0, a.g.inv) == bx + (n & 1) &&
+                   cell_coord(qv.y, a.g.o1, a.g.inv) == by + ((n >> 1) & 1) &&
+                   cell_coord(qv.z, a.g.o2, a.g.inv) == bz + (n >> 2);
+            }
+            cand = (uint64_t)__double_as_longlong(pack_key(dd, __float_as_int(qv.w)));
           }
-          jj = rs[0];
-          je = re[0];
-          jf = rf[0];
-          --left;
-          continue;
-        }
-        const float4 qv = a.sorted[jj++];
-        const float d0 = x0 - qv.x, d1 = x1 - qv.y, d2 = x2 - qv.z;
-        const float dd = (d0 * d0 + d1 * d1) + d2 * d2;
-        bool ok;
-        if (KER == PNR_GATHER_IDW) ok = dd <= a.r2;
-        else ok = fabsf(d0) < a.h0 && fabsf(d1) < a.h1 && fabsf(d2) < a.h2;
-        if (jf & 8) {  // colliding bucket: the point must lie in this probe cell
-          ok = ok && cell_coord(qv.x, a.g.o0, a.g.inv) == bx + (jf & 1) &&
-               cell_coord(qv.y, a.g.o1, a.g.inv) == by + ((jf >> 1) & 1) &&
-               cell_coord(qv.z, a.g.o2, a.g.inv) == bz + ((jf >> 2) & 1);
-        }
-        // branch-free insertion into the sorted top-k list (min/max of float64 keys)
-        double kn = ok ? pack_key(dd, __float_as_int(qv.w)) : kInf;
-#pragma unroll
-        for (int t = 0; t < PNR_MAX_K; ++t) {
-          const double lo = fmin(key[t], kn);
-          kn = fmax(key[t], kn);
-          key[t] = lo;
+          uint32_t bits = (uint32_t)(__ballot(ok) >> gb) & 0xFFu;
+          while (__ballot(bits != 0) != 0) {
+            const int src = bits ? __ffs(bits) - 1 : 0;
+            uint64_t kn = shfl64(cand, gb + src);
+            if (!bits) kn = kInfKey;
+            key = group_insert(key, kn, q);
+            bits &= bits - 1;
+          }
         }
       }
-    }
-    // weights of the first k, normalised by their sequential sum (ascending distance)
-    float wv_[PNR_MAX_K];
-    int ki[PNR_MAX_K];
-    float W = 0.f;
-#pragma unroll
-    for (int t = 0; t < PNR_MAX_K; ++t) {
+      // lane q: the q-th neighbour's weight; the normaliser is the sequential sum over q = 0..7
+      const bool v = q < a.k && key != kInfKey;
+      const int id = v ? (int)(uint32_t)key : -1;
       float w = 0.f;
-      const bool v = t < a.k && key[t] != kInf;
-      ki[t] = v ? key_id(key[t]) : -1;
       if (v) {
         if (KER == PNR_GATHER_IDW) {
-          w = 1.0f / fmaxf(sqrtf(key_d2(key[t])), a.eps);
+          w = 1.0f / fmaxf(sqrtf(key_d2(__longlong_as_double((long long)key))), a.eps);
         } else {  // per-axis offsets of the kept point (same f32 arithmetic as the search)
-          const float* xi = a.xyz + (int64_t)ki[t] * 3;
+          const float* xi = a.xyz + (int64_t)id * 3;
           const float t0 = 1.0f - fabsf(x0 - xi[0]) / a.h0;
           const float t1 = 1.0f - fabsf(x1 - xi[1]) / a.h1;
           const float t2 = 1.0f - fabsf(x2 - xi[2]) / a.h2;
           w = (t0 * t1) * t2;
         }
       }
-      wv_[t] = w;
-      W = W + w;
-    }
-    const float Wd = W > 0.f ? W : 1.0f;
-    __syncthreads();  // the previous iteration's readers are done with the LDS lists
-    s_row[threadIdx.x] = row;
+      float W = 0.f;
 #pragma unroll
-    for (int t = 0; t < PNR_MAX_K; ++t) {
-      const float wn = ki[t] >= 0 ? wv_[t] / Wd : 0.f;
-      s_idx[threadIdx.x * PNR_MAX_K + t] = ki[t];
-      s_w[threadIdx.x * PNR_MAX_K + t] = wn;
-      if (row >= 0 && t < a.k && a.idx) {
-        a.idx[(int64_t)row * a.k + t] = ki[t];
-        a.w[(int64_t)row * a.k + t] = wn;
+      for (int t = 0; t < PNR_MAX_K; ++t) W = W + __shfl(w, gb + t);
+      const float Wd = W > 0.f ? W : 1.0f;
+      const float wn = id >= 0 ? w / Wd : 0.f;
+      if (live && q < a.k && a.idx) {
+        a.idx[(int64_t)row * a.k + q] = id;
+        a.w[(int64_t)row * a.k + q] = wn;
       }
-    }
-    __syncthreads();
-    // feature sum: 8 lanes per sample, lane q owns channels 4q..4q+3
-#pragma unroll 1
-    for (int rr = 0; rr < 8; ++rr) {
-      const int sl = wv * 64 + rr * 8 + gq;
-      const int r = s_row[sl];
-      if (r < 0) continue;
       float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-      for (int kk = 0; kk < PNR_MAX_K; ++kk) {
-        const int id = s_idx[sl * PNR_MAX_K + kk];
-        if (id < 0) continue;
-        const float wn = s_w[sl * PNR_MAX_K + kk];
-        const float4 f = a.feats4[(int64_t)id * 8 + q];
-        acc.x = acc.x + wn * f.x;
-        acc.y = acc.y + wn * f.y;
-        acc.z = acc.z + wn * f.z;
-        acc.w = acc.w + wn * f.w;
+      for (int t = 0; t < PNR_MAX_K; ++t) {
+        const int idt = __shfl(id, gb + t);
+        const float wt = __shfl(wn, gb + t);
+        if (idt >= 0) {
+          const float4 f = a.feats4[(int64_t)idt * 8 + q];
+          acc.x = acc.x + wt * f.x;
+          acc.y = acc.y + wt * f.y;
+          acc.z = acc.z + wt * f.z;
+          acc.w = acc.w + wt * f.w;
+        }
       }
-      reinterpret_cast<float4*>(a.c)[(int64_t)r * 8 + q] = acc;
+      if (live) reinterpret_cast<float4*>(a.c)[(int64_t)row * 8 + q] = acc;
     }
   }
 }

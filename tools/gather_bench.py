@@ -95,6 +95,27 @@ def main():
     # bwd algorithmic bytes: 24 B point + 128 g_c + 128 c + k*8 idx/w + per neighbour (128 feats + 12 xyz
     # + 128 B feature-grad atomics) + 12 B g_p
     bbyt = P * (24 + 128 + 128 + args.k * 8 + 12) + nb * (128 + 12 + 128)
+    # candidate statistics: points scanned per sample = points in its 8 probe cells (torch, untimed)
+    with torch.no_grad():
+        o = torch.tensor(pts.origin, device=dev, dtype=torch.float32)
+        inv = 1.0 / pts.cell
+        cq = torch.floor((xyz - o) * inv).long()
+        off = 1 << 20
+        ck = ((cq[:, 0] + off) << 42) | ((cq[:, 1] + off) << 21) | (cq[:, 2] + off)
+        uk, cnt = torch.unique(ck, return_counts=True)
+        t = (p.float() - o) * inv
+        fl = torch.floor(t)
+        b = fl.long() - (t - fl < 0.5).long()
+        cand = torch.zeros(P, device=dev, dtype=torch.long)
+        for n in range(8):
+            k3 = ((b[:, 0] + (n & 1) + off) << 42) | ((b[:, 1] + ((n >> 1) & 1) + off) << 21) | (b[:, 2] + (n >> 2) + off)
+            pos = torch.searchsorted(uk, k3).clamp(max=uk.numel() - 1)
+            cand += torch.where(uk[pos] == k3, cnt[pos], torch.zeros_like(cnt[pos]))
+        cw = cand[cand > 0]
+        nw = cw.numel() // 64 * 64
+        wmax = cw[:nw].view(-1, 64).max(1).values.float().mean().item() if nw else 0.0
+        print(f'cells {uk.numel()} (points/cell {cnt.float().mean().item():.2f}); samples with candidates '
+              f'{cw.numel()}: {cw.float().mean().item():.1f} candidates each, mean per-wave max {wmax:.1f}')
     print(f'voxel {args.voxel} points {args.points} samples {P} ({args.rays} rays x 44) mode {args.mode} r {args.radius} k {args.k}')
     print(f'neighbours: mean {nb / P:.2f}/sample, histogram {hist}; samples with candidates {n_work} '
           f'({100 * n_work / P:.1f}%)')

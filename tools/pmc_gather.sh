@@ -8,6 +8,6 @@ for C in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ
          "TA_TA_BUSY_sum TA_BUFFER_WAVEFRONTS_sum TCP_TOTAL_CACHE_ACCESSES_sum" \
          "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum"; do
   n=$(echo $C | cut -d' ' -f1)
-  timeout -k 10 200 rocprofv3 --kernel-trace --pmc $C --output-format csv -d gpurun_out/pmcg -o $n -- python3 tools/gather_bench.py --reps 2 $ARGS > gpurun_out/pmcg_$n.log 2>&1 || { echo FAIL $n; tail -5 gpurun_out/pmcg_$n.log; }
+  timeout -k 10 200 rocprofv3 --kernel-trace --pmc $C --output-format csv -d gpurun_out/pmcg -o $n -- python3 tools/gather_bench.py --reps 2 $ARGS > gpurun_out/pmcg_$n.log 2>&1 || { echo FAIL $n; tail -5 gpurun_out/pmcg_$n.log; exit 1; }
 done
 echo DONE
