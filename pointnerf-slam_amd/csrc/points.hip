@@ -346,11 +346,19 @@ __global__ __launch_bounds__(256) void k_gather_probe(GatherArgs a) {
     float4* c4 = reinterpret_cast<float4*>(a.c) + r0 * 8;
     for (int e = threadIdx.x; e < nrow * 8; e += 256)
       if (!s_has[e >> 3]) c4[e] = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (a.idx) {
-      for (int e = threadIdx.x; e < nrow * a.k; e += 256) {
-        if (s_has[e / a.k]) continue;
-        a.idx[r0 * a.k + e] = -1;
-        a.w[r0 * a.k + e] = 0.f;
+    if (a.idx && p < a.rows && !has) {  // this row's k (index, weight) slots
+      if (a.k == 8 && ((reinterpret_cast<uintptr_t>(a.idx) | reinterpret_cast<uintptr_t>(a.w)) & 15) == 0) {
+        int4* i4 = reinterpret_cast<int4*>(a.idx) + p * 2;
+        float4* w4 = reinterpret_cast<float4*>(a.w) + p * 2;
+        i4[0] = make_int4(-1, -1, -1, -1);
+        i4[1] = make_int4(-1, -1, -1, -1);
+        w4[0] = make_float4(0.f, 0.f, 0.f, 0.f);
+        w4[1] = make_float4(0.f, 0.f, 0.f, 0.f);
+      } else {
+        for (int t = 0; t < a.k; ++t) {
+          a.idx[p * a.k + t] = -1;
+          a.w[p * a.k + t] = 0.f;
+        }
       }
     }
   }
@@ -483,15 +491,24 @@ __global__ __launch_bounds__(256) void k_gather_search(GatherArgs a) {
       }
       float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-      for (int t = 0; t < PNR_MAX_K; ++t) {
-        const int idt = __shfl(id, gb + t);
-        const float wt = __shfl(wn, gb + t);
-        if (idt >= 0) {
-          const float4 f = a.feats4[(int64_t)idt * 8 + q];
-          acc.x = acc.x + wt * f.x;
-          acc.y = acc.y + wt * f.y;
-          acc.z = acc.z + wt * f.z;
-          acc.w = acc.w + wt * f.w;
+      for (int t0 = 0; t0 < PNR_MAX_K; t0 += 4) {  // 4 feature loads in flight per batch
+        int idt[4];
+        float4 f[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          idt[t] = __shfl(id, gb + t0 + t);
+          f[t] = make_float4(0.f, 0.f, 0.f, 0.f);
+          if (idt[t] >= 0) f[t] = a.feats4[(int64_t)idt[t] * 8 + q];
+        }
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const float wt = __shfl(wn, gb + t0 + t);
+          if (idt[t] >= 0) {
+            acc.x = acc.x + wt * f[t].x;
+            acc.y = acc.y + wt * f[t].y;
+            acc.z = acc.z + wt * f[t].z;
+            acc.w = acc.w + wt * f[t].w;
+          }
         }
       }
       if (live) reinterpret_cast<float4*>(a.c)[(int64_t)row * 8 + q] = acc;

@@ -74,6 +74,14 @@ def main():
     torch.cuda.synchronize()
     lib.pnr_timing_enable(0)
     launches, ms, _ = timing_read(4)
+    if hasattr(lib, 'pnr_dbg_phase'):  # experiment build: per-phase s_memtime cycles of k_gather_search
+        buf = (ctypes.c_ulonglong * 16)()
+        lib.pnr_dbg_phase(buf)
+        ph = [buf[i] for i in range(8)]
+        tot = max(ph[5], 1)
+        names = ['setup', 'scan', 'select', 'weights', 'features', 'total', 'rounds', 'trips']
+        print('phases (wave-cycles, share of total):', ', '.join(f'{n} {ph[i]:.3e} ({ph[i] / tot:.2f})' for i, n in enumerate(names[:6])),
+              f'rounds {ph[6]}, trips {ph[7]}, cycles/round {ph[5] / max(ph[6], 1):.0f}')
     avg = ms / launches
     byt = gather_bytes(P, nb, args.k)
     gbs = byt / (avg * 1e-3) / 1e9
