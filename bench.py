@@ -338,9 +338,12 @@ def main():
             'metric': METRIC, 'value': round(value, 1), 'unit': 'rays/s', 'n_gpus': world, 'steps': args.steps,
             'warmup': args.warmup, 'ms_per_step': round(ms_per_step, 3), 'higher_is_better': True, 'scaling': 'weak',
             'vs_baseline': None,
-            'dtype': {'fp32': 'fp32', 'f16x3': 'fp32-class: f16x3 split MFMA forward (fp32 accumulate) + fp32 backward',
-                      'bf16x3': 'bf16x3 split MFMA forward (fp32 accumulate) + fp32 backward',
-                      'bf16': 'bf16 MFMA forward (fp32 accumulate) + fp32 backward'}[prec],
+            'dtype': {'fp32': 'fp32',
+                      'f16x3': 'fp32-class: f16x3 split MFMA forward, bf16x3 split delta chain (fp32 accumulate); '
+                               'weight gradients f16 MFMA on f16-stored activations / scaled-f16 deltas',
+                      'bf16x3': 'bf16x3 split MFMA forward and delta chain (fp32 accumulate); weight gradients f16 MFMA '
+                                'on f16-stored activations / scaled-f16 deltas',
+                      'bf16': 'bf16 MFMA forward (fp32 accumulate), bf16x3 delta chain; weight gradients f16 MFMA'}[prec],
             'data': 'synthetic (640x480 ScanNet-intrinsics rays at room0 pose 1000, U[0.05,0.6] gt depth, trained '
                     'room0 decoder fixture)',
             'config': {'workload': wl_name,

@@ -1,0 +1,79 @@
+"""Per-unit HBM traffic (profiles/r*_traffic.json, read by bench.py pmc_traffic) from a
+tools/prof_bench.sh traffic directory.
+
+  python tools/traffic_json.py <gpurun_out/prof_<tag>_traffic> <out.json> [source note]
+
+Per kernel family, the mean over its launches of (2 x FETCH_SIZE + WRITE_SIZE) bytes divided by the
+units of that launch (tools/traffic.py documents the counter units and the gfx950 FETCH correction):
+  k_mlp_fwd16_train  split-precision forward with activation saves, per point (128 points / 256-thread block)
+  k_mlp_fwd16_eval   the same without saves
+  k_mlp_bwd16        split-precision delta chain, per point (128 points / block)
+  k_mlp_fwd_train    fp32 forward with saves, per point (grid = points)
+  k_gather           probe + search of one gather, per sample (probe grid = sample rows)
+"""
+import collections
+import csv
+import json
+import os
+import sys
+
+
+def per_launch(d):
+    """[(kernel, grid, bytes)] in launch order, FETCH x2 + WRITE, from the two pass directories."""
+    out = {}
+    for c, scale in (('FETCH_SIZE', 2.0), ('WRITE_SIZE', 1.0)):
+        p = os.path.join(d, f'{c}_counter_collection.csv')
+        rows = list(csv.DictReader(open(p)))
+        per = collections.defaultdict(list)
+        for r in rows:
+            per[(r['Kernel_Name'], int(r['Grid_Size']))].append(float(r['Counter_Value']) * 1024.0 * scale)
+        out[c] = per
+    return out
+
+
+def family(name):
+    if 'k_mlp_fwd16<' in name:
+        return 'k_mlp_fwd16_train' if name.split('>')[0].endswith('true') else 'k_mlp_fwd16_eval'
+    if 'k_mlp_bwd16<' in name:
+        return 'k_mlp_bwd16'
+    if 'k_mlp_fwd<' in name and 'true' in name.split('>')[0]:
+        return 'k_mlp_fwd_train'
+    if 'k_gather_probe' in name:
+        return 'k_gather_probe'
+    if 'k_gather_search' in name:
+        return 'k_gather_search'
+    return None
+
+
+def main():
+    d, dst = sys.argv[1], sys.argv[2]
+    note = sys.argv[3] if len(sys.argv) > 3 else ''
+    pl = per_launch(d)
+    acc = collections.defaultdict(lambda: [0.0, 0.0, 0])  # fetch, write, units
+    for c, per in pl.items():
+        for (name, grid), vals in per.items():
+            fam = family(name)
+            if fam is None or fam == 'k_gather_search':
+                continue
+            units = grid / 2 if fam.startswith('k_mlp_') and '16' in fam else grid
+            a = acc['k_gather' if fam == 'k_gather_probe' else fam]
+            a[0 if c == 'FETCH_SIZE' else 1] += sum(vals)
+            if c == 'FETCH_SIZE':
+                a[2] += units * len(vals)
+    # the search launches belong to the gather whose probe they follow: add their bytes
+    for c, per in pl.items():
+        for (name, grid), vals in per.items():
+            if family(name) == 'k_gather_search':
+                acc['k_gather'][0 if c == 'FETCH_SIZE' else 1] += sum(vals)
+    res = {'source': note}
+    for fam, (f, w, u) in sorted(acc.items()):
+        if u <= 0:
+            continue
+        res[fam] = {'unit': 'sample' if fam == 'k_gather' else 'point',
+                    'fetch_B': round(f / u, 1), 'write_B': round(w / u, 1)}
+    json.dump(res, open(dst, 'w'), indent=1)
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == '__main__':
+    main()
