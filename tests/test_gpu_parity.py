@@ -274,3 +274,64 @@ def test_psnr_vs_oracle_frame(pnr_mod, dev, scene, oracle_frame):
     p = ref.psnr(c.cpu().clamp(0, 1), cr.clamp(0, 1))
     assert p > 80.0, p
     close(d, dr, 1e-4, 1e-9, 'depth')
+
+
+def _track_scene(scene):
+    """A 68x120 frame (edge 10 px) rendered by the oracle at room0 pose 1, every 7th row / 5th
+    column depth zeroed, and a camera tensor perturbed off that pose."""
+    from oracle import ref_render as ref
+    import pnr
+    params = golden_params('trained')
+    H, W, fx, fy, cx, cy = 68, 120, 60., 60., 59.5, 33.5
+    c2w = torch.from_numpy(scene['poses'][1]).float()
+    gd, _, gc = ref.render_img(params, c2w, scene['bound_t'], H, W, fx, fy, cx, cy)
+    gd = gd.float().clone()
+    gd[::7, ::5] = 0.
+    ct_true = pnr.get_tensor_from_camera(c2w)
+    ct0 = ct_true + torch.tensor([0.003, -0.002, 0.001, 0.002, 0.004, -0.003, 0.002])
+    return params, (H, W, fx, fy, cx, cy), gd, gc.float(), ct_true, ct0
+
+
+def test_track_step_vs_oracle(pnr_mod, dev, scene):
+    """Tracker.optimize_cam_in_batch (src/Tracker.py:253-335, weak depth): loss and camera-tensor
+    gradient of one step vs the oracle (rays, render and loss restated on the CPU)."""
+    from oracle import ref_render as ref
+    params, (H, W, fx, fy, cx, cy), gd, gc, _, ct0 = _track_scene(scene)
+    e = 10
+    crop = gd[e:H - e, e:W - e].reshape(-1)
+    idx = torch.nonzero(crop > 0.01).reshape(-1)
+    i = (idx % (W - 2 * e) + e).float()
+    j = (idx // (W - 2 * e) + e).float()
+    ct_r = ct0.clone().requires_grad_(True)
+    ro, rd = ref.rays_from_uv(i, j, ref.camera_from_tensor(ct_r), fx, fy, cx, cy)
+    ro, rd = ro.reshape(-1, 3), rd.reshape(-1, 3)
+    g_d, g_c = crop[idx], gc[e:H - e, e:W - e].reshape(-1, 3)[idx]
+    d, v, c = ref.render_batch_ray(params, rd, ro, scene['bound_t'], gt_depth=g_d)
+    loss_r = ref.tracking_loss(d, v, c, g_d, g_c)
+    loss_r.backward()
+
+    dec = make_decoder(pnr_mod, params, dev)
+    r = make_renderer(pnr_mod, scene, H=H, W=W, fx=fx, fy=fy, cx=cx, cy=cy)
+    step = pnr_mod.TrackStep(r, dec, ignore_edge_W=e, ignore_edge_H=e)
+    ct = ct0.clone().to(dev).requires_grad_(True)
+    loss = step.loss(ct, gc.to(dev), gd.to(dev), 0)
+    loss.backward()
+    assert all(p.grad is None for p in dec.parameters())  # the Tracker optimises the camera only
+    close(loss.detach(), loss_r.detach(), 1e-4, 0, 'tracking loss')
+    gref = ct_r.grad
+    close(ct.grad, gref, 0, 2e-3 * gref.abs().max().item(), 'camera tensor grad')
+
+
+def test_track_frame_converges(pnr_mod, dev, scene):
+    """src/Tracker.py:860-921: 12 Adam iterations from the perturbed pose lower the loss, and the
+    minimum-loss candidate is closer to the rendering pose than the start."""
+    params, (H, W, fx, fy, cx, cy), gd, gc, ct_true, ct0 = _track_scene(scene)
+    dec = make_decoder(pnr_mod, params, dev)
+    r = make_renderer(pnr_mod, scene, H=H, W=W, fx=fx, fy=fy, cx=cx, cy=cy)
+    step = pnr_mod.TrackStep(r, dec, ignore_edge_W=10, ignore_edge_H=10)
+    best, c2w, losses = pnr_mod.track_frame(step, ct0.to(dev), gc.to(dev), gd.to(dev), 12, 1e-3, 0)
+    assert len(losses) == 12 and min(losses) < 0.7 * losses[0]
+    err0 = (ct0 - ct_true).abs().mean().item()
+    err = (best.cpu() - ct_true).abs().mean().item()
+    assert err < err0
+    assert c2w.shape == (4, 4)
