@@ -174,9 +174,11 @@ def gather_roofline(dev, voxel=0.001, k=8, reps=5):
             'bytes_per_launch': byt}
 
 
-def cpu_baseline(bound, pose, params, workload, n_rays=2048, reps=3):
+def cpu_baseline(bound, pose, params, workload, n_rays=2048, reps=3, gpu_render=None):
     """The oracle (oracle/ref_render.py, a bit-exact restatement of the reference CPU path pinned
-    by tests/test_oracle_golden.py) timed on this host: bounded sample, median of `reps`."""
+    by tests/test_oracle_golden.py) timed on this host: bounded sample, median of `reps`.
+    `gpu_render(ro, rd, gt) -> (depth, colour)` renders the same rays on the measured HIP path
+    with the initial weights; the leg then reports the metric's PSNR condition on them."""
     from oracle import ref_render as ref
     cores = torch.get_num_threads()
     ro, rd, gt, col = [t.cpu() for t in synth_batch(n_rays, 0, pose, 'cpu', seed=7)]
@@ -201,9 +203,23 @@ def cpu_baseline(bound, pose, params, workload, n_rays=2048, reps=3):
         step()
         ts.append(time.perf_counter() - t0)
     t = float(np.median(ts))
-    return {'value': round(n_rays / t, 1), 'unit': 'rays/s', 'cores': cores, 'kind': 'port',
-            'sample': f'{workload} step on {n_rays} rays, oracle (torch CPU restatement of src/utils/Renderer.py), '
-                      f'median of {reps} after 1 warm-up, {cores} threads'}
+    out = {'value': round(n_rays / t, 1), 'unit': 'rays/s', 'cores': cores, 'kind': 'port',
+           'sample': f'{workload} step on {n_rays} rays, oracle (torch CPU restatement of src/utils/Renderer.py), '
+                     f'median of {reps} after 1 warm-up, {cores} threads'}
+    if gpu_render is not None:
+        with torch.no_grad():
+            if workload == 'map':
+                d_r, _, c_r = ref.render_batch_ray(params, rd, ro, bound, gt_depth=gt)
+            else:
+                d_r, _, c_r = ref.render_batch_ray(params, rd, ro, bound, n_samples=64, n_importance=0)
+        d_g, c_g = gpu_render(ro, rd, gt if workload == 'map' else None)
+        rel = ((d_g.double() - d_r.double()).abs() / d_r.double().abs().clamp_min(1e-12)).max().item()
+        out['parity'] = {'psnr_db': round(ref.psnr(c_g, c_r), 2), 'depth_max_rel': float(f'{rel:.3g}'),
+                         'rays': n_rays,
+                         'what': 'PSNR of the HIP render vs the oracle render of the same rays (initial weights); '
+                                 'the metric\'s PSNR delta vs GT <= 0.1 dB holds when this exceeds PSNR(ref, GT) '
+                                 '+ 39 dB (SURVEY.md 8(d))'}
+    return out
 
 
 def main():
@@ -328,7 +344,15 @@ def main():
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu_baseline and params is not None and args.workload != 'map-points':
-            cpu = cpu_baseline(bound, pose, params, args.workload)
+            def gpu_render(ro_c, rd_c, gt_c):
+                d0 = pnr.get_model(cfg, nice=False)
+                d0.load_state_dict(params)
+                d0 = d0.to(dev)
+                with torch.no_grad():
+                    d, _, c = renderer.render_batch_ray({}, d0, rd_c.to(dev), ro_c.to(dev), dev, 'color',
+                                                        gt_depth=None if gt_c is None else gt_c.to(dev))
+                return d.cpu(), c.cpu()
+            cpu = cpu_baseline(bound, pose, params, args.workload, gpu_render=gpu_render)
         samples = '64' if args.workload == 'fwd' else '32+12 (+32 regulation)'
         wl_name = {'map': 'S-map: full mapping iteration (render+regulation+L1 losses+backward+Adam)',
                    'fwd': 'S-fwd: render_batch_ray forward',
