@@ -14,12 +14,12 @@
 //                   occupancy-filter test of the sample's 2x2x2 probe block; samples that may have
 //                   neighbours go to a work list (one atomic per wave, 64 sub-lists).  Free space -- most of a
 //                   ray -- costs one L2-resident bit load.
-//   k_gather_search persistent blocks over the work list, 8 lanes per sample: lane q loads probe
-//                   cell q's bucket header (foreign buckets of a hash collision are skipped by their
-//                   key); each range is scanned 8 candidates per trip with one coalesced 128-B load;
-//                   hits go one by one into a top-k list held one key per lane (packed (d2, index)
-//                   keys as u64, insertion = DPP shift + 64-bit compares); lane q then computes the
-//                   q-th weight and sums channels 4q..4q+3 of the features.
+//   k_gather_search persistent blocks over the work list (grid = resident blocks), one thread per
+//                   sample: 8 bucket headers (foreign buckets of a hash collision are skipped by
+//                   their key), the non-empty ranges compacted into the thread's LDS row, ONE flat
+//                   candidate loop over them (uniform exit, next range read ahead), a branch-free
+//                   top-k network on packed (d2, index) float64 keys (v_min/v_max_f64, 2 VALU per
+//                   stage); normalised weights, then the feature sum with 8 lanes per sample.
 //   k_gather_bwd    dL/df_i += w_k dL/dc (float atomics) and dL/dp through the weights.
 #include "pnr_internal.h"
 
@@ -365,153 +365,176 @@ __global__ __launch_bounds__(256) void k_gather_probe(GatherArgs a) {
   wl_append(a.wl, has, make_float4(x0, x1, x2, __int_as_float((int)p)));
 }
 
-// Pass 2 helpers.  A sample's top-k list lives across the 8 lanes of its group: lane q holds the
-// q-th smallest (d2, index) key, as the unsigned 64-bit pattern of pack_key (positive doubles order
-// like their bit patterns, +inf last).
-__device__ __forceinline__ uint64_t lane_shr1(uint64_t v) {  // lane l-1's value (row_shr:1)
-  const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)v, 0x111, 0xF, 0xF, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(v >> 32), 0x111, 0xF, 0xF, false);
-  return (uint64_t)(uint32_t)lo | ((uint64_t)(uint32_t)hi << 32);
-}
-__device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
-  const int lo = __shfl((int)(uint32_t)v, src), hi = __shfl((int)(uint32_t)(v >> 32), src);
-  return (uint64_t)(uint32_t)lo | ((uint64_t)(uint32_t)hi << 32);
-}
-// insert the group-uniform key kn into the group's sorted list (kn = +inf leaves it unchanged)
-__device__ __forceinline__ uint64_t group_insert(uint64_t key, uint64_t kn, int q) {
-  uint64_t prev = lane_shr1(key);
-  if (q == 0) prev = 0;
-  const uint64_t up = prev > kn ? prev : kn;
-  return key <= kn ? key : up;
+// Pass 2, persistent blocks over the work list, one thread per sample.  A thread's non-empty
+// probe ranges (own bucket whole; colliding bucket with a per-point cell test; foreign bucket not
+// at all) are compacted into its LDS row, so the candidate loop is ONE flat loop over all of them
+// (trip count = the wave's largest candidate total) with the next range read ahead.  Top-k is a
+// branch-free insertion network on (d2, index) keys packed into positive doubles (their order is
+// the lexicographic one): v_min_f64 / v_max_f64 by inline asm, 2 VALU per stage (the builtins add
+// an IEEE canonicalisation per operand).  The feature sum then runs 8 lanes per sample, 4 feature
+// rows in flight per lane.
+// one network stage: key <- min(key, kn), return max(key, kn); key is updated in place (a tied
+// operand), so the unrolled network carries no register copies around the candidate loop
+__device__ __forceinline__ double kstage(double& key, double kn) {
+  double hi;
+  asm("v_max_f64 %1, %0, %2\n\tv_min_f64 %0, %0, %2" : "+v"(key), "=&v"(hi) : "v"(kn));
+  return hi;
 }
 
-// Pass 2, persistent blocks over the work list.  8 lanes per sample, 8 samples per wave and round:
-// lane q loads the bucket header of probe cell q; each of the 8 ranges is scanned 8 candidates per
-// trip (one coalesced 128-B load per group); candidates inside the reach are inserted one by one
-// into the group's distributed top-k list (a DPP shift and three 64-bit compares per insertion);
-// then lane q computes the weight of the q-th neighbour, the sequential weight sum is gathered in
-// order over the group, and lane q sums channels 4q..4q+3 of the features.
+constexpr int kSearchBlock = 256;
+union SearchLds {
+  struct {
+    int2 rng[8][kSearchBlock];      // [range][thread] (start, end): conflict-free per-thread access
+    uint8_t cell[8][kSearchBlock];  // probe cell n | 8 if the bucket collides
+  } r;
+  struct {
+    int32_t idx[kSearchBlock * PNR_MAX_K];
+    float w[kSearchBlock * PNR_MAX_K];
+    int32_t row[kSearchBlock];
+  } f;
+};
+
 template <int KER>
-__global__ __launch_bounds__(256) void k_gather_search(GatherArgs a) {
+__global__ __launch_bounds__(kSearchBlock) void k_gather_search(GatherArgs a) {
   PNR_FP_STRICT
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, g = lane >> 3, q = lane & 7, gb = lane & ~7;
-  constexpr uint64_t kInfKey = 0x7FF0000000000000ull;
-  const int64_t nchunk = (a.wl.cap + 255) / 256;
+  __shared__ SearchLds L;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, gq = lane >> 3, q = lane & 7;
+  const double kInf = __longlong_as_double(0x7FF0000000000000ll);
+  const int64_t nchunk = (a.wl.cap + kSearchBlock - 1) / kSearchBlock;
   for (int64_t task = blockIdx.x; task < kLists * nchunk; task += gridDim.x) {
     const int r = (int)(task % kLists);
-    const int64_t j0 = task / kLists * 256;
+    const int64_t j0 = task / kLists * kSearchBlock;
     const int64_t n_work = (int64_t)a.wl.cnt[r * 32];
     if (j0 >= n_work) continue;  // uniform over the block
-    const float4* items = a.wl.items + r * a.wl.cap;
-#pragma unroll 1
-    for (int rd = 0; rd < 8; ++rd) {
-      const int64_t i = j0 + wv * 64 + rd * 8 + g;
-      if (j0 + wv * 64 + rd * 8 >= n_work) break;  // uniform over the wave
-      const bool live = i < n_work;                  // uniform over the group
-      float x0 = 0.f, x1 = 0.f, x2 = 0.f;
-      int row = -1;
-      if (live) {
-        const float4 wk = items[i];
-        x0 = wk.x; x1 = wk.y; x2 = wk.z;
-        row = __float_as_int(wk.w);
-      }
-      int bx, by, bz;
+    const int64_t i = j0 + tid;
+    double key[PNR_MAX_K];
+#pragma unroll
+    for (int t = 0; t < PNR_MAX_K; ++t) key[t] = kInf;
+    float x0 = 0.f, x1 = 0.f, x2 = 0.f;
+    int row = -1, bx = 0, by = 0, bz = 0, nr = 0;
+    __syncthreads();  // the previous task's feature phase is done with the LDS
+    if (i < n_work) {
+      const float4 wk = a.wl.items[r * a.wl.cap + i];
+      x0 = wk.x; x1 = wk.y; x2 = wk.z;
+      row = __float_as_int(wk.w);
       base_cell(x0, a.g.o0, a.g.inv, bx);
       base_cell(x1, a.g.o1, a.g.inv, by);
       base_cell(x2, a.g.o2, a.g.inv, bz);
-      // lane q: probe cell q's range -- own bucket whole, colliding bucket with the per-point cell
-      // test (end bit 31), foreign bucket empty; every point is seen exactly once
-      int rs = 0, re = 0;
-      if (live) {
-        const int cx = bx + (q & 1), cy = by + ((q >> 1) & 1), cz = bz + (q >> 2);
-        const int4 h = a.hdr[cell_hash(cx, cy, cz, a.g.mask)];
-        const uint64_t hk = (uint64_t)(uint32_t)h.z | ((uint64_t)(uint32_t)h.w << 32);
+      int4 h[8];
+#pragma unroll
+      for (int n = 0; n < 8; ++n)  // the 8 bucket headers in flight at once
+        h[n] = a.hdr[cell_hash(bx + (n & 1), by + ((n >> 1) & 1), bz + (n >> 2), a.g.mask)];
+#pragma unroll
+      for (int n = 0; n < 8; ++n) {
+        const int cx = bx + (n & 1), cy = by + ((n >> 1) & 1), cz = bz + (n >> 2);
+        const uint64_t hk = (uint64_t)(uint32_t)h[n].z | ((uint64_t)(uint32_t)h[n].w << 32);
         const bool coll = (hk & kCollision) != 0;
         const bool own = (hk & ~kCollision) == cell_key(cx, cy, cz);
-        rs = h.x;
-        re = (coll || own) ? (h.y | (coll ? (int)0x80000000u : 0)) : h.x;
-      }
-      uint64_t key = kInfKey;
-#pragma unroll 1
-      for (int n = 0; n < 8; ++n) {
-        const int s = __shfl(rs, gb + n);
-        const int ef = __shfl(re, gb + n);
-        const int e = ef & 0x7FFFFFFF;
-        const bool cf = ef < 0;
-#pragma unroll 1
-        for (int j = s + q; __ballot(j - q < e) != 0; j += 8) {
-          bool ok = false;
-          uint64_t cand = kInfKey;
-          if (j < e) {
-            const float4 qv = a.sorted[j];
-            const float d0 = x0 - qv.x, d1 = x1 - qv.y, d2 = x2 - qv.z;
-            const float dd = (d0 * d0 + d1 * d1) + d2 * d2;
-            if (KER == PNR_GATHER_IDW) ok = dd <= a.r2;
-            else ok = fabsf(d0) < a.h0 && fabsf(d1) < a.h1 && fabsf(d2) < a.h2;
-            if (cf) {  // colliding bucket: the point must lie in this probe cell
-              ok = ok && cell_coord(qv.x, a.g.o0, a.g.inv) == bx + (n & 1) &&
-                   cell_coord(qv.y, a.g.o1, a.g.inv) == by + ((n >> 1) & 1) &&
-                   cell_coord(qv.z, a.g.o2, a.g.inv) == bz + (n >> 2);
-            }
-            cand = (uint64_t)__double_as_longlong(pack_key(dd, __float_as_int(qv.w)));
-          }
-          uint32_t bits = (uint32_t)(__ballot(ok) >> gb) & 0xFFu;
-          while (__ballot(bits != 0) != 0) {
-            const int src = bits ? __ffs(bits) - 1 : 0;
-            uint64_t kn = shfl64(cand, gb + src);
-            if (!bits) kn = kInfKey;
-            key = group_insert(key, kn, q);
-            bits &= bits - 1;
-          }
+        if ((coll || own) && h[n].y > h[n].x) {
+          L.r.rng[nr][tid] = make_int2(h[n].x, h[n].y);
+          L.r.cell[nr][tid] = (uint8_t)(n | (coll ? 8 : 0));
+          ++nr;
         }
       }
-      // lane q: the q-th neighbour's weight; the normaliser is the sequential sum over q = 0..7
-      const bool v = q < a.k && key != kInfKey;
-      const int id = v ? (int)(uint32_t)key : -1;
+    }
+    // flat candidate loop over the nr ranges; uniform over the wave (finished lanes insert +inf, a
+    // no-op), so the key registers are updated in place with no copies at the loop head
+    int jj = 0, je = 0, cf = 0, k = 0;
+    int2 nx = nr > 0 ? L.r.rng[0][tid] : make_int2(0, 0);
+    while (true) {
+      const bool act = jj < je || k < nr;
+      if (__ballot(act) == 0) break;
+      double kn = kInf;
+      if (act) {
+        if (jj >= je) {
+          jj = nx.x;
+          je = nx.y;
+          cf = L.r.cell[k][tid];
+          ++k;
+          if (k < nr) nx = L.r.rng[k][tid];  // read ahead
+        }
+        const float4 qv = a.sorted[jj++];
+        const float d0 = x0 - qv.x, d1 = x1 - qv.y, d2 = x2 - qv.z;
+        const float dd = (d0 * d0 + d1 * d1) + d2 * d2;
+        bool ok;
+        if (KER == PNR_GATHER_IDW) ok = dd <= a.r2;
+        else ok = fabsf(d0) < a.h0 && fabsf(d1) < a.h1 && fabsf(d2) < a.h2;
+        if (cf & 8) {  // colliding bucket: the point must lie in this probe cell
+          ok = ok && cell_coord(qv.x, a.g.o0, a.g.inv) == bx + (cf & 1) &&
+               cell_coord(qv.y, a.g.o1, a.g.inv) == by + ((cf >> 1) & 1) &&
+               cell_coord(qv.z, a.g.o2, a.g.inv) == bz + ((cf >> 2) & 1);
+        }
+        if (ok) kn = pack_key(dd, __float_as_int(qv.w));
+      }
+#pragma unroll
+      for (int t = 0; t < PNR_MAX_K; ++t) kn = kstage(key[t], kn);
+    }
+    // weights of the first k, normalised by their sequential sum (ascending distance)
+    float wv_[PNR_MAX_K];
+    int ki[PNR_MAX_K];
+    float W = 0.f;
+#pragma unroll
+    for (int t = 0; t < PNR_MAX_K; ++t) {
       float w = 0.f;
+      const bool v = t < a.k && key[t] != kInf;
+      ki[t] = v ? key_id(key[t]) : -1;
       if (v) {
         if (KER == PNR_GATHER_IDW) {
-          w = 1.0f / fmaxf(sqrtf(key_d2(__longlong_as_double((long long)key))), a.eps);
+          w = 1.0f / fmaxf(sqrtf(key_d2(key[t])), a.eps);
         } else {  // per-axis offsets of the kept point (same f32 arithmetic as the search)
-          const float* xi = a.xyz + (int64_t)id * 3;
+          const float* xi = a.xyz + (int64_t)ki[t] * 3;
           const float t0 = 1.0f - fabsf(x0 - xi[0]) / a.h0;
           const float t1 = 1.0f - fabsf(x1 - xi[1]) / a.h1;
           const float t2 = 1.0f - fabsf(x2 - xi[2]) / a.h2;
           w = (t0 * t1) * t2;
         }
       }
-      float W = 0.f;
+      wv_[t] = w;
+      W = W + w;
+    }
+    const float Wd = W > 0.f ? W : 1.0f;
+    __syncthreads();  // every thread is past its range reads: the LDS becomes the feature lists
+    L.f.row[tid] = row;
 #pragma unroll
-      for (int t = 0; t < PNR_MAX_K; ++t) W = W + __shfl(w, gb + t);
-      const float Wd = W > 0.f ? W : 1.0f;
-      const float wn = id >= 0 ? w / Wd : 0.f;
-      if (live && q < a.k && a.idx) {
-        a.idx[(int64_t)row * a.k + q] = id;
-        a.w[(int64_t)row * a.k + q] = wn;
+    for (int t = 0; t < PNR_MAX_K; ++t) {
+      const float wn = ki[t] >= 0 ? wv_[t] / Wd : 0.f;
+      L.f.idx[tid * PNR_MAX_K + t] = ki[t];
+      L.f.w[tid * PNR_MAX_K + t] = wn;
+      if (row >= 0 && t < a.k && a.idx) {
+        a.idx[(int64_t)row * a.k + t] = ki[t];
+        a.w[(int64_t)row * a.k + t] = wn;
       }
+    }
+    __syncthreads();
+    // feature sum: 8 lanes per sample, lane q owns channels 4q..4q+3
+#pragma unroll 1
+    for (int rr = 0; rr < 8; ++rr) {
+      const int sl = wv * 64 + rr * 8 + gq;
+      const int rw = L.f.row[sl];
+      if (rw < 0) continue;
       float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-      for (int t0 = 0; t0 < PNR_MAX_K; t0 += 4) {  // 4 feature loads in flight per batch
-        int idt[4];
+      for (int t0 = 0; t0 < PNR_MAX_K; t0 += 4) {  // 4 feature rows in flight
+        int id[4];
         float4 f[4];
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
-          idt[t] = __shfl(id, gb + t0 + t);
+          id[t] = L.f.idx[sl * PNR_MAX_K + t0 + t];
           f[t] = make_float4(0.f, 0.f, 0.f, 0.f);
-          if (idt[t] >= 0) f[t] = a.feats4[(int64_t)idt[t] * 8 + q];
+          if (id[t] >= 0) f[t] = a.feats4[(int64_t)id[t] * 8 + q];
         }
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
-          const float wt = __shfl(wn, gb + t0 + t);
-          if (idt[t] >= 0) {
-            acc.x = acc.x + wt * f[t].x;
-            acc.y = acc.y + wt * f[t].y;
-            acc.z = acc.z + wt * f[t].z;
-            acc.w = acc.w + wt * f[t].w;
+          if (id[t] >= 0) {
+            const float wn = L.f.w[sl * PNR_MAX_K + t0 + t];
+            acc.x = acc.x + wn * f[t].x;
+            acc.y = acc.y + wn * f[t].y;
+            acc.z = acc.z + wn * f[t].z;
+            acc.w = acc.w + wn * f[t].w;
           }
         }
       }
-      if (live) reinterpret_cast<float4*>(a.c)[(int64_t)row * 8 + q] = acc;
+      reinterpret_cast<float4*>(a.c)[(int64_t)rw * 8 + q] = acc;
     }
   }
 }
@@ -679,10 +702,23 @@ int launch_gather(const pnr_points& pts, const PointSrc& src, int mode, int64_t 
   if (hipMemsetAsync(a.wl.cnt, 0, kLists * 32 * 4, st) != hipSuccess) return (int)hipGetLastError();
   TimingScope ts(kTimeGather, P, st);
   gather_probe(mode, dim3((unsigned)((rows + 255) / 256)), st, a);
-  const int64_t tasks = kLists * ((a.wl.cap + 255) / 256);
-  const dim3 grid((unsigned)(tasks < 2048 ? tasks : 2048));
-  if (pts.mode == PNR_GATHER_IDW) hipLaunchKernelGGL((k_gather_search<PNR_GATHER_IDW>), grid, dim3(256), 0, st, a);
-  else hipLaunchKernelGGL((k_gather_search<PNR_GATHER_TRILINEAR>), grid, dim3(256), 0, st, a);
+  const int64_t tasks = kLists * ((a.wl.cap + kSearchBlock - 1) / kSearchBlock);
+  // persistent grid = the blocks that are resident at once (a later wave of blocks would run as a tail)
+  static int resident[2] = {0, 0};
+  const int km = pts.mode == PNR_GATHER_IDW ? 0 : 1;
+  if (!resident[km]) {
+    int dev = 0, cus = 0, per = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (km == 0)
+      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_gather_search<PNR_GATHER_IDW>, kSearchBlock, 0);
+    else
+      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_gather_search<PNR_GATHER_TRILINEAR>, kSearchBlock, 0);
+    resident[km] = (cus > 0 && per > 0) ? cus * per : 2048;
+  }
+  const dim3 grid((unsigned)(tasks < resident[km] ? tasks : resident[km]));
+  if (km == 0) hipLaunchKernelGGL((k_gather_search<PNR_GATHER_IDW>), grid, dim3(kSearchBlock), 0, st, a);
+  else hipLaunchKernelGGL((k_gather_search<PNR_GATHER_TRILINEAR>), grid, dim3(kSearchBlock), 0, st, a);
   return hip_status(hipGetLastError());
 }
 
