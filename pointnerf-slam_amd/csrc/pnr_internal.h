@@ -202,8 +202,10 @@ struct IndexView {
   int32_t* bucket;
   int32_t* slot;
   int32_t* partial;
-  float4* sorted;
+  float4* sorted;  // bucket-sorted points, each bucket ordered by half-cell (sub-cell) index
+  float4* tmp;     // bucket-scattered points before the sub-cell order (build scratch)
   int4* hdr;       // [T] {start, end, cell key lo, key hi | collision bit}
+  int4* sub;       // [T] 8 x u16: end offsets of sub-cells 0..7 in the bucket (0xFFFF last: unordered)
   uint32_t* occ;   // occupancy filter (points.hip k_occ_mark)
   int64_t occ_words;
   int64_t T;

@@ -5,9 +5,10 @@
 // is specified by oracle/ref_points.py and include/pnr.h (pnr_points).
 //
 // Index (pnr_points_build): points hashed by cell (edge `cell` >= 2 x reach) into T = 2^bits
-// buckets, bucket-sorted float4 (x, y, z, index bits), one 16-B header per bucket
-// {start, end, packed cell key | collision flag}, and an occupancy filter (one bit per hashed
-// probe-block base cell).
+// buckets, bucket-sorted float4 (x, y, z, index bits) with each bucket ordered by sub-cell (the
+// 2x2x2 half-cells of a cell), one 16-B header per bucket {start, end, packed cell key |
+// collision flag}, one 16-B sub-cell end-offset table per bucket, and an occupancy filter (one
+// bit per hashed probe-block base cell).
 //
 // Gather, two passes:
 //   k_gather_probe  one thread per sample row: coalesced zero fill of the block's output rows,
@@ -15,11 +16,13 @@
 //                   neighbours go to a work list (one atomic per wave, 64 sub-lists).  Free space -- most of a
 //                   ray -- costs one L2-resident bit load.
 //   k_gather_search persistent blocks over the work list (grid = resident blocks), one thread per
-//                   sample: 8 bucket headers (foreign buckets of a hash collision are skipped by
-//                   their key), the non-empty ranges compacted into the thread's LDS row, ONE flat
-//                   candidate loop over them (uniform exit, next range read ahead), a branch-free
-//                   top-k network on packed (d2, index) float64 keys (v_min/v_max_f64, 2 VALU per
-//                   stage); normalised weights, then the feature sum with 8 lanes per sample.
+//                   sample: 8 bucket headers and sub-cell tables (foreign buckets of a hash collision
+//                   are skipped by their key); per probe cell one span from the first to the last
+//                   sub-cell (half-cell) the reach box touches, the spans compacted into the
+//                   thread's LDS row and scanned by ONE flat candidate loop (uniform exit, next span
+//                   read ahead); a branch-free top-k network on packed (d2, index) float64 keys
+//                   (v_min/v_max_f64, 2 VALU per stage); normalised weights, then the feature sum
+//                   with 8 lanes per sample.
 //   k_gather_bwd    dL/df_i += w_k dL/dc (float atomics) and dL/dp through the weights.
 #include "pnr_internal.h"
 
@@ -54,6 +57,18 @@ __device__ __forceinline__ int cell_coord(float x, float o, float inv) {
   float f = floorf((x - o) * inv);
   f = fminf(fmaxf(f, -1.0e9f), 1.0e9f);  // far-away / non-finite samples: any cell, never UB
   return (int)f;
+}
+
+// half of its cell a coordinate lies in (0 lower, 1 upper), from the same f32 value as cell_coord
+__device__ __forceinline__ int sub_bit(float x, float o, float inv) {
+  PNR_FP_STRICT
+  float t = (x - o) * inv;
+  t = fminf(fmaxf(t, -1.0e9f), 1.0e9f);
+  return t - floorf(t) >= 0.5f ? 1 : 0;
+}
+// sub-cell (2x2x2 halves of a cell) of a point, x fastest
+__device__ __forceinline__ int sub_index(float x, float y, float z, float o0, float o1, float o2, float inv) {
+  return sub_bit(x, o0, inv) | (sub_bit(y, o1, inv) << 1) | (sub_bit(z, o2, inv) << 2);
 }
 
 // lower of the two cells per axis that cover [x - reach, x + reach] when cell >= 2 reach
@@ -121,7 +136,9 @@ IndexView index_view(void* base, int64_t M, int32_t bits, size_t* bytes) {
   v.slot = reinterpret_cast<int32_t*>(take((size_t)M * 4));
   v.partial = reinterpret_cast<int32_t*>(take((size_t)scan_scratch_ints(v.T) * 4));
   v.sorted = reinterpret_cast<float4*>(take((size_t)M * 16));
+  v.tmp = reinterpret_cast<float4*>(take((size_t)M * 16));
   v.hdr = reinterpret_cast<int4*>(take((size_t)v.T * 16));
+  v.sub = reinterpret_cast<int4*>(take((size_t)v.T * 16));
   v.occ_words = (1ll << occ_bits_log2(bits)) / 32;
   v.occ = reinterpret_cast<uint32_t*>(take((size_t)v.occ_words * 4));
   if (bytes) *bytes = off;
@@ -205,6 +222,49 @@ __global__ void k_hash_scatter(const float* __restrict__ xyz, int64_t M, const i
   sorted[pos] = make_float4(xyz[i * 3 + 0], xyz[i * 3 + 1], xyz[i * 3 + 2], __int_as_float((int)i));
 }
 
+// Order each bucket by sub-cell (counting sort, one thread per bucket; buckets hold a few points)
+// and record the 8 sub-cell end offsets as u16.  A bucket of >= 65535 points keeps its order and
+// gets 0xFFFF as last offset: the search then scans it whole (the distance test keeps it exact).
+__global__ void k_bucket_sub(const int32_t* __restrict__ start, const float4* __restrict__ tmp, int64_t T,
+                             HashGrid g, float4* __restrict__ sorted, int4* __restrict__ sub) {
+  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= T) return;
+  const int s = start[b], e = start[b + 1], n = e - s;
+  if (n >= 65535) {
+    for (int j = s; j < e; ++j) sorted[j] = tmp[j];
+    sub[b] = make_int4(-1, -1, -1, -1);
+    return;
+  }
+  uint32_t c[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int j = s; j < e; ++j) {
+    const float4 q = tmp[j];
+    const int si = sub_index(q.x, q.y, q.z, g.o0, g.o1, g.o2, g.inv);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) c[k] += si == k ? 1u : 0u;
+  }
+  uint32_t end[8], pos[8];
+  uint32_t run = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    pos[k] = (uint32_t)s + run;
+    run += c[k];
+    end[k] = run;
+  }
+  for (int j = s; j < e; ++j) {
+    const float4 q = tmp[j];
+    const int si = sub_index(q.x, q.y, q.z, g.o0, g.o1, g.o2, g.inv);
+    uint32_t dst = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      dst = si == k ? pos[k] : dst;
+      pos[k] += si == k ? 1u : 0u;
+    }
+    sorted[dst] = q;
+  }
+  sub[b] = make_int4((int)(end[0] | (end[1] << 16)), (int)(end[2] | (end[3] << 16)), (int)(end[4] | (end[5] << 16)),
+                     (int)(end[6] | (end[7] << 16)));
+}
+
 // bucket header {start, end, key lo, key hi}: the cell of the bucket's first point, plus the
 // collision flag when the bucket also holds points of other cells
 __global__ void k_bucket_hdr(const int32_t* __restrict__ start, const float4* __restrict__ sorted, int64_t T,
@@ -254,9 +314,11 @@ int launch_points_build(const pnr_points& pts, hipStream_t st) {
   int rc = scan_exclusive(v.count, v.start, v.T, v.partial, st);
   if (rc) return rc;
   if (M > 0) {
-    hipLaunchKernelGGL(k_hash_scatter, dim3(nbm), dim3(256), 0, st, pts.xyz, M, v.start, v.bucket, v.slot, v.sorted);
+    hipLaunchKernelGGL(k_hash_scatter, dim3(nbm), dim3(256), 0, st, pts.xyz, M, v.start, v.bucket, v.slot, v.tmp);
     hipLaunchKernelGGL(k_occ_mark, dim3(nbm), dim3(256), 0, st, pts.xyz, M, g, v.occ);
   }
+  hipLaunchKernelGGL(k_bucket_sub, dim3((unsigned)((v.T + 255) / 256)), dim3(256), 0, st, v.start, v.tmp, v.T, g,
+                     v.sorted, v.sub);
   hipLaunchKernelGGL(k_bucket_hdr, dim3((unsigned)((v.T + 255) / 256)), dim3(256), 0, st, v.start, v.sorted, v.T, g,
                      v.hdr);
   return hip_status(hipGetLastError());
@@ -305,6 +367,7 @@ struct GatherArgs {
   int64_t P, rows;
   HashGrid g;
   const int4* hdr;
+  const int4* sub;       // per bucket: sub-cell end offsets (k_bucket_sub)
   const float4* sorted;
   const float4* feats4;  // (M, 8) float4
   const float* xyz;      // (M, 3)
@@ -312,6 +375,7 @@ struct GatherArgs {
   int k;
   float r2, eps;
   float h0, h1, h2;      // trilinear spacing
+  float rho0, rho1, rho2;  // neighbourhood reach per axis in cell units, with a 2^-10 margin
   float* c;              // (rows, 32)
   int32_t* idx;          // (rows, k) or null
   float* w;              // (rows, k) or null
@@ -373,6 +437,25 @@ __global__ __launch_bounds__(256) void k_gather_probe(GatherArgs a) {
 // the lexicographic one): v_min_f64 / v_max_f64 by inline asm, 2 VALU per stage (the builtins add
 // an IEEE canonicalisation per operand).  The feature sum then runs 8 lanes per sample, 4 feature
 // rows in flight per lane.
+// end offset of sub-cell k (0..7) in a bucket's sub table (8 x u16)
+__device__ __forceinline__ int sub_end(const int4& sb, int k) {
+  const int w = k < 2 ? sb.x : (k < 4 ? sb.y : (k < 6 ? sb.z : sb.w));
+  return (int)(((uint32_t)w >> (16 * (k & 1))) & 0xFFFFu);
+}
+// per axis: bits 2c+h (c = block cell 0/1, h = half) of the half-cells that [u - rho', u + rho']
+// touches, u = (x - o) * inv as in cell_coord and b = the block's first cell
+__device__ __forceinline__ uint32_t half_mask(float x, float o, float inv, float rho, int b) {
+  PNR_FP_STRICT
+  float u = (x - o) * inv;
+  u = fminf(fmaxf(u, -1.0e9f), 1.0e9f);
+  const float r = rho + fabsf(u) * 6.0e-7f;
+  const int lo = (int)floorf(2.0f * (u - r)) - 2 * b, hi = (int)floorf(2.0f * (u + r)) - 2 * b;
+  uint32_t m = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) m |= (lo <= k && k <= hi) ? (1u << k) : 0u;
+  return m;
+}
+
 // one network stage: key <- min(key, kn), return max(key, kn); key is updated in place (a tied
 // operand), so the unrolled network carries no register copies around the candidate loop
 __device__ __forceinline__ double kstage(double& key, double kn) {
@@ -420,20 +503,44 @@ __global__ __launch_bounds__(kSearchBlock) void k_gather_search(GatherArgs a) {
       base_cell(x0, a.g.o0, a.g.inv, bx);
       base_cell(x1, a.g.o1, a.g.inv, by);
       base_cell(x2, a.g.o2, a.g.inv, bz);
-      int4 h[8];
+      // half-cells (block-relative, 0..3 per axis) that the reach box [u - rho, u + rho] touches;
+      // the margin (2^-10 of rho + 5 ulp of u) covers the f32 rounding of both sides' coordinates
+      const uint32_t am0 = half_mask(x0, a.g.o0, a.g.inv, a.rho0, bx);
+      const uint32_t am1 = half_mask(x1, a.g.o1, a.g.inv, a.rho1, by);
+      const uint32_t am2 = half_mask(x2, a.g.o2, a.g.inv, a.rho2, bz);
 #pragma unroll
-      for (int n = 0; n < 8; ++n)  // the 8 bucket headers in flight at once
-        h[n] = a.hdr[cell_hash(bx + (n & 1), by + ((n >> 1) & 1), bz + (n >> 2), a.g.mask)];
+      for (int n0 = 0; n0 < 8; n0 += 4) {  // 4 bucket headers + sub-cell tables in flight at a time
+        int4 h[4], sb[4];
 #pragma unroll
-      for (int n = 0; n < 8; ++n) {
-        const int cx = bx + (n & 1), cy = by + ((n >> 1) & 1), cz = bz + (n >> 2);
-        const uint64_t hk = (uint64_t)(uint32_t)h[n].z | ((uint64_t)(uint32_t)h[n].w << 32);
-        const bool coll = (hk & kCollision) != 0;
-        const bool own = (hk & ~kCollision) == cell_key(cx, cy, cz);
-        if ((coll || own) && h[n].y > h[n].x) {
-          L.r.rng[nr][tid] = make_int2(h[n].x, h[n].y);
-          L.r.cell[nr][tid] = (uint8_t)(n | (coll ? 8 : 0));
-          ++nr;
+        for (int u = 0; u < 4; ++u) {
+          const int n = n0 + u;
+          const uint32_t bk = cell_hash(bx + (n & 1), by + ((n >> 1) & 1), bz + (n >> 2), a.g.mask);
+          h[u] = a.hdr[bk];
+          sb[u] = a.sub[bk];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int n = n0 + u;
+          const int cx = bx + (n & 1), cy = by + ((n >> 1) & 1), cz = bz + (n >> 2);
+          const uint64_t hk = (uint64_t)(uint32_t)h[u].z | ((uint64_t)(uint32_t)h[u].w << 32);
+          const bool coll = (hk & kCollision) != 0;
+          const bool own = (hk & ~kCollision) == cell_key(cx, cy, cz);
+          // this cell's wanted sub-cells (x fastest) and the one span from the first to the last
+          const uint32_t xm = (am0 >> (2 * (n & 1))) & 3u, ym = (am1 >> (2 * ((n >> 1) & 1))) & 3u,
+                         zm = (am2 >> (2 * (n >> 2))) & 3u;
+          const uint32_t plane = ((ym & 1u) ? xm : 0u) | ((ym & 2u) ? xm << 2 : 0u);
+          const uint32_t m = ((zm & 1u) ? plane : 0u) | ((zm & 2u) ? plane << 4 : 0u);
+          int s0 = h[u].x, s1 = h[u].y;
+          if (m != 0u && (((uint32_t)sb[u].w >> 16) != 0xFFFFu)) {  // an ordered bucket: the span only
+            const int f = __ffs((int)m) - 1, l = 31 - __clz((int)m);
+            s0 = h[u].x + (f == 0 ? 0 : sub_end(sb[u], f - 1));
+            s1 = h[u].x + sub_end(sb[u], l);
+          }
+          if ((coll || own) && m != 0u && s1 > s0) {
+            L.r.rng[nr][tid] = make_int2(s0, s1);
+            L.r.cell[nr][tid] = (uint8_t)(n | (coll ? 8 : 0));
+            ++nr;
+          }
         }
       }
     }
@@ -685,6 +792,7 @@ int launch_gather(const pnr_points& pts, const PointSrc& src, int mode, int64_t 
   a.rows = rows;
   a.g = make_grid(pts);
   a.hdr = v.hdr;
+  a.sub = v.sub;
   a.sorted = v.sorted;
   a.feats4 = reinterpret_cast<const float4*>(pts.feats);
   a.xyz = pts.xyz;
@@ -695,6 +803,13 @@ int launch_gather(const pnr_points& pts, const PointSrc& src, int mode, int64_t 
   a.h0 = pts.spacing[0];
   a.h1 = pts.spacing[1];
   a.h2 = pts.spacing[2];
+  {
+    const float inv = 1.0f / pts.cell, mg = 1.0f + 1.0f / 1024.0f;
+    const bool idw = pts.mode == PNR_GATHER_IDW;
+    a.rho0 = (idw ? pts.radius : pts.spacing[0]) * inv * mg;
+    a.rho1 = (idw ? pts.radius : pts.spacing[1]) * inv * mg;
+    a.rho2 = (idw ? pts.radius : pts.spacing[2]) * inv * mg;
+  }
   a.c = c;
   a.idx = idx;
   a.w = w;
