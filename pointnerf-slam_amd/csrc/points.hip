@@ -690,21 +690,51 @@ __global__ __launch_bounds__(256) void k_gather_bwd(GatherBwdArgs a) {
 #pragma unroll 1
     for (int64_t t = half; t < jn; t += 8) {  // uniform over each half-wave
       const int64_t p = __float_as_int(a.wl.items[rl * a.wl.cap + j0 + t].w);
+      // every load of the row issued at once: g_c / c rows, the k (index, weight) pairs (broadcast
+      // within the half-wave), then the k feature rows and atomics predicated, no dependent branches
       const float g = a.g_c[p * 32 + ch];
-      float dots[PNR_MAX_K];
-      float gcd = 0.f;
-      if (a.g_p) gcd = g * a.c[p * 32 + ch];
+      const float cc = a.g_p ? a.c[p * 32 + ch] : 0.f;
+      int id[PNR_MAX_K];
+      float wn[PNR_MAX_K];
 #pragma unroll
       for (int kk = 0; kk < PNR_MAX_K; ++kk) {
-        dots[kk] = 0.f;
-        if (kk >= a.k) continue;
-        const int id = a.idx[p * a.k + kk];
-        if (id < 0) continue;
-        const float wn = a.w[p * a.k + kk];
-        if (a.g_feats) unsafeAtomicAdd(a.g_feats + (int64_t)id * 32 + ch, wn * g);
-        if (a.g_p) dots[kk] = g * reinterpret_cast<const float*>(a.feats4)[(int64_t)id * 32 + ch];
+        id[kk] = kk < a.k ? a.idx[p * a.k + kk] : -1;
+        wn[kk] = kk < a.k ? a.w[p * a.k + kk] : 0.f;
+      }
+      float x0 = 0.f, x1 = 0.f, x2 = 0.f;
+      float xi[PNR_MAX_K][3];
+      if (a.g_p && ch == 0) {  // the point and its neighbours' positions, in flight during the sums
+        if (a.xP) {
+          const float4 xv = a.xP[p];
+          x0 = xv.x; x1 = xv.y; x2 = xv.z;
+        } else {
+          bool inside;
+          load_point<SRC>(a.src, p, x0, x1, x2, inside);
+        }
+#pragma unroll
+        for (int kk = 0; kk < PNR_MAX_K; ++kk) {
+          const int64_t j = id[kk] >= 0 ? id[kk] : 0;
+          xi[kk][0] = a.xyz[j * 3 + 0];
+          xi[kk][1] = a.xyz[j * 3 + 1];
+          xi[kk][2] = a.xyz[j * 3 + 2];
+        }
+      }
+      float dots[PNR_MAX_K];
+      if (a.g_p) {
+        float f[PNR_MAX_K];
+#pragma unroll
+        for (int kk = 0; kk < PNR_MAX_K; ++kk)
+          f[kk] = id[kk] >= 0 ? reinterpret_cast<const float*>(a.feats4)[(int64_t)id[kk] * 32 + ch] : 0.f;
+#pragma unroll
+        for (int kk = 0; kk < PNR_MAX_K; ++kk) dots[kk] = g * f[kk];
+      }
+      if (a.g_feats) {
+#pragma unroll
+        for (int kk = 0; kk < PNR_MAX_K; ++kk)
+          if (id[kk] >= 0) unsafeAtomicAdd(a.g_feats + (int64_t)id[kk] * 32 + ch, wn[kk] * g);
       }
       if (!a.g_p) continue;
+      float gcd = g * cc;
 #pragma unroll
       for (int m = 1; m < 32; m <<= 1) {  // sums over the 32 channels (xor stays inside the half-wave)
         gcd += __shfl_xor(gcd, m);
@@ -712,30 +742,18 @@ __global__ __launch_bounds__(256) void k_gather_bwd(GatherBwdArgs a) {
         for (int kk = 0; kk < PNR_MAX_K; ++kk) dots[kk] += __shfl_xor(dots[kk], m);
       }
       if (ch != 0) continue;
-      float x0, x1, x2;
-      if (a.xP) {
-        const float4 xv = a.xP[p];
-        x0 = xv.x; x1 = xv.y; x2 = xv.z;
-      } else {
-        bool inside;
-        load_point<SRC>(a.src, p, x0, x1, x2, inside);
-      }
       // dL/dp = sum_k wn_k (g.f_k - g.c) (1/w_k) dw_k/dp
       float gp0 = 0.f, gp1 = 0.f, gp2 = 0.f;
 #pragma unroll
       for (int kk = 0; kk < PNR_MAX_K; ++kk) {
-        if (kk >= a.k) continue;
-        const int id = a.idx[p * a.k + kk];
-        if (id < 0) continue;
-        const float wn = a.w[p * a.k + kk];
-        const float* xi = a.xyz + (int64_t)id * 3;
-        const float d0 = x0 - xi[0], d1 = x1 - xi[1], d2 = x2 - xi[2];
-        const float coef = wn * (dots[kk] - gcd);
+        if (id[kk] < 0) continue;
+        const float d0 = x0 - xi[kk][0], d1 = x1 - xi[kk][1], d2 = x2 - xi[kk][2];
+        const float coef = wn[kk] * (dots[kk] - gcd);
         if (KER == PNR_GATHER_IDW) {
           const float dd = (d0 * d0 + d1 * d1) + d2 * d2;
           if (sqrtf(dd) > a.eps) {  // w = 1/|d|: (1/w) dw/dp = -d / |d|^2
-            const float f = -coef / dd;
-            gp0 += f * d0; gp1 += f * d1; gp2 += f * d2;
+            const float fq = -coef / dd;
+            gp0 += fq * d0; gp1 += fq * d1; gp2 += fq * d2;
           }
         } else {  // w = prod (1 - |d_a|/h_a): (1/w) dw/dp_a = -sign(d_a) / (h_a t_a)
           const float t0 = 1.0f - fabsf(d0) / a.h0, t1 = 1.0f - fabsf(d1) / a.h1, t2 = 1.0f - fabsf(d2) / a.h2;
@@ -767,6 +785,21 @@ static bool points_ok(const pnr_points& pts) {
   return pts.n_points >= 0 && pts.k >= 1 && pts.k <= PNR_MAX_K && pts.table_bits >= 10 && pts.table_bits <= 24 &&
          pts.index && (pts.mode == PNR_GATHER_IDW || pts.mode == PNR_GATHER_TRILINEAR) && reach > 0.f &&
          pts.cell >= 2.0f * reach && (pts.n_points == 0 || (pts.xyz && pts.feats));
+}
+
+// persistent grid = the blocks of `kern` resident at once (a later wave of blocks would run as a
+// tail), at most `tasks`; queried once per kernel
+template <typename K>
+static unsigned resident_grid(K kern, int block, int64_t tasks) {
+  static int resident = 0;
+  if (!resident) {
+    int dev = 0, cus = 0, per = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kern, block, 0);
+    resident = (cus > 0 && per > 0) ? cus * per : 2048;
+  }
+  return (unsigned)(tasks < resident ? tasks : resident);
 }
 
 static void gather_probe(int mode, dim3 grid, hipStream_t st, const GatherArgs& a) {
@@ -818,32 +851,28 @@ int launch_gather(const pnr_points& pts, const PointSrc& src, int mode, int64_t 
   TimingScope ts(kTimeGather, P, st);
   gather_probe(mode, dim3((unsigned)((rows + 255) / 256)), st, a);
   const int64_t tasks = kLists * ((a.wl.cap + kSearchBlock - 1) / kSearchBlock);
-  // persistent grid = the blocks that are resident at once (a later wave of blocks would run as a tail)
-  static int resident[2] = {0, 0};
-  const int km = pts.mode == PNR_GATHER_IDW ? 0 : 1;
-  if (!resident[km]) {
-    int dev = 0, cus = 0, per = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (km == 0)
-      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_gather_search<PNR_GATHER_IDW>, kSearchBlock, 0);
-    else
-      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_gather_search<PNR_GATHER_TRILINEAR>, kSearchBlock, 0);
-    resident[km] = (cus > 0 && per > 0) ? cus * per : 2048;
+  if (pts.mode == PNR_GATHER_IDW) {
+    auto kern = k_gather_search<PNR_GATHER_IDW>;
+    hipLaunchKernelGGL(kern, dim3(resident_grid(kern, kSearchBlock, tasks)), dim3(kSearchBlock), 0, st, a);
+  } else {
+    auto kern = k_gather_search<PNR_GATHER_TRILINEAR>;
+    hipLaunchKernelGGL(kern, dim3(resident_grid(kern, kSearchBlock, tasks)), dim3(kSearchBlock), 0, st, a);
   }
-  const dim3 grid((unsigned)(tasks < resident[km] ? tasks : resident[km]));
-  if (km == 0) hipLaunchKernelGGL((k_gather_search<PNR_GATHER_IDW>), grid, dim3(kSearchBlock), 0, st, a);
-  else hipLaunchKernelGGL((k_gather_search<PNR_GATHER_TRILINEAR>), grid, dim3(kSearchBlock), 0, st, a);
   return hip_status(hipGetLastError());
 }
 
+template <int SRC, int KER>
+static void gather_bwd_launch(int64_t tasks, hipStream_t st, const GatherBwdArgs& a) {
+  auto kern = k_gather_bwd<SRC, KER>;
+  hipLaunchKernelGGL(kern, dim3(resident_grid(kern, 256, tasks)), dim3(256), 0, st, a);
+}
 template <int KER>
-static void gather_bwd_mode(int mode, dim3 grid, hipStream_t st, const GatherBwdArgs& a) {
+static void gather_bwd_mode(int mode, int64_t tasks, hipStream_t st, const GatherBwdArgs& a) {
   switch (mode) {
-    case kPtsF64: hipLaunchKernelGGL((k_gather_bwd<kPtsF64, KER>), grid, dim3(256), 0, st, a); break;
-    case kPtsF32: hipLaunchKernelGGL((k_gather_bwd<kPtsF32, KER>), grid, dim3(256), 0, st, a); break;
-    case kRaysZ64: hipLaunchKernelGGL((k_gather_bwd<kRaysZ64, KER>), grid, dim3(256), 0, st, a); break;
-    default: hipLaunchKernelGGL((k_gather_bwd<kRaysZ32, KER>), grid, dim3(256), 0, st, a); break;
+    case kPtsF64: gather_bwd_launch<kPtsF64, KER>(tasks, st, a); break;
+    case kPtsF32: gather_bwd_launch<kPtsF32, KER>(tasks, st, a); break;
+    case kRaysZ64: gather_bwd_launch<kRaysZ64, KER>(tasks, st, a); break;
+    default: gather_bwd_launch<kRaysZ32, KER>(tasks, st, a); break;
   }
 }
 
@@ -879,9 +908,8 @@ int launch_gather_bwd(const pnr_points& pts, const PointSrc* src, int mode, cons
   TimingScope ts(kTimeGatherBwd, P, st);
   hipLaunchKernelGGL(k_gather_bwd_probe, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, st, a);
   const int64_t tasks = kLists * ((a.wl.cap + 255) / 256);
-  const dim3 grid((unsigned)(tasks < 2048 ? tasks : 2048));
-  if (pts.mode == PNR_GATHER_IDW) gather_bwd_mode<PNR_GATHER_IDW>(mode, grid, st, a);
-  else gather_bwd_mode<PNR_GATHER_TRILINEAR>(mode, grid, st, a);
+  if (pts.mode == PNR_GATHER_IDW) gather_bwd_mode<PNR_GATHER_IDW>(mode, tasks, st, a);
+  else gather_bwd_mode<PNR_GATHER_TRILINEAR>(mode, tasks, st, a);
   return hip_status(hipGetLastError());
 }
 
