@@ -297,19 +297,27 @@ static int launch_bwd16(const float* packed, const BwdArgs& a, int64_t P, hipStr
   return hip_status(hipGetLastError());
 }
 
+// max |g| as uint bits (non-negative floats order as uints): grid-stride, block reduction, ONE
+// atomic per block (same-address atomics serialise at ~90 per microsecond)
 __global__ void k_gmax(const float* __restrict__ g, int64_t n, uint32_t* __restrict__ out) {
+  __shared__ float red[4];
   float m = 0.f;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
     m = fmaxf(m, fabsf(g[i]));
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
-  if ((threadIdx.x & 63) == 0 && m > 0.f) atomicMax(out, __float_as_uint(m));  // non-negative floats order as uints
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    if (m > 0.f) atomicMax(out, __float_as_uint(m));
+  }
 }
 
 int launch_gmax(const float* g, int64_t n, uint32_t* out, hipStream_t st) {
   if (n <= 0) return 0;
-  int64_t blocks = (n + 255) / 256;
-  if (blocks > 2048) blocks = 2048;
+  int64_t blocks = (n + 4095) / 4096;  // >= 16 elements per thread
+  if (blocks > 512) blocks = 512;
   hipLaunchKernelGGL(k_gmax, dim3((unsigned)blocks), dim3(256), 0, st, g, n, out);
   return hip_status(hipGetLastError());
 }

@@ -10,26 +10,33 @@ int64_t fc_packed_floats_all() { return kFcPackedFloatsAll; }
 // Packing
 // ---------------------------------------------------------------------------------------------
 // Per-tensor power-of-two scale of the f16 images: s = 2^e, e = floor(log2(2^14 / max|W|)),
-// clamped to [-20, 20]; scl[i] = s, inv[i] = 1/s (both exact).  One block per tensor.
+// clamped to [-20, 20]; scl[i] = s, inv[i] = 1/s (both exact).  One 1024-thread block per tensor.
 struct ScaleArgs {
   const float* w[5];
   int n[5];
   float* inv;
   float* scl;
 };
-__global__ void k_wscale(ScaleArgs a) {
-  __shared__ float red[256];
+__global__ __launch_bounds__(1024) void k_wscale(ScaleArgs a) {
+  __shared__ float red[16];
   const float* w = a.w[blockIdx.x];
   const int n = a.n[blockIdx.x];
-  float m = 0.f;
-  for (int i = threadIdx.x; i < n; i += 256) m = fmaxf(m, fabsf(w[i]));
-  red[threadIdx.x] = m;
-  __syncthreads();
-  for (int s = 128; s > 0; s >>= 1) {
-    if ((int)threadIdx.x < s) red[threadIdx.x] = fmaxf(red[threadIdx.x], red[threadIdx.x + s]);
-    __syncthreads();
+  float m0 = 0.f, m1 = 0.f, m2 = 0.f, m3 = 0.f;  // 4 loads in flight per thread
+  int i = threadIdx.x;
+  for (; i + 3 * 1024 < n; i += 4 * 1024) {
+    m0 = fmaxf(m0, fabsf(w[i]));
+    m1 = fmaxf(m1, fabsf(w[i + 1024]));
+    m2 = fmaxf(m2, fabsf(w[i + 2048]));
+    m3 = fmaxf(m3, fabsf(w[i + 3072]));
   }
+  for (; i < n; i += 1024) m0 = fmaxf(m0, fabsf(w[i]));
+  float m = fmaxf(fmaxf(m0, m1), fmaxf(m2, m3));
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
   if (threadIdx.x == 0) {
+    for (int k = 1; k < 16; ++k) red[0] = fmaxf(red[0], red[k]);
     int e = 20;
     if (red[0] > 0.f) {
       int ex;
@@ -156,7 +163,7 @@ int launch_pack_bf(const RawParams& rp, float* packed, hipStream_t st) {
   }
   sa.inv = raw + kRawInv;
   sa.scl = raw + kRawScl;
-  hipLaunchKernelGGL(k_wscale, dim3(5), dim3(256), 0, st, sa);
+  hipLaunchKernelGGL(k_wscale, dim3(5), dim3(1024), 0, st, sa);
   const int64_t n = 2 * (bf_main_bytes(2) / 2) + bf_main_bytes(1) / 2 + kRawInv;
   const int threads = 256;
   hipLaunchKernelGGL(k_pack16, dim3((unsigned)((n + threads - 1) / threads)), dim3(threads), 0, st, rp,

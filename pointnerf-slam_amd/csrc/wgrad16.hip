@@ -21,6 +21,7 @@
 // [32w, 32w + 32) x all NB columns in NTB accumulator tiles for the whole K range, added into C with
 // one float atomic per element at the end.  The bias row sums come from the A fragments.
 // K must be a multiple of 32 and rows in [real K, K) zero in A (padded points: delta = 0).
+#include <cmath>
 #include "mlp16.h"
 
 namespace pnr {
@@ -168,9 +169,13 @@ int launch_wgrad16(int kind, const void* A, const void* B, int64_t K, float* C, 
                    const uint32_t* gmax, hipStream_t st) {
   if (K <= 0) return 0;
   K = (K + 31) / 32 * 32;
-  int64_t ks = (K + 255) / 256;  // one workgroup per CU
+  // split-K: each workgroup flushes its whole C tile (256 KB of float atomics for a hidden layer,
+  // ~0.2 us of the chip's atomic rate) and spends ~0.5 us per 32-point tile, so the time
+  // (K / 32 / n) * 0.5 + n * 0.2 is least at n = sqrt(2.5 K / 32); at most one workgroup per CU
+  int64_t nwg = (int64_t)sqrt(2.5 * (double)K / 32.0);
+  nwg = nwg < 4 ? 4 : (nwg > 256 ? 256 : nwg);
+  int64_t ks = (K + nwg - 1) / nwg;
   ks = (ks + 31) / 32 * 32;
-  if (ks < 128) ks = 128;
   Wg16Args a{static_cast<const _Float16*>(A), static_cast<const _Float16*>(B), 256, K, ks, C, ldc, bias, gmax};
   TimingScope ts(kTimeWgrad, K, st);
   if (kind == kWgradHidden) return launch_k<8, 256>(a, st);
