@@ -229,6 +229,9 @@ def main():
     ap.add_argument('--warmup', type=int, default=2)
     ap.add_argument('--workload', choices=['map', 'fwd', 'map-points'], default='map')
     ap.add_argument('--rays', type=int, default=W * H, help='rays per GPU per step')
+    ap.add_argument('--graph', action='store_true',
+                    help='replay the mapping iteration from a captured HIP graph (pnr.mapping.MapGraph; '
+                         'single GPU, for the latency-bound faithful batches N=1000 / 5000)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-gather', action='store_true', help='skip the point-gather roofline line')
     ap.add_argument('--precision', default=None, help="decoder forward matmuls: fp32 | f16x3 (default) | bf16x3 | bf16")
@@ -286,6 +289,14 @@ def main():
         def step():
             t_rand = torch.rand((n, cfg['rendering']['N_samples']), device=dev)
             mstep(ro, rd, gt, col, t_rand)
+
+        if args.graph and world == 1 and points is None:
+            from pnr.mapping import MapGraph
+            mgraph = MapGraph(mstep, ro, rd, gt, col, torch.rand((n, cfg['rendering']['N_samples']), device=dev))
+
+            def step():  # noqa: F811  (the same iteration, replayed; a fresh jitter drawn per step)
+                t_rand = torch.rand((n, cfg['rendering']['N_samples']), device=dev)
+                mgraph(ro, rd, gt, col, t_rand)
     else:
         def step():
             with torch.no_grad():
@@ -372,7 +383,8 @@ def main():
                     'room0 decoder fixture)',
             'config': {'workload': wl_name,
                        'rays_per_gpu': n, 'global_batch': n * world, 'samples_per_ray': samples,
-                       'parallelism': f'dp{world}', 'decoder_precision': prec},
+                       'parallelism': f'dp{world}', 'decoder_precision': prec,
+                       'graph': bool(args.graph and world == 1 and args.workload == 'map')},
             'roofline': roofline, 'cpu_baseline': cpu,
             'kernels': {k: {'launches': v[0], 'ms': round(v[1], 3), 'units': v[2]} for k, v in kt.items()},
         }

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define PNR_ABI_VERSION 3
+#define PNR_ABI_VERSION 4
 #define PNR_N_PARAMS 11
 #define PNR_MAX_SAMPLES 64      /* N_samples + N_importance per ray */
 #define PNR_C_DIM 32            /* neural-point feature width (decoder.py:122-125 fc_c input) */
@@ -229,6 +229,13 @@ int pnr_rays_from_uv(const float* i, const float* j, int64_t n, float fx, float 
 /* One Adam step over `n` float32 words: p -= lr * mhat / (sqrt(vhat) + eps).  step >= 1. */
 int pnr_adam_step(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1,
                   float beta2, float eps, int64_t step, void* stream);
+/* The same step with the step number read on the device: step = *step_count + 1, where
+ * step_count (int32, device) counts completed steps and is advanced by pnr_step_advance after the
+ * step's last Adam launch.  Host-free, so a captured graph (hipGraph / torch.cuda.CUDAGraph) of a
+ * whole mapping iteration replays with the right bias corrections. */
+int pnr_adam_step_dev(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1,
+                      float beta2, float eps, const int32_t* step_count, void* stream);
+int pnr_step_advance(int32_t* step_count, void* stream);
 
 /* ---- diagnostics (not on the reference API) ----------------------------------------------- */
 /* Kernel timing: while enabled, every launch of the timed kernels is bracketed by hipEvents on

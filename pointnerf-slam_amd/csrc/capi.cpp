@@ -41,6 +41,9 @@ int launch_get_rays(int, int, float, float, float, float, const float*, float*, 
 int launch_rays_from_uv(const float*, const float*, int64_t, float, float, float, float, const float*, float*,
                         float*, hipStream_t);
 int launch_adam(float*, const float*, float*, float*, int64_t, float, float, float, float, float, hipStream_t);
+int launch_adam_dev(float*, const float*, float*, float*, int64_t, float, float, float, float, const int32_t*,
+                    hipStream_t);
+int launch_step_advance(int32_t*, hipStream_t);
 
 }  // namespace pnr
 
@@ -759,6 +762,17 @@ int pnr_adam_step(float* p, const float* g, float* m, float* v, int64_t n, float
   const float step_size = (float)((double)lr / bc1);
   const float bc2_sqrt = (float)std::sqrt(bc2);
   return launch_adam(p, g, m, v, n, beta1, beta2, eps, step_size, bc2_sqrt, (hipStream_t)stream);
+}
+
+int pnr_adam_step_dev(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1, float beta2,
+                      float eps, const int32_t* step_count, void* stream) {
+  if (n < 0 || !step_count || (n > 0 && (!p || !g || !m || !v))) return PNR_E_ARG;
+  return launch_adam_dev(p, g, m, v, n, lr, beta1, beta2, eps, step_count, (hipStream_t)stream);
+}
+
+int pnr_step_advance(int32_t* step_count, void* stream) {
+  if (!step_count) return PNR_E_ARG;
+  return launch_step_advance(step_count, (hipStream_t)stream);
 }
 
 }  // extern "C"

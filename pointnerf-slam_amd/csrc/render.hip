@@ -380,6 +380,30 @@ __global__ void k_adam(float* __restrict__ p, const float* __restrict__ g, float
   p[i] = p[i] + (-step_size) * (mi / denom);
 }
 
+// the same with the step read on the device (*step_count + 1); the bias corrections follow
+// pnr_adam_step's host arithmetic (double pow, then float)
+__global__ void k_adam_dev(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                           float* __restrict__ v, int64_t n, float lr, float beta1, float beta2, float eps,
+                           const int32_t* __restrict__ step_count) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const double t = (double)(*step_count + 1);
+  const double bc1 = 1.0 - pow((double)beta1, t), bc2 = 1.0 - pow((double)beta2, t);
+  const float step_size = (float)((double)lr / bc1);
+  const float bc2_sqrt = (float)sqrt(bc2);
+  const float gi = g[i];
+  float mi = m[i];
+  mi = mi + (1.f - beta1) * (gi - mi);
+  float vi = v[i] * beta2 + (1.f - beta2) * gi * gi;
+  m[i] = mi;
+  v[i] = vi;
+  const float denom = sqrtf(vi) / bc2_sqrt + eps;
+  p[i] = p[i] + (-step_size) * (mi / denom);
+}
+__global__ void k_step_advance(int32_t* step_count) {
+  if (threadIdx.x == 0) atomicAdd(step_count, 1);
+}
+
 // ---------------------------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------------------------
@@ -461,6 +485,17 @@ int launch_rays_from_uv(const float* i, const float* j, int64_t n, float fx, flo
                         const float* c2w, float* ro, float* rd, hipStream_t st) {
   if (n <= 0) return 0;
   hipLaunchKernelGGL(k_rays_from_uv, dim3(nblk(n, 256)), dim3(256), 0, st, i, j, n, fx, fy, cx, cy, c2w, ro, rd);
+  return hip_status(hipGetLastError());
+}
+int launch_adam_dev(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1, float beta2,
+                    float eps, const int32_t* step_count, hipStream_t st) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(k_adam_dev, dim3(nblk(n, 256)), dim3(256), 0, st, p, g, m, v, n, lr, beta1, beta2, eps,
+                     step_count);
+  return hip_status(hipGetLastError());
+}
+int launch_step_advance(int32_t* step_count, hipStream_t st) {
+  hipLaunchKernelGGL(k_step_advance, dim3(1), dim3(64), 0, st, step_count);
   return hip_status(hipGetLastError());
 }
 int launch_adam(float* p, const float* g, float* m, float* v, int64_t n, float beta1, float beta2, float eps,

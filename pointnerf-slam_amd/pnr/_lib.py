@@ -98,6 +98,9 @@ _SIGS = {
                                         c_void_p, c_void_p, c_void_p]),
     'pnr_adam_step': (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_float, c_float, c_float,
                                      c_float, c_int64, c_void_p]),
+    'pnr_adam_step_dev': (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_float, c_float,
+                                         c_float, c_float, c_void_p, c_void_p]),
+    'pnr_step_advance': (ctypes.c_int, [c_void_p, c_void_p]),
     'pnr_points_index_bytes': (c_size_t, [c_int64, c_int32]),
     'pnr_points_build': (ctypes.c_int, [PPoints, c_void_p]),
     'pnr_point_gather_workspace_bytes': (c_size_t, [c_int64]),

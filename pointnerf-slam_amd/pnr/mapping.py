@@ -44,7 +44,9 @@ class FlatParams:
 
 class Adam:
     """torch.optim.Adam(lr, betas=(0.9, 0.999), eps=1e-8) over a FlatParams buffer, one launch per
-    learning-rate segment.  `segments` = [(first word, words, lr)], default the whole buffer."""
+    learning-rate segment.  `segments` = [(first word, words, lr)], default the whole buffer.
+    `use_device_step()` switches the step number to a device counter (pnr_adam_step_dev +
+    pnr_step_advance), so a step captured in a graph replays with the right bias corrections."""
 
     def __init__(self, flat: FlatParams, lr: float, betas=(0.9, 0.999), eps=1e-8, on_update=None, segments=None):
         self.flat = flat
@@ -56,6 +58,11 @@ class Adam:
         self.m = torch.zeros_like(flat.data)
         self.v = torch.zeros_like(flat.data)
         self.step_count = 0
+        self.step_dev = None  # int32 device counter of completed steps (graph mode)
+
+    def use_device_step(self):
+        if self.step_dev is None:
+            self.step_dev = torch.tensor([self.step_count], dtype=torch.int32, device=self.flat.data.device)
 
     def step(self):
         self.step_count += 1
@@ -63,9 +70,16 @@ class Adam:
         f = self.flat
         st = _lib.stream_of(f.data.device)
         for a, n, lr in self.segments:
-            _lib.check(lib.pnr_adam_step(_lib.ptr(f.data[a:]), _lib.ptr(f.grad[a:]), _lib.ptr(self.m[a:]),
-                                         _lib.ptr(self.v[a:]), n, lr, self.b1, self.b2, self.eps, self.step_count,
-                                         st), 'adam_step')
+            if self.step_dev is not None:
+                _lib.check(lib.pnr_adam_step_dev(_lib.ptr(f.data[a:]), _lib.ptr(f.grad[a:]), _lib.ptr(self.m[a:]),
+                                                 _lib.ptr(self.v[a:]), n, lr, self.b1, self.b2, self.eps,
+                                                 _lib.ptr(self.step_dev), st), 'adam_step_dev')
+            else:
+                _lib.check(lib.pnr_adam_step(_lib.ptr(f.data[a:]), _lib.ptr(f.grad[a:]), _lib.ptr(self.m[a:]),
+                                             _lib.ptr(self.v[a:]), n, lr, self.b1, self.b2, self.eps, self.step_count,
+                                             st), 'adam_step')
+        if self.step_dev is not None:
+            _lib.check(lib.pnr_step_advance(_lib.ptr(self.step_dev), st), 'step_advance')
         if self.on_update is not None:  # weights changed behind autograd: drop the packed image
             self.on_update()
 
@@ -101,8 +115,8 @@ class MapStep:
         r, dec = self.renderer, self.decoder
         dev = rays_o.device
         d, _, c = r.render_batch_ray(self.c, dec, rays_d, rays_o, dev, 'color', gt_depth, far_clamp=far_clamp)
-        m = gt_depth > 0
-        loss = torch.abs(gt_depth[m] - d[m]).sum()
+        m = gt_depth > 0  # a masked sum, not a masked gather: no host sync, so the step can be captured
+        loss = torch.where(m, torch.abs(gt_depth - d), torch.zeros_like(d)).sum()
         loss = loss + self.w_color * torch.abs(gt_color - c).sum()
         sigma = r.regulation(self.c, dec, rays_d, rays_o, gt_depth, dev, 'color', t_rand=t_rand)
         return loss + self.w_reg * torch.abs(sigma).sum()
@@ -117,3 +131,41 @@ class MapStep:
         self.opt.step()
         return loss.detach()
 
+
+
+class MapGraph:
+    """A MapStep captured once in a HIP graph (torch.cuda.CUDAGraph) and replayed per iteration.
+
+    The Mapper runs `mapping.iters` (60) iterations per keyframe on a fixed-size pixel batch
+    (1,000 rays under configs/pointNeRF_slam.yaml); at that size a step is ~130 launches whose host
+    overhead rivals the GPU time.  Replaying the captured step removes it.  The graph owns static
+    input buffers (rays, gt depth / colour and the regulation jitter t_rand): each call copies the
+    batch in, replays, and returns the loss tensor (overwritten by the next call).  Capture needs a
+    fixed batch shape, the single-GPU step (ddp=None) and Adam's device step counter
+    (`Adam.use_device_step`).  `warmup` ordinary steps run first on the given batch (torch requires
+    work on a side stream before a capture); they are real optimisation steps.
+    """
+
+    def __init__(self, mstep: MapStep, rays_o, rays_d, gt_depth, gt_color, t_rand, warmup=2):
+        if mstep.ddp is not None:
+            raise NotImplementedError('pnr.MapGraph: capture of the data-parallel step (RCCL) is not supported')
+        self.mstep = mstep
+        dev = rays_o.device
+        self.inputs = [t.detach().clone() for t in (rays_o, rays_d, gt_depth, gt_color, t_rand)]
+        mstep.opt.use_device_step()
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            for _ in range(warmup):
+                mstep(*self.inputs)
+        torch.cuda.current_stream(dev).wait_stream(side)
+        mstep._invalidate()  # the captured step starts with the weight repack
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.loss = mstep(*self.inputs)
+
+    def __call__(self, rays_o, rays_d, gt_depth, gt_color, t_rand):
+        for dst, src in zip(self.inputs, (rays_o, rays_d, gt_depth, gt_color, t_rand)):
+            dst.copy_(src, non_blocking=True)
+        self.graph.replay()
+        return self.loss

@@ -221,9 +221,14 @@ class Renderer(object):
 
     # -- helpers --------------------------------------------------------------------------------
     def _bound6(self):
-        b = self.bound
-        b = b.detach().cpu().double().reshape(3, 2) if isinstance(b, torch.Tensor) else torch.tensor(b).double()
-        return [float(v) for v in b.reshape(-1)]
+        # the bound is fixed per renderer (src/NICE_SLAM.py:208-213): read once, so a render issues no
+        # device-to-host copy (a graph capture of the mapping step forbids one)
+        if getattr(self, '_b6_src', None) is not self.bound:
+            self._b6_src = self.bound
+            b = self.bound
+            b = b.detach().cpu().double().reshape(3, 2) if isinstance(b, torch.Tensor) else torch.tensor(b).double()
+            self._b6 = [float(v) for v in b.reshape(-1)]
+        return self._b6
 
     def params(self, n_samples=None, n_importance=None):
         prm = _lib.RenderParams()

@@ -43,7 +43,7 @@ def test_python_binding_covers_header():
 
 def test_host_only_calls(lib):
     lib.pnr_abi_version.restype = ctypes.c_int
-    assert lib.pnr_abi_version() == 3
+    assert lib.pnr_abi_version() == 4
     lib.pnr_mlp_packed_floats.restype = ctypes.c_size_t
     # fp32 images 486,688 + bf16x3 / bf16 / f16x3 forward streams 229,376 / 118,784 / 229,376
     # + bf16x3 delta-chain stream 225,280 + raw table 2,048
@@ -86,6 +86,8 @@ def test_workspace_queries_and_arg_errors(lib):
     assert L.pnr_render_fwd(ctypes.byref(bad), None, None, None, None, 10, None, None, None, None, 0, None) == -1
     assert L.pnr_eval_points(None, None, 5, None, None, 0, None) == -1
     assert L.pnr_adam_step(None, None, None, None, 5, 1e-3, 0.9, 0.999, 1e-8, 0, None) == -1
+    assert L.pnr_adam_step_dev(None, None, None, None, 5, 1e-3, 0.9, 0.999, 1e-8, None, None) == -1
+    assert L.pnr_step_advance(None, None) == -1
     # zero-sized calls are no-ops
     assert L.pnr_eval_points(ctypes.c_void_p(1), None, 0, None, None, 0, None) == 0
 

@@ -64,7 +64,7 @@ def close(a, b, rtol, atol, what):
 
 def test_library_info(pnr_mod):
     lib = pnr_mod.library()
-    assert lib.pnr_abi_version() == 3
+    assert lib.pnr_abi_version() == 4
     assert lib.pnr_mlp_packed_floats() > 0
 
 
@@ -335,3 +335,50 @@ def test_track_frame_converges(pnr_mod, dev, scene):
     err = (best.cpu() - ct_true).abs().mean().item()
     assert err < err0
     assert c2w.shape == (4, 4)
+
+
+def test_map_graph_matches_eager(pnr_mod, dev, scene):
+    """pnr.mapping.MapGraph: the mapping iteration captured in a HIP graph and replayed gives the
+    same weights and losses as the same iterations run eagerly (device-step Adam in both)."""
+    from pnr.mapping import MapStep, MapGraph
+    params = golden_params('trained')
+    g = torch.Generator().manual_seed(5)
+    n = 1024
+    c2w = torch.from_numpy(scene['poses'][1]).float()
+    i = torch.randint(0, 1200, (n,), generator=g).float()
+    j = torch.randint(0, 680, (n,), generator=g).float()
+    ro, rd = pnr_mod.get_rays_from_uv(i.to(dev), j.to(dev), c2w.to(dev), 680, 1200, 600., 600., 599.5, 339.5, dev)
+    batches = []
+    for s in range(4):
+        gt = (torch.rand(n, generator=g) * 0.4 + 0.15).to(dev)
+        col = torch.rand((n, 3), generator=g).to(dev)
+        t_rand = torch.rand((n, 32), generator=g).to(dev)
+        batches.append((ro, rd, gt, col, t_rand))
+    runs = []
+    for graph in (False, True):
+        dec = make_decoder(pnr_mod, params, dev)
+        r = make_renderer(pnr_mod, scene)
+        ms = MapStep(r, dec, lr=2e-4, w_color_loss=0.05)
+        ms.opt.use_device_step()
+        losses = []
+        if graph:
+            mg = MapGraph(ms, *batches[0], warmup=2)  # two eager steps on batch 0, then the capture
+            for b in batches[1:]:
+                losses.append(float(mg(*b)))
+        else:
+            for _ in range(2):
+                ms(*batches[0])
+            for b in batches[1:]:
+                losses.append(float(ms(*b)))
+        torch.cuda.synchronize()
+        runs.append((losses, ms.flat.data.detach().cpu().clone(), int(ms.opt.step_dev.item())))
+    (l_e, w_e, s_e), (l_g, w_g, s_g) = runs
+    assert s_e == s_g == 5
+    close(np.array(l_g), np.array(l_e), 1e-5, 0, 'losses')
+    # the weight-gradient GEMMs flush with float atomics, so two runs (eager or replayed) differ in
+    # summation order; Adam normalises a near-zero gradient, so such an element may move by up to
+    # ~2 lr per step.  Bound both: 99.9% of the weights within 1e-5 rel, none beyond 5 x 2 lr.
+    d = (w_g - w_e).abs()
+    off = d > 1e-7 + 1e-5 * w_e.abs()
+    assert off.float().mean().item() < 1e-3, int(off.sum())
+    assert d.max().item() <= 5 * 2 * 2e-4
