@@ -146,10 +146,44 @@ __device__ __forceinline__ bool lt_nan(double a, double b) { return (a < b) || (
 __device__ __forceinline__ bool eq_nan(double a, double b) { return (a == b) || (a != a && b != b); }
 
 // Sort the S+I depths of ray n into ascending order; ord[q] = source index (< S: coarse).
+// torch.sort's order here is the stable one (coarse before importance on ties, NaN last).  The
+// coarse depths (near..far linspace) and the importance depths (inverse-cdf of increasing u) are
+// each non-decreasing unless far < near or a value is NaN: then a stable merge gives exactly that
+// order in O(S+I); otherwise the rank sort below does.
 __device__ void sort_ray(const double* zc, const double* zi, int S, int I, double (*zl)[64], uint8_t (*ord)[64],
                          int tid) {
   const int M = S + I;
-  for (int m = 0; m < M; ++m) zl[m][tid] = m < S ? zc[m] : zi[m - S];
+  bool sorted = true;
+  double prev = zc[0];
+  zl[0][tid] = prev;
+  sorted = prev == prev;
+  for (int m = 1; m < S; ++m) {
+    const double v = zc[m];
+    zl[m][tid] = v;
+    sorted = sorted && prev <= v;  // false for NaN
+    prev = v;
+  }
+  if (I > 0) {
+    prev = zi[0];
+    zl[S][tid] = prev;
+    sorted = sorted && prev == prev;
+    for (int k = 1; k < I; ++k) {
+      const double v = zi[k];
+      zl[S + k][tid] = v;
+      sorted = sorted && prev <= v;
+      prev = v;
+    }
+  }
+  if (sorted) {
+    int i = 0, k = 0;
+    for (int q = 0; q < M; ++q) {
+      const bool coarse = k >= I || (i < S && zl[i][tid] <= zl[S + k][tid]);
+      ord[q][tid] = (uint8_t)(coarse ? i : S + k);
+      i += coarse ? 1 : 0;
+      k += coarse ? 0 : 1;
+    }
+    return;
+  }
   for (int i = 0; i < M; ++i) {
     const double v = zl[i][tid];
     int r = 0;
