@@ -63,6 +63,13 @@ constexpr int64_t kBfFcBytes = 32LL * 4096;
 // f16 weight scales: inverse [5] (W0..W3, Wo) and forward [5]
 constexpr int kRawB = 0, kRawBo = 1024, kRawFB = 1056, kRawInv = 1344, kRawScl = 1352;
 constexpr int64_t kRawBytes = 8192;   // padded to 2 x 4 KiB (two DMA pieces)
+// then Wo [4][256] fp32: the VALU output layer of the kernels without the feature branch (one
+// more 4 KiB piece, loaded only by them: the feature-branch variant has no LDS left for it)
+constexpr int kRawWo = 2048;
+constexpr int64_t kRawWoBytes = 4096;
+constexpr int64_t kRawPackedBytes = kRawBytes + kRawWoBytes;
+// hidden steps (layer 0 + the three 256-wide layers); the feature-branch kernels add 8 output steps
+constexpr int kHidSteps = 27;
 // fc raw: bc_0..bc_3 [4][256], then the f16 scales of Wc_0..Wc_3: inverse [4], forward [4]
 constexpr int kFcRawInv = 1024, kFcRawScl = 1028;
 constexpr int64_t kFcRawBytes = 8192;
@@ -83,7 +90,7 @@ constexpr int64_t kOffBf1 = kOffBf2 + bf_main_bytes(2) / 4;
 constexpr int64_t kOffH2 = kOffBf1 + bf_main_bytes(1) / 4;
 constexpr int64_t kOffBwd = kOffH2 + bf_main_bytes(2) / 4;
 constexpr int64_t kOffRaw = kOffBwd + kBwdBytes / 4;
-constexpr int64_t kPackedFloatsAll = kOffRaw + kRawBytes / 4;
+constexpr int64_t kPackedFloatsAll = kOffRaw + kRawPackedBytes / 4;
 // fc buffer (floats): [fp32 fc image][BF16X3 fc][BF16 fc][F16X3 fc][BF16X3 fc bwd][raw]
 constexpr int64_t kOffFcBf2 = kFcPackedFloats;
 constexpr int64_t kOffFcBf1 = kOffFcBf2 + kBfFcBytes / 4;
@@ -124,11 +131,14 @@ struct BfGeo {
   static constexpr int kSlot = kMainH + (HASC ? 4096 : 0);   // LDS slot bytes
   static constexpr int kNbuf = NP == 2 ? 4 : 6;
   static constexpr int kDist = kNbuf - 1;                    // steps in flight
-  static constexpr int kRawLds = kRawBytes + (HASC ? kFcRawBytes : 0);
+  static constexpr int kRawLds = kRawBytes + (HASC ? kFcRawBytes : kRawWoBytes);
   static constexpr int kLds = kNbuf * kSlot + kRawLds;
+  // steps of the DMA / MFMA program: without the feature branch the output layer runs on the VALU
+  // after the hidden steps (BfFwd::out_layer)
+  static constexpr int kSteps = HASC ? kBfSteps : kHidSteps;
   __host__ __device__ static constexpr int main_n(int g) { return g < 27 ? kMainH / 4096 : 1; }
   __host__ __device__ static constexpr int fc_n(int g) { return (HASC && g >= 2 && g <= 33) ? 1 : 0; }
-  __host__ __device__ static constexpr int n_glds(int g) { return g < kBfSteps ? main_n(g) + fc_n(g) : 0; }
+  __host__ __device__ static constexpr int n_glds(int g) { return g < kSteps ? main_n(g) + fc_n(g) : 0; }
   __host__ __device__ static constexpr int64_t main_off(int g) {
     return g <= 27 ? (int64_t)g * kMainH : 27LL * kMainH + (int64_t)(g - 27) * 4096;
   }
@@ -258,7 +268,7 @@ struct BfFwd {
   // issue the DMA of step g into its ring slot (wave-uniform, lane-linear 4 KiB pieces)
   template <int g>
   static __device__ __forceinline__ void stage_step(const BfFwdArgs& a, const char* lds) {
-    if constexpr (g < kBfSteps) {
+    if constexpr (g < G::kSteps) {
       const int w = wave_id(), lane = threadIdx.x & 63;
       const uint32_t slot = lds_addr(reinterpret_cast<const float*>(lds + (g % G::kNbuf) * G::kSlot)) + w * 1024;
       const char* src = a.wmain + G::main_off(g) + w * 1024 + lane * 16;
@@ -400,7 +410,7 @@ struct BfFwd {
   // VMEM ops issued after DMA(i) and before the wait of barrier B_i (i >= 1, in step i-1)
   __host__ __device__ static constexpr int younger_b(int i) {
     int n = 0;
-    for (int j = i + 1; j <= i + kD - 1 && j < kBfSteps; ++j) n += G::n_glds(j);
+    for (int j = i + 1; j <= i + kD - 1 && j < G::kSteps; ++j) n += G::n_glds(j);
     if (SAVE) {
       int first = 0;  // first step whose stores all follow the DMA
       if (i >= kD && i - kD >= 1) {
@@ -478,7 +488,7 @@ struct BfFwd {
       // feature-branch product, one group before its consumers (conv2 from group 4 on)
       if constexpr (HASC && CONV && T == clamp_t(3, g)) mfma_frag<PR, true>(S.FC, S.ct, S.f);
       if constexpr (CONV) conv_pieces<CL, CT, SET, SHIFT, NT, T>(a, S, lds);
-      if constexpr (g + 1 < kBfSteps) {
+      if constexpr (g + 1 < G::kSteps) {
         if constexpr (T == sync_t(g)) {
           PNR_TICK(3 + g);
 #if defined(PNR_EXP_NODMA)
@@ -500,7 +510,7 @@ struct BfFwd {
 
   template <int g>
   static __device__ __forceinline__ void step(const BfFwdArgs& a, St& S, const char* lds) {
-    if constexpr (g < kBfSteps) {
+    if constexpr (g < G::kSteps) {
       // both accumulator sets live in the 256 AGPRs for the whole kernel; out / f stay in VGPRs
 #pragma unroll
       for (int st = 0; st < 2; ++st)
@@ -546,6 +556,56 @@ struct BfFwd {
     next_frag<0, 2>(S, lds);
     next_consts<0>(S, lds);
   }
+
+  // ---- output layer on the VALU (no feature branch) ------------------------------------------
+  // out[i] (+)= sum over this lane's 16 units of h4 tile t of Wo[i][u] h4[u] (fp32 FMAs; Wo fp32
+  // in LDS after the main raw table).  Units of register r: 32 t + perm(r, hh).
+  template <int t>
+  static __device__ __forceinline__ void out_dot(const St& S, const char* lds, float (&o)[4]) {
+    const int hh = (threadIdx.x >> 5) & 1;
+    const float* wo = raw_lds(lds) + kRawBytes / 4;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float4 w = *reinterpret_cast<const float4*>(wo + i * kHidden + 32 * t + 8 * q + 4 * hh);
+        o[i] = __builtin_fmaf(w.x, S.v[4 * q + 0], o[i]);
+        o[i] = __builtin_fmaf(w.y, S.v[4 * q + 1], o[i]);
+        o[i] = __builtin_fmaf(w.z, S.v[4 * q + 2], o[i]);
+        o[i] = __builtin_fmaf(w.w, S.v[4 * q + 3], o[i]);
+      }
+  }
+  // h4 tile t: bias + ReLU (+ mask bits, f16 save), then its share of the output layer
+  template <int t>
+  static __device__ __forceinline__ void out_tile(const BfFwdArgs& a, St& S, const char* lds, float (&o)[4]) {
+    if constexpr (t < 8) {
+      if constexpr (t > 0) {  // tile 0 was converted by the last hidden step (S.v holds it)
+        preload<3, t>(S, lds);
+        conv1<3, t, 0>(a, S, S.acc[1][t], lds);
+        conv1<3, t, 1>(a, S, S.acc[1][t], lds);
+        conv1<3, t, 2>(a, S, S.acc[1][t], lds);
+        conv1<3, t, 3>(a, S, S.acc[1][t], lds);
+        if constexpr (SAVE) {
+          const int hh = (threadIdx.x >> 5) & 1;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            f16x4 hv = {(_Float16)S.v[4 * q], (_Float16)S.v[4 * q + 1], (_Float16)S.v[4 * q + 2],
+                        (_Float16)S.v[4 * q + 3]};
+            *reinterpret_cast<f16x4*>(reinterpret_cast<_Float16*>(a.save.hP) +
+                                      ((int64_t)3 * a.save.ld + S.col) * kHidden + 32 * t + 8 * q + 4 * hh) = hv;
+          }
+        }
+      }
+      out_dot<t>(S, lds, o);
+      out_tile<t + 1>(a, S, lds, o);
+    }
+  }
+  static __device__ __forceinline__ void out_layer(const BfFwdArgs& a, St& S, const char* lds, float (&o)[4]) {
+    o[0] = o[1] = o[2] = o[3] = 0.f;
+    out_tile<0>(a, S, lds, o);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) o[i] += __shfl_xor(o[i], 32);  // the other lane half's 128 units
+  }
 };
 
 template <int PR, bool HASC, bool SAVE>
@@ -567,6 +627,8 @@ __global__ __launch_bounds__(256, 1) void k_mlp_fwd16(BfFwdArgs a, int mode) {
       for (int i = 0; i < (int)(kFcRawBytes / 4096); ++i)
         glds16(reinterpret_cast<const float*>(a.fcraw + i * 4096 + w * 1024 + lane * 16),
                rbase + kRawBytes + i * 4096);
+    } else {  // Wo for the VALU output layer
+      glds16(reinterpret_cast<const float*>(a.raw + kRawBytes + w * 1024 + lane * 16), rbase + kRawBytes);
     }
   }
   PNR_TICK(0);
@@ -644,15 +706,20 @@ __global__ __launch_bounds__(256, 1) void k_mlp_fwd16(BfFwdArgs a, int mode) {
                 "vmcnt range");
   K::start(a, S, lds);
   K::template step<0>(a, S, lds);
+  float o[4];
+  if constexpr (HASC) {  // output layer = the last 8 MFMA steps, scaled accumulator
+    const float inv = Prec<PR>::F16 ? K::raw_lds(lds)[kRawInv + 4] : 1.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) o[i] = Prec<PR>::F16 ? S.out[i] * inv : S.out[i];
+  } else {
+    K::out_layer(a, S, lds, o);
+  }
   PNR_TICK(40);
 
   if (S.valid && hh == 0) {
-    const float* rawl = K::raw_lds(lds);
-    const float* bo = rawl + kRawBo;
-    const float inv = Prec<PR>::F16 ? rawl[kRawInv + 4] : 1.f;
-    float o[4];
+    const float* bo = K::raw_lds(lds) + kRawBo;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) o[i] = (Prec<PR>::F16 ? S.out[i] * inv : S.out[i]) + bo[i];
+    for (int i = 0; i < 4; ++i) o[i] += bo[i];
     reinterpret_cast<float4*>(a.raw_out)[p] = make_float4(o[0], o[1], o[2], S.inside ? o[3] : 100.f);
   }
 }

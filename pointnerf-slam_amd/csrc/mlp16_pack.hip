@@ -105,6 +105,10 @@ __global__ void k_pack16(RawParams rp, uint16_t* __restrict__ bf2, uint16_t* __r
     return;
   }
   const int64_t ri = idx - 2 * n2 - n1;
+  if (ri >= kRawWo && ri < kRawWo + 4 * kHidden) {  // Wo fp32 (the VALU output layer)
+    raw[ri] = rp.p[9][ri - kRawWo];
+    return;
+  }
   if (ri < kRawInv) {
     float v = 0.f;
     const int i = (int)ri;
@@ -164,7 +168,7 @@ int launch_pack_bf(const RawParams& rp, float* packed, hipStream_t st) {
   sa.inv = raw + kRawInv;
   sa.scl = raw + kRawScl;
   hipLaunchKernelGGL(k_wscale, dim3(5), dim3(1024), 0, st, sa);
-  const int64_t n = 2 * (bf_main_bytes(2) / 2) + bf_main_bytes(1) / 2 + kRawInv;
+  const int64_t n = 2 * (bf_main_bytes(2) / 2) + bf_main_bytes(1) / 2 + kRawWo + 4 * kHidden;
   const int threads = 256;
   hipLaunchKernelGGL(k_pack16, dim3((unsigned)((n + threads - 1) / threads)), dim3(threads), 0, st, rp,
                      reinterpret_cast<uint16_t*>(packed + kOffBf2), reinterpret_cast<uint16_t*>(packed + kOffBf1),
