@@ -167,7 +167,8 @@ struct BwdWS {
   float* g_nrm;   // [N]
   float* dP;      // [4][C][256]
   float* gargP;   // [C][96]
-  float* gH;      // [4][C][256]  features only: dL/dh_l
+  float* gH;      // [4][C][256]  features only: dL/dh_l (split precisions: f16 * 2^e)
+  void* c16;      // [C][32]      features only, split precisions: f16 copy of the chunk's c rows
   float* g_c;     // [P][32]      features only: dL/dc
   void* gws;      // features only: gather-backward work list
   size_t gws_bytes;
@@ -188,6 +189,7 @@ BwdWS carve_bwd(int64_t P, int64_t n, void* ws, size_t* bytes, bool feat = false
   b.gargP = c.take<float>(kFourierPad * b.C);
   if (feat) {
     b.gH = c.take<float>((size_t)4 * kHidden * b.C);
+    b.c16 = c.take<char>((size_t)kCDim * 2 * b.C);
     b.g_c = c.take<float>((size_t)P * kCDim);
     b.gws_bytes = gather_workspace_bytes(P);
     b.gws = c.take<char>(b.gws_bytes);
@@ -268,10 +270,17 @@ int mlp_backward_core(int prec, const float* packed, const SaveArgs& sv, int64_t
                               grads[0], kFourier, nullptr, st);
     if (rc) return rc;
     // feature branch: dWc_l (256x32) += (dL/dh_l)^T c ; dbc_l += colsum(dL/dh_l)
-    if (fb && fb->g_fc)
+    if (fb && fb->g_fc && split) {  // f16 operands: gH * 2^e from k_mlp_bwd16, an f16 copy of c
+      rc = launch_to_f16(fb->c + p0 * kCDim, b.c16, C * kCDim, st);
+      const _Float16* g16 = reinterpret_cast<const _Float16*>(b.gH);
+      for (int l = 0; l < 4 && rc == 0; ++l)
+        rc = launch_wgrad16(kWgradFc, g16 + l * dstride, b.c16, C, fb->g_fc[2 * l], kCDim, fb->g_fc[2 * l + 1],
+                            b.gmax, st);
+    } else if (fb && fb->g_fc) {
       for (int l = 0; l < 4 && rc == 0; ++l)
         rc = launch_wgrad(kWgradFc, b.gH + l * dstride, kHidden, fb->c + p0 * kCDim, kCDim, C, fb->g_fc[2 * l], kCDim,
                           fb->g_fc[2 * l + 1], st);
+    }
     if (rc) return rc;
   }
   return hip_status(hipGetLastError());

@@ -79,9 +79,11 @@ struct BfBwd {
     constexpr int li = 3 - CC;
 #pragma unroll
     for (int i = 0; i < 4; ++i) S.v[4 * q + i] = S.acc[CC & 1][t][4 * q + i];
-    if constexpr (HASC) {
-      *reinterpret_cast<float4*>(a.gH + ((int64_t)li * a.ld_d + S.dcol) * kHidden + 32 * t + 8 * q + 4 * hh) =
-          make_float4(S.v[4 * q], S.v[4 * q + 1], S.v[4 * q + 2], S.v[4 * q + 3]);
+    if constexpr (HASC) {  // f16 dL/dh * 2^e (the delta scale) for dWc = gH^T c (wgrad16.hip)
+      f16x4 gv = {(_Float16)(S.v[4 * q] * S.dscale), (_Float16)(S.v[4 * q + 1] * S.dscale),
+                  (_Float16)(S.v[4 * q + 2] * S.dscale), (_Float16)(S.v[4 * q + 3] * S.dscale)};
+      *reinterpret_cast<f16x4*>(reinterpret_cast<_Float16*>(a.gH) + ((int64_t)li * a.ld_d + S.dcol) * kHidden +
+                                32 * t + 8 * q + 4 * hh) = gv;
       split_quad<PR>(S.v + 4 * q, q, S.tmp);
     }
   }

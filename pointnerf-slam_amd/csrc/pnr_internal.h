@@ -227,11 +227,13 @@ int launch_gather_bwd(const pnr_points& pts, const PointSrc* src, int mode, cons
 enum WgradKind : int { kWgradHidden = 0, kWgradFirst = 1, kWgradOut = 2, kWgradFourier = 3, kWgradFc = 4 };
 int launch_wgrad(int kind, const float* A, int ma, const float* B, int nb, int64_t K, float* C, int64_t ldc,
                  float* bias, hipStream_t st);
-// split precisions (wgrad16.hip): kWgradHidden / kWgradFirst on f16 operands (A = deltas scaled by
-// delta_scale(*gmax), B = f16 activations), and dWo from fp32 g_out and f16 h4
+// split precisions (wgrad16.hip): kWgradHidden / kWgradFirst / kWgradFc on f16 operands (A = deltas
+// or dL/dh scaled by delta_scale(*gmax), B = f16 activations / features), and dWo from fp32 g_out
+// and f16 h4
 int launch_wgrad16(int kind, const void* A, const void* B, int64_t K, float* C, int64_t ldc, float* bias,
                    const uint32_t* gmax, hipStream_t st);
 int launch_wgrad_out16(const float* g_out, const void* h4, int64_t K, float* C, float* bias, hipStream_t st);
+int launch_to_f16(const float* x, void* y, int64_t n, hipStream_t st);
 int launch_wgrad_fourier16(const float4* xP, const void* garg, int64_t K, float* C, const uint32_t* gmax,
                            hipStream_t st);
 

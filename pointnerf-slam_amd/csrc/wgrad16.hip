@@ -34,7 +34,9 @@ constexpr int kTileB = 2112;  // bytes of one [32 points][64 B] block, +64 B pad
 template <int NTB, int WB>
 struct Wg16 {
   static constexpr int kThreads = 512;                     // 8 waves, 2 per SIMD
-  static constexpr int kTB = NTB == 3 ? 4 : NTB;           // B blocks staged (dW0: 4, one duplicate)
+  // B blocks staged: a multiple of 4 so every wave issues the same DMA pieces (dW0: 4 with one
+  // duplicate, dWc: 4 with three duplicates of the one 32-column block)
+  static constexpr int kTB = NTB < 4 ? 4 : NTB;
   static constexpr int kImgA = 8 * kTileB;
   static constexpr int kSlot = kImgA + kTB * kTileB;
   static constexpr int kNbuf = 4, kDist = kNbuf - 1;
@@ -163,7 +165,8 @@ static int launch_k(const Wg16Args& a, hipStream_t st) {
   return hip_status(hipGetLastError());
 }
 
-// kind: kWgradHidden (B [K][256]) or kWgradFirst (B [K][96], 93 columns); K is rounded up to 32
+// kind: kWgradHidden (B [K][256]), kWgradFirst (B [K][96], 93 columns) or kWgradFc (B [K][32]);
+// K is rounded up to 32
 // (the rows up to it exist and carry zero deltas)
 int launch_wgrad16(int kind, const void* A, const void* B, int64_t K, float* C, int64_t ldc, float* bias,
                    const uint32_t* gmax, hipStream_t st) {
@@ -179,6 +182,10 @@ int launch_wgrad16(int kind, const void* A, const void* B, int64_t K, float* C, 
   Wg16Args a{static_cast<const _Float16*>(A), static_cast<const _Float16*>(B), 256, K, ks, C, ldc, bias, gmax};
   TimingScope ts(kTimeWgrad, K, st);
   if (kind == kWgradHidden) return launch_k<8, 256>(a, st);
+  if (kind == kWgradFc) {  // dWc_l (256 x 32) += gH_l^T c : B = f16 copy of the features [K][32]
+    a.nb = kCDim;
+    return launch_k<1, 32>(a, st);
+  }
   if (kind == kWgradFirst) {
     a.nb = kFourier;
     return launch_k<3, 96>(a, st);
@@ -258,6 +265,19 @@ __global__ __launch_bounds__(256) void k_wgrad_skinny16(const float4* __restrict
     if (m < M) atomicAdd(C + (int64_t)m * ldc + n, red[m][n] * inv);
   }
   if (bias && tid < M) atomicAdd(bias + tid, red[tid][256 + 4]);
+}
+
+// f16 copy of n floats (the per-point features c, the B operand of dWc)
+__global__ void k_to_f16(const float* __restrict__ x, _Float16* __restrict__ y, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    y[i] = (_Float16)x[i];
+}
+int launch_to_f16(const float* x, void* y, int64_t n, hipStream_t st) {
+  if (n <= 0) return 0;
+  int64_t blocks = (n + 1023) / 1024;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(k_to_f16, dim3((unsigned)blocks), dim3(256), 0, st, x, static_cast<_Float16*>(y), n);
+  return hip_status(hipGetLastError());
 }
 
 // dWo (4 x 256) += g_out^T h4 (f16), dbo += colsum(g_out)
