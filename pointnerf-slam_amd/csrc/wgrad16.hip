@@ -221,26 +221,31 @@ __global__ __launch_bounds__(256) void k_wgrad_skinny16(const float4* __restrict
     for (int j = 0; j < 8; ++j) acc[m][j] = 0.f;
   float bs[4] = {0.f, 0.f, 0.f, 0.f};
   if (act) {
-    for (int64_t k = kb + r; k < ke; k += 2 * RPI) {
-      const bool two = k + RPI < ke;
-      const float4 a0 = A[k];
-      const h8 b0 = *reinterpret_cast<const h8*>(B + k * WB + 8 * c);
-      float4 a1 = make_float4(0.f, 0.f, 0.f, 0.f);
-      h8 b1 = b0;
-      if (two) {
-        a1 = A[k + RPI];
-        b1 = *reinterpret_cast<const h8*>(B + (k + RPI) * WB + 8 * c);
+    constexpr int U = 4;  // rows in flight per thread (HBM latency: bytes in flight per CU)
+    for (int64_t k = kb + r; k < ke; k += U * RPI) {
+      float4 av[U];
+      h8 bv[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t ku = k + u * RPI;
+        const int64_t kc = ku < ke ? ku : k;  // rows past the range: re-read row k, weighted 0
+        av[u] = A[kc];
+        bv[u] = *reinterpret_cast<const h8*>(B + kc * WB + 8 * c);
+        if (ku >= ke) av[u] = make_float4(0.f, 0.f, 0.f, 0.f);
       }
-      const float av0[4] = {a0.x, a0.y, a0.z, a0.w}, av1[4] = {a1.x, a1.y, a1.z, a1.w};
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float x0 = (float)b0[j], x1 = two ? (float)b1[j] : 0.f;
+      for (int u = 0; u < U; ++u) {
+        const float a4[4] = {av[u].x, av[u].y, av[u].z, av[u].w};
 #pragma unroll
-        for (int m = 0; m < 4; ++m) acc[m][j] = __builtin_fmaf(av1[m], x1, __builtin_fmaf(av0[m], x0, acc[m][j]));
-      }
-      if (c == 0) {
+        for (int j = 0; j < 8; ++j) {
+          const float x = (float)bv[u][j];
 #pragma unroll
-        for (int m = 0; m < 4; ++m) bs[m] += av0[m] + av1[m];
+          for (int m = 0; m < 4; ++m) acc[m][j] = __builtin_fmaf(a4[m], x, acc[m][j]);
+        }
+        if (c == 0) {
+#pragma unroll
+          for (int m = 0; m < 4; ++m) bs[m] += a4[m];
+        }
       }
     }
   }
