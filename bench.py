@@ -332,8 +332,11 @@ def main():
         if launches == 0 or name not in ('mlp_fwd', 'mlp_bwd'):
             continue
         fl = FLOP_PER_POINT_FWD if name == 'mlp_fwd' else FLOP_PER_POINT_BWD
-        kprec = prec if name == 'mlp_fwd' else 'fp32'  # the delta chain is fp32 in every mode
-        cand = {'kernel': ('k_mlp_fwd16' if prec != 'fp32' else 'k_mlp_fwd') if name == 'mlp_fwd' else 'k_mlp_bwd',
+        # the delta chain is fp32 in the fp32 mode and the bf16x3 split in every other mode
+        kprec = prec if name == 'mlp_fwd' else ('fp32' if prec == 'fp32' else 'bf16x3')
+        kname = ('k_mlp_fwd16' if prec != 'fp32' else 'k_mlp_fwd') if name == 'mlp_fwd' else \
+            ('k_mlp_bwd16' if prec != 'fp32' else 'k_mlp_bwd')
+        cand = {'kernel': kname,
                 'launches': launches, 'prec': kprec, 'peak': ALGO_PEAK_TF[kprec],
                 'avg_ms': ms / launches, 'share_of_step': ms / (el * 1e3), 'units': units / launches,
                 'achieved': fl * units / launches / (ms / launches * 1e-3) / 1e12}
@@ -341,7 +344,8 @@ def main():
             best = dict(cand, _ms=ms)
     roofline = None
     if best is not None:
-        tkey = {'k_mlp_fwd': 'k_mlp_fwd_train', 'k_mlp_fwd16': 'k_mlp_fwd16_train', 'k_mlp_bwd': 'k_mlp_bwd'}
+        tkey = {'k_mlp_fwd': 'k_mlp_fwd_train', 'k_mlp_fwd16': 'k_mlp_fwd16_train', 'k_mlp_bwd': 'k_mlp_bwd',
+                'k_mlp_bwd16': 'k_mlp_bwd16'}
         traffic = pmc_traffic(tkey[best['kernel']], best['units']) if args.workload == 'map' else None
         roofline = {'bound': 'mfma', 'achieved': round(best['achieved'], 2), 'peak': round(best['peak'], 1),
                     'unit': 'TFLOP/s', 'frac': round(best['achieved'] / best['peak'], 4), 'traffic': traffic,

@@ -21,22 +21,23 @@ __global__ __launch_bounds__(1024) void k_wscale(ScaleArgs a) {
   __shared__ float red[16];
   const float* w = a.w[blockIdx.x];
   const int n = a.n[blockIdx.x];
+  const int nt = blockDim.x, nw = nt >> 6;  // any multiple of 64 up to 1024
   float m0 = 0.f, m1 = 0.f, m2 = 0.f, m3 = 0.f;  // 4 loads in flight per thread
   int i = threadIdx.x;
-  for (; i + 3 * 1024 < n; i += 4 * 1024) {
+  for (; i + 3 * nt < n; i += 4 * nt) {
     m0 = fmaxf(m0, fabsf(w[i]));
-    m1 = fmaxf(m1, fabsf(w[i + 1024]));
-    m2 = fmaxf(m2, fabsf(w[i + 2048]));
-    m3 = fmaxf(m3, fabsf(w[i + 3072]));
+    m1 = fmaxf(m1, fabsf(w[i + nt]));
+    m2 = fmaxf(m2, fabsf(w[i + 2 * nt]));
+    m3 = fmaxf(m3, fabsf(w[i + 3 * nt]));
   }
-  for (; i < n; i += 1024) m0 = fmaxf(m0, fabsf(w[i]));
+  for (; i < n; i += nt) m0 = fmaxf(m0, fabsf(w[i]));
   float m = fmaxf(fmaxf(m0, m1), fmaxf(m2, m3));
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
   __syncthreads();
   if (threadIdx.x == 0) {
-    for (int k = 1; k < 16; ++k) red[0] = fmaxf(red[0], red[k]);
+    for (int k = 1; k < nw; ++k) red[0] = fmaxf(red[0], red[k]);
     int e = 20;
     if (red[0] > 0.f) {
       int ex;
@@ -238,7 +239,7 @@ int launch_fc_pack_bf(const float* const* fcp, float* out, hipStream_t st) {
   }
   sa.inv = raw + kFcRawInv;
   sa.scl = raw + kFcRawScl;
-  hipLaunchKernelGGL(k_wscale, dim3(4), dim3(256), 0, st, sa);
+  hipLaunchKernelGGL(k_wscale, dim3(4), dim3(1024), 0, st, sa);
   const int64_t n = 3 * (kBfFcBytes / 2) + kFcRawInv;
   const int threads = 256;
   hipLaunchKernelGGL(k_fc_pack16, dim3((unsigned)((n + threads - 1) / threads)), dim3(threads), 0, st, r,

@@ -477,27 +477,21 @@ union SearchLds {
   } f;
 };
 
+// One search round of a block: thread tid searches work item `wk` (x, y, z, row bits) when `has`;
+// block-uniform call (it holds barriers).
 template <int KER>
-__global__ __launch_bounds__(kSearchBlock) void k_gather_search(GatherArgs a) {
+__device__ __forceinline__ void search_round(const GatherArgs& a, SearchLds& L, const float4 wk, const bool has) {
   PNR_FP_STRICT
-  __shared__ SearchLds L;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, gq = lane >> 3, q = lane & 7;
   const double kInf = __longlong_as_double(0x7FF0000000000000ll);
-  const int64_t nchunk = (a.wl.cap + kSearchBlock - 1) / kSearchBlock;
-  for (int64_t task = blockIdx.x; task < kLists * nchunk; task += gridDim.x) {
-    const int r = (int)(task % kLists);
-    const int64_t j0 = task / kLists * kSearchBlock;
-    const int64_t n_work = (int64_t)a.wl.cnt[r * 32];
-    if (j0 >= n_work) continue;  // uniform over the block
-    const int64_t i = j0 + tid;
+  {
     double key[PNR_MAX_K];
 #pragma unroll
     for (int t = 0; t < PNR_MAX_K; ++t) key[t] = kInf;
     float x0 = 0.f, x1 = 0.f, x2 = 0.f;
     int row = -1, bx = 0, by = 0, bz = 0, nr = 0;
     __syncthreads();  // the previous task's feature phase is done with the LDS
-    if (i < n_work) {
-      const float4 wk = a.wl.items[r * a.wl.cap + i];
+    if (has) {
       x0 = wk.x; x1 = wk.y; x2 = wk.z;
       row = __float_as_int(wk.w);
       base_cell(x0, a.g.o0, a.g.inv, bx);
@@ -646,6 +640,23 @@ __global__ __launch_bounds__(kSearchBlock) void k_gather_search(GatherArgs a) {
   }
 }
 
+// Pass 2: persistent blocks over the probe's work list, one search round per 256-item chunk.
+template <int KER>
+__global__ __launch_bounds__(kSearchBlock) void k_gather_search(GatherArgs a) {
+  __shared__ SearchLds L;
+  const int64_t nchunk = (a.wl.cap + kSearchBlock - 1) / kSearchBlock;
+  for (int64_t task = blockIdx.x; task < kLists * nchunk; task += gridDim.x) {
+    const int r = (int)(task % kLists);
+    const int64_t j0 = task / kLists * kSearchBlock;
+    const int64_t n_work = (int64_t)a.wl.cnt[r * 32];
+    if (j0 >= n_work) continue;  // uniform over the block
+    const int64_t i = j0 + threadIdx.x;
+    const bool has = i < n_work;
+    const float4 wk = has ? a.wl.items[r * a.wl.cap + i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    search_round<KER>(a, L, wk, has);
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 // Backward
 // ---------------------------------------------------------------------------------------------
@@ -687,8 +698,19 @@ __global__ __launch_bounds__(256) void k_gather_bwd(GatherBwdArgs a) {
     const int64_t n_work = (int64_t)a.wl.cnt[rl * 32];
     if (j0 >= n_work) continue;  // uniform over the block
     const int64_t jn = n_work - j0 < 256 ? n_work - j0 : 256;
+    // half-wave `half` takes 32 consecutive items: rows of one ray, whose neighbour lists overlap.
+    // A neighbour shared with the previous row carries its partial sum forward instead of being
+    // flushed: the atomic goes out when it leaves the list (or at the end of the run).
+    int pid[PNR_MAX_K];
+    float pacc[PNR_MAX_K];
+#pragma unroll
+    for (int kk = 0; kk < PNR_MAX_K; ++kk) {
+      pid[kk] = -1;
+      pacc[kk] = 0.f;
+    }
+    const int64_t te = 32 * half + 32 < jn ? 32 * half + 32 : jn;
 #pragma unroll 1
-    for (int64_t t = half; t < jn; t += 8) {  // uniform over each half-wave
+    for (int64_t t = 32 * half; t < te; ++t) {  // uniform over each half-wave
       const int64_t p = __float_as_int(a.wl.items[rl * a.wl.cap + j0 + t].w);
       // every load of the row issued at once: g_c / c rows, the k (index, weight) pairs (broadcast
       // within the half-wave), then the k feature rows and atomics predicated, no dependent branches
@@ -729,9 +751,25 @@ __global__ __launch_bounds__(256) void k_gather_bwd(GatherBwdArgs a) {
         for (int kk = 0; kk < PNR_MAX_K; ++kk) dots[kk] = g * f[kk];
       }
       if (a.g_feats) {
+        float cur[PNR_MAX_K];
 #pragma unroll
-        for (int kk = 0; kk < PNR_MAX_K; ++kk)
-          if (id[kk] >= 0) unsafeAtomicAdd(a.g_feats + (int64_t)id[kk] * 32 + ch, wn[kk] * g);
+        for (int kk = 0; kk < PNR_MAX_K; ++kk) cur[kk] = id[kk] >= 0 ? wn[kk] * g : 0.f;
+#pragma unroll
+        for (int j = 0; j < PNR_MAX_K; ++j) {  // ids within a row are distinct: at most one match
+          bool kept = false;
+#pragma unroll
+          for (int kk = 0; kk < PNR_MAX_K; ++kk) {
+            const bool mt = pid[j] >= 0 && id[kk] == pid[j];
+            cur[kk] += mt ? pacc[j] : 0.f;
+            kept = kept || mt;
+          }
+          if (pid[j] >= 0 && !kept) unsafeAtomicAdd(a.g_feats + (int64_t)pid[j] * 32 + ch, pacc[j]);
+        }
+#pragma unroll
+        for (int kk = 0; kk < PNR_MAX_K; ++kk) {
+          pid[kk] = id[kk];
+          pacc[kk] = cur[kk];
+        }
       }
       if (!a.g_p) continue;
       float gcd = g * cc;
@@ -771,6 +809,11 @@ __global__ __launch_bounds__(256) void k_gather_bwd(GatherBwdArgs a) {
       } else {
         o[0] = gp0; o[1] = gp1; o[2] = gp2;
       }
+    }
+    if (a.g_feats) {
+#pragma unroll
+      for (int j = 0; j < PNR_MAX_K; ++j)
+        if (pid[j] >= 0) unsafeAtomicAdd(a.g_feats + (int64_t)pid[j] * 32 + ch, pacc[j]);
     }
   }
 }

@@ -95,6 +95,35 @@ def test_gather_idw_matches_oracle(pnr_mod, dev, k):
     close(c, c_ref, 1e-5 * c_ref.abs().max().item(), 'c')
 
 
+def test_gather_many_tasks_per_block(pnr_mod, dev):
+    """2M samples: every persistent search block walks many work-list chunks of several
+    sub-lists. A random subset of rows is checked against the oracle (rows are independent)."""
+    import ctypes
+    lib = pnr_mod.library()
+    xyz, feats, _ = random_cloud(seed=11)
+    gen = torch.Generator().manual_seed(12)
+    P = 2_000_000
+    q = (xyz[torch.randint(0, xyz.shape[0], (P,), generator=gen)] + 0.08 * torch.randn((P, 3), generator=gen)).double()
+    pts = pnr_mod.NeuralPoints(xyz.to(dev), feats.to(dev), mode='idw', radius=0.03, k=8).to(dev)
+    s, _ = pts.descriptor()
+    qd = q.to(dev)
+    ws = torch.empty(lib.pnr_point_gather_workspace_bytes(P), dtype=torch.uint8, device=dev)
+    c = torch.full((P, 32), float('nan'), device=dev)
+    idx = torch.full((P, 8), -7, device=dev, dtype=torch.int32)
+    w = torch.full((P, 8), float('nan'), device=dev)
+    assert lib.pnr_point_gather(ctypes.byref(s), qd.data_ptr(), P, c.data_ptr(), idx.data_ptr(), w.data_ptr(),
+                                ws.data_ptr(), ws.numel(), None) == 0
+    torch.cuda.synchronize()
+    assert not torch.isnan(c).any() and not torch.isnan(w).any() and not (idx == -7).any(), 'every row written'
+    frac = (idx[:, 0] >= 0).float().mean().item()
+    assert 0.05 < frac < 0.95, f'a mix of samples with and without neighbours ({frac:.2f})'
+    sel = torch.randint(0, P, (4096,), generator=gen)
+    c_ref, idx_ref, w_ref = RP.point_gather(q[sel], xyz, feats, 'idw', radius=0.03, k=8, return_idx=True)
+    assert np.array_equal(idx[sel.to(dev)].cpu().numpy(), idx_ref.numpy().astype(np.int32))
+    close(w[sel.to(dev)], w_ref, 1e-6, 'weights')
+    close(c[sel.to(dev)], c_ref, 1e-5 * c_ref.abs().max().item(), 'c')
+
+
 def test_gather_backward_matches_oracle(pnr_mod, dev):
     xyz, feats, q = random_cloud(seed=5)
     pts = pnr_mod.NeuralPoints(xyz.to(dev), feats.to(dev), mode='idw', radius=0.06, k=8).to(dev)
@@ -123,6 +152,25 @@ def test_decoder_c32_matches_reference(pnr_mod, dev):
     ref = RP.grid_features(torch.from_numpy(g['grad_grid'])).numpy()
     close(pts.feats.grad, ref, 2e-3 * np.abs(ref).max(), 'dL/dgrid')
     close(p.grad, g['grad_p'], 2e-3 * np.abs(g['grad_p']).max(), 'dL/dp')
+
+
+def test_fc_weight_scale_covers_every_weight(pnr_mod, dev):
+    """The f16 scale of each fc_c weight (k_wscale) must come from ALL its entries: the largest one
+    sits alone at the last flat index, 1000x the rest. A scale from a partial scan overflows f16
+    there, so the split path must still match the fp32 path."""
+    g, pts, dec = grid_setup(pnr_mod, dev)
+    with torch.no_grad():
+        for i in range(4):
+            wt = getattr(dec.fc_c[i], 'weight')
+            wt.mul_(1e-3)
+            wt.view(-1)[-1] = 0.5
+    p = torch.from_numpy(g['p']).to(dev)
+    with torch.no_grad():
+        raw = dec(p, c_grid={'points_color': pts}).clone()
+        dec.precision = 'fp32'
+        ref = dec(p, c_grid={'points_color': pts})
+    assert torch.isfinite(raw).all()
+    close(raw, ref, 2e-5 * ref.abs().max().item(), 'raw vs the fp32 path')
 
 
 def surface_cloud(dev, seed=4):

@@ -100,6 +100,22 @@ def main():
     lib.pnr_timing_enable(0)
     bl, bms, _ = timing_read(5)
     bavg = bms / bl
+    # feature grads only (the Mapper's case: no dL/dp)
+    lib.pnr_timing_enable(1)
+    timing_read(5)
+    for _ in range(args.reps):
+        pnr._lib.check(lib.pnr_point_gather_bwd(ctypes.byref(sb), p.data_ptr(), P, idx.data_ptr(), w.data_ptr(),
+                                                c.data_ptr(), gc.data_ptr(), None, ws.data_ptr(), ws.numel(),
+                                                st), 'gather_bwd')
+    torch.cuda.synchronize()
+    lib.pnr_timing_enable(0)
+    fl, fms, _ = timing_read(5)
+    with torch.no_grad():  # neighbours shared with the previous row that has neighbours
+        rows = idx[idx[:, 0] >= 0].long()
+        prev, cur = rows[:-1], rows[1:]
+        shared = ((cur[:, :, None] == prev[:, None, :]) & (cur[:, :, None] >= 0)).any(2).sum().item()
+        print(f'bwd rows {rows.shape[0]}, neighbour slots {int((rows >= 0).sum().item())}, shared with the '
+              f'previous row {shared}; feature-grad-only bwd {fms / fl:.3f} ms/launch')
     # bwd algorithmic bytes: 24 B point + 128 g_c + 128 c + k*8 idx/w + per neighbour (128 feats + 12 xyz
     # + 128 B feature-grad atomics) + 12 B g_p
     bbyt = P * (24 + 128 + 128 + args.k * 8 + 12) + nb * (128 + 12 + 128)
