@@ -16,6 +16,8 @@
 // |d| are fma chains, and no floating-point contraction is allowed elsewhere (fp contract off).
 #include <math.h>
 
+#include <algorithm>
+
 #include "pnr_internal.h"
 
 #pragma clang fp contract(off)
@@ -31,24 +33,29 @@ __device__ __forceinline__ float ray_norm(const float* d) {
 }
 
 // ---------------------------------------------------------------------------------------------
-__global__ void k_gt_max(const float* __restrict__ gt, int64_t n, float* __restrict__ out) {
-  __shared__ float red[1024];
-  float m = -INFINITY;
-  for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
-    const float v = gt[i] * 1.2f;
-    m = (v > m || v != v) ? v : m;
-  }
-  red[threadIdx.x] = m;
+// batch max of 1.2 gt in two launches: kGtParts blocks write partial maxima to out[1..], then one
+// block reduces them into out[0] (the workspace slot holds 64 floats).  NaN propagates (torch.max).
+constexpr int kGtParts = 63;
+__device__ __forceinline__ float max_nanf(float m, float v) { return (v > m || v != v) ? v : m; }
+__device__ __forceinline__ float block_max_256(float m, float* red) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = max_nanf(m, __shfl_xor(m, o));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
   __syncthreads();
-  for (int s = blockDim.x / 2; s > 0; s >>= 1) {
-    if ((int)threadIdx.x < s) {
-      const float o = red[threadIdx.x + s];
-      const float c = red[threadIdx.x];
-      red[threadIdx.x] = (o > c || o != o) ? o : c;
-    }
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) *out = red[0];
+  return max_nanf(max_nanf(red[0], red[1]), max_nanf(red[2], red[3]));
+}
+__global__ __launch_bounds__(256) void k_gt_max_part(const float* __restrict__ gt, int64_t n, float* __restrict__ out) {
+  __shared__ float red[4];
+  float m = -INFINITY;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    m = max_nanf(m, gt[i] * 1.2f);
+  m = block_max_256(m, red);
+  if (threadIdx.x == 0) out[1 + blockIdx.x] = m;
+}
+__global__ __launch_bounds__(256) void k_gt_max(int parts, float* __restrict__ out) {
+  __shared__ float red[4];
+  const float m = block_max_256((int)threadIdx.x < parts ? out[1 + threadIdx.x] : -INFINITY, red);
+  if (threadIdx.x == 0) out[0] = m;
 }
 
 // near/far and the stratified z of the first pass.  z: (N, S) float64.
@@ -251,11 +258,11 @@ __global__ __launch_bounds__(64) void k_fine_bwd(pnr_render_params prm, const fl
   const int tid = threadIdx.x;
   const int64_t n = (int64_t)blockIdx.x * 64 + tid;
   const int S = prm.n_samples, I = prm.n_importance, M = S + I;
-  double* zs = reinterpret_cast<double*>(smem);                 // [M][64]
-  float* wl = reinterpret_cast<float*>(zs + M * 64);            // [M][64]
-  float* al = wl + M * 64;
+  // [M][64] per-ray columns: z (sorted), alpha and T; w = alpha * T and dz are recomputed from
+  // them bit-for-bit, which keeps the LDS per block at 16 B per sample (3 blocks per CU at M = 44)
+  double* zs = reinterpret_cast<double*>(smem);
+  float* al = reinterpret_cast<float*>(zs + M * 64);
   float* Tl = al + M * 64;
-  float* dzl = Tl + M * 64;
   if (n >= n_rays) return;
   const uint8_t* ord = ord_in + n * PNR_MAX_SAMPLES;
   const float* dvec = rd + n * 3;
@@ -272,9 +279,7 @@ __global__ __launch_bounds__(64) void k_fine_bwd(pnr_render_params prm, const fl
     const float w = a * (float)T;
     Tl[q * 64 + tid] = (float)T;
     T *= (double)(1.f - a + 1e-10f);
-    wl[q * 64 + tid] = w;
     al[q * 64 + tid] = a;
-    dzl[q * 64 + tid] = dz;
     D += (double)w * zq;
   }
   const double gd = g_depth ? g_depth[n] : 0.0;
@@ -283,7 +288,7 @@ __global__ __launch_bounds__(64) void k_fine_bwd(pnr_render_params prm, const fl
   const float gr1 = g_rgb ? g_rgb[n * 3 + 1] : 0.f;
   const float gr2 = g_rgb ? g_rgb[n * 3 + 2] : 0.f;
   double sdev = 0.0;
-  for (int q = 0; q < M; ++q) sdev += (double)wl[q * 64 + tid] * (zs[q * 64 + tid] - D);
+  for (int q = 0; q < M; ++q) sdev += (double)(al[q * 64 + tid] * Tl[q * 64 + tid]) * (zs[q * 64 + tid] - D);
   const double gD = gd - 2.0 * gv * sdev;  // d var / d depth = -2 sum w (z - depth)
   float R = 0.f, gn = 0.f;
   for (int q = M - 1; q >= 0; --q) {
@@ -291,12 +296,12 @@ __global__ __launch_bounds__(64) void k_fine_bwd(pnr_render_params prm, const fl
     const float4 c = rsrc(s);
     const double zq = zs[q * 64 + tid];
     const double dd = zq - D;
-    const float w = wl[q * 64 + tid];
-    const float gw = (gr0 * c.x + gr1 * c.y + gr2 * c.z) + (float)(gD * zq) + (float)(gv * dd * dd);
     const float a = al[q * 64 + tid];
+    const float w = a * Tl[q * 64 + tid];
+    const float gw = (gr0 * c.x + gr1 * c.y + gr2 * c.z) + (float)(gD * zq) + (float)(gv * dd * dd);
     const float ga = Tl[q * 64 + tid] * (gw - R);
     R = gw * a + (1.f - a + 1e-10f) * R;
-    const float dz = dzl[q * 64 + tid];
+    const float dz = q < M - 1 ? (float)(zs[(q + 1) * 64 + tid] - zq) : 1e10f;
     const float delta = dz * nrm;
     const float sr = relu(c.w);
     const float ex = expf(-sr * delta);
@@ -343,19 +348,20 @@ __global__ void k_ray_grads(const float* __restrict__ rd, const ZT* __restrict__
 
 // ---------------------------------------------------------------------------------------------
 // regulation (Renderer.py:280-294): float32 z in [0, 0.85*gt], jittered by t_rand
+// one thread per (ray, sample): coalesced t_rand reads and z writes
 __global__ void k_reg_z(pnr_render_params prm, const float* __restrict__ gt, const float* __restrict__ t_rand,
                         int64_t n_rays, float* __restrict__ z) {
-  const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (n >= n_rays) return;
   const int S = prm.n_samples;
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n_rays * S) return;
+  const int64_t n = e / S;
+  const int s = (int)(e - n * S);
   const float far = gt[n] * 0.85f;
-  auto z0 = [&](int s) { return (0.0f * (1.f - prm.t_vals[s])) + far * prm.t_vals[s]; };
-  for (int s = 0; s < S; ++s) {
-    const float zs = z0(s);
-    const float lower = s > 0 ? .5f * (zs + z0(s - 1)) : zs;
-    const float upper = s < S - 1 ? .5f * (z0(s + 1) + zs) : zs;
-    z[n * S + s] = lower + (upper - lower) * t_rand[n * S + s];
-  }
+  auto z0 = [&](int k) { return (0.0f * (1.f - prm.t_vals[k])) + far * prm.t_vals[k]; };
+  const float zs = z0(s);
+  const float lower = s > 0 ? .5f * (zs + z0(s - 1)) : zs;
+  const float upper = s < S - 1 ? .5f * (z0(s + 1) + zs) : zs;
+  z[e] = lower + (upper - lower) * t_rand[e];
 }
 
 __global__ void k_extract_sigma(const float4* __restrict__ raw, int64_t P, float* __restrict__ sigma) {
@@ -444,7 +450,9 @@ __global__ void k_step_advance(int32_t* step_count) {
 static inline unsigned nblk(int64_t n, int b) { return (unsigned)((n + b - 1) / b); }
 
 int launch_gt_max(const float* gt, int64_t n, float* out, hipStream_t st) {
-  hipLaunchKernelGGL(k_gt_max, dim3(1), dim3(1024), 0, st, gt, n, out);
+  const int parts = (int)std::min<int64_t>(kGtParts, std::max<int64_t>(1, (n + 4095) / 4096));
+  hipLaunchKernelGGL(k_gt_max_part, dim3(parts), dim3(256), 0, st, gt, n, out);
+  hipLaunchKernelGGL(k_gt_max, dim3(1), dim3(256), 0, st, parts, out);
   return hip_status(hipGetLastError());
 }
 int launch_coarse_z(const pnr_render_params& prm, const float* ro, const float* rd, const float* gt,
@@ -473,7 +481,7 @@ int launch_fine_bwd(const pnr_render_params& prm, const float* rd, const double*
                     float* goc, float* goi, float* g_nrm, hipStream_t st) {
   if (n <= 0) return 0;
   const int M = prm.n_samples + prm.n_importance;
-  const size_t sh = (size_t)M * 64 * (8 + 4 * 4);
+  const size_t sh = (size_t)M * 64 * (8 + 2 * 4);
   hipLaunchKernelGGL(k_fine_bwd, dim3(nblk(n, 64)), dim3(64), sh, st, prm, rd, zc, zi, (const float4*)rawc,
                      (const float4*)rawi, insc, insi, ord, n, gd, gv, grgb, (float4*)goc, (float4*)goi, g_nrm);
   return hip_status(hipGetLastError());
@@ -495,7 +503,7 @@ int launch_ray_grads_f32(const float* rd, const float* za, int sa, const float* 
 int launch_reg_z(const pnr_render_params& prm, const float* gt, const float* t_rand, int64_t n, float* z,
                  hipStream_t st) {
   if (n <= 0) return 0;
-  hipLaunchKernelGGL(k_reg_z, dim3(nblk(n, 128)), dim3(128), 0, st, prm, gt, t_rand, n, z);
+  hipLaunchKernelGGL(k_reg_z, dim3(nblk(n * prm.n_samples, 256)), dim3(256), 0, st, prm, gt, t_rand, n, z);
   return hip_status(hipGetLastError());
 }
 int launch_extract_sigma(const float* raw, int64_t P, float* sigma, hipStream_t st) {
