@@ -663,12 +663,8 @@ __global__ __launch_bounds__(256, 1) void k_mlp_fwd16(BfFwdArgs a, int mode) {
       }
     split_tile<PR>(cv, S.ct);
   }
-#pragma unroll
-  for (int st = 0; st < 2; ++st)
-#pragma unroll
-    for (int t = 0; t < 8; ++t)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) S.acc[st][t][r] = 0.f;
+  // no accumulator zero fill: the first input tile of every layer starts its tiles from 0 (ZERO in
+  // mfma_frag), and nothing reads a tile before that (256 v_accvgpr_mov saved per workgroup)
 
   // Fourier features: the raw tables must have landed (they are older than the step DMAs)
   sync_chunk<K::prologue_glds()>();

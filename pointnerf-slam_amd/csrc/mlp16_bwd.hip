@@ -223,12 +223,7 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd16(const float* __restrict__ 
   }
 #pragma unroll
   for (int r = 0; r < 16; ++r) S.gc[r] = 0.f;
-#pragma unroll
-  for (int st = 0; st < 2; ++st)
-#pragma unroll
-    for (int t = 0; t < 8; ++t)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) S.acc[st][t][r] = 0.f;
+  // no accumulator zero fill: each layer's first input tile starts its tiles from 0 (ZERO)
   K::template step<0>(a, S, wmain, wfc, lds);
 
   // g_arg = g_e * cos(x@B), g_x = B g_arg (the k_mlp_bwd epilogue on set 0, tiles 0..2)
