@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define PNR_ABI_VERSION 4
+#define PNR_ABI_VERSION 5
 #define PNR_N_PARAMS 11
 #define PNR_MAX_SAMPLES 64      /* N_samples + N_importance per ray */
 #define PNR_C_DIM 32            /* neural-point feature width (decoder.py:122-125 fc_c input) */
@@ -191,7 +191,8 @@ int pnr_render_fwd(const pnr_render_params* prm, const float* packed,
                    void* workspace, size_t ws_bytes, void* stream);
 /* Backward of the final (44-sample) pass.  Inputs are dL/ddepth, dL/dvar (float64, may be NULL
  * = zero), dL/drgb (float32, may be NULL).  Outputs: `grads` = host array of 11 device pointers
- * receiving dL/dparam (ACCUMULATED: +=, reference layout), g_rays_o / g_rays_d (N,3) float32
+ * receiving dL/dparam (ACCUMULATED: +=, reference layout), or NULL for no decoder weight gradients
+ * (ABI 5: the Tracker's camera-only backward skips every weight-gradient launch), g_rays_o / g_rays_d (N,3) float32
  * written (not accumulated) when prm->need_ray_grads, else ignored (may be NULL).
  * `params` = the same 11 raw tensors (needed for the transposed weight images). */
 size_t pnr_render_bwd_workspace_bytes(const pnr_render_params* prm, int64_t n_rays);

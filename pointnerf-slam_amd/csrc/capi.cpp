@@ -240,7 +240,8 @@ int mlp_backward_core(int prec, const float* packed, const SaveArgs& sv, int64_t
     if (rc) return rc;
     const int64_t hstride = sv.ld * kHidden;  // h_l rows of this chunk: h + l_idx * ld * 256 + p0 * 256
     const int64_t dstride = b.C * kHidden;
-    if (split) {  // f16 operands: h / e saved by k_mlp_fwd16, scaled deltas by k_mlp_bwd16
+    if (!grads) {  // no decoder weight gradients (the Tracker's camera-only backward)
+    } else if (split) {  // f16 operands: h / e saved by k_mlp_fwd16, scaled deltas by k_mlp_bwd16
       const _Float16* h16 = reinterpret_cast<const _Float16*>(sv.hP) + p0 * kHidden;
       const _Float16* d16 = reinterpret_cast<const _Float16*>(b.dP);
       const _Float16* e16 = reinterpret_cast<const _Float16*>(sv.eP) + p0 * kFourierPad;
@@ -265,9 +266,10 @@ int mlp_backward_core(int prec, const float* packed, const SaveArgs& sv, int64_t
     }
     if (rc) return rc;
     // Fourier: dB (3x93) += x^T g_arg   (x rows are float4 (x0,x1,x2,inside): 3 of 4 used)
-    rc = split ? launch_wgrad_fourier16(sv.xP + p0, b.gargP, C, grads[0], b.gmax, st)
-               : launch_wgrad(kWgradFourier, reinterpret_cast<const float*>(sv.xP + p0), 3, b.gargP, kFourier, C,
-                              grads[0], kFourier, nullptr, st);
+    if (grads)
+      rc = split ? launch_wgrad_fourier16(sv.xP + p0, b.gargP, C, grads[0], b.gmax, st)
+                 : launch_wgrad(kWgradFourier, reinterpret_cast<const float*>(sv.xP + p0), 3, b.gargP, kFourier, C,
+                                grads[0], kFourier, nullptr, st);
     if (rc) return rc;
     // feature branch: dWc_l (256x32) += (dL/dh_l)^T c ; dbc_l += colsum(dL/dh_l)
     if (fb && fb->g_fc && split) {  // f16 operands: gH * 2^e from k_mlp_bwd16, an f16 copy of c
@@ -498,9 +500,10 @@ int pnr_render_bwd(const pnr_render_params* prm, const float* packed, const floa
   (void)rays_o;
   if (!valid_prm(prm) || !packed || n < 0 || !prm->save_for_backward) return PNR_E_ARG;
   if (n == 0) return PNR_OK;
-  if (!grads || !workspace || !bwd_ws || !rays_d) return PNR_E_ARG;
-  for (int i = 0; i < PNR_N_PARAMS; ++i)
-    if (!grads[i]) return PNR_E_ARG;
+  if (!workspace || !bwd_ws || !rays_d) return PNR_E_ARG;
+  if (grads)  // NULL: no decoder weight gradients
+    for (int i = 0; i < PNR_N_PARAMS; ++i)
+      if (!grads[i]) return PNR_E_ARG;
   if (prm->need_ray_grads && (!g_rays_o || !g_rays_d)) return PNR_E_ARG;
   size_t need = 0, bneed = 0;
   RenderWS w = carve_render(prm, n, workspace, &need);
@@ -618,9 +621,10 @@ int pnr_regulation_bwd(const pnr_render_params* prm, const float* packed, const 
   (void)rays_o;
   if (!valid_prm(prm) || !packed || n < 0 || !prm->save_for_backward) return PNR_E_ARG;
   if (n == 0) return PNR_OK;
-  if (!grads || !workspace || !bwd_ws || !g_sigma) return PNR_E_ARG;
-  for (int i = 0; i < PNR_N_PARAMS; ++i)
-    if (!grads[i]) return PNR_E_ARG;
+  if (!workspace || !bwd_ws || !g_sigma) return PNR_E_ARG;
+  if (grads)  // NULL: no decoder weight gradients
+    for (int i = 0; i < PNR_N_PARAMS; ++i)
+      if (!grads[i]) return PNR_E_ARG;
   if (prm->need_ray_grads && (!g_rays_o || !g_rays_d || !rays_d)) return PNR_E_ARG;
   size_t need = 0, bneed = 0;
   RegWS w = carve_reg(prm, n, workspace, &need);

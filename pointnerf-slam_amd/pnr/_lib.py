@@ -83,14 +83,14 @@ _SIGS = {
                                       c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
     'pnr_render_bwd_workspace_bytes': (c_size_t, [ctypes.POINTER(RenderParams), c_int64]),
     'pnr_render_bwd': (ctypes.c_int, [ctypes.POINTER(RenderParams), c_void_p, c_void_p, c_void_p, c_void_p, c_int64,
-                                      c_void_p, c_void_p, c_void_p, PtrArray, c_void_p, c_void_p,
-                                      c_void_p, c_size_t, c_void_p, c_size_t, c_void_p]),
+                                      c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                      c_void_p, c_size_t, c_void_p, c_size_t, c_void_p]),  # grads: PtrArray or None
     'pnr_regulation_workspace_bytes': (c_size_t, [ctypes.POINTER(RenderParams), c_int64]),
     'pnr_regulation_fwd': (ctypes.c_int, [ctypes.POINTER(RenderParams), c_void_p, c_void_p, c_void_p, c_void_p,
                                           c_void_p, c_int64, c_void_p, c_void_p, c_size_t, c_void_p]),
     'pnr_regulation_bwd_workspace_bytes': (c_size_t, [ctypes.POINTER(RenderParams), c_int64]),
     'pnr_regulation_bwd': (ctypes.c_int, [ctypes.POINTER(RenderParams), c_void_p, c_void_p, c_void_p, c_void_p,
-                                          c_int64, c_void_p, PtrArray, c_void_p, c_void_p, c_void_p, c_size_t,
+                                          c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t,
                                           c_void_p, c_size_t, c_void_p]),
     'pnr_get_rays': (ctypes.c_int, [c_int32, c_int32, c_float, c_float, c_float, c_float, c_void_p, c_void_p,
                                     c_void_p, c_void_p]),

@@ -88,6 +88,16 @@ class _Feat:
         return g_feats, g_fc, [*g_fc, g_feats]
 
 
+def _param_grads(ctx, dev):
+    """Zeroed decoder weight-gradient buffers and their pointer array, or 11 Nones and NULL when
+    no decoder tensor needs a gradient (the Tracker: the C ABI then skips every weight-gradient
+    launch).  The decoder tensors are autograd inputs 7..17 of both Functions."""
+    if not any(ctx.needs_input_grad[7:7 + _lib.N_PARAMS]):
+        return [None] * _lib.N_PARAMS, None
+    grads = [torch.zeros(s, device=dev, dtype=torch.float32) for s in _GRAD_SHAPES]
+    return grads, _lib.PtrArray(*[g.data_ptr() for g in grads])
+
+
 class _RenderFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, prm_bytes, packer, feat, rays_o, rays_d, gt_depth, far_clamp, *tensors):
@@ -124,7 +134,7 @@ class _RenderFn(torch.autograd.Function):
         prm = _lib.RenderParams.from_buffer_copy(ctx.prm)
         n = rays_o.shape[0]
         dev = rays_o.device
-        grads = [torch.zeros(s, device=dev, dtype=torch.float32) for s in _GRAD_SHAPES]
+        grads, arr = _param_grads(ctx, dev)
         g_feats, g_fc, extra = ctx.feat.grads(dev, ctx.needs_input_grad)
         ctx.feat.attach(prm, g_feats, g_fc)
         g_o = g_d = None
@@ -132,7 +142,6 @@ class _RenderFn(torch.autograd.Function):
             g_o = torch.empty((n, 3), device=dev, dtype=torch.float32)
             g_d = torch.empty((n, 3), device=dev, dtype=torch.float32)
         bws = torch.empty(lib.pnr_render_bwd_workspace_bytes(ctypes_ref(prm), n), dtype=torch.uint8, device=dev)
-        arr = _lib.PtrArray(*[g.data_ptr() for g in grads])
         gd = None if g_depth is None else g_depth.contiguous()
         gv = None if g_var is None else g_var.contiguous()
         gc = None if g_rgb is None else g_rgb.contiguous()
@@ -174,7 +183,7 @@ class _RegulationFn(torch.autograd.Function):
         prm = _lib.RenderParams.from_buffer_copy(ctx.prm)
         n = rays_o.shape[0]
         dev = rays_o.device
-        grads = [torch.zeros(s, device=dev, dtype=torch.float32) for s in _GRAD_SHAPES]
+        grads, arr = _param_grads(ctx, dev)
         g_feats, g_fc, extra = ctx.feat.grads(dev, ctx.needs_input_grad)
         ctx.feat.attach(prm, g_feats, g_fc)
         g_o = g_d = None
@@ -182,7 +191,6 @@ class _RegulationFn(torch.autograd.Function):
             g_o = torch.empty((n, 3), device=dev, dtype=torch.float32)
             g_d = torch.empty((n, 3), device=dev, dtype=torch.float32)
         bws = torch.empty(lib.pnr_regulation_bwd_workspace_bytes(ctypes_ref(prm), n), dtype=torch.uint8, device=dev)
-        arr = _lib.PtrArray(*[g.data_ptr() for g in grads])
         _lib.check(lib.pnr_regulation_bwd(ctypes_ref(prm), _lib.ptr(packed), None, _lib.ptr(rays_o),
                                           _lib.ptr(rays_d), n, _lib.ptr(g_sigma.contiguous()), arr, _lib.ptr(g_o),
                                           _lib.ptr(g_d), _lib.ptr(ws), ws.numel(), _lib.ptr(bws), bws.numel(),
