@@ -7,13 +7,13 @@ from . import _lib
 from .config import load_config, get_model, ROOM0_CFG
 from .decoder import MLP, PARAM_ORDER, FC_ORDER
 from .points import NeuralPoints
-from .renderer import Renderer, get_rays, get_rays_from_uv
-from .common import scaled_bound, get_camera_from_tensor, get_tensor_from_camera, quad2rotation
+from .renderer import Renderer, get_rays, get_rays_from_uv, get_samples
+from .common import scaled_bound, get_camera_from_tensor, get_tensor_from_camera, quad2rotation, random_select
 from .tracking import TrackStep, track_frame
 
 __all__ = ['Renderer', 'MLP', 'PARAM_ORDER', 'FC_ORDER', 'NeuralPoints', 'get_model', 'load_config', 'ROOM0_CFG', 'get_rays',
            'get_rays_from_uv', 'scaled_bound', 'get_camera_from_tensor', 'get_tensor_from_camera',
-           'quad2rotation', 'TrackStep', 'track_frame']
+           'quad2rotation', 'TrackStep', 'track_frame', 'get_samples', 'random_select']
 
 
 def library():

@@ -66,3 +66,9 @@ def select_uv_indices(n_pixels, n, device, generator=None):
     """src/common.py:99-100: uniform torch.randint pixel indices (clamped like the reference)."""
     idx = torch.randint(n_pixels, (n,), device=device, generator=generator)
     return idx.clamp(0, n_pixels)
+
+
+def random_select(l, k):
+    """src/common.py:66-71: k distinct values of 0..l-1 in random order (keyframe window)."""
+    return list(np.random.permutation(np.array(range(l)))[:min(l, k)])
+

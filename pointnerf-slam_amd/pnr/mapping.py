@@ -169,3 +169,16 @@ class MapGraph:
             dst.copy_(src, non_blocking=True)
         self.graph.replay()
         return self.loss
+
+
+def window_batch(frames, pixs_per_image, H, W, fx, fy, cx, cy, device, generator=None):
+    """The per-iteration pixel batch of Mapper.optimize_map (src/Mapper.py:560-606): for every
+    frame of the optimisation window, in window order, `pixs_per_image` uniform pixels of the whole
+    image (the effective path for every frame index: SURVEY.md appendix item 7), concatenated.
+    frames: iterable of (c2w (3x4 or 4x4), gt depth (H,W), gt colour (H,W,3)) device tensors.
+    Returns rays_o, rays_d (N,3), gt depth (N,), gt colour (N,3) float32."""
+    from .renderer import get_samples
+    out = [get_samples(0, H, 0, W, pixs_per_image, H, W, fx, fy, cx, cy, c2w, d, c, device, generator)
+           for c2w, d, c in frames]
+    return tuple(torch.cat([o[k].float() for o in out], 0) for k in range(4))
+

@@ -366,3 +366,20 @@ def get_rays_from_uv(i, j, c2w, H, W, fx, fy, cx, cy, device):
                                     _lib.ptr(c2w), _lib.ptr(ro), _lib.ptr(rd), _lib.stream_of(c2w.device)),
                'rays_from_uv')
     return ro, rd
+
+
+def get_samples(H0, H1, W0, W1, n, H, W, fx, fy, cx, cy, c2w, depth, color, device, generator=None):
+    """src/common.py:110-134 (get_sample_uv + select_uv + get_rays_from_uv) on the device: n uniform
+    torch.randint pixels of the region H0..H1 x W0..W1 (row-major region index), their rays
+    (pnr_rays_from_uv), depth and colour.  The reference's linspace pixel grid holds exact
+    integers, so pixel (i, j) = (idx % w + W0, idx // w + H0)."""
+    from .common import select_uv_indices
+    d = depth[H0:H1, W0:W1].reshape(-1)
+    col = color[H0:H1, W0:W1].reshape(-1, 3)
+    w = W1 - W0
+    idx = select_uv_indices(d.numel(), n, d.device, generator)
+    i = (idx % w + W0).float()
+    j = (torch.div(idx, w, rounding_mode='floor') + H0).float()
+    ro, rd = get_rays_from_uv(i, j, c2w, H, W, fx, fy, cx, cy, device)
+    return ro, rd, d[idx], col[idx]
+

@@ -185,6 +185,33 @@ def test_rays_vs_oracle(pnr_mod, dev, scene):
     close(ro2, ro2r.reshape(-1, 3), 0, 0, 'uv rays_o')
 
 
+def test_window_batch_vs_oracle(pnr_mod, dev, scene):
+    """Mapper.optimize_map's per-iteration batch (src/Mapper.py:560-606): pixs_per_image uniform
+    pixels per window frame through get_samples (src/common.py:110-134), concatenated."""
+    from oracle import ref_render as ref
+    from pnr.mapping import window_batch
+    H, W, fx, fy, cx, cy = 48, 64, 50., 51., 31.5, 23.5
+    g = torch.Generator().manual_seed(5)
+    frames = []
+    for k in (1, 2):
+        c2w = torch.from_numpy(scene['poses'][k]).float()
+        frames.append((c2w, torch.rand((H, W), generator=g), torch.rand((H, W, 3), generator=g)))
+    n = 100
+    gen = torch.Generator(device=dev).manual_seed(7)
+    ro, rd, gd, gc = window_batch([(c.to(dev), d.to(dev), col.to(dev)) for c, d, col in frames], n, H, W,
+                                  fx, fy, cx, cy, dev, generator=gen)
+    assert ro.shape == (2 * n, 3) and gd.shape == (2 * n,) and gc.shape == (2 * n, 3)
+    gen = torch.Generator(device=dev).manual_seed(7)
+    for f, (c2w, d, col) in enumerate(frames):
+        idx = torch.randint(H * W, (n,), device=dev, generator=gen).cpu()
+        i, j = (idx % W).float(), (idx // W).float()
+        ro_r, rd_r = ref.rays_from_uv(i, j, c2w, fx, fy, cx, cy)
+        sl = slice(f * n, (f + 1) * n)
+        close(rd[sl], rd_r.reshape(-1, 3), 1e-6, 1e-7, 'rays_d')
+        close(ro[sl], ro_r.reshape(-1, 3), 0, 0, 'rays_o')
+        assert torch.equal(gd[sl].cpu(), d.reshape(-1)[idx]) and torch.equal(gc[sl].cpu(), col.reshape(-1, 3)[idx])
+
+
 def test_adam_matches_torch(pnr_mod, dev):
     import ctypes
     lib = pnr_mod.library()

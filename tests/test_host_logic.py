@@ -155,3 +155,15 @@ def test_fourier_sincos_reduction_matches_libm():
     es = max(abs(float(sc(x, False)) - np.sin(np.float64(x))) for x in xs)
     ec = max(abs(float(sc(x, True)) - np.cos(np.float64(x))) for x in xs)
     assert es < 1e-7 and ec < 1e-7, (es, ec)
+
+
+def test_random_select_keyframe_window():
+    """src/common.py:66-71: k distinct indices of 0..l-1 (min(l, k) of them), numpy's RNG stream."""
+    import numpy as np
+    from pnr.common import random_select
+    np.random.seed(3)
+    a = random_select(10, 4)
+    np.random.seed(3)
+    assert a == list(np.random.permutation(np.array(range(10)))[:4])
+    assert len(set(a)) == 4 and all(0 <= x < 10 for x in a)
+    assert sorted(random_select(3, 8)) == [0, 1, 2]
