@@ -126,14 +126,14 @@ def neural_point_scene(dev, voxel=0.001, n_rays=W * H, seed=0):
     return xyz, feats, p, (o.float().contiguous(), d.float().contiguous(), gt.float().contiguous())
 
 
-def gather_bytes(n_samples, n_nb_total, k, save=True):
+def gather_bytes(n_samples, n_nb_total, k, save=True, feat_bytes=128):
     """Algorithmic bytes of one pnr_point_gather (with the 8 probes made): per
     sample 24 B point + 8 x 8 B bucket headers + 128 B c (+ k x 8 B idx/weight saves), per
-    neighbour 4 B idx + 12 B xyz + 128 B features."""
-    return n_samples * (24 + 8 * 8 + 128 + (k * 8 if save else 0)) + n_nb_total * (4 + 12 + 128)
+    neighbour 4 B idx + 12 B xyz + 128 B features (64 B with float16 features)."""
+    return n_samples * (24 + 8 * 8 + 128 + (k * 8 if save else 0)) + n_nb_total * (4 + 12 + feat_bytes)
 
 
-def gather_roofline(dev, voxel=0.001, k=8, reps=5):
+def gather_roofline(dev, voxel=0.001, k=8, reps=5, feat_dtype='float32'):
     """Time the point-gather kernels (k_gather_probe + k_gather_search, hipEvents on their
     stream) on the neural-point scene; roofline against the HBM peak."""
     import ctypes
@@ -141,7 +141,7 @@ def gather_roofline(dev, voxel=0.001, k=8, reps=5):
     from pnr._lib import timing_read
     lib = pnr.library()
     xyz, feats, p, _ = neural_point_scene(dev, voxel)
-    pts = pnr.NeuralPoints(xyz, feats, mode='idw', radius=2 * voxel, k=k).to(dev)
+    pts = pnr.NeuralPoints(xyz, feats, mode='idw', radius=2 * voxel, k=k, feat_dtype=feat_dtype).to(dev)
     P = p.shape[0]
     c = torch.empty((P, 32), device=dev)
     idx = torch.empty((P, k), device=dev, dtype=torch.int32)
@@ -164,13 +164,13 @@ def gather_roofline(dev, voxel=0.001, k=8, reps=5):
     lib.pnr_timing_enable(0)
     launches, ms, _ = timing_read(4)
     avg = ms / launches
-    byt = gather_bytes(P, nb, k)
+    byt = gather_bytes(P, nb, k, feat_bytes=64 if feat_dtype == 'float16' else 128)
     gbs = byt / (avg * 1e-3) / 1e9
     return {'bound': 'hbm', 'achieved': round(gbs, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
             'frac': round(gbs / HBM_PEAK_GBS, 4), 'traffic': pmc_traffic('k_gather', P),
             'kernel': 'k_gather_probe+k_gather_search',
             'avg_launch_ms': round(avg, 3), 'launches': launches, 'samples': P, 'points': int(xyz.shape[0]),
-            'neighbours_per_sample': round(nb / P, 3), 'radius': 2 * voxel, 'k': k,
+            'neighbours_per_sample': round(nb / P, 3), 'radius': 2 * voxel, 'k': k, 'point_features': feat_dtype,
             'bytes_per_launch': byt}
 
 
@@ -235,6 +235,8 @@ def main():
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-gather', action='store_true', help='skip the point-gather roofline line')
     ap.add_argument('--precision', default=None, help="decoder forward matmuls: fp32 | f16x3 (default) | bf16x3 | bf16")
+    ap.add_argument('--feat-dtype', default='float32', choices=['float32', 'float16'],
+                    help='neural-point feature storage (map-points workload and the gather line; C5: float16)')
     args = ap.parse_args()
 
     import pnr
@@ -270,7 +272,7 @@ def main():
         dec.load_state_dict(sd)
         dec = dec.to(dev)
         xyz, feats, _, (ro, rd, gt) = neural_point_scene(dev, n_rays=args.rays, seed=rank)
-        points = pnr.NeuralPoints(xyz, feats, mode='idw', radius=0.002, k=8).to(dev)
+        points = pnr.NeuralPoints(xyz, feats, mode='idw', radius=0.002, k=8, feat_dtype=args.feat_dtype).to(dev)
         col = torch.rand((args.rays, 3), device=dev, generator=torch.Generator(device=dev).manual_seed(rank))
     else:
         dec = pnr.get_model(cfg, nice=False)
@@ -388,7 +390,8 @@ def main():
             'config': {'workload': wl_name,
                        'rays_per_gpu': n, 'global_batch': n * world, 'samples_per_ray': samples,
                        'parallelism': f'dp{world}', 'decoder_precision': prec,
-                       'graph': bool(args.graph and world == 1 and args.workload == 'map')},
+                       'graph': bool(args.graph and world == 1 and args.workload == 'map'),
+                       **({'point_features': args.feat_dtype} if args.workload == 'map-points' else {})},
             'roofline': roofline, 'cpu_baseline': cpu,
             'kernels': {k: {'launches': v[0], 'ms': round(v[1], 3), 'units': v[2]} for k, v in kt.items()},
         }
@@ -396,7 +399,7 @@ def main():
             out['speedup_vs_cpu'] = round(value / cpu['value'], 1)
         if world == 1 and not args.no_gather and params is not None and args.workload != 'fwd':
             # the neural-point gather on its own roofline, after the timed region
-            out['gather_roofline'] = gather_roofline(dev)
+            out['gather_roofline'] = gather_roofline(dev, feat_dtype=args.feat_dtype)
         print(json.dumps(out), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define PNR_ABI_VERSION 5
+#define PNR_ABI_VERSION 6
 #define PNR_N_PARAMS 11
 #define PNR_MAX_SAMPLES 64      /* N_samples + N_importance per ray */
 #define PNR_C_DIM 32            /* neural-point feature width (decoder.py:122-125 fc_c input) */
@@ -101,6 +101,8 @@ typedef struct pnr_points {
                                the standalone gather                                           */
   float* g_feats;           /* backward: dL/dfeats (M,32) ACCUMULATED, or NULL                */
   float* const* g_fc;       /* backward: host array of 8 device ptrs accumulating dL/dfc_c, or NULL */
+  int32_t feat_half;        /* ABI 6: 1 = `feats` holds (M,32) float16 (read-only copy of an fp32
+                               master; sums, weights and g_feats stay float32), 0 = float32     */
 } pnr_points;
 
 /* Renderer configuration: the cfg keys Renderer.__init__ reads (src/utils/Renderer.py:6-21)

@@ -14,6 +14,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstddef>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
@@ -299,6 +300,8 @@ bool check_params(const float* const* params) {
 
 extern "C" {
 
+// the ctypes mirror (pnr/_lib.py) and tests/test_capi.py assume these offsets
+static_assert(offsetof(pnr_points, feat_half) == 104 && sizeof(pnr_points) == 112, "pnr_points layout (ABI 6)");
 int pnr_abi_version(void) { return PNR_ABI_VERSION; }
 
 int pnr_timing_enable(int on) {

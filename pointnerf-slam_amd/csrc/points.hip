@@ -327,6 +327,17 @@ int launch_points_build(const pnr_points& pts, hipStream_t st) {
 // ---------------------------------------------------------------------------------------------
 // Gather
 // ---------------------------------------------------------------------------------------------
+// Point features are float32 (M,32), or float16 (M,32) when pnr_points.feat_half (SURVEY.md
+// A15: the C5 budget's fp16 features); every sum and weight stays float32.
+typedef _Float16 pnr_h4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 load_feat4(const float4* f, int half, int64_t i4) {
+  if (!half) return f[i4];
+  const pnr_h4 h = reinterpret_cast<const pnr_h4*>(f)[i4];
+  return make_float4((float)h.x, (float)h.y, (float)h.z, (float)h.w);
+}
+__device__ __forceinline__ float load_feat1(const float4* f, int half, int64_t i) {
+  return half ? (float)reinterpret_cast<const _Float16*>(f)[i] : reinterpret_cast<const float*>(f)[i];
+}
 // Work lists: samples are appended by wave (one atomic per wave) to one of kLists sub-lists, each
 // with its own counter on its own 128-B line, dealt round-robin by wave -- a single counter would
 // serialise ~10^5 same-address atomics.  Consumers walk (sub-list, 256-item chunk) tasks.
@@ -369,9 +380,10 @@ struct GatherArgs {
   const int4* hdr;
   const int4* sub;       // per bucket: sub-cell end offsets (k_bucket_sub)
   const float4* sorted;
-  const float4* feats4;  // (M, 8) float4
+  const float4* feats4;  // (M, 8) float4, or (M, 32) f16 when feat_half
   const float* xyz;      // (M, 3)
   const uint32_t* occ;   // occupancy filter
+  int feat_half;         // features stored as float16 (pnr_points.feat_half)
   int k;
   float r2, eps;
   float h0, h1, h2;      // trilinear spacing
@@ -622,7 +634,7 @@ __device__ __forceinline__ void search_round(const GatherArgs& a, SearchLds& L, 
         for (int t = 0; t < 4; ++t) {
           id[t] = L.f.idx[sl * PNR_MAX_K + t0 + t];
           f[t] = make_float4(0.f, 0.f, 0.f, 0.f);
-          if (id[t] >= 0) f[t] = a.feats4[(int64_t)id[t] * 8 + q];
+          if (id[t] >= 0) f[t] = load_feat4(a.feats4, a.feat_half, (int64_t)id[t] * 8 + q);
         }
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
@@ -665,6 +677,7 @@ struct GatherBwdArgs {
   const float4* xP;      // MLP inputs (fused path) or null (positions from src)
   int64_t P;
   const float* xyz;
+  int feat_half;
   const float4* feats4;
   int k;
   float eps, h0, h1, h2;
@@ -746,7 +759,7 @@ __global__ __launch_bounds__(256) void k_gather_bwd(GatherBwdArgs a) {
         float f[PNR_MAX_K];
 #pragma unroll
         for (int kk = 0; kk < PNR_MAX_K; ++kk)
-          f[kk] = id[kk] >= 0 ? reinterpret_cast<const float*>(a.feats4)[(int64_t)id[kk] * 32 + ch] : 0.f;
+          f[kk] = id[kk] >= 0 ? load_feat1(a.feats4, a.feat_half, (int64_t)id[kk] * 32 + ch) : 0.f;
 #pragma unroll
         for (int kk = 0; kk < PNR_MAX_K; ++kk) dots[kk] = g * f[kk];
       }
@@ -871,6 +884,7 @@ int launch_gather(const pnr_points& pts, const PointSrc& src, int mode, int64_t 
   a.sub = v.sub;
   a.sorted = v.sorted;
   a.feats4 = reinterpret_cast<const float4*>(pts.feats);
+  a.feat_half = pts.feat_half ? 1 : 0;
   a.xyz = pts.xyz;
   a.occ = v.occ;
   a.k = pts.k;
@@ -933,6 +947,7 @@ int launch_gather_bwd(const pnr_points& pts, const PointSrc* src, int mode, cons
   a.P = P;
   a.xyz = pts.xyz;
   a.feats4 = reinterpret_cast<const float4*>(pts.feats);
+  a.feat_half = pts.feat_half ? 1 : 0;
   a.k = pts.k;
   a.eps = pts.eps;
   a.h0 = pts.spacing[0];

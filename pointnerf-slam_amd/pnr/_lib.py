@@ -45,7 +45,7 @@ class Points(ctypes.Structure):
         ('xyz', c_void_p), ('feats', c_void_p), ('n_points', c_int64), ('mode', c_int32), ('k', c_int32),
         ('radius', c_float), ('eps', c_float), ('spacing', c_float * 3), ('cell', c_float),
         ('origin', c_float * 3), ('table_bits', c_int32), ('index', c_void_p), ('fc_packed', c_void_p),
-        ('g_feats', c_void_p), ('g_fc', c_void_p),
+        ('g_feats', c_void_p), ('g_fc', c_void_p), ('feat_half', c_int32),
     ]
 
 

@@ -21,7 +21,7 @@ from .points import NeuralPoints
 
 CKPT_KEYS = ('c', 'decoder_state_dict', 'gt_c2w_list', 'estimate_c2w_list', 'keyframe_list',
              'selected_keyframes', 'idx')  # src/utils/Logger.py:23-31
-_PT_FIELDS = ('mode', 'k', 'radius', 'eps', 'spacing', 'cell', 'origin', 'table_bits')
+_PT_FIELDS = ('mode', 'k', 'radius', 'eps', 'spacing', 'cell', 'origin', 'table_bits', 'feat_dtype')
 
 
 def c_state(c):

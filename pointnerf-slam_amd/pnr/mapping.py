@@ -110,6 +110,7 @@ class MapStep:
         self.decoder._packed.invalidate()
         if self.points is not None:
             self.decoder._packed_fc.invalidate()
+            self.points.invalidate_feats()  # the f16 feature copy, if any
 
     def loss(self, rays_o, rays_d, gt_depth, gt_color, t_rand=None, far_clamp=None):
         r, dec = self.renderer, self.decoder

@@ -30,8 +30,10 @@ _MODES = {'idw': _lib.GATHER_IDW, 'trilinear': _lib.GATHER_TRILINEAR}
 class NeuralPoints(nn.Module):
     def __init__(self, xyz: torch.Tensor, feats: torch.Tensor = None, c_dim: int = 32, mode: str = 'idw',
                  k: int = 8, radius: float = 0.02, eps: float = 1e-6, spacing=None, cell: float = None,
-                 origin=None, table_bits: int = None):
+                 origin=None, table_bits: int = None, feat_dtype: str = 'float32'):
         super().__init__()
+        if feat_dtype not in ('float32', 'float16'):
+            raise ValueError("pnr.NeuralPoints: feat_dtype must be 'float32' or 'float16'")
         if c_dim != _lib.C_DIM:
             raise NotImplementedError(f'pnr.NeuralPoints: c_dim must be {_lib.C_DIM}')
         if mode not in _MODES:
@@ -63,6 +65,30 @@ class NeuralPoints(nn.Module):
         self.table_bits = int(table_bits)
         self._index = None
         self._index_key = None
+        # float16 features (the C5 budget): the gather reads an f16 copy of the fp32
+        # master `feats` (the optimiser's parameter); the copy is refreshed when feats changed
+        self.feat_dtype = feat_dtype
+        self._feats_h = None
+        self._feats_h_key = None
+
+    def invalidate_feats(self):
+        """Mark the f16 copy stale (after an in-place update torch does not version, e.g. the
+        pnr Adam kernel writing through a raw pointer)."""
+        self._feats_h_key = None
+
+    def _feats_for_gather(self):
+        if self.feat_dtype == 'float32':
+            return self.feats
+        f = self.feats
+        key = (f.data_ptr(), f._version)
+        if self._feats_h is None or self._feats_h.shape != f.shape or self._feats_h.device != f.device:
+            self._feats_h = torch.empty(f.shape, dtype=torch.float16, device=f.device)
+            self._feats_h_key = None
+        if self._feats_h_key != key:
+            with torch.no_grad():
+                self._feats_h.copy_(f)
+            self._feats_h_key = key
+        return self._feats_h
 
     @classmethod
     def from_grid(cls, grid: torch.Tensor, bound: torch.Tensor, **kw):
@@ -82,7 +108,8 @@ class NeuralPoints(nn.Module):
     def _struct(self) -> _lib.Points:
         s = _lib.Points()
         s.xyz = self.xyz.data_ptr()
-        s.feats = self.feats.data_ptr()
+        s.feats = self._feats_for_gather().data_ptr()
+        s.feat_half = 1 if self.feat_dtype == 'float16' else 0
         s.n_points = self.xyz.shape[0]
         s.mode = _MODES[self.mode]
         s.k = self.k
@@ -136,6 +163,8 @@ class NeuralPoints(nn.Module):
         st = self.__dict__.copy()
         st['_index'] = None  # device caches never cross pickling / deepcopy
         st['_index_key'] = None
+        st['_feats_h'] = None
+        st['_feats_h_key'] = None
         return st
 
 

@@ -43,7 +43,7 @@ def test_python_binding_covers_header():
 
 def test_host_only_calls(lib):
     lib.pnr_abi_version.restype = ctypes.c_int
-    assert lib.pnr_abi_version() == 5
+    assert lib.pnr_abi_version() == 6
     lib.pnr_mlp_packed_floats.restype = ctypes.c_size_t
     # fp32 images 486,688 + bf16x3 / bf16 / f16x3 forward streams 229,376 / 118,784 / 229,376
     # + bf16x3 delta-chain stream 225,280 + raw table 2,048 + fp32 Wo 1,024
@@ -61,10 +61,10 @@ def test_params_struct_layout():
     assert _lib.RenderParams.precision.offset == 600
     assert _lib.RenderParams.bound.offset == 16 and _lib.RenderParams.t_vals.offset == 72
     assert _lib.RenderParams.points.offset == 592
-    # pnr_points: 2 ptr, int64, 2 int32, 2 float, float[3], float, float[3], int32, 4 ptr
+    # pnr_points: 2 ptr, int64, 2 int32, 2 float, float[3], float, float[3], int32, 4 ptr, int32 (ABI 6)
     assert _lib.Points.n_points.offset == 16 and _lib.Points.spacing.offset == 40
     assert _lib.Points.table_bits.offset == 68 and _lib.Points.index.offset == 72
-    assert ctypes.sizeof(_lib.Points) == 104
+    assert _lib.Points.feat_half.offset == 104 and ctypes.sizeof(_lib.Points) == 112
 
 
 def test_workspace_queries_and_arg_errors(lib):

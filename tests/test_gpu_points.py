@@ -282,3 +282,57 @@ def test_regulation_with_points(pnr_mod, dev):
     for k in ('fc_c.0.weight', 'fc_c.3.bias', 'pts_linears.2.weight'):
         ref = ref_p[k].grad
         close(dict(dec.named_parameters())[k].grad, ref, 2e-3 * ref.abs().max().item(), k)
+
+
+def test_gather_f16_features_equal_rounded_fp32(pnr_mod, dev):
+    """feat_dtype='float16' (pnr_points.feat_half, the C5 budget): the gather reads an f16 copy
+    of the fp32 features and sums in fp32, so it equals the fp32 gather over the f16-rounded
+    features -- c bit for bit, dL/dfeats (independent of the features) and dL/dp to fp32 atomic
+    ordering (1e-6 of max)."""
+    xyz, feats, q = random_cloud(seed=6)
+    kw = dict(mode='idw', radius=0.06, k=8)
+    p16 = pnr_mod.NeuralPoints(xyz.to(dev), feats.to(dev), feat_dtype='float16', **kw).to(dev)
+    p32 = pnr_mod.NeuralPoints(xyz.to(dev), feats.half().float().to(dev), **kw).to(dev)
+    gc = torch.randn((q.shape[0], 32), generator=torch.Generator().manual_seed(2)).to(dev)
+    outs = []
+    for pts in (p16, p32):
+        qd = q.to(dev).requires_grad_(True)
+        c = pts.gather(qd)
+        (c * gc).sum().backward()
+        outs.append((c.detach(), pts.feats.grad.clone(), qd.grad.clone()))
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert (outs[0][0] != 0).any()
+    close(outs[0][1], outs[1][1], 1e-6 * outs[1][1].abs().max().item(), 'dL/dfeats')
+    close(outs[0][2], outs[1][2], 1e-6 * outs[1][2].abs().max().item(), 'dL/dp')
+    # the f16 copy follows in-place updates of the fp32 master
+    with torch.no_grad():
+        p16.feats.mul_(0.5)
+        p32.feats.copy_((feats * 0.5).half().float().to(dev))
+    assert torch.equal(p16.gather(q.to(dev)), p32.gather(q.to(dev)))
+
+
+def test_map_step_with_f16_features(pnr_mod, dev):
+    """A mapping step with f16 features: loss equal to the fp32-feature step on the rounded
+    features; Adam updates the fp32 master and the next gather sees the new f16 copy."""
+    from pnr.mapping import MapStep
+    scene = load_golden('scene.npz')
+    bound = torch.from_numpy(scene['bound'])
+    ro, rd, gt, xyz, feats = surface_cloud(dev)
+    n = 512
+    ro, rd, gt = ro[:n].to(dev), rd[:n].to(dev), gt[:n].to(dev)
+    col = torch.rand((n, 3), generator=torch.Generator().manual_seed(1)).to(dev)
+    t_rand = torch.rand((n, 32), generator=torch.Generator().manual_seed(2)).to(dev)
+    params = RP.init_fc_c(golden_params('trained'), seed=1)
+    losses = []
+    for fd, f0 in (('float16', feats), ('float32', feats.half().float())):
+        pts = pnr_mod.NeuralPoints(xyz.to(dev), f0.to(dev), mode='idw', radius=0.04, k=8, feat_dtype=fd).to(dev)
+        dec = pnr_mod.MLP(name='color', dim=3, c_dim=32, color=True, skips=[], n_blocks=4, hidden_size=256)
+        dec.load_state_dict({k: v.clone() for k, v in params.items()})
+        ms = MapStep(make_renderer(pnr_mod, bound), dec.to(dev), points=pts, feat_lr=1e-2)
+        l1 = float(ms(ro, rd, gt, col, t_rand))
+        l2 = float(ms(ro, rd, gt, col, t_rand))
+        losses.append((l1, l2))
+        if fd == 'float16':
+            assert torch.equal(pts._feats_for_gather(), pts.feats.detach().half())
+    assert abs(losses[0][0] - losses[1][0]) <= 1e-5 * abs(losses[1][0])
+    assert losses[0][1] != losses[0][0]
