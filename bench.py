@@ -167,7 +167,9 @@ def gather_roofline(dev, voxel=0.001, k=8, reps=5, feat_dtype='float32'):
     byt = gather_bytes(P, nb, k, feat_bytes=64 if feat_dtype == 'float16' else 128)
     gbs = byt / (avg * 1e-3) / 1e9
     return {'bound': 'hbm', 'achieved': round(gbs, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
-            'frac': round(gbs / HBM_PEAK_GBS, 4), 'traffic': pmc_traffic('k_gather', P),
+            'frac': round(gbs / HBM_PEAK_GBS, 4),
+            # PMC bytes per sample were measured on the float32-feature gather only
+            'traffic': pmc_traffic('k_gather', P) if feat_dtype == 'float32' else None,
             'kernel': 'k_gather_probe+k_gather_search',
             'avg_launch_ms': round(avg, 3), 'launches': launches, 'samples': P, 'points': int(xyz.shape[0]),
             'neighbours_per_sample': round(nb / P, 3), 'radius': 2 * voxel, 'k': k, 'point_features': feat_dtype,
