@@ -394,6 +394,27 @@ struct GatherArgs {
   WorkList wl;           // (x, y, z, sample row bits) of the samples that may have neighbours
 };
 
+// Streaming (non-temporal) 16-B stores for the probe's zero fill: whole 128-B lines per 8 lanes,
+// read by no kernel of this launch.  Measured (profiles/r01f_gather_nt_ablation.txt): the gather
+// 1.53 -> 1.39 ms, and 1.36 ms with the search's c rows (8 lanes x 16 B = one 128-B row) streamed
+// too.  On partial lines they cost far more: with the search's 4-B idx/w stores streamed the
+// gather took 2.05 ms, and the MLP's 8-B activation saves made the training forward 5x slower
+// (10.8 -> 51.7 ms), so both keep ordinary stores.
+#ifndef PNR_NT_FILL
+#define PNR_NT_FILL 1
+#endif
+template <typename T>
+__device__ __forceinline__ void nt_store(T* p, const T& v) {
+  if (PNR_NT_FILL) {
+    __builtin_nontemporal_store(v.x, &p->x);
+    __builtin_nontemporal_store(v.y, &p->y);
+    __builtin_nontemporal_store(v.z, &p->z);
+    __builtin_nontemporal_store(v.w, &p->w);
+  } else {
+    *p = v;
+  }
+}
+
 // Pass 1, one thread per sample row: the occupancy bit of each sample's probe block; the hits go
 // to the work list, the block zero-fills the other rows of its 256 with coalesced stores.
 template <int SRC>
@@ -421,15 +442,15 @@ __global__ __launch_bounds__(256) void k_gather_probe(GatherArgs a) {
   {
     float4* c4 = reinterpret_cast<float4*>(a.c) + r0 * 8;
     for (int e = threadIdx.x; e < nrow * 8; e += 256)
-      if (!s_has[e >> 3]) c4[e] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (!s_has[e >> 3]) nt_store(c4 + e, make_float4(0.f, 0.f, 0.f, 0.f));
     if (a.idx && p < a.rows && !has) {  // this row's k (index, weight) slots
       if (a.k == 8 && ((reinterpret_cast<uintptr_t>(a.idx) | reinterpret_cast<uintptr_t>(a.w)) & 15) == 0) {
         int4* i4 = reinterpret_cast<int4*>(a.idx) + p * 2;
         float4* w4 = reinterpret_cast<float4*>(a.w) + p * 2;
-        i4[0] = make_int4(-1, -1, -1, -1);
-        i4[1] = make_int4(-1, -1, -1, -1);
-        w4[0] = make_float4(0.f, 0.f, 0.f, 0.f);
-        w4[1] = make_float4(0.f, 0.f, 0.f, 0.f);
+        nt_store(i4, make_int4(-1, -1, -1, -1));
+        nt_store(i4 + 1, make_int4(-1, -1, -1, -1));
+        nt_store(w4, make_float4(0.f, 0.f, 0.f, 0.f));
+        nt_store(w4 + 1, make_float4(0.f, 0.f, 0.f, 0.f));
       } else {
         for (int t = 0; t < a.k; ++t) {
           a.idx[p * a.k + t] = -1;
@@ -647,7 +668,7 @@ __device__ __forceinline__ void search_round(const GatherArgs& a, SearchLds& L, 
           }
         }
       }
-      reinterpret_cast<float4*>(a.c)[(int64_t)rw * 8 + q] = acc;
+      nt_store(reinterpret_cast<float4*>(a.c) + (int64_t)rw * 8 + q, acc);  // 8 lanes: one 128-B row
     }
   }
 }
