@@ -338,6 +338,27 @@ __device__ __forceinline__ float4 load_feat4(const float4* f, int half, int64_t 
 __device__ __forceinline__ float load_feat1(const float4* f, int half, int64_t i) {
   return half ? (float)reinterpret_cast<const _Float16*>(f)[i] : reinterpret_cast<const float*>(f)[i];
 }
+// Streaming (non-temporal) 16-B stores for the probe's zero fill: whole 128-B lines per 8 lanes,
+// read by no kernel of this launch.  Measured (profiles/r01f_gather_nt_ablation.txt): the gather
+// 1.53 -> 1.39 ms, and 1.36 ms with the search's c rows (8 lanes x 16 B = one 128-B row) streamed
+// too.  On partial lines they cost far more: with the search's 4-B idx/w stores streamed the
+// gather took 2.05 ms, and the MLP's 8-B activation saves made the training forward 5x slower
+// (10.8 -> 51.7 ms), so both keep ordinary stores.
+#ifndef PNR_NT_FILL
+#define PNR_NT_FILL 1
+#endif
+template <typename T>
+__device__ __forceinline__ void nt_store(T* p, const T& v) {
+  if (PNR_NT_FILL) {
+    __builtin_nontemporal_store(v.x, &p->x);
+    __builtin_nontemporal_store(v.y, &p->y);
+    __builtin_nontemporal_store(v.z, &p->z);
+    __builtin_nontemporal_store(v.w, &p->w);
+  } else {
+    *p = v;
+  }
+}
+
 // Work lists: samples are appended by wave (one atomic per wave) to one of kLists sub-lists, each
 // with its own counter on its own 128-B line, dealt round-robin by wave -- a single counter would
 // serialise ~10^5 same-address atomics.  Consumers walk (sub-list, 256-item chunk) tasks.
@@ -393,27 +414,6 @@ struct GatherArgs {
   float* w;              // (rows, k) or null
   WorkList wl;           // (x, y, z, sample row bits) of the samples that may have neighbours
 };
-
-// Streaming (non-temporal) 16-B stores for the probe's zero fill: whole 128-B lines per 8 lanes,
-// read by no kernel of this launch.  Measured (profiles/r01f_gather_nt_ablation.txt): the gather
-// 1.53 -> 1.39 ms, and 1.36 ms with the search's c rows (8 lanes x 16 B = one 128-B row) streamed
-// too.  On partial lines they cost far more: with the search's 4-B idx/w stores streamed the
-// gather took 2.05 ms, and the MLP's 8-B activation saves made the training forward 5x slower
-// (10.8 -> 51.7 ms), so both keep ordinary stores.
-#ifndef PNR_NT_FILL
-#define PNR_NT_FILL 1
-#endif
-template <typename T>
-__device__ __forceinline__ void nt_store(T* p, const T& v) {
-  if (PNR_NT_FILL) {
-    __builtin_nontemporal_store(v.x, &p->x);
-    __builtin_nontemporal_store(v.y, &p->y);
-    __builtin_nontemporal_store(v.z, &p->z);
-    __builtin_nontemporal_store(v.w, &p->w);
-  } else {
-    *p = v;
-  }
-}
 
 // Pass 1, one thread per sample row: the occupancy bit of each sample's probe block; the hits go
 // to the work list, the block zero-fills the other rows of its 256 with coalesced stores.
@@ -629,14 +629,28 @@ __device__ __forceinline__ void search_round(const GatherArgs& a, SearchLds& L, 
     const float Wd = W > 0.f ? W : 1.0f;
     __syncthreads();  // every thread is past its range reads: the LDS becomes the feature lists
     L.f.row[tid] = row;
+    float wnv[PNR_MAX_K];
 #pragma unroll
     for (int t = 0; t < PNR_MAX_K; ++t) {
       const float wn = ki[t] >= 0 ? wv_[t] / Wd : 0.f;
+      wnv[t] = wn;
       L.f.idx[tid * PNR_MAX_K + t] = ki[t];
       L.f.w[tid * PNR_MAX_K + t] = wn;
-      if (row >= 0 && t < a.k && a.idx) {
-        a.idx[(int64_t)row * a.k + t] = ki[t];
-        a.w[(int64_t)row * a.k + t] = wn;
+    }
+    if (row >= 0 && a.idx) {
+      // k = 8: the row's 8 indices and 8 weights as 16-B stores (1.37 -> 1.31 ms per gather)
+      if (PNR_MAX_K == 8 && a.k == 8 && ((reinterpret_cast<uintptr_t>(a.idx) | reinterpret_cast<uintptr_t>(a.w)) & 15) == 0) {
+        int4* i4 = reinterpret_cast<int4*>(a.idx) + (int64_t)row * 2;
+        float4* w4 = reinterpret_cast<float4*>(a.w) + (int64_t)row * 2;
+        i4[0] = make_int4(ki[0], ki[1], ki[2], ki[3]);
+        i4[1] = make_int4(ki[4], ki[5], ki[6], ki[7]);
+        w4[0] = make_float4(wnv[0], wnv[1], wnv[2], wnv[3]);
+        w4[1] = make_float4(wnv[4], wnv[5], wnv[6], wnv[7]);
+      } else {
+        for (int t = 0; t < a.k; ++t) {
+          a.idx[(int64_t)row * a.k + t] = ki[t];
+          a.w[(int64_t)row * a.k + t] = wnv[t];
+        }
       }
     }
     __syncthreads();
