@@ -7,6 +7,9 @@ there are exactly two collectives:
     src/utils/Renderer.py:112 (a cross-ray coupling), so sharded results equal 1-GPU results;
   * all_reduce(SUM) of the one flat fp32 gradient buffer (222,747 words = 891 KB), latency-bound
     on xGMI, issued once per step; Adam then runs identically on every rank.
+With neural points and `DataParallel(shard_points=True)` the point-feature tail of that buffer
+is reduce-scattered instead, Adam updates each rank's owned feature range, and the features are
+all-gathered (reduce_scatter_ / all_gather_).
 """
 from __future__ import annotations
 
@@ -40,8 +43,9 @@ def shard_bounds(n, rank, world):
 
 
 class DataParallel:
-    def __init__(self, group=None):
+    def __init__(self, group=None, shard_points=False):
         self.group = group
+        self.shard_points = bool(shard_points)
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
 
     def global_far_clamp(self, gt_depth_local):
@@ -56,6 +60,47 @@ class DataParallel:
         if self.world > 1:
             dist.all_reduce(flat_grad, op=dist.ReduceOp.SUM, group=self.group)
         return flat_grad
+
+    # -- sharded point-feature update (the 1M-point C5 budget) --------------------
+    # The point features are the bulk of the gradient (1M x 32 fp32 = 128 MB) and each rank only
+    # needs the update of its own slice: reduce-scatter the feature gradient into owned ranges,
+    # run Adam on the owned range, all-gather the updated features.  The bytes on the wire equal
+    # one all-reduce; the Adam work is divided by the world size.
+    def feature_shard(self, n):
+        """This rank's owned range [a, b) of an n-word segment (equal padded shards)."""
+        per = -(-n // self.world) if n > 0 else 0
+        rank = dist.get_rank(self.group) if self.world > 1 else 0
+        a = min(n, rank * per)
+        return a, min(n, a + per), per
+
+    def reduce_scatter_(self, seg):
+        """Sum `seg` (1-D) over ranks into this rank's owned range of `seg` (other words are left
+        as they were).  Returns (a, b)."""
+        n = seg.numel()
+        a, b, per = self.feature_shard(n)
+        if self.world == 1:
+            return a, b
+        buf = seg
+        if per * self.world != n:
+            buf = torch.zeros(per * self.world, dtype=seg.dtype, device=seg.device)
+            buf[:n].copy_(seg)
+        out = torch.empty(per, dtype=seg.dtype, device=seg.device)
+        dist.reduce_scatter_tensor(out, buf, op=dist.ReduceOp.SUM, group=self.group)
+        seg[a:b].copy_(out[:b - a])
+        return a, b
+
+    def all_gather_(self, seg):
+        """Every rank's owned range of `seg` (1-D) to every rank."""
+        n = seg.numel()
+        a, b, per = self.feature_shard(n)
+        if self.world == 1:
+            return seg
+        mine = torch.zeros(per, dtype=seg.dtype, device=seg.device)
+        mine[:b - a].copy_(seg[a:b])
+        out = torch.empty(per * self.world, dtype=seg.dtype, device=seg.device)
+        dist.all_gather_into_tensor(out, mine, group=self.group)
+        seg.copy_(out[:n])
+        return seg
 
     def barrier(self):
         if self.world > 1:

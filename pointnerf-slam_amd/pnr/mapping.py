@@ -98,8 +98,16 @@ class MapStep:
             params.append(points.feats)
         self.flat = FlatParams(params)
         segs = [(0, n_dec, lr)]
+        self.n_dec = n_dec
+        self.shard = points is not None and ddp is not None and getattr(ddp, 'shard_points', False)
         if points is not None:
-            segs.append((n_dec, points.feats.numel(), lr if feat_lr is None else feat_lr))
+            flr = lr if feat_lr is None else feat_lr
+            if self.shard:  # Adam on this rank's owned feature range only (pnr.dist reduce_scatter_)
+                a, b, _ = ddp.feature_shard(points.feats.numel())
+                if b > a:
+                    segs.append((n_dec + a, b - a, flr))
+            else:
+                segs.append((n_dec, points.feats.numel(), flr))
         self.opt = Adam(self.flat, lr, on_update=self._invalidate, segments=segs)
         self.c = {} if points is None else {'points_' + getattr(decoder, 'name', ''): points}
         self.w_color = w_color_loss
@@ -127,9 +135,15 @@ class MapStep:
         far_clamp = self.ddp.global_far_clamp(gt_depth) if self.ddp is not None else None
         loss = self.loss(rays_o, rays_d, gt_depth, gt_color, t_rand, far_clamp)
         loss.backward()
-        if self.ddp is not None:
+        if self.ddp is not None and self.shard:
+            self.ddp.allreduce_(self.flat.grad[:self.n_dec])
+            self.ddp.reduce_scatter_(self.flat.grad[self.n_dec:])
+        elif self.ddp is not None:
             self.ddp.allreduce_(self.flat.grad)
         self.opt.step()
+        if self.shard:
+            self.ddp.all_gather_(self.flat.data[self.n_dec:])
+            self.points.invalidate_feats()
         return loss.detach()
 
 

@@ -104,3 +104,59 @@ def test_dp_mapping_grads_match_single_process():
     ref.mapping_loss(d, c, gt, torch.from_numpy(G['map_gt_color'][:n].copy()), sig).backward()
     g_full = _flat_grad(params).numpy()
     np.testing.assert_allclose(g_dp, g_full, rtol=1e-4, atol=1e-6 * np.abs(g_full).max())
+
+
+def _adam(p, g, m, v, step, lr, b1=0.9, b2=0.999, eps=1e-8):
+    """torch.optim.Adam's update on a slice (the arithmetic pnr_adam_step follows)."""
+    m.mul_(b1).add_(g, alpha=1 - b1)
+    v.mul_(b2).addcmul_(g, g, value=1 - b2)
+    den = (v.sqrt() / (1 - b2 ** step) ** 0.5).add_(eps)
+    p.addcdiv_(m, den, value=-lr / (1 - b1 ** step))
+
+
+def _shard_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    sys.path.insert(0, os.path.join(REPO, 'pointnerf-slam_amd'))
+    torch.set_num_threads(1)
+    from pnr import dist as pdist
+    pdist.init(backend='gloo')
+    ddp = pdist.DataParallel(shard_points=True)
+    n_dec, n_f = 100, 3203  # odd feature length: padded shards
+    gen = torch.Generator().manual_seed(0)
+    init = torch.randn(n_dec + n_f, generator=gen)
+    dense, shard = init.clone(), init.clone()
+    md, vd, ms_, vs = (torch.zeros(n_dec + n_f) for _ in range(4))
+    a, b, _ = ddp.feature_shard(n_f)
+    for step in (1, 2, 3):
+        g_local = torch.randn(n_dec + n_f, generator=torch.Generator().manual_seed(100 * step + rank))
+        gd = g_local.clone()  # dense: one all-reduce, Adam everywhere
+        ddp.allreduce_(gd)
+        _adam(dense, gd, md, vd, step, 1e-2)
+        gs = g_local.clone()  # sharded: decoder all-reduce, feature reduce-scatter, owned Adam, all-gather
+        ddp.allreduce_(gs[:n_dec])
+        assert ddp.reduce_scatter_(gs[n_dec:]) == (a, b)
+        _adam(shard[:n_dec], gs[:n_dec], ms_[:n_dec], vs[:n_dec], step, 1e-2)
+        sl = slice(n_dec + a, n_dec + b)
+        _adam(shard[sl], gs[sl], ms_[sl], vs[sl], step, 1e-2)
+        ddp.all_gather_(shard[n_dec:])
+    q.put((rank, bool(torch.equal(dense, shard)), (a, b)))
+    dist.destroy_process_group()
+
+
+def test_sharded_feature_update_equals_dense():
+    """pnr.dist reduce_scatter_ / all_gather_ (the sharded point-feature update of
+    MapStep(ddp=DataParallel(shard_points=True))): identical parameters to the dense all-reduce
+    update, over 3 Adam steps, with a feature length that does not divide by the world size."""
+    world = 2
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_shard_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(world))
+    for p in ps:
+        p.join(timeout=60)
+    assert all(ok for _, ok, _ in res), res
+    assert [r[2] for r in res] == [(0, 1602), (1602, 3203)]

@@ -336,3 +336,29 @@ def test_map_step_with_f16_features(pnr_mod, dev):
             assert torch.equal(pts._feats_for_gather(), pts.feats.detach().half())
     assert abs(losses[0][0] - losses[1][0]) <= 1e-5 * abs(losses[1][0])
     assert losses[0][1] != losses[0][0]
+
+
+def test_map_step_sharded_features_single_rank(pnr_mod, dev):
+    """MapStep(ddp=DataParallel(shard_points=True)) at world size 1 takes the sharded code path
+    (owned-range Adam segment, reduce-scatter / all-gather no-ops) and must equal the plain step."""
+    from pnr.mapping import MapStep
+    from pnr.dist import DataParallel
+    scene = load_golden('scene.npz')
+    bound = torch.from_numpy(scene['bound'])
+    ro, rd, gt, xyz, feats = surface_cloud(dev)
+    n = 256
+    ro, rd, gt = ro[:n].to(dev), rd[:n].to(dev), gt[:n].to(dev)
+    col = torch.rand((n, 3), generator=torch.Generator().manual_seed(1)).to(dev)
+    t_rand = torch.rand((n, 32), generator=torch.Generator().manual_seed(2)).to(dev)
+    params = RP.init_fc_c(golden_params('trained'), seed=1)
+    out = []
+    for ddp in (None, DataParallel(shard_points=True)):
+        pts = pnr_mod.NeuralPoints(xyz.to(dev), feats.to(dev), mode='idw', radius=0.04, k=8).to(dev)
+        dec = pnr_mod.MLP(name='color', dim=3, c_dim=32, color=True, skips=[], n_blocks=4, hidden_size=256)
+        dec.load_state_dict({k: v.clone() for k, v in params.items()})
+        ms = MapStep(make_renderer(pnr_mod, bound), dec.to(dev), points=pts, feat_lr=1e-2, ddp=ddp)
+        assert ms.shard == (ddp is not None)
+        losses = [float(ms(ro, rd, gt, col, t_rand)) for _ in range(2)]
+        out.append((losses, ms.flat.data.clone()))
+    assert out[0][0] == out[1][0]
+    assert torch.equal(out[0][1], out[1][1])
