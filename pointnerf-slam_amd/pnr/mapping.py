@@ -9,7 +9,9 @@ The decoder parameters live in ONE flat float32 buffer (and so do their grads), 
 parallel caller reduces a single 891 KB buffer per step and Adam is one kernel
 (pnr_adam_step).  With neural points the fc_c tensors and the point features
 join the same buffer (features last, with their own learning rate: a second Adam launch over the
-tail of the buffer), still one all-reduce per step.  `ddp` (pnr.dist.DataParallel) adds the cross-GPU gradient all-reduce and the
+tail of the buffer), still one all-reduce per step -- or, with DataParallel(shard_points=True), a
+reduce-scatter of the feature tail, Adam on the owned feature range and an all-gather.  `ddp`
+(pnr.dist.DataParallel) adds the cross-GPU gradient all-reduce and the
 global far clamp; without it the step is single-GPU and bit-identical to the reference order of
 operations of a 1-process Mapper.
 """
