@@ -689,7 +689,14 @@ __device__ __forceinline__ void search_round(const GatherArgs& a, SearchLds& L, 
 
 // Pass 2: persistent blocks over the probe's work list, one search round per 256-item chunk.
 template <int KER>
-__global__ __launch_bounds__(kSearchBlock) void k_gather_search(GatherArgs a) {
+// The search is latency-bound: 7 waves per SIMD (72 VGPRs, one 8-B spill) instead of the 6 its
+// free allocation gives: 1.31 -> 1.25 ms per gather.  8 waves (64 VGPRs, 11 spills) measured the
+// same as 7; 8 header loads in flight instead of 4 cost 2 waves of occupancy and took 1.49 ms
+// (profiles/r01g_gather_occupancy_ablation.txt).
+#ifndef PNR_SEARCH_WAVES
+#define PNR_SEARCH_WAVES 7
+#endif
+__global__ __launch_bounds__(kSearchBlock, PNR_SEARCH_WAVES) void k_gather_search(GatherArgs a) {
   __shared__ SearchLds L;
   const int64_t nchunk = (a.wl.cap + kSearchBlock - 1) / kSearchBlock;
   for (int64_t task = blockIdx.x; task < kLists * nchunk; task += gridDim.x) {
