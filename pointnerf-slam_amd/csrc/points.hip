@@ -497,7 +497,13 @@ __device__ __forceinline__ double kstage(double& key, double kn) {
   return hi;
 }
 
-constexpr int kSearchBlock = 256;
+// One wave per search block: a round's barriers then never hold a finished wave behind the
+// block's slowest one.  1.25 -> 1.20 ms per gather against 256-thread blocks (128: 1.22 ms;
+// profiles/r01g_gather_occupancy_ablation.txt).
+#ifndef PNR_SEARCH_BLOCK
+#define PNR_SEARCH_BLOCK 64
+#endif
+constexpr int kSearchBlock = PNR_SEARCH_BLOCK;
 union SearchLds {
   struct {
     int2 rng[8][kSearchBlock];      // [range][thread] (start, end): conflict-free per-thread access
@@ -687,7 +693,7 @@ __device__ __forceinline__ void search_round(const GatherArgs& a, SearchLds& L, 
   }
 }
 
-// Pass 2: persistent blocks over the probe's work list, one search round per 256-item chunk.
+// Pass 2: persistent blocks over the probe's work list, one search round per kSearchBlock-item chunk.
 template <int KER>
 // The search is latency-bound: 7 waves per SIMD (72 VGPRs, one 8-B spill) instead of the 6 its
 // free allocation gives: 1.31 -> 1.25 ms per gather.  8 waves (64 VGPRs, 11 spills) measured the
