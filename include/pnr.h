@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define PNR_ABI_VERSION 6
+#define PNR_ABI_VERSION 7
 #define PNR_N_PARAMS 11
 #define PNR_MAX_SAMPLES 64      /* N_samples + N_importance per ray */
 #define PNR_C_DIM 32            /* neural-point feature width (decoder.py:122-125 fc_c input) */
@@ -70,19 +70,27 @@ enum { PNR_GATHER_IDW = 0, PNR_GATHER_TRILINEAR = 1 };
 /* Arithmetic of the decoder matmuls (build-defined; the reference runs torch fp32 matmuls).
  *   PNR_PREC_FP32:   v_mfma_f32_32x32x2_f32, an exact fp32 fma chain (bitwise the CPU order per
  *                    product; only the summation order differs from torch CPU).
- *   PNR_PREC_BF16X3: every fp32 operand split x = hi + lo into two bf16 parts, W x computed as
- *                    Wh xh + Wh xl + Wl xh on v_mfma_f32_32x32x16_bf16 with fp32 accumulation:
- *                    ~2^-16 relative per product (fp32-class), 5.3x the fp32 MFMA rate.
- *   PNR_PREC_BF16:   plain bf16 operands, fp32 accumulation (BASELINE config C3).
- *   PNR_PREC_F16X3:  the split of BF16X3 in f16 (22 significant bits, ~2^-21 per product) on
- *                    v_mfma_f32_32x32x16_f16; the packer scales each weight tensor by a power of
- *                    two (max |W| s <= 2^14) and the kernel scales the accumulator back exactly.
- *                    Needs |activations| < 65504 (f16 range).
+ *   PNR_PREC_F16X3:  (default) every fp32 operand split x = hi + lo into two f16 parts (22
+ *                    significant bits), W x computed as Wh xh + Wh xl + Wl xh on
+ *                    v_mfma_f32_32x32x16_f16 with fp32 accumulation (~2^-21 relative per product),
+ *                    5.3x the fp32 MFMA rate.  The packer scales each weight tensor by a power of two
+ *                    (max |W| s <= 2^14) and the kernel scales the accumulator back exactly.  The
+ *                    forward needs |activations| < 65504 (f16 range): a larger value sets
+ *                    PNR_STATUS_F16_RANGE in *prm->status.
+ *   PNR_PREC_BF16X3: the same split in bf16 parts (16 significant bits, no range limit).
+ *   PNR_PREC_BF16:   plain bf16 forward operands, fp32 accumulation (BASELINE config C3).
  * Fourier features, bias, ReLU, compositing and all float64 work stay fp32 / fp64 in every mode.
- * Backward: PNR_PREC_FP32 runs the delta chain on fp32 MFMA; every other mode runs it as bf16x3
- * (bf16 parts keep the fp32 exponent range of tiny gradients), and so do the 256-row weight-gradient
- * GEMMs (dW0..dW3); the small ones (dWo, dB, dWc) stay fp32. */
+ * Backward of every mode but PNR_PREC_FP32 (which runs fp32 MFMA throughout): the delta chain is
+ * f16x3 with an exact per-point power-of-two scale (any gradient magnitude), and the weight-gradient
+ * GEMMs dW0..dW3, dWc are f16x3 on fp32-stored activations and deltas (per-wave power-of-two scale of
+ * the deltas); dWo and dB are fp32 FMA reductions.  Every GEMM of the backward thus carries >= 22
+ * significant bits per operand and accumulates in fp32. */
 enum { PNR_PREC_FP32 = 0, PNR_PREC_BF16X3 = 1, PNR_PREC_BF16 = 2, PNR_PREC_F16X3 = 3 };
+
+/* Status bits (ABI 7) the kernels OR into the caller's device word pnr_render_params.status:
+ *   PNR_STATUS_F16_RANGE  an F16X3 forward met a value >= 65504 to split into f16 parts (the result
+ *                         of that call is not fp32-faithful; re-run it in PNR_PREC_FP32). */
+enum { PNR_STATUS_F16_RANGE = 1 };
 
 typedef struct pnr_points {
   const float* xyz;         /* (M,3) float32 point positions                                  */
@@ -112,7 +120,9 @@ typedef struct pnr_render_params {
   int32_t n_importance;     /* cfg['rendering']['N_importance'] (n_samples+n_importance <= 64) */
   int32_t lindisp;          /* cfg['rendering']['lindisp']                       */
   int32_t far_mode;         /* 0: clamp far to max(1.2*gt) of THIS batch (Renderer.py:112);
-                               1: clamp to `far_clamp` (global max supplied by a sharded caller) */
+                               1: clamp to `far_clamp` (global max supplied by a sharded caller);
+                               2: clamp to *far_clamp_dev (a device float32, e.g. the all-reduced
+                                  max of a sharded batch: no host round trip, graph-capturable) */
   double bound[6];          /* slam.bound (3,2) float64 row-major: x0,x1,y0,y1,z0,z1   */
   double far_clamp;         /* used when far_mode == 1                                 */
   float t_vals[PNR_MAX_SAMPLES];   /* torch.linspace(0,1,n_samples) float32           */
@@ -121,6 +131,8 @@ typedef struct pnr_render_params {
   int32_t need_ray_grads;          /* backward also produces dL/drays_o, dL/drays_d (tracking) */
   const pnr_points* points;        /* neural-point features, NULL = the reference decoder (c_dim=0) */
   int32_t precision;               /* PNR_PREC_* of the decoder matmuls                           */
+  int32_t* status;                 /* ABI 7: device int32 receiving PNR_STATUS_* bits (ORed), or NULL */
+  const float* far_clamp_dev;      /* ABI 7: device float32 far clamp of far_mode 2                */
 } pnr_render_params;
 
 /* ---- library identity -------------------------------------------------------------------- */

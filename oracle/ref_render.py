@@ -142,6 +142,41 @@ def mlp_forward(params: Params, p: torch.Tensor) -> torch.Tensor:
     return F.linear(h, params['output_linear.weight'], params['output_linear.bias'])
 
 
+class _RoundF32(torch.autograd.Function):
+    """float64 -> float32 rounding with the gradient rounded the same way on the way back."""
+
+    @staticmethod
+    def forward(ctx, x):
+        return x.float()
+
+    @staticmethod
+    def backward(ctx, g):
+        return g.double()
+
+
+def mlp_forward_cr(params: Params, p: torch.Tensor) -> torch.Tensor:
+    """mlp_forward with every GEMM CORRECTLY ROUNDED: the hidden and output layers sum in float64
+    and round each layer's output (and, in the backward, each layer's input gradient) to float32;
+    the Fourier argument x @ B stays the reference's float32 product (decoder.py:26-30).  Not the
+    reference's arithmetic -- its float32 sums carry their own rounding -- but the same function
+    without summation-order noise: the yardstick for fp32-class gradients
+    (tests/golden/make_grads_cr.py)."""
+    x = p.reshape(-1, 3).float()
+    h = torch.sin(x @ params['embedder._B'])
+    for li in range(N_LAYERS):
+        h = _RoundF32.apply(F.relu(F.linear(h.double(), params[f'pts_linears.{li}.weight'].double(),
+                                            params[f'pts_linears.{li}.bias'].double())))
+    return _RoundF32.apply(F.linear(h.double(), params['output_linear.weight'].double(),
+                                    params['output_linear.bias'].double()))
+
+
+def eval_points_cr(params: Params, p: torch.Tensor, bound: torch.Tensor) -> torch.Tensor:
+    """eval_points on mlp_forward_cr (bound mask and sigma := 100 as the reference)."""
+    ret = mlp_forward_cr(params, p).clone()
+    ret[~inside_bound(p, bound), 3] = OUT_OF_BOUND_SIGMA
+    return ret
+
+
 def inside_bound(p: torch.Tensor, bound: torch.Tensor) -> torch.Tensor:
     """src/utils/Renderer.py:43-46: strict inequalities, evaluated in p's dtype (float64)."""
     m = torch.ones(p.shape[0], dtype=torch.bool)

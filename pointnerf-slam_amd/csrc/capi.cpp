@@ -105,7 +105,8 @@ struct Carver {
 };
 
 bool valid_prm(const pnr_render_params* p) {
-  return p && p->n_samples >= 2 && p->n_importance >= 0 && p->n_samples + p->n_importance <= PNR_MAX_SAMPLES;
+  return p && p->n_samples >= 2 && p->n_importance >= 0 && p->n_samples + p->n_importance <= PNR_MAX_SAMPLES &&
+         p->far_mode >= 0 && p->far_mode <= 2 && (p->far_mode != 2 || p->far_clamp_dev != nullptr);
 }
 
 // Forward workspace of render_batch_ray.
@@ -168,12 +169,10 @@ struct BwdWS {
   float* g_nrm;   // [N]
   float* dP;      // [4][C][256]
   float* gargP;   // [C][96]
-  float* gH;      // [4][C][256]  features only: dL/dh_l (split precisions: f16 * 2^e)
-  void* c16;      // [C][32]      features only, split precisions: f16 copy of the chunk's c rows
+  float* gH;      // [4][C][256]  features only: dL/dh_l
   float* g_c;     // [P][32]      features only: dL/dc
   void* gws;      // features only: gather-backward work list
   size_t gws_bytes;
-  uint32_t* gmax; // split precisions: max |g_out| (float bits) -> scale of the f16 deltas
   int64_t C;
 };
 
@@ -185,12 +184,10 @@ BwdWS carve_bwd(int64_t P, int64_t n, void* ws, size_t* bytes, bool feat = false
   b.g_out = c.take<float>(P * 4);
   b.g_x = c.take<float>(P * 3);
   b.g_nrm = c.take<float>(n);
-  b.gmax = c.take<uint32_t>(64);
   b.dP = c.take<float>((size_t)4 * kHidden * b.C);
   b.gargP = c.take<float>(kFourierPad * b.C);
   if (feat) {
     b.gH = c.take<float>((size_t)4 * kHidden * b.C);
-    b.c16 = c.take<char>((size_t)kCDim * 2 * b.C);
     b.g_c = c.take<float>((size_t)P * kCDim);
     b.gws_bytes = gather_workspace_bytes(P);
     b.gws = c.take<char>(b.gws_bytes);
@@ -214,12 +211,7 @@ __global__ void k_fill(float* p, int64_t n, float v) {
 // Shared backward core over P points with saved activations `sv` and dL/draw in b.g_out.
 int mlp_backward_core(int prec, const float* packed, const SaveArgs& sv, int64_t P, BwdWS& b, float* const* grads,
                       bool want_gx, hipStream_t st, const FeatBwd* fb = nullptr) {
-  const bool split = prec != PNR_PREC_FP32;  // split MFMA delta chain + f16 operands (wgrad16.hip)
-  if (split) {  // one delta scale for the whole call, from max |g_out| over every saved row
-    if (hipMemsetAsync(b.gmax, 0, 4, st) != hipSuccess) return (int)hipGetLastError();
-    const int rc = launch_gmax(b.g_out, sv.ld * 4, b.gmax, st);
-    if (rc) return rc;
-  }
+  const bool split = prec != PNR_PREC_FP32;  // f16x3 delta chain + f16x3 weight-gradient GEMMs
   for (int64_t p0 = 0; p0 < P; p0 += b.C) {
     const int64_t C = (P - p0) < b.C ? (P - p0) : b.C;
     BwdArgs a;
@@ -235,25 +227,23 @@ int mlp_backward_core(int prec, const float* packed, const SaveArgs& sv, int64_t
     a.fcw = fb ? fb->fcw : nullptr;
     a.gH = b.gH;
     a.g_c = fb ? b.g_c + p0 * kCDim : nullptr;
-    a.gmax = b.gmax;
-    // the delta chain: exact fp32 MFMA for PNR_PREC_FP32, bf16x3 split MFMA otherwise
+    // the delta chain: exact fp32 MFMA for PNR_PREC_FP32, f16x3 split MFMA otherwise
     int rc = prec == PNR_PREC_FP32 ? launch_mlp_bwd(packed, a, C, st) : launch_mlp_bwd_bf(packed, a, C, st);
     if (rc) return rc;
     const int64_t hstride = sv.ld * kHidden;  // h_l rows of this chunk: h + l_idx * ld * 256 + p0 * 256
     const int64_t dstride = b.C * kHidden;
     if (!grads) {  // no decoder weight gradients (the Tracker's camera-only backward)
-    } else if (split) {  // f16 operands: h / e saved by k_mlp_fwd16, scaled deltas by k_mlp_bwd16
-      const _Float16* h16 = reinterpret_cast<const _Float16*>(sv.hP) + p0 * kHidden;
-      const _Float16* d16 = reinterpret_cast<const _Float16*>(b.dP);
-      const _Float16* e16 = reinterpret_cast<const _Float16*>(sv.eP) + p0 * kFourierPad;
+    } else if (split) {  // f16x3 GEMMs on the fp32 saves (h / e by k_mlp_fwd16, deltas by k_mlp_bwd16)
+      const float* hp = sv.hP + p0 * kHidden;
+      const float* ep = sv.eP + p0 * kFourierPad;
       // output layer: dWo (4x256) += g_out^T h4 ; dbo += colsum(g_out)
-      rc = launch_wgrad_out16(b.g_out + p0 * 4, h16 + 3 * hstride, C, grads[9], grads[10], st);
+      rc = launch_wgrad_out16(b.g_out + p0 * 4, hp + 3 * hstride, C, grads[9], grads[10], st);
       // hidden layers: dW_l += delta_{l+1}^T h_l  (W3: delta4.h3, W2: delta3.h2, W1: delta2.h1)
       for (int l = 3; l >= 1 && rc == 0; --l)
-        rc = launch_wgrad16(kWgradHidden, d16 + l * dstride, h16 + (l - 1) * hstride, C, grads[1 + 2 * l], kHidden,
-                            grads[2 + 2 * l], b.gmax, st);
+        rc = launch_wgrad16(kWgradHidden, b.dP + l * dstride, hp + (l - 1) * hstride, C, C, grads[1 + 2 * l],
+                            kHidden, grads[2 + 2 * l], st);
       // first layer: dW0 (256x93) += delta1^T e ; db0
-      if (rc == 0) rc = launch_wgrad16(kWgradFirst, d16, e16, C, grads[1], kFourier, grads[2], b.gmax, st);
+      if (rc == 0) rc = launch_wgrad16(kWgradFirst, b.dP, ep, C, C, grads[1], kFourier, grads[2], st);
     } else {
       const float* hp = sv.hP + p0 * kHidden;
       rc = launch_wgrad(kWgradOut, b.g_out + p0 * 4, 4, hp + 3 * hstride, kHidden, C, grads[9], kHidden, grads[10],
@@ -268,17 +258,15 @@ int mlp_backward_core(int prec, const float* packed, const SaveArgs& sv, int64_t
     if (rc) return rc;
     // Fourier: dB (3x93) += x^T g_arg   (x rows are float4 (x0,x1,x2,inside): 3 of 4 used)
     if (grads)
-      rc = split ? launch_wgrad_fourier16(sv.xP + p0, b.gargP, C, grads[0], b.gmax, st)
+      rc = split ? launch_wgrad_fourier16(sv.xP + p0, b.gargP, C, grads[0], st)
                  : launch_wgrad(kWgradFourier, reinterpret_cast<const float*>(sv.xP + p0), 3, b.gargP, kFourier, C,
                                 grads[0], kFourier, nullptr, st);
     if (rc) return rc;
     // feature branch: dWc_l (256x32) += (dL/dh_l)^T c ; dbc_l += colsum(dL/dh_l)
-    if (fb && fb->g_fc && split) {  // f16 operands: gH * 2^e from k_mlp_bwd16, an f16 copy of c
-      rc = launch_to_f16(fb->c + p0 * kCDim, b.c16, C * kCDim, st);
-      const _Float16* g16 = reinterpret_cast<const _Float16*>(b.gH);
+    if (fb && fb->g_fc && split) {  // f16x3 GEMMs: dL/dh from k_mlp_bwd16, the fp32 features
       for (int l = 0; l < 4 && rc == 0; ++l)
-        rc = launch_wgrad16(kWgradFc, g16 + l * dstride, b.c16, C, fb->g_fc[2 * l], kCDim, fb->g_fc[2 * l + 1],
-                            b.gmax, st);
+        rc = launch_wgrad16(kWgradFc, b.gH + l * dstride, fb->c + p0 * kCDim, C, C, fb->g_fc[2 * l], kCDim,
+                            fb->g_fc[2 * l + 1], st);
     } else if (fb && fb->g_fc) {
       for (int l = 0; l < 4 && rc == 0; ++l)
         rc = launch_wgrad(kWgradFc, b.gH + l * dstride, kHidden, fb->c + p0 * kCDim, kCDim, C, fb->g_fc[2 * l], kCDim,
@@ -302,6 +290,8 @@ extern "C" {
 
 // the ctypes mirror (pnr/_lib.py) and tests/test_capi.py assume these offsets
 static_assert(offsetof(pnr_points, feat_half) == 104 && sizeof(pnr_points) == 112, "pnr_points layout (ABI 6)");
+static_assert(offsetof(pnr_render_params, status) == 608 && sizeof(pnr_render_params) == 624,
+              "pnr_render_params layout (ABI 7)");
 int pnr_abi_version(void) { return PNR_ABI_VERSION; }
 
 int pnr_timing_enable(int on) {
@@ -441,7 +431,9 @@ int pnr_render_fwd(const pnr_render_params* prm, const float* packed, const floa
   int rc = 0;
   if (gt_depth && prm->far_mode == 0) rc = launch_gt_max(gt_depth, n, w.gmax, st);
   if (rc) return rc;
-  rc = launch_coarse_z(*prm, rays_o, rays_d, gt_depth, w.gmax, n, w.z, w.far, st);
+  // far_mode 2: the clamp is a device value (k_coarse_z reads it like the batch max of mode 0)
+  rc = launch_coarse_z(*prm, rays_o, rays_d, gt_depth, prm->far_mode == 2 ? prm->far_clamp_dev : w.gmax, n, w.z,
+                       w.far, st);
   if (rc) return rc;
   PointSrc src{};
   src.rays_o = rays_o;
@@ -459,7 +451,8 @@ int pnr_render_fwd(const pnr_render_params* prm, const float* packed, const floa
                        w.gws_bytes, st);
     if (rc) return rc;
   }
-  rc = mlp_fwd(prm->precision, packed, src, kRaysZ64, n * S, w.raw, sv, st, pts ? &fa : nullptr);
+  uint32_t* status = reinterpret_cast<uint32_t*>(prm->status);
+  rc = mlp_fwd(prm->precision, packed, src, kRaysZ64, n * S, w.raw, sv, st, pts ? &fa : nullptr, status);
   if (rc) return rc;
   double* zi = w.z + n * S;
   float* rawi = w.raw + n * S * 4;
@@ -481,7 +474,7 @@ int pnr_render_fwd(const pnr_render_params* prm, const float* packed, const floa
       if (rc) return rc;
       fa.c = w.c + o * kCDim;
     }
-    rc = mlp_fwd(prm->precision, packed, src, kRaysZ64, n * I, rawi, sv, st, pts ? &fa : nullptr);
+    rc = mlp_fwd(prm->precision, packed, src, kRaysZ64, n * I, rawi, sv, st, pts ? &fa : nullptr, status);
     if (rc) return rc;
   }
   return launch_fine(*prm, rays_d, w.z, zi, w.raw, rawi, n, depth, var, rgb, w.ord, st);
@@ -604,7 +597,7 @@ int pnr_regulation_fwd(const pnr_render_params* prm, const float* packed, const 
     if (rc) return rc;
   }
   rc = mlp_fwd(prm->precision, packed, src, kRaysZ32, P, w.raw, sv ? &w.save : nullptr, st,
-               prm->points ? &fa : nullptr);
+               prm->points ? &fa : nullptr, reinterpret_cast<uint32_t*>(prm->status));
   if (rc) return rc;
   return launch_extract_sigma(w.raw, P, sigma, st);
 }

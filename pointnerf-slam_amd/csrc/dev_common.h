@@ -69,4 +69,18 @@ __device__ __forceinline__ float fourier_sc(float x) {
   return (q & 2) ? -v : v;
 }
 
+// Power of two s with m s in [2^13, 2^14) (1 for m = 0, inf, NaN): the scale under which a block
+// of values with max |x| = m is split into f16 hi + lo parts (in range, 22 bits below the max).
+// s is clamped to [2^-60, 2^60]: its products with the weight-image scales (<= 2^20) and their
+// inverses stay normal fp32 numbers (a block below 2^-46 keeps ~18 bits; nothing overflows).
+constexpr int kScaleExpMax = 60;
+__device__ __forceinline__ float pt_scale(float m) {
+  if (!(m > 0.f) || !(m < 3.0e38f)) return 1.f;
+  int ex;
+  (void)frexpf(m, &ex);  // m = f 2^ex, f in [0.5, 1)
+  int e = 14 - ex;
+  e = e < -kScaleExpMax ? -kScaleExpMax : (e > kScaleExpMax ? kScaleExpMax : e);
+  return __int_as_float((e + 127) << 23);
+}
+
 }  // namespace pnr

@@ -13,6 +13,11 @@
 // The split forms run 3 MFMAs per 16-deep k-step at 32 cycles: 5.3x the fp32 MFMA rate (8 MFMAs
 // of 64 cycles for the same depth).
 //
+// Training saves (SAVE) are fp32 in every precision: the weight-gradient GEMMs (wgrad16.hip) split
+// them into hi/lo f16 parts themselves, so the backward stays fp32-class.  Every value the forward
+// splits into f16 parts (hidden activations, features) is checked against the f16 range: a value
+// >= 65504 would turn into inf; the kernel then ORs PNR_STATUS_F16_RANGE into *status (when given).
+//
 // Execution model (one workgroup = 4 waves = 128 points, one wave per SIMD, 32 points per wave):
 //  - The point index sits on the MFMA column (lane & 31).  A 256-unit layer output is 8 fp32
 //    accumulator tiles; register r of tile t in lane half hh is unit 32t + perm(r, hh).
@@ -156,6 +161,7 @@ struct BfFwdArgs {
   float* raw_out;
   SaveArgs save;
   const float* c;      // (rows, 32) features of the launch's points
+  uint32_t* status;    // PNR_STATUS_* bits (f16 range) or null
 };
 
 // A fragments of one 32-row output tile over one 32-deep input tile: [part][k-step]
@@ -187,6 +193,7 @@ struct BfState {
   uint32_t mw[4];      // ReLU bit words of the layer being converted
   Frag<PR> F[R];       // fragment ring (one 32-row output tile of the current / next step each)
   Frag<PR> FC;         // feature-branch fragments of the step's epilogue tile
+  float vmax;          // max |value| split into f16 parts so far (f16 range check)
   int64_t col, mask_word0;
   bool valid, inside;
 };
@@ -340,11 +347,11 @@ struct BfFwd {
 #pragma unroll
       for (int i = 0; i < 4; ++i) S.v[4 * q + i] += (F16 ? S.f[4 * q + i] * inv : S.f[4 * q + i]) + b4[i];
     }
-    if constexpr (SAVE) {  // f16 activation save (pnr_internal.h SaveArgs)
-      f16x4 hv = {(_Float16)S.v[4 * q], (_Float16)S.v[4 * q + 1], (_Float16)S.v[4 * q + 2], (_Float16)S.v[4 * q + 3]};
-      *reinterpret_cast<f16x4*>(reinterpret_cast<_Float16*>(a.save.hP) +
-                                ((int64_t)L * a.save.ld + S.col) * kHidden + 32 * t + 8 * q + 4 * hh) = hv;
-    }
+    if constexpr (SAVE)  // fp32 activation save (pnr_internal.h SaveArgs)
+      *reinterpret_cast<float4*>(a.save.hP + ((int64_t)L * a.save.ld + S.col) * kHidden + 32 * t + 8 * q + 4 * hh) =
+          make_float4(S.v[4 * q], S.v[4 * q + 1], S.v[4 * q + 2], S.v[4 * q + 3]);
+    S.vmax = fmaxf(S.vmax, fmaxf(fmaxf(fabsf(S.v[4 * q]), fabsf(S.v[4 * q + 1])),
+                                 fmaxf(fabsf(S.v[4 * q + 2]), fabsf(S.v[4 * q + 3]))));
     split_quad<PR>(S.v + 4 * q, q, S.nxt);
   }
 
@@ -588,12 +595,9 @@ struct BfFwd {
         if constexpr (SAVE) {
           const int hh = (threadIdx.x >> 5) & 1;
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            f16x4 hv = {(_Float16)S.v[4 * q], (_Float16)S.v[4 * q + 1], (_Float16)S.v[4 * q + 2],
-                        (_Float16)S.v[4 * q + 3]};
-            *reinterpret_cast<f16x4*>(reinterpret_cast<_Float16*>(a.save.hP) +
-                                      ((int64_t)3 * a.save.ld + S.col) * kHidden + 32 * t + 8 * q + 4 * hh) = hv;
-          }
+          for (int q = 0; q < 4; ++q)
+            *reinterpret_cast<float4*>(a.save.hP + ((int64_t)3 * a.save.ld + S.col) * kHidden + 32 * t + 8 * q +
+                                       4 * hh) = make_float4(S.v[4 * q], S.v[4 * q + 1], S.v[4 * q + 2], S.v[4 * q + 3]);
         }
       }
       out_dot<t>(S, lds, o);
@@ -650,6 +654,7 @@ __global__ __launch_bounds__(256, 1) void k_mlp_fwd16(BfFwdArgs a, int mode) {
   S.col = a.save.p0 + p;
   S.mask_word0 = ((a.save.p0 + (int64_t)blockIdx.x * 128) / 32 + wave_id()) * 64;
   S.mw[0] = S.mw[1] = S.mw[2] = S.mw[3] = 0u;
+  S.vmax = 0.f;
   if (HASC) {
     float cv[16];
 #pragma unroll
@@ -661,6 +666,8 @@ __global__ __launch_bounds__(256, 1) void k_mlp_fwd16(BfFwdArgs a, int mode) {
         cv[8 * s + 4 * jq + 0] = v.x; cv[8 * s + 4 * jq + 1] = v.y;
         cv[8 * s + 4 * jq + 2] = v.z; cv[8 * s + 4 * jq + 3] = v.w;
       }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) S.vmax = fmaxf(S.vmax, fabsf(cv[r]));
     split_tile<PR>(cv, S.ct);
   }
   // no accumulator zero fill: the first input tile of every layer starts its tiles from 0 (ZERO in
@@ -686,12 +693,10 @@ __global__ __launch_bounds__(256, 1) void k_mlp_fwd16(BfFwdArgs a, int mode) {
         v[r] = k < kFourier ? fourier_sc<false>(arg) : 0.f;
       }
       if constexpr (SAVE) {
-        _Float16* row = reinterpret_cast<_Float16*>(a.save.eP) + S.col * kFourierPad + 32 * t + 4 * hh;
+        float* row = a.save.eP + S.col * kFourierPad + 32 * t + 4 * hh;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          f16x4 ev = {(_Float16)v[4 * q], (_Float16)v[4 * q + 1], (_Float16)v[4 * q + 2], (_Float16)v[4 * q + 3]};
-          *reinterpret_cast<f16x4*>(row + 8 * q) = ev;
-        }
+        for (int q = 0; q < 4; ++q)
+          *reinterpret_cast<float4*>(row + 8 * q) = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
       }
       split_tile<PR>(v, S.ft[t]);
     }
@@ -711,6 +716,8 @@ __global__ __launch_bounds__(256, 1) void k_mlp_fwd16(BfFwdArgs a, int mode) {
     K::out_layer(a, S, lds, o);
   }
   PNR_TICK(40);
+  // f16 range: a split value >= 65504 became inf (bf16 parts have the fp32 range)
+  if (Prec<PR>::F16 && a.status != nullptr && !(S.vmax < 65504.f)) atomicOr(a.status, (uint32_t)PNR_STATUS_F16_RANGE);
 
   if (S.valid && hh == 0) {
     const float* bo = K::raw_lds(lds) + kRawBo;

@@ -1,16 +1,29 @@
-// mlp16_bwd.hip -- bf16x3 delta chain of the decoder backward (k_mlp_bwd16).
+// mlp16_bwd.hip -- f16x3 delta chain of the decoder backward (k_mlp_bwd16).
+#include <cmath>
+
 #include "mlp16.h"
 
 namespace pnr {
 // ---------------------------------------------------------------------------------------------
-// Backward delta chain on bf16x3 (every non-fp32 precision): the k_mlp_bwd math (mlp.hip) --
+// Backward delta chain for every non-fp32 precision: the k_mlp_bwd math (mlp.hip) --
 //   g_h4 = Wo^T g_out, delta_l = (W_l^T delta_{l+1}) * [h_l > 0], g_e = W0^T delta_1,
 //   g_arg = g_e * cos(x@B), g_x = B g_arg; with features dL/dh_l is saved before the mask and
 //   dL/dc = sum_l Wc_l^T dL/dh_l
 // -- on the forward's machinery: chain c = 0 (Wo^T), 1..3 (W3^T..W1^T), 4 (W0^T) alternate between
 // the two accumulator sets, each delta tile is built (mask, save, split) in pieces placed between
-// the next chain's MFMA groups, weights stream through the same LDS-DMA ring.  bf16 parts keep the
-// fp32 exponent range (gradients can be tiny); ~2^-16 per product against a 2e-3 gradient budget.
+// the next chain's MFMA groups, weights stream through the same LDS-DMA ring.
+//
+// Arithmetic: f16x3 (x = hi + lo in f16, 22 significant bits; Wl xh + Wh xl + Wh xh with fp32
+// accumulation), the forward's split.  Gradients span far more than the f16 exponent range, so each
+// point's chain input is scaled by its own power of two s_p before the split: the MFMA output
+// column p is W^T (delta_p s_p), and s_p (with the per-tensor weight scale 2^w of the image) is
+// undone exactly on the fp32 accumulator.  s_p puts the point's max |delta| in [2^13, 2^14): every
+// split operand is inside the f16 range and keeps 22 bits relative to its point's largest entry,
+// whatever the loss scale.  At a chain boundary the point's max over all 8 output tiles is needed
+// before tile 0 can be split, so a boundary step folds each finished tile into a running max
+// (between the MFMA groups) and converts tile 0 after its last group.
+// The deltas, dL/dh (features) and g_arg go to HBM in fp32 (point-major) for the weight-gradient
+// GEMMs of wgrad16.hip, which split them again under their own scales.
 // ---------------------------------------------------------------------------------------------
 __host__ __device__ constexpr int bwd_chain(int g) { return g == 0 ? 0 : (g <= 24 ? 1 + (g - 1) / 8 : 4); }
 __host__ __device__ constexpr int bwd_kc(int g) { return g == 0 ? 0 : (g <= 24 ? (g - 1) % 8 : g - 25); }
@@ -40,21 +53,40 @@ struct BwdGeo {
 };
 static_assert(BwdGeo<true>::younger(4) < 64, "vmcnt range");
 
+// max |a| over an accumulator tile.  The AGPRs are read from inline asm: written as plain reads,
+// hipcc keeps VGPR copies of whole tiles alive and the feature-branch kernel spills.
+__device__ __forceinline__ float tile_absmax(const f32x16& a) {
+  float m = 0.f;
+#pragma unroll
+  for (int r = 0; r < 16; r += 2) {
+    float x, y;
+    asm volatile("v_accvgpr_read_b32 %0, %2\n\tv_accvgpr_read_b32 %1, %3"
+                 : "=&v"(x), "=&v"(y)
+                 : "a"(a[r]), "a"(a[r + 1]));
+    m = fmaxf(m, fmaxf(fabsf(x), fabsf(y)));
+  }
+  return m;
+}
+
 struct BwdState {
   f32x16 acc[2][8];     // chain c output in set c & 1
-  f32x16 gc;            // dL/dc (32 channels)
-  bf16x8 cur[2][2];
-  bf16x8 nxt[2][2];
-  bf16x8 tmp[2][2];     // split dL/dh tile (feature branch operand)
+  f32x16 gc;            // dL/dc (32 channels), times gcf
+  f16x8 cur[2][2];
+  f16x8 nxt[2][2];
+  f16x8 tmp[2][2];      // split dL/dh tile (feature branch operand)
   float v[16];
   uint4 m[4];           // ReLU bit words of h1..h4 (this lane)
-  float dscale;         // 2^e of the f16 delta saves
+  float kacc;           // true value = acc * kacc for the chain accumulating now (2^-w / s_p)
+  float kconv;          // the same for the chain being converted
+  float sig;            // s_p of the chain being converted (its deltas enter the next chain times sig)
+  float mx;             // running max |acc| over the finished tiles of a boundary step
+  float gcf;            // gc = true dL/dc * gcf
   int64_t dcol;
 };
 
 template <bool HASC>
 struct BfBwd {
-  static constexpr int PR = PNR_PREC_BF16X3;
+  static constexpr int PR = PNR_PREC_F16X3;
   using G = BwdGeo<HASC>;
 
   template <int g>
@@ -71,6 +103,13 @@ struct BfBwd {
     }
   }
 
+  // values of quad q times s, split into the f16 parts of tile operand t
+  template <typename T>
+  static __device__ __forceinline__ void split_scaled(const float* v4, float s, int q, T (&t)[2][2]) {
+    const float u[4] = {v4[0] * s, v4[1] * s, v4[2] * s, v4[3] * s};
+    split_quad<PR>(u, q, t);
+  }
+
   // delta of chain CC (li = 3 - CC), tile t: phase 1 = dL/dh (save, split for the feature
   // branch), phase 2 = mask, save delta, split into the next B operand
   template <int CC, int t, int q>
@@ -78,13 +117,11 @@ struct BfBwd {
     const int hh = (threadIdx.x >> 5) & 1;
     constexpr int li = 3 - CC;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) S.v[4 * q + i] = S.acc[CC & 1][t][4 * q + i];
-    if constexpr (HASC) {  // f16 dL/dh * 2^e (the delta scale) for dWc = gH^T c (wgrad16.hip)
-      f16x4 gv = {(_Float16)(S.v[4 * q] * S.dscale), (_Float16)(S.v[4 * q + 1] * S.dscale),
-                  (_Float16)(S.v[4 * q + 2] * S.dscale), (_Float16)(S.v[4 * q + 3] * S.dscale)};
-      *reinterpret_cast<f16x4*>(reinterpret_cast<_Float16*>(a.gH) + ((int64_t)li * a.ld_d + S.dcol) * kHidden +
-                                32 * t + 8 * q + 4 * hh) = gv;
-      split_quad<PR>(S.v + 4 * q, q, S.tmp);
+    for (int i = 0; i < 4; ++i) S.v[4 * q + i] = S.acc[CC & 1][t][4 * q + i] * S.kconv;
+    if constexpr (HASC) {  // fp32 dL/dh for dWc = gH^T c (wgrad16.hip)
+      *reinterpret_cast<float4*>(a.gH + ((int64_t)li * a.ld_d + S.dcol) * kHidden + 32 * t + 8 * q + 4 * hh) =
+          make_float4(S.v[4 * q], S.v[4 * q + 1], S.v[4 * q + 2], S.v[4 * q + 3]);
+      split_scaled(S.v + 4 * q, S.sig, q, S.tmp);
     }
   }
   template <int CC, int t, int q>
@@ -95,12 +132,10 @@ struct BfBwd {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
       if (!((wd >> ((t & 1) * 16 + 4 * q + i)) & 1u)) S.v[4 * q + i] = 0.f;
-    // f16 delta * 2^e for the weight-gradient GEMMs (wgrad16.hip undoes the scale)
-    f16x4 dv = {(_Float16)(S.v[4 * q] * S.dscale), (_Float16)(S.v[4 * q + 1] * S.dscale),
-                (_Float16)(S.v[4 * q + 2] * S.dscale), (_Float16)(S.v[4 * q + 3] * S.dscale)};
-    *reinterpret_cast<f16x4*>(reinterpret_cast<_Float16*>(a.dP) + ((int64_t)li * a.ld_d + S.dcol) * kHidden + 32 * t +
-                              8 * q + 4 * hh) = dv;
-    split_quad<PR>(S.v + 4 * q, q, S.nxt);
+    // fp32 delta for the weight-gradient GEMMs
+    *reinterpret_cast<float4*>(a.dP + ((int64_t)li * a.ld_d + S.dcol) * kHidden + 32 * t + 8 * q + 4 * hh) =
+        make_float4(S.v[4 * q], S.v[4 * q + 1], S.v[4 * q + 2], S.v[4 * q + 3]);
+    split_scaled(S.v + 4 * q, S.sig, q, S.nxt);
   }
 
   template <int CC, int t, int SHIFT, int NT, int T>
@@ -128,22 +163,52 @@ struct BfBwd {
     }
   }
 
-  template <int NS, int NT, int T, int OUTSET, bool ZERO, bool CONV, int CC, int CT, int SHIFT>
+  // Chain boundary (all output tiles of chain CC finished, S.mx their max |acc| in this lane):
+  // fix the point's split scale for chain CC's deltas and the multipliers of both chains.
+  template <int CC>
+  static __device__ __forceinline__ void boundary(BwdState& S, const float* inv, const float* fscl) {
+    float m = fmaxf(S.mx, __shfl_xor(S.mx, 32));  // both lane halves hold the same point
+    S.mx = 0.f;
+    S.kconv = S.kacc;
+    S.sig = pt_scale(m * S.kacc);
+    S.kacc = inv[3 - CC] / S.sig;  // chain CC+1 runs on W_{3-CC}^T (inv[4 - c] for chain c)
+    if constexpr (HASC) {  // dL/dc: the products of layer li = 3 - CC carry 2^wc_li * sig
+      const float f = fscl[3 - CC] * S.sig;
+      const float r = f / S.gcf;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) S.gc[i] *= r;
+      S.gcf = f;
+    }
+  }
+
+  template <int NS, int NT, int T, int OUTSET, bool ZERO, bool CONV, bool BND, int CC, int CT, int SHIFT>
   static __device__ __forceinline__ void group(const BwdArgs& a, BwdState& S, const char* slot,
-                                               const bf16x8 (&act)[2][2], Frag<PR> (&F)[3], const Frag<PR>& FC) {
+                                               const f16x8 (&act)[2][2], Frag<PR> (&F)[3], const Frag<PR>& FC,
+                                               const float* inv, const float* fscl) {
     if constexpr (T < NT) {
       if constexpr (T + 2 < NT) load_frag<PR, NS>(slot + (T + 2) * NS * 2 * 1024, F[(T + 2) % 3]);
-      mfma_frag<PR, ZERO, bf16x8, NS>(F[T % 3], act, S.acc[OUTSET][T]);
+      mfma_frag<PR, ZERO, f16x8, NS>(F[T % 3], act, S.acc[OUTSET][T]);
       asm volatile("" : "+a"(S.acc[OUTSET][T]));
-      if constexpr (CONV) conv_pieces<CC, CT, SHIFT, NT, T>(a, S, FC);
+      if constexpr (BND) {
+        // boundary step: fold the tile finished one group earlier into the running max; after the
+        // last group, the last tile, the point scale, and all of tile 0's conversion
+        if constexpr (T >= 1) S.mx = fmaxf(S.mx, tile_absmax(S.acc[OUTSET][T - 1]));
+        if constexpr (T == NT - 1) {
+          S.mx = fmaxf(S.mx, tile_absmax(S.acc[OUTSET][T]));
+          boundary<CC>(S, inv, fscl);
+          conv_pieces<CC, 0, 0, 1, 0>(a, S, FC);  // as a one-group step: every piece here
+        }
+      } else if constexpr (CONV) {
+        conv_pieces<CC, CT, SHIFT, NT, T>(a, S, FC);
+      }
       __builtin_amdgcn_sched_barrier(0);
-      group<NS, NT, T + 1, OUTSET, ZERO, CONV, CC, CT, SHIFT>(a, S, slot, act, F, FC);
+      group<NS, NT, T + 1, OUTSET, ZERO, CONV, BND, CC, CT, SHIFT>(a, S, slot, act, F, FC, inv, fscl);
     }
   }
 
   template <int g>
   static __device__ __forceinline__ void step(const BwdArgs& a, BwdState& S, const char* wmain, const char* wfc,
-                                              const char* lds) {
+                                              const char* lds, const float* inv, const float* fscl) {
     if constexpr (g < kBwdSteps) {
       constexpr int c = bwd_chain(g);
       constexpr int kc = bwd_kc(g);
@@ -154,6 +219,8 @@ struct BfBwd {
       constexpr bool CONV = bwd_conv(g);
       constexpr int CC = bwd_conv_chain(g);
       constexpr int CT = bwd_conv_tile(g);
+      constexpr bool BND = CONV && CT == 0;  // the step that finishes chain CC (g = 0, 8, 16, 24)
+      static_assert(!BND || (NT == 8 && CC == c), "boundary steps finish their own chain");
       constexpr int SHIFT = CT == 0 ? 1 : 0;
       sync_chunk<G::younger(g)>();
       stage_step<g + G::kDist>(a, wmain, wfc, lds);
@@ -175,8 +242,8 @@ struct BfBwd {
 #pragma unroll
           for (int s = 0; s < 2; ++s) S.cur[pt][s] = S.nxt[pt][s];
       }
-      group<NS, NT, 0, OUTSET, ZERO, CONV, CC, CT, SHIFT>(a, S, slot, S.cur, F, FC);
-      step<g + 1>(a, S, wmain, wfc, lds);
+      group<NS, NT, 0, OUTSET, ZERO, CONV, BND, CC, CT, SHIFT>(a, S, slot, S.cur, F, FC, inv, fscl);
+      step<g + 1>(a, S, wmain, wfc, lds, inv, fscl);
     }
   }
 
@@ -201,30 +268,41 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd16(const float* __restrict__ 
   const char* wfc = HASC ? reinterpret_cast<const char*>(a.fcw + kOffFcBwd) : nullptr;
   K::template prologue<0>(a, wmain, wfc, lds);
 
+  // inverse weight-image scales (W0..W3, Wo) and the forward fc scales (Wc_0..Wc_3): k_wscale
+  const float* rawt = W + kOffRaw;
+  float inv[5], fscl[4];
+#pragma unroll
+  for (int i = 0; i < 5; ++i) inv[i] = rawt[kRawInv + i];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) fscl[i] = HASC ? a.fcw[kOffFcRaw + kFcRawScl + i] : 1.f;
+
   BwdState S;
   S.dcol = p;
-  S.dscale = delta_scale(*a.gmax);
+  S.mx = 0.f;
+  S.gcf = 1.f;
   const int64_t col = a.p0 + p;
   const int64_t mstride = (a.ld / 32) * 64;
   const uint4* mk = a.masks + ((a.p0 + (int64_t)blockIdx.x * 128) / 32 + wave_id()) * 64;
 #pragma unroll
   for (int l = 0; l < 4; ++l) S.m[l] = mk[l * mstride + lane];
   // B operand of the Wo^T step: k = o = 0..3 sit in elements 0..3 of lane half 0 (g_out rows
-  // exist for every padded point of the launch: the caller zero-fills them)
+  // exist for every padded point of the launch: the caller zero-fills them), times the point's scale
   {
     const float4 go = reinterpret_cast<const float4*>(a.g_out)[p];
+    const float s0 = pt_scale(fmaxf(fmaxf(fabsf(go.x), fabsf(go.y)), fmaxf(fabsf(go.z), fabsf(go.w))));
     float gv[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) gv[r] = 0.f;
     if (hh == 0) {
-      gv[0] = go.x; gv[1] = go.y; gv[2] = go.z; gv[3] = go.w;
+      gv[0] = go.x * s0; gv[1] = go.y * s0; gv[2] = go.z * s0; gv[3] = go.w * s0;
     }
-    split_tile<PNR_PREC_BF16X3>(gv, S.cur);
+    split_tile<PNR_PREC_F16X3>(gv, S.cur);
+    S.kacc = inv[4] / s0;
   }
 #pragma unroll
   for (int r = 0; r < 16; ++r) S.gc[r] = 0.f;
   // no accumulator zero fill: each layer's first input tile starts its tiles from 0 (ZERO)
-  K::template step<0>(a, S, wmain, wfc, lds);
+  K::template step<0>(a, S, wmain, wfc, lds, inv, fscl);
 
   // g_arg = g_e * cos(x@B), g_x = B g_arg (the k_mlp_bwd epilogue on set 0, tiles 0..2)
   float x0 = 0.f, x1 = 0.f, x2 = 0.f;
@@ -249,27 +327,26 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd16(const float* __restrict__ 
           arg = __builtin_fmaf(x1, FB[kFourierPad + k], arg);
           arg = __builtin_fmaf(x2, FB[2 * kFourierPad + k], arg);
         }
-        g = S.acc[0][t][r] * fourier_sc<true>(arg);
+        g = (S.acc[0][t][r] * S.kacc) * fourier_sc<true>(arg);
         s0 = __builtin_fmaf(FB[k], g, s0);
         s1 = __builtin_fmaf(FB[kFourierPad + k], g, s1);
         s2 = __builtin_fmaf(FB[2 * kFourierPad + k], g, s2);
       }
       gv[r] = g;
     }
-    // f16 g_arg * 2^e (same scale as the deltas) for the dB GEMM (wgrad16.hip k_wgrad_skinny16)
-    _Float16* row = reinterpret_cast<_Float16*>(a.gargP) + p * kFourierPad + 32 * t + 4 * hh;
+    // fp32 g_arg for the dB GEMM (wgrad16.hip k_wgrad_skinny)
+    float* row = a.gargP + p * kFourierPad + 32 * t + 4 * hh;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      f16x4 gq = {(_Float16)(gv[4 * q] * S.dscale), (_Float16)(gv[4 * q + 1] * S.dscale),
-                  (_Float16)(gv[4 * q + 2] * S.dscale), (_Float16)(gv[4 * q + 3] * S.dscale)};
-      *reinterpret_cast<f16x4*>(row + 8 * q) = gq;
-    }
+    for (int q = 0; q < 4; ++q)
+      *reinterpret_cast<float4*>(row + 8 * q) = make_float4(gv[4 * q], gv[4 * q + 1], gv[4 * q + 2], gv[4 * q + 3]);
   }
   if (HASC && valid) {
+    const float gi = 1.f / S.gcf;
     float* row = a.g_c + p * kCDim + 4 * hh;
 #pragma unroll
     for (int q = 0; q < 4; ++q)
-      *reinterpret_cast<float4*>(row + 8 * q) = make_float4(S.gc[4 * q], S.gc[4 * q + 1], S.gc[4 * q + 2], S.gc[4 * q + 3]);
+      *reinterpret_cast<float4*>(row + 8 * q) =
+          make_float4(S.gc[4 * q] * gi, S.gc[4 * q + 1] * gi, S.gc[4 * q + 2] * gi, S.gc[4 * q + 3] * gi);
   }
   if (a.g_x != nullptr) {
     s0 += __shfl_xor(s0, 32);
@@ -291,31 +368,6 @@ static int launch_bwd16(const float* packed, const BwdArgs& a, int64_t P, hipStr
                                                (int)lds) == hipSuccess;
   if (!attr) return PNR_E_ARG;
   hipLaunchKernelGGL(kern, dim3((unsigned)((P + 127) / 128)), dim3(256), lds, st, packed, a, P);
-  return hip_status(hipGetLastError());
-}
-
-// max |g| as uint bits (non-negative floats order as uints): grid-stride, block reduction, ONE
-// atomic per block (same-address atomics serialise at ~90 per microsecond)
-__global__ void k_gmax(const float* __restrict__ g, int64_t n, uint32_t* __restrict__ out) {
-  __shared__ float red[4];
-  float m = 0.f;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-    m = fmaxf(m, fabsf(g[i]));
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-    if (m > 0.f) atomicMax(out, __float_as_uint(m));
-  }
-}
-
-int launch_gmax(const float* g, int64_t n, uint32_t* out, hipStream_t st) {
-  if (n <= 0) return 0;
-  int64_t blocks = (n + 4095) / 4096;  // >= 16 elements per thread
-  if (blocks > 512) blocks = 512;
-  hipLaunchKernelGGL(k_gmax, dim3((unsigned)blocks), dim3(256), 0, st, g, n, out);
   return hip_status(hipGetLastError());
 }
 

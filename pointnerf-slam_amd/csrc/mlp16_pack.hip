@@ -123,8 +123,9 @@ __global__ void k_pack16(RawParams rp, uint16_t* __restrict__ bf2, uint16_t* __r
   }
 }
 
-// Transposed bf16x3 images of the delta chain (element e of the backward stream)
-__global__ void k_pack16_bwd(RawParams rp, uint16_t* __restrict__ out) {
+// Transposed f16x3 images of the delta chain (element e of the backward stream), each tensor
+// scaled by the forward image's power of two (raw[kRawScl + tensor], k_wscale)
+__global__ void k_pack16_bwd(RawParams rp, uint16_t* __restrict__ out, const float* __restrict__ raw) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= kBwdBytes / 2) return;
   const int64_t byte = 2 * e;
@@ -135,6 +136,7 @@ __global__ void k_pack16_bwd(RawParams rp, uint16_t* __restrict__ out) {
   const int lane = (int)(r % 64); r /= 64;
   const int part = (int)(r % 2); r /= 2;
   float v = 0.f;
+  int tensor = 4;
   if (g == 0) {  // Wo^T: A[row = unit 32T + i][k = o = perm(j, hh)], k < 4
     const int T = (int)r, row = 32 * T + (lane & 31), k = perm(j, lane >> 5);
     v = k < 4 ? rp.p[9][k * kHidden + row] : 0.f;
@@ -146,19 +148,16 @@ __global__ void k_pack16_bwd(RawParams rp, uint16_t* __restrict__ out) {
     if (g <= 24) {
       const int l = 3 - (g - 1) / 8;  // W3, W2, W1
       v = rp.p[1 + 2 * l][k * kHidden + row];
+      tensor = l;
     } else {
       v = row < kFourier ? rp.p[1][k * kFourier + row] : 0.f;
+      tensor = 0;
     }
   }
-  out[e] = part_bits<__bf16>(v, part);
+  out[e] = part_bits<_Float16>(v * raw[kRawScl + tensor], part);
 }
 
 int launch_pack_bf(const RawParams& rp, float* packed, hipStream_t st) {
-  {
-    const int64_t n = kBwdBytes / 2;
-    hipLaunchKernelGGL(k_pack16_bwd, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, rp,
-                       reinterpret_cast<uint16_t*>(packed + kOffBwd));
-  }
   float* raw = packed + kOffRaw;
   ScaleArgs sa;
   const int nw[5] = {kHidden * kFourier, kHidden * kHidden, kHidden * kHidden, kHidden * kHidden, 4 * kHidden};
@@ -169,6 +168,11 @@ int launch_pack_bf(const RawParams& rp, float* packed, hipStream_t st) {
   sa.inv = raw + kRawInv;
   sa.scl = raw + kRawScl;
   hipLaunchKernelGGL(k_wscale, dim3(5), dim3(1024), 0, st, sa);
+  {
+    const int64_t n = kBwdBytes / 2;
+    hipLaunchKernelGGL(k_pack16_bwd, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, rp,
+                       reinterpret_cast<uint16_t*>(packed + kOffBwd), raw);
+  }
   const int64_t n = 2 * (bf_main_bytes(2) / 2) + bf_main_bytes(1) / 2 + kRawWo + 4 * kHidden;
   const int threads = 256;
   hipLaunchKernelGGL(k_pack16, dim3((unsigned)((n + threads - 1) / threads)), dim3(threads), 0, st, rp,
@@ -213,8 +217,8 @@ __global__ void k_fc_pack16(FcRaw16 fc, uint16_t* __restrict__ bf2, uint16_t* __
 }
 
 // fc backward entry e = 8(3 - l) + t: A[row = channel (lane&31)][k = unit 32t + perm(8s+j, lane>>5)]
-// = Wc_l[unit][channel], bf16x3
-__global__ void k_fc_pack16_bwd(FcRaw16 fc, uint16_t* __restrict__ out) {
+// = Wc_l[unit][channel], f16x3 scaled like the forward image (raw[kFcRawScl + l])
+__global__ void k_fc_pack16_bwd(FcRaw16 fc, uint16_t* __restrict__ out, const float* __restrict__ raw) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= kBfFcBytes / 2) return;
   const int ent = (int)(e / 2048);
@@ -225,7 +229,7 @@ __global__ void k_fc_pack16_bwd(FcRaw16 fc, uint16_t* __restrict__ out) {
   const int s = (int)(r / 2);
   const int l = 3 - ent / 8, t = ent % 8;
   const int unit = 32 * t + perm(8 * s + j, lane >> 5);
-  out[e] = part_bits<__bf16>(fc.p[2 * l][unit * kCDim + (lane & 31)], part);
+  out[e] = part_bits<_Float16>(fc.p[2 * l][unit * kCDim + (lane & 31)] * raw[kFcRawScl + l], part);
 }
 
 int launch_fc_pack_bf(const float* const* fcp, float* out, hipStream_t st) {
@@ -246,12 +250,12 @@ int launch_fc_pack_bf(const float* const* fcp, float* out, hipStream_t st) {
                      reinterpret_cast<uint16_t*>(out + kOffFcBf2), reinterpret_cast<uint16_t*>(out + kOffFcBf1),
                      reinterpret_cast<uint16_t*>(out + kOffFcH2), raw);
   hipLaunchKernelGGL(k_fc_pack16_bwd, dim3((unsigned)((kBfFcBytes / 2 + 255) / 256)), dim3(256), 0, st, r,
-                     reinterpret_cast<uint16_t*>(out + kOffFcBwd));
+                     reinterpret_cast<uint16_t*>(out + kOffFcBwd), raw);
   return hip_status(hipGetLastError());
 }
 
 int launch_mlp_fwd_bf(int prec, const float* packed, const PointSrc& src, int mode, int64_t P, float* raw,
-                      const SaveArgs* save, hipStream_t st, const FeatArgs* feat) {
+                      const SaveArgs* save, hipStream_t st, const FeatArgs* feat, uint32_t* status) {
   if (P <= 0) return 0;
   if (mode < kPtsF64 || mode > kRaysZ32) return PNR_E_ARG;
   if (prec != PNR_PREC_BF16X3 && prec != PNR_PREC_BF16 && prec != PNR_PREC_F16X3) return PNR_E_ARG;
@@ -265,6 +269,7 @@ int launch_mlp_fwd_bf(int prec, const float* packed, const PointSrc& src, int mo
   a.src = src;
   a.P = P;
   a.raw_out = raw;
+  a.status = status;
   const bool sv = save != nullptr;
   if (save) a.save = *save;
   else a.save = SaveArgs{nullptr, nullptr, nullptr, nullptr, 0, 0};

@@ -132,12 +132,10 @@ __device__ __forceinline__ void load_point(const PointSrc& s, int64_t p, float& 
 
 // Activation save area for training, POINT-major (row p = one point), ld = total points
 // (multiple of 128; padded points hold finite activations of x = 0 and get zero gradient).
-// PNR_PREC_FP32 stores e / h as fp32; the split precisions store them as f16 (first half of the
-// same regions): the weight-gradient GEMMs read half the bytes and use the values as exact f16
-// MFMA operands (one storage rounding, <= 2^-12 relative).
+// fp32 in every precision (the split weight-gradient GEMMs split the values themselves).
 struct SaveArgs {
-  float* eP;       // [ld][96]        Fourier features sin(x@B)   (fp32 or f16)
-  float* hP;       // [4][ld][256]    h1..h4                      (fp32 or f16)
+  float* eP;       // [ld][96]        Fourier features sin(x@B)
+  float* hP;       // [4][ld][256]    h1..h4
   float4* xP;      // [ld]            (x0, x1, x2, inside ? 1 : 0), f32 MLP input
   uint4* masks;    // [4][ld/32][64 lanes] ReLU bit words of h1..h4 (mlp.hip save_mask)
   int64_t ld;
@@ -167,12 +165,10 @@ struct BwdArgs {
   const float* fcw;
   float* gH;           // [4][ld_d][256]
   float* g_c;          // [C][32] chunk-local rows
-  // split precisions (launch_mlp_bwd_bf): dP holds f16 delta * 2^e, e from max |g_out| (*gmax,
-  // k_gmax); see delta_scale
-  const uint32_t* gmax;
 };
 int launch_mlp_bwd(const float* packed, const BwdArgs& a, int64_t P, hipStream_t st);
-// bf16x3 delta chain (mlp_bf.hip): same arguments; used for every precision but PNR_PREC_FP32
+// f16x3 delta chain (mlp16_bwd.hip, per-point scaled): same arguments; every precision but
+// PNR_PREC_FP32
 int launch_mlp_bwd_bf(const float* packed, const BwdArgs& a, int64_t P, hipStream_t st);
 
 int launch_pack(const RawParams& rp, float* packed, hipStream_t st);
@@ -184,13 +180,16 @@ int64_t fc_packed_floats_all();
 int launch_pack_bf(const RawParams& rp, float* packed, hipStream_t st);
 int launch_fc_pack_bf(const float* const* fc, float* out, hipStream_t st);
 // prec = PNR_PREC_BF16X3 / PNR_PREC_BF16 / PNR_PREC_F16X3
+// status: PNR_STATUS_* bits ORed in on the device (f16 range check of F16X3), or null
 int launch_mlp_fwd_bf(int prec, const float* packed, const PointSrc& src, int mode, int64_t P, float* raw,
-                      const SaveArgs* save, hipStream_t st, const FeatArgs* feat = nullptr);
+                      const SaveArgs* save, hipStream_t st, const FeatArgs* feat = nullptr,
+                      uint32_t* status = nullptr);
 // forward dispatch on PNR_PREC_*
 inline int mlp_fwd(int prec, const float* packed, const PointSrc& src, int mode, int64_t P, float* raw,
-                   const SaveArgs* save, hipStream_t st, const FeatArgs* feat = nullptr) {
+                   const SaveArgs* save, hipStream_t st, const FeatArgs* feat = nullptr,
+                   uint32_t* status = nullptr) {
   if (prec == PNR_PREC_FP32) return launch_mlp_fwd(packed, src, mode, P, raw, save, st, feat);
-  return launch_mlp_fwd_bf(prec, packed, src, mode, P, raw, save, st, feat);
+  return launch_mlp_fwd_bf(prec, packed, src, mode, P, raw, save, st, feat, status);
 }
 
 // ---- neural-point gather (points.hip) --------------------------------------------------------
@@ -227,31 +226,16 @@ int launch_gather_bwd(const pnr_points& pts, const PointSrc* src, int mode, cons
 enum WgradKind : int { kWgradHidden = 0, kWgradFirst = 1, kWgradOut = 2, kWgradFourier = 3, kWgradFc = 4 };
 int launch_wgrad(int kind, const float* A, int ma, const float* B, int nb, int64_t K, float* C, int64_t ldc,
                  float* bias, hipStream_t st);
-// split precisions (wgrad16.hip): kWgradHidden / kWgradFirst / kWgradFc on f16 operands (A = deltas
-// or dL/dh scaled by delta_scale(*gmax), B = f16 activations / features), and dWo from fp32 g_out
-// and f16 h4
-int launch_wgrad16(int kind, const void* A, const void* B, int64_t K, float* C, int64_t ldc, float* bias,
-                   const uint32_t* gmax, hipStream_t st);
-int launch_wgrad_out16(const float* g_out, const void* h4, int64_t K, float* C, float* bias, hipStream_t st);
-int launch_to_f16(const float* x, void* y, int64_t n, hipStream_t st);
-int launch_wgrad_fourier16(const float4* xP, const void* garg, int64_t K, float* C, const uint32_t* gmax,
-                           hipStream_t st);
+// split precisions (wgrad16.hip): kWgradHidden / kWgradFirst / kWgradFc as f16x3 GEMMs on fp32
+// operands (A = deltas or dL/dh [K][256], B = activations / Fourier features / point features
+// [K][WB]; B rows >= kb_rows are not read), dWo and dB as fp32 FMA reductions
+int launch_wgrad16(int kind, const float* A, const float* B, int64_t K, int64_t kb_rows, float* C, int64_t ldc,
+                   float* bias, hipStream_t st);
+int launch_wgrad_out16(const float* g_out, const float* h4, int64_t K, float* C, float* bias, hipStream_t st);
+int launch_wgrad_fourier16(const float4* xP, const float* garg, int64_t K, float* C, hipStream_t st);
 
 inline int hip_status(hipError_t e) { return e == hipSuccess ? 0 : (int)e; }
 
-// Power-of-two scale of the f16 deltas: max |g_out| * 2^e <= 4 (the delta chain may grow it by
-// 1.6e4 before f16 overflows); gmax = float bits of max |g_out| (k_gmax).  2^e exactly.
-__device__ inline float delta_scale(uint32_t gmax_bits) {
-  const float m = __uint_as_float(gmax_bits);
-  if (!(m > 0.f) || m != m) return 1.f;
-  int ex;
-  frexpf(4.f / m, &ex);
-  int e = ex - 1;
-  e = e < -60 ? -60 : (e > 60 ? 60 : e);
-  return ldexpf(1.f, e);
-}
-// max |g| over n floats into *out (float bits, atomicMax; *out zeroed by the caller)
-int launch_gmax(const float* g, int64_t n, uint32_t* out, hipStream_t st);
 
 // Diagnostics: bracket a launch with hipEvents when pnr_timing_enable(1) (capi.cpp).
 enum TimedKernel : int {

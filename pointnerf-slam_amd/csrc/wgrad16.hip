@@ -1,27 +1,37 @@
 // wgrad16.hip -- weight-gradient GEMMs of the decoder backward for the split precisions.
 //
-//   C[256][NB] += s^-1 * A[K][256]^T B[K][WB]     (A, B point-major f16: row k = one point)
-//   bias[256]  += s^-1 * sum_k A[k][:]            (optional)
+//   C[256][nb] += A[K][256]^T B[K][WB]     (A, B point-major fp32: row k = one point)
+//   bias[256]  += sum_k A[k][:]            (optional)
 //
-// Used for every precision but PNR_PREC_FP32 (wgrad.hip keeps the fp32 form) on the two large shapes
-// of src/conv_onet/models/decoder.py:149-159:
+// Used for every precision but PNR_PREC_FP32 (wgrad.hip keeps the fp32-MFMA form) on the shapes of
+// src/conv_onet/models/decoder.py:149-159 (and the fc_c branch, :122-125):
 //   dW3 = delta4^T h3, dW2 = delta3^T h2, dW1 = delta2^T h1     WB = 256 (8 column tiles)
 //   dW0 = delta1^T e                                            WB = 96 (3 column tiles, 93 used)
-// A = deltas stored by k_mlp_bwd16 as f16 * s (s = 2^e from max |g_out|, delta_scale), B = f16
-// activations stored by k_mlp_fwd16.  The products of f16 values are exact in fp32, so the only
-// error is the one storage rounding of each operand (<= 2^-12 relative).
+//   dWc_l = (dL/dh_l)^T c                                       WB = 32 (1 column tile)
+// A = deltas / dL/dh stored by k_mlp_bwd16, B = activations / Fourier features stored by
+// k_mlp_fwd16 (or the gathered point features), all fp32.
 //
-// The training step is HBM-bound on these operands: the kernel only moves them.  K (points) is
-// split over workgroups of 8 waves (2 per SIMD).  Each 32-point tile of A and B goes straight from
-// HBM into LDS by global_load_lds (16-B pieces: the LDS side is lane-linear, the source address is
-// free, so the DMA itself lays the tile out as [32-column block T][32 points][64 B]); a 4-slot ring
-// keeps 3 tiles (~100 KB) in flight per CU.  The MFMA operands need 8 consecutive points of one
-// column per lane: ds_read_b64_tr_b16 reads them transposed out of the image (a 16-lane group
-// covers 4 rows x 32 B = 64 distinct banks; cdna_hip_programming.md T10).  Wave w owns output rows
-// [32w, 32w + 32) x all NB columns in NTB accumulator tiles for the whole K range, added into C with
-// one float atomic per element at the end.  The bias row sums come from the A fragments.
-// K must be a multiple of 32 and rows in [real K, K) zero in A (padded points: delta = 0).
+// Arithmetic: f16x3, the forward's split.  Each operand x = hi + lo (hi = f16(x), lo = f16(x - hi),
+// 22 significant bits); A B ~= Ah Bh + Ah Bl + Al Bh on v_mfma_f32_32x32x16_f16 with fp32
+// accumulation (the dropped Al Bl term is 2^-22 relative).  A (gradients: any magnitude) is split
+// under a per-wave running power of two sc (max |A| sc < 2^15 on every tile; when a tile needs a
+// smaller sc -- the first nonzero one does -- the accumulator is rescaled by the exact ratio).
+// B is split unscaled: activations < 65504 (the forward's PNR_STATUS_F16_RANGE check), |e| <= 1,
+// point features.  The bias row sums are fp32 sums of A.
+//
+// The GEMM moves 2 x 4 B per point and unit and is HBM-bound (the kernel streams 64 KB per 32-point
+// tile at ~3 flops per byte of f16 MFMA work).  K (points) is split over workgroups of 8 waves
+// (2 per SIMD, one workgroup per CU); wave w owns output rows [32w, 32w + 32) for the whole K range
+// in NTB accumulator tiles and flushes them with one float atomic per element at the end.
+//  - A: each wave reads its own 32 columns straight into registers in MFMA operand order (lane l:
+//    column 32w + (l & 31), points 16s + 8(l >> 5) + j): two 128-B lines per load instruction.
+//  - B: shared by the 8 waves; the block loads a 32 x WB tile with 16-B loads, splits it and writes
+//    the hi and lo planes into LDS as [32-column block T][32 points][64 B];
+//    ds_read_b64_tr_b16 returns the MFMA operand (8 consecutive points of one column) transposed.
+//  - One register set: tile t+1 is loaded while tile t runs its MFMAs; the LDS planes are double
+//    buffered, so one barrier per tile orders both.
 #include <cmath>
+
 #include "mlp16.h"
 
 namespace pnr {
@@ -29,58 +39,78 @@ namespace pnr {
 typedef short v4i16 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
 
-constexpr int kTileB = 2112;  // bytes of one [32 points][64 B] block, +64 B pad (store banks)
+constexpr int kTileB = 2112;  // bytes of one [32 points][64 B] block, +64 B pad
 
 template <int NTB, int WB>
-struct Wg16 {
-  static constexpr int kThreads = 512;                     // 8 waves, 2 per SIMD
-  // B blocks staged: a multiple of 4 so every wave issues the same DMA pieces (dW0: 4 with one
-  // duplicate, dWc: 4 with three duplicates of the one 32-column block)
-  static constexpr int kTB = NTB < 4 ? 4 : NTB;
-  static constexpr int kImgA = 8 * kTileB;
-  static constexpr int kSlot = kImgA + kTB * kTileB;
-  static constexpr int kNbuf = 4, kDist = kNbuf - 1;
-  static constexpr int kLds = kNbuf * kSlot;
-  // DMA pieces (1 KiB = 16 points x 64 B of one block) per wave per tile: A 16 / 8 waves, B 2 kTB / 8
-  static constexpr int kPA = 2, kPB = 2 * kTB / 8;
-  static constexpr int kPieces = kPA + kPB;
+struct Wx3 {
+  static constexpr int kThreads = 512;                   // 8 waves, 2 per SIMD
+  static constexpr int kPlane = NTB * kTileB;            // one plane (hi or lo) of a B tile
+  static constexpr int kSlot = 2 * kPlane;
+  static constexpr int kLds = 2 * kSlot;                 // double-buffered
+  static constexpr int kC4 = WB / 4;                     // float4 per B row
+  static constexpr int kB4 = 32 * kC4;                   // float4 per B tile
+  static constexpr int kBPer = (kB4 + kThreads - 1) / kThreads;
 };
 
-struct Wg16Args {
-  const _Float16* A;   // [K][256]
-  const _Float16* B;   // [K][WB]
+struct WxArgs {
+  const float* A;      // [K][256]
+  const float* B;      // [kb_rows][WB]
   int nb;              // valid columns of B (columns of C)
-  int64_t K;           // multiple of 32
+  int64_t K;           // multiple of 32 (rows [real K, K) of A exist and are zero)
+  int64_t kb_rows;     // rows of B that exist (reads clamp to the last one: A is zero there)
   int64_t ks;          // points per workgroup (multiple of 32)
   float* C;
   int64_t ldc;
   float* bias;
-  const uint32_t* gmax;  // scale of A: delta_scale(*gmax)
 };
 
-__device__ __forceinline__ void glds16b(const void* gsrc, uint32_t lds_byte) {
-  glds16(reinterpret_cast<const float*>(gsrc), lds_byte);
+template <int NTB, int WB>
+struct WxRegs {
+  float a[16];                                 // A element (k-step s, j) -> a[8s + j]
+  float4 b[Wx3<NTB, WB>::kBPer];
+};
+
+template <int NTB, int WB>
+__device__ __forceinline__ void wx_load(const WxArgs& a, int64_t k0, WxRegs<NTB, WB>& R) {
+  using Cfg = Wx3<NTB, WB>;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const float* Ab = a.A + (k0 + 8 * (lane >> 5)) * 256 + 32 * wave_id() + (lane & 31);
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) R.a[8 * s + j] = Ab[(16 * s + j) * 256];
+#pragma unroll
+  for (int i = 0; i < Cfg::kBPer; ++i) {
+    const int q = tid + Cfg::kThreads * i;
+    if (Cfg::kB4 % Cfg::kThreads == 0 || q < Cfg::kB4) {  // wave-uniform
+      int64_t row = k0 + q / Cfg::kC4;
+      row = row < a.kb_rows ? row : a.kb_rows - 1;
+      R.b[i] = *reinterpret_cast<const float4*>(a.B + row * WB + 4 * (q % Cfg::kC4));
+    }
+  }
 }
 
-// stage 32-point tile k0 into `slot`: piece pc of an operand = (block T = pc >> 1, half h = pc & 1),
-// lane L -> point 16h + (L >> 2), 16-B chunk (L & 3) of the block's 64 B
+// B tile -> hi / lo f16 planes of `slot`
 template <int NTB, int WB>
-__device__ __forceinline__ void stage_tile(const Wg16Args& a, int64_t k0, uint32_t slot) {
-  using Cfg = Wg16<NTB, WB>;
-  const int w = wave_id(), L = threadIdx.x & 63;
-  const int row = L >> 2, c16 = L & 3;
+__device__ __forceinline__ void wx_stage_b(const WxRegs<NTB, WB>& R, char* slot) {
+  using Cfg = Wx3<NTB, WB>;
+  const int tid = threadIdx.x;
 #pragma unroll
-  for (int i = 0; i < Cfg::kPA; ++i) {
-    const int pc = w + 8 * i, T = pc >> 1, h = pc & 1;
-    const char* src = reinterpret_cast<const char*>(a.A + (k0 + 16 * h + row) * 256) + T * 64 + c16 * 16;
-    glds16b(src, slot + T * kTileB + h * 1024);
-  }
+  for (int i = 0; i < Cfg::kBPer; ++i) {
+    const int q = tid + Cfg::kThreads * i;
+    if (Cfg::kB4 % Cfg::kThreads == 0 || q < Cfg::kB4) {
+      const int r = q / Cfg::kC4, c = 4 * (q % Cfg::kC4);
+      const float v[4] = {R.b[i].x, R.b[i].y, R.b[i].z, R.b[i].w};
+      f16x4 hi, lo;
 #pragma unroll
-  for (int i = 0; i < Cfg::kPB; ++i) {
-    const int pc = w + 8 * i, T = pc >> 1, h = pc & 1;
-    const int Ts = T < NTB ? T : 0;  // dW0: the 4th block duplicates block 0 (never read)
-    const char* src = reinterpret_cast<const char*>(a.B + (k0 + 16 * h + row) * WB) + Ts * 64 + c16 * 16;
-    glds16b(src, slot + Cfg::kImgA + T * kTileB + h * 1024);
+      for (int e = 0; e < 4; ++e) {
+        hi[e] = (_Float16)v[e];
+        lo[e] = (_Float16)(v[e] - (float)hi[e]);
+      }
+      char* base = slot + (c >> 5) * kTileB + r * 64 + (c & 31) * 2;
+      *reinterpret_cast<f16x4*>(base) = hi;
+      *reinterpret_cast<f16x4*>(base + Cfg::kPlane) = lo;
+    }
   }
 }
 
@@ -100,49 +130,73 @@ __device__ __forceinline__ f16x8 tr_frag(const char* img, int T, int s) {
 }
 
 template <int NTB, int WB>
-__global__ __launch_bounds__(512, 1) void k_wgrad16(Wg16Args a) {
-  using Cfg = Wg16<NTB, WB>;
+__global__ __launch_bounds__(512, 1) void k_wgrad16(WxArgs a) {
+  using Cfg = Wx3<NTB, WB>;
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int lane = threadIdx.x & 63, hh = lane >> 5;
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // output row block of this wave
+  const int w = wave_id();  // output row block of this wave
   const int64_t kb = (int64_t)blockIdx.x * a.ks;
   const int64_t ke = kb + a.ks < a.K ? kb + a.ks : a.K;
   const int64_t ntile = (ke - kb) / 32;
-  const uint32_t lbase = lds_addr(reinterpret_cast<const float*>(lds));
 
   f32x16 acc[NTB];
 #pragma unroll
   for (int y = 0; y < NTB; ++y)
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[y][r] = 0.f;
-  float cs = 0.f;  // row sums of A (bias) for column 32w + (lane & 31), this lane half's points
-
-  // the ring always issues exactly kDist tiles ahead (the tail re-stages the last tile into the
-  // free slot) so that every wait below has the same constant count
-#pragma unroll
-  for (int t = 0; t < Cfg::kDist; ++t)
-    stage_tile<NTB, WB>(a, kb + 32 * (t < ntile ? t : ntile - 1), lbase + t * Cfg::kSlot);
+  float cs = 0.f;          // fp32 row sums of A (bias) for row 32w + (lane & 31), this lane's points
+  float sc = 0x1p60f;      // running scale of A (wave-uniform, <= 2^60 as pt_scale); lowered by a tile
+  WxRegs<NTB, WB> R;
+  if (ntile > 0) wx_load<NTB, WB>(a, kb, R);
   for (int64_t t = 0; t < ntile; ++t) {
-    sync_chunk<(Cfg::kDist - 1) * Cfg::kPieces>();  // this wave's pieces of tile t landed; all waves met
-    {
-      const int64_t tn = t + Cfg::kDist < ntile ? t + Cfg::kDist : ntile - 1;
-      stage_tile<NTB, WB>(a, kb + 32 * tn, lbase + (uint32_t)(((t + Cfg::kDist) % Cfg::kNbuf) * Cfg::kSlot));
+    char* slot = lds + (t & 1) * Cfg::kSlot;
+    wx_stage_b<NTB, WB>(R, slot);
+    float m = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      m = fmaxf(m, fabsf(R.a[i]));
+      cs += R.a[i];
     }
-    const char* ia = lds + (t % Cfg::kNbuf) * Cfg::kSlot;
-    const char* ib = ia + Cfg::kImgA;
+    if (__builtin_amdgcn_ballot_w64(m * sc >= 32768.f) != 0) {  // this tile needs a smaller scale
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const f16x8 af = tr_frag(ia, w, s);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) cs += (float)af[j];
+      for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+      const float ns = pt_scale(m);
+      const float r = ns / sc;
 #pragma unroll
       for (int y = 0; y < NTB; ++y)
-        acc[y] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af, tr_frag(ib, y, s), acc[y], 0, 0, 0);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[y][i] *= r;
+      sc = ns;
     }
+    f16x8 ah[2], al[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float x = R.a[8 * s + j] * sc;
+        const _Float16 h = (_Float16)x;
+        ah[s][j] = h;
+        al[s][j] = (_Float16)(x - (float)h);
+      }
+    {  // next tile into the (now free) registers; the last tile is re-read (keeps the loop uniform)
+      const int64_t tn = t + 1 < ntile ? t + 1 : t;
+      wx_load<NTB, WB>(a, kb + 32 * tn, R);
+    }
+    __syncthreads();  // planes of tile t written; every wave is done with the slot of tile t - 2
+    const char* ph = slot;
+    const char* pl = slot + Cfg::kPlane;
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int y = 0; y < NTB; ++y) {
+        const f16x8 bh = tr_frag(ph, y, s), bl = tr_frag(pl, y, s);
+        acc[y] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[s], bh, acc[y], 0, 0, 0);
+        acc[y] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[s], bl, acc[y], 0, 0, 0);
+        acc[y] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[s], bh, acc[y], 0, 0, 0);
+      }
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the re-staged tail DMAs
-  const float inv = 1.f / delta_scale(*a.gmax);
-  // C[32w + perm(r,hh)][32y + (lane&31)] += acc / s
+  const float inv = 1.f / sc;
+  // C[32w + perm(r,hh)][32y + (lane&31)] += acc / sc
 #pragma unroll
   for (int y = 0; y < NTB; ++y) {
     const int col = 32 * y + (lane & 31);
@@ -151,12 +205,12 @@ __global__ __launch_bounds__(512, 1) void k_wgrad16(Wg16Args a) {
     for (int r = 0; r < 16; ++r) atomicAdd(a.C + (int64_t)(32 * w + perm(r, hh)) * a.ldc + col, acc[y][r] * inv);
   }
   cs += __shfl_xor(cs, 32);
-  if (a.bias && hh == 0) atomicAdd(a.bias + 32 * w + lane, cs * inv);
+  if (a.bias && hh == 0) atomicAdd(a.bias + 32 * w + lane, cs);
 }
 
 template <int NTB, int WB>
-static int launch_k(const Wg16Args& a, hipStream_t st) {
-  using Cfg = Wg16<NTB, WB>;
+static int launch_k(const WxArgs& a, hipStream_t st) {
+  using Cfg = Wx3<NTB, WB>;
   auto kern = k_wgrad16<NTB, WB>;
   static const bool attr = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                                                Cfg::kLds) == hipSuccess;
@@ -166,23 +220,23 @@ static int launch_k(const Wg16Args& a, hipStream_t st) {
 }
 
 // kind: kWgradHidden (B [K][256]), kWgradFirst (B [K][96], 93 columns) or kWgradFc (B [K][32]);
-// K is rounded up to 32
-// (the rows up to it exist and carry zero deltas)
-int launch_wgrad16(int kind, const void* A, const void* B, int64_t K, float* C, int64_t ldc, float* bias,
-                   const uint32_t* gmax, hipStream_t st) {
+// K is rounded up to 32 (the A rows up to it exist and carry zero deltas)
+int launch_wgrad16(int kind, const float* A, const float* B, int64_t K, int64_t kb_rows, float* C, int64_t ldc,
+                   float* bias, hipStream_t st) {
   if (K <= 0) return 0;
+  if (kb_rows <= 0) return PNR_E_ARG;
   K = (K + 31) / 32 * 32;
   // split-K: each workgroup flushes its whole C tile (256 KB of float atomics for a hidden layer,
-  // ~0.2 us of the chip's atomic rate) and spends ~0.5 us per 32-point tile, so the time
-  // (K / 32 / n) * 0.5 + n * 0.2 is least at n = sqrt(2.5 K / 32); at most one workgroup per CU
-  int64_t nwg = (int64_t)sqrt(2.5 * (double)K / 32.0);
+  // ~0.2 us of the chip's atomic rate) and spends ~1 us per 32-point tile, so the time
+  // (K / 32 / n) + n * 0.2 is least at n = sqrt(5 K / 32); at most one workgroup per CU
+  int64_t nwg = (int64_t)sqrt(5.0 * (double)K / 32.0);
   nwg = nwg < 4 ? 4 : (nwg > 256 ? 256 : nwg);
   int64_t ks = (K + nwg - 1) / nwg;
   ks = (ks + 31) / 32 * 32;
-  Wg16Args a{static_cast<const _Float16*>(A), static_cast<const _Float16*>(B), 256, K, ks, C, ldc, bias, gmax};
+  WxArgs a{A, B, 256, K, kb_rows, ks, C, ldc, bias};
   TimingScope ts(kTimeWgrad, K, st);
   if (kind == kWgradHidden) return launch_k<8, 256>(a, st);
-  if (kind == kWgradFc) {  // dWc_l (256 x 32) += gH_l^T c : B = f16 copy of the features [K][32]
+  if (kind == kWgradFc) {  // dWc_l (256 x 32) += gH_l^T c
     a.nb = kCDim;
     return launch_k<1, 32>(a, st);
   }
@@ -193,19 +247,17 @@ int launch_wgrad16(int kind, const void* A, const void* B, int64_t K, float* C, 
   return PNR_E_ARG;
 }
 
-// Skinny weight-gradient GEMMs, bandwidth-bound on B:
-//   C[m][n] += inv * sum_k A[k][m] B[k][n]   m < M (<= 4), n < N      (bias[m] += sum_k A[k][m])
-// A fp32 rows of 4 (float4: g_out, or x = (x0, x1, x2, inside) with M = 3), B f16 rows of WB.
-//   dWo (4 x 256) = g_out^T h4 (+ dbo)       dB (3 x 93) = x^T (g_arg * s)  (inv = 1/s)
-// A block streams its K range 16 rows at a time: thread (r, c) = (tid / CPR, tid % CPR) loads 16 B
-// (8 columns) of row r and the row's float4 of A, keeping 4 x 8 partial sums; the rows are then
-// reduced through LDS and flushed with one atomic per output element per block.
+// Skinny weight-gradient GEMMs (fp32 FMAs), bandwidth-bound on B:
+//   C[m][n] += sum_k A[k][m] B[k][n]   m < M (<= 4), n < N      (bias[m] += sum_k A[k][m])
+// A fp32 rows of 4 (float4: g_out, or x = (x0, x1, x2, inside) with M = 3), B fp32 rows of WB.
+//   dWo (4 x 256) = g_out^T h4 (+ dbo)       dB (3 x 93) = x^T g_arg
+// A block streams its K range: thread (r, c) = (tid / CPR, tid % CPR) loads 32 B (8 columns) of row
+// r and the row's float4 of A, keeping 4 x 8 partial sums; the rows are then reduced through LDS and
+// flushed with one atomic per output element per block.
 template <int WB>
-__global__ __launch_bounds__(256) void k_wgrad_skinny16(const float4* __restrict__ A, const _Float16* __restrict__ B,
-                                                        int64_t K, int64_t ks, int M, int N, float* __restrict__ C,
-                                                        int64_t ldc, float* __restrict__ bias,
-                                                        const uint32_t* __restrict__ gmax) {
-  typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+__global__ __launch_bounds__(256) void k_wgrad_skinny(const float4* __restrict__ A, const float* __restrict__ B,
+                                                      int64_t K, int64_t ks, int M, int N, float* __restrict__ C,
+                                                      int64_t ldc, float* __restrict__ bias) {
   constexpr int CPR = WB / 8;          // threads per row (32 for 256, 12 for 96)
   constexpr int RPI = 256 / CPR;       // rows per iteration (8 or 21)
   __shared__ float red[4][256 + 8];
@@ -223,25 +275,24 @@ __global__ __launch_bounds__(256) void k_wgrad_skinny16(const float4* __restrict
   if (act) {
     constexpr int U = 4;  // rows in flight per thread (HBM latency: bytes in flight per CU)
     for (int64_t k = kb + r; k < ke; k += U * RPI) {
-      float4 av[U];
-      h8 bv[U];
+      float4 av[U], b0[U], b1[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int64_t ku = k + u * RPI;
         const int64_t kc = ku < ke ? ku : k;  // rows past the range: re-read row k, weighted 0
         av[u] = A[kc];
-        bv[u] = *reinterpret_cast<const h8*>(B + kc * WB + 8 * c);
+        b0[u] = *reinterpret_cast<const float4*>(B + kc * WB + 8 * c);
+        b1[u] = *reinterpret_cast<const float4*>(B + kc * WB + 8 * c + 4);
         if (ku >= ke) av[u] = make_float4(0.f, 0.f, 0.f, 0.f);
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const float a4[4] = {av[u].x, av[u].y, av[u].z, av[u].w};
+        const float bv[8] = {b0[u].x, b0[u].y, b0[u].z, b0[u].w, b1[u].x, b1[u].y, b1[u].z, b1[u].w};
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float x = (float)bv[u][j];
+        for (int j = 0; j < 8; ++j)
 #pragma unroll
-          for (int m = 0; m < 4; ++m) acc[m][j] = __builtin_fmaf(a4[m], x, acc[m][j]);
-        }
+          for (int m = 0; m < 4; ++m) acc[m][j] = __builtin_fmaf(a4[m], bv[j], acc[m][j]);
         if (c == 0) {
 #pragma unroll
           for (int m = 0; m < 4; ++m) bs[m] += a4[m];
@@ -249,7 +300,6 @@ __global__ __launch_bounds__(256) void k_wgrad_skinny16(const float4* __restrict
       }
     }
   }
-  const float inv = gmax ? 1.f / delta_scale(*gmax) : 1.f;
   // reduce the RPI row groups: column n = 8c + j
   for (int m = 0; m < 4; ++m) {
     for (int i = tid; i < 256 + 8; i += 256) red[m][i] = 0.f;
@@ -267,45 +317,30 @@ __global__ __launch_bounds__(256) void k_wgrad_skinny16(const float4* __restrict
   __syncthreads();
   for (int i = tid; i < 4 * N; i += 256) {
     const int m = i / N, n = i % N;
-    if (m < M) atomicAdd(C + (int64_t)m * ldc + n, red[m][n] * inv);
+    if (m < M) atomicAdd(C + (int64_t)m * ldc + n, red[m][n]);
   }
   if (bias && tid < M) atomicAdd(bias + tid, red[tid][256 + 4]);
 }
 
-// f16 copy of n floats (the per-point features c, the B operand of dWc)
-__global__ void k_to_f16(const float* __restrict__ x, _Float16* __restrict__ y, int64_t n) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-    y[i] = (_Float16)x[i];
-}
-int launch_to_f16(const float* x, void* y, int64_t n, hipStream_t st) {
-  if (n <= 0) return 0;
-  int64_t blocks = (n + 1023) / 1024;
-  if (blocks > 4096) blocks = 4096;
-  hipLaunchKernelGGL(k_to_f16, dim3((unsigned)blocks), dim3(256), 0, st, x, static_cast<_Float16*>(y), n);
-  return hip_status(hipGetLastError());
-}
-
-// dWo (4 x 256) += g_out^T h4 (f16), dbo += colsum(g_out)
-int launch_wgrad_out16(const float* g_out, const void* h4, int64_t K, float* C, float* bias, hipStream_t st) {
+// dWo (4 x 256) += g_out^T h4, dbo += colsum(g_out)
+int launch_wgrad_out16(const float* g_out, const float* h4, int64_t K, float* C, float* bias, hipStream_t st) {
   if (K <= 0) return 0;
   int64_t ks = (K + 1023) / 1024;
   if (ks < 256) ks = 256;
   TimingScope ts(kTimeWgrad, K, st);
-  hipLaunchKernelGGL(k_wgrad_skinny16<256>, dim3((unsigned)((K + ks - 1) / ks)), dim3(256), 0, st,
-                     reinterpret_cast<const float4*>(g_out), static_cast<const _Float16*>(h4), K, ks, 4, kHidden, C,
-                     (int64_t)kHidden, bias, nullptr);
+  hipLaunchKernelGGL(k_wgrad_skinny<256>, dim3((unsigned)((K + ks - 1) / ks)), dim3(256), 0, st,
+                     reinterpret_cast<const float4*>(g_out), h4, K, ks, 4, kHidden, C, (int64_t)kHidden, bias);
   return hip_status(hipGetLastError());
 }
 
-// dB (3 x 93) += x^T g_arg: x rows float4 (x0, x1, x2, inside), g_arg f16 * s [K][96]
-int launch_wgrad_fourier16(const float4* xP, const void* garg, int64_t K, float* C, const uint32_t* gmax,
-                           hipStream_t st) {
+// dB (3 x 93) += x^T g_arg: x rows float4 (x0, x1, x2, inside), g_arg fp32 [K][96]
+int launch_wgrad_fourier16(const float4* xP, const float* garg, int64_t K, float* C, hipStream_t st) {
   if (K <= 0) return 0;
   int64_t ks = (K + 1023) / 1024;
   if (ks < 256) ks = 256;
   TimingScope ts(kTimeWgrad, K, st);
-  hipLaunchKernelGGL(k_wgrad_skinny16<96>, dim3((unsigned)((K + ks - 1) / ks)), dim3(256), 0, st, xP,
-                     static_cast<const _Float16*>(garg), K, ks, 3, kFourier, C, (int64_t)kFourier, nullptr, gmax);
+  hipLaunchKernelGGL(k_wgrad_skinny<96>, dim3((unsigned)((K + ks - 1) / ks)), dim3(256), 0, st, xP, garg, K, ks,
+                     3, kFourier, C, (int64_t)kFourier, nullptr);
   return hip_status(hipGetLastError());
 }
 

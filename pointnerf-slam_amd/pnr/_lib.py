@@ -21,9 +21,11 @@ MAX_K = 8
 GATHER_IDW, GATHER_TRILINEAR = 0, 1
 # decoder matmul arithmetic (include/pnr.h PNR_PREC_*)
 PRECISIONS = {'fp32': 0, 'bf16x3': 1, 'bf16': 2, 'f16x3': 3}
-# f16x3: fp32-class results (tests/test_gpu_parity.py runs every case under fp32 and f16x3 at the
-# same tolerances) at 2.9x the fp32 MFMA kernel's speed
+# f16x3: fp32-class forward AND backward (every GEMM on 22-bit split operands with fp32
+# accumulation; tests/test_gpu_parity.py runs every case under fp32 and f16x3 at the same tolerances)
 DEFAULT_PRECISION = os.environ.get('PNR_PRECISION', 'f16x3')
+ABI_VERSION = 7
+STATUS_F16_RANGE = 1  # include/pnr.h PNR_STATUS_F16_RANGE
 
 
 def precision_code(name) -> int:
@@ -57,6 +59,7 @@ class RenderParams(ctypes.Structure):
         ('t_vals', c_float * MAX_SAMPLES), ('u_vals', c_float * MAX_SAMPLES),
         ('save_for_backward', c_int32), ('need_ray_grads', c_int32),
         ('points', ctypes.POINTER(Points)), ('precision', c_int32),
+        ('status', c_void_p), ('far_clamp_dev', c_void_p),
     ]
 
 

@@ -49,12 +49,17 @@ class DataParallel:
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
 
     def global_far_clamp(self, gt_depth_local):
-        m = (gt_depth_local.reshape(-1).float() * 1.2).max() if gt_depth_local.numel() else \
-            torch.tensor(float('-inf'), device=gt_depth_local.device)
-        m = m.reshape(1).clone()
+        """max(1.2 * gt) over every rank's rays (Renderer.py:112), as a one-element float32 device
+        tensor: the renderer reads it on the device (far_mode 2), so the step has no host sync and
+        can be captured in a graph."""
+        g = gt_depth_local.reshape(-1).float()
+        if g.numel():
+            m = (g * 1.2).amax().reshape(1)
+        else:
+            m = torch.full((1,), float('-inf'), device=g.device)
         if self.world > 1:
             dist.all_reduce(m, op=dist.ReduceOp.MAX, group=self.group)
-        return float(m.item())
+        return m
 
     def allreduce_(self, flat_grad):
         if self.world > 1:

@@ -110,7 +110,11 @@ class _RenderFn(torch.autograd.Function):
         need = any(ctx.needs_input_grad)  # (inside forward grad mode is off; ask autograd)
         prm.save_for_backward = 1 if need else 0
         prm.need_ray_grads = 1 if (ctx.needs_input_grad[3] or ctx.needs_input_grad[4]) else 0
-        if far_clamp is not None:
+        if isinstance(far_clamp, torch.Tensor):  # device value (sharded batch): no host round trip
+            far_clamp = far_clamp.reshape(-1)[:1].float().contiguous()
+            prm.far_mode = 2
+            prm.far_clamp_dev = far_clamp.data_ptr()
+        elif far_clamp is not None:
             prm.far_mode = 1
             prm.far_clamp = float(far_clamp)
         ws = torch.empty(lib.pnr_render_workspace_bytes(ctypes_ref(prm), n), dtype=torch.uint8, device=dev)
@@ -227,6 +231,35 @@ class Renderer(object):
         if self.N_samples + self.N_importance > _lib.MAX_SAMPLES or self.N_samples < 3:
             raise ValueError('pnr.Renderer: need 3 <= N_samples and N_samples + N_importance <= 64')
 
+    def __getstate__(self):  # the status words are per process (device memory)
+        st = dict(self.__dict__)
+        st.pop('_status', None)
+        return st
+
+    # -- f16-range status (include/pnr.h PNR_STATUS_*) ------------------------------------------
+    def status_word(self, device):
+        """Device int32 the kernels OR PNR_STATUS_* bits into (one per device, lazily created)."""
+        sw = self.__dict__.setdefault('_status', {})
+        dev = torch.device(device)
+        if dev not in sw:
+            sw[dev] = torch.zeros(1, dtype=torch.int32, device=dev)
+        return sw[dev]
+
+    def status(self, device='cuda:0', clear=False):
+        """PNR_STATUS_* bits raised since the last clear (synchronises with the device)."""
+        w = self.status_word(device)
+        v = int(w.item())
+        if clear:
+            w.zero_()
+        return v
+
+    def check_status(self, device='cuda:0'):
+        """Raise FloatingPointError when an f16x3 forward met a value outside the f16 range: its
+        results are not fp32-faithful (include/pnr.h PNR_STATUS_F16_RANGE).  Use precision 'fp32'."""
+        if self.status(device) & _lib.STATUS_F16_RANGE:
+            raise FloatingPointError('pnr: an f16x3 decoder forward met |value| >= 65504 (f16 range); '
+                                     "results since the last check are not fp32-faithful: use precision 'fp32'")
+
     # -- helpers --------------------------------------------------------------------------------
     def _bound6(self):
         # the bound is fixed per renderer (src/NICE_SLAM.py:208-213): read once, so a render issues no
@@ -285,12 +318,14 @@ class Renderer(object):
         """Renderer.py:63-203 -> (depth f64 (N,), uncertainty f64 (N,), color f32 (N,3)).
 
         `far_clamp` (extension, default None = reference behaviour) overrides the batch-global
-        max(1.2*gt) of Renderer.py:112 -- used by a ray-sharded caller to keep 1-GPU semantics."""
+        max(1.2*gt) of Renderer.py:112 -- used by a ray-sharded caller to keep 1-GPU semantics: a
+        float, or a one-element device tensor (read on the device: no host sync, graph-capturable)."""
         _lib.require_cuda(rays_o, rays_d, gt_depth)
         rays_o = rays_o.float().contiguous()
         rays_d = rays_d.float().contiguous()
         gt = None if gt_depth is None else gt_depth.reshape(-1).float().contiguous()
         prm = self.params()
+        prm.status = self.status_word(rays_o.device).data_ptr()
         params = _decoder_params(decoders)
         pts, fc_owner, extra = _feature_inputs(c, decoders)
         feat = _Feat(pts, fc_owner, [*params, *extra])
@@ -324,6 +359,7 @@ class Renderer(object):
             t_rand = torch.rand((n, self.N_samples), device=rays_o.device)
         t_rand = t_rand.float().contiguous()
         prm = self.params(n_importance=0)
+        prm.status = self.status_word(rays_o.device).data_ptr()
         params = _decoder_params(decoders)
         pts, fc_owner, extra = _feature_inputs(c, decoders)
         feat = _Feat(pts, fc_owner, [*params, *extra])

@@ -43,10 +43,10 @@ def test_python_binding_covers_header():
 
 def test_host_only_calls(lib):
     lib.pnr_abi_version.restype = ctypes.c_int
-    assert lib.pnr_abi_version() == 6
+    assert lib.pnr_abi_version() == 7
     lib.pnr_mlp_packed_floats.restype = ctypes.c_size_t
     # fp32 images 486,688 + bf16x3 / bf16 / f16x3 forward streams 229,376 / 118,784 / 229,376
-    # + bf16x3 delta-chain stream 225,280 + raw table 2,048 + fp32 Wo 1,024
+    # + f16x3 delta-chain stream 225,280 + raw table 2,048 + fp32 Wo 1,024
     assert lib.pnr_mlp_packed_floats() == 486688 + 229376 + 118784 + 229376 + 225280 + 3072
     lib.pnr_build_info.restype = ctypes.c_char_p
     assert b'gfx950' in lib.pnr_build_info()
@@ -56,9 +56,10 @@ def test_params_struct_layout():
     import sys
     sys.path.insert(0, os.path.join(REPO, 'pointnerf-slam_amd'))
     from pnr import _lib
-    # int32 x4, double[6], double, float[64] x2, int32 x2, pointer -> 600 bytes with natural alignment
-    assert ctypes.sizeof(_lib.RenderParams) == 608
+    # int32 x4, double[6], double, float[64] x2, int32 x2, pointer, int32, 2 pointers (ABI 7)
+    assert ctypes.sizeof(_lib.RenderParams) == 624
     assert _lib.RenderParams.precision.offset == 600
+    assert _lib.RenderParams.status.offset == 608 and _lib.RenderParams.far_clamp_dev.offset == 616
     assert _lib.RenderParams.bound.offset == 16 and _lib.RenderParams.t_vals.offset == 72
     assert _lib.RenderParams.points.offset == 592
     # pnr_points: 2 ptr, int64, 2 int32, 2 float, float[3], float, float[3], int32, 4 ptr, int32 (ABI 6)
@@ -82,6 +83,9 @@ def test_workspace_queries_and_arg_errors(lib):
     bad = _lib.RenderParams()
     bad.n_samples, bad.n_importance = 40, 30          # > 64 samples per ray
     assert L.pnr_render_workspace_bytes(ctypes.byref(bad), 10) == 0
+    bad2 = _lib.RenderParams()
+    bad2.n_samples, bad2.n_importance, bad2.far_mode = 32, 12, 2   # device far clamp without a pointer
+    assert L.pnr_render_workspace_bytes(ctypes.byref(bad2), 10) == 0
     # argument errors are reported without touching the device
     assert L.pnr_render_fwd(ctypes.byref(bad), None, None, None, None, 10, None, None, None, None, 0, None) == -1
     assert L.pnr_eval_points(None, None, 5, None, None, 0, None) == -1

@@ -53,7 +53,7 @@ def _worker(rank, world, port, q):
     gc = torch.from_numpy(G['map_gt_color'][:n][a:b].copy())
     tr = torch.from_numpy(G['map_t_rand'][:n][a:b].copy())
     ddp = pdist.DataParallel()
-    fc = ddp.global_far_clamp(gt)
+    fc = float(ddp.global_far_clamp(gt))  # a device tensor (far_mode 2); the oracle takes a float
     params = {k: v.clone().requires_grad_(True) for k, v in golden_params('trained').items()}
     d, v, c = ref.render_batch_ray(params, rd, ro, bound, gt_depth=gt, far_clamp=fc)
     sig = ref.regulation(params, rd, ro, gt, bound, t_rand=tr)

@@ -64,7 +64,7 @@ def close(a, b, rtol, atol, what):
 
 def test_library_info(pnr_mod):
     lib = pnr_mod.library()
-    assert lib.pnr_abi_version() == 6
+    assert lib.pnr_abi_version() == 7
     assert lib.pnr_mlp_packed_floats() > 0
 
 
