@@ -1,23 +1,36 @@
 #!/usr/bin/env python3
 """Benchmark: rendered rays/s per mapping iteration (BASELINE.json metric) on MI355X.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload map|fwd] [--rays R]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload map|fwd|map-points] [--rays R]
+                  [--global-batch B] [--precision P] [--graph] [--no-extras] [--no-cpu-baseline]
 
 Workload `map` (default; SURVEY.md 8(d) "S-map"): one full Mapper iteration of
 src/Mapper.py:507-662 for the effective room0 config (configs/pointNeRF_slam.yaml +
 configs/Replica/room0_point.yaml: 32 stratified + 12 importance samples, gt-depth near/far,
 regulation with 32 jittered samples, L1 depth + 0.05 L1 colour + 0.0005 |sigma|, backward,
-Adam lr 2e-4) over R rays per GPU (default 307,200 = one 640x480 pixel batch), fp32.
+Adam lr 2e-4) over R rays per GPU (default 307,200 = one 640x480 pixel batch).  Decoder
+arithmetic: f16x3 by default -- fp32-class end to end (every forward and backward GEMM on 22-bit
+split operands with fp32 accumulation, include/pnr.h); `--precision fp32` runs fp32 MFMA.
 Workload `fwd` ("S-fwd"): render_batch_ray forward, 640x480 rays x 64 stratified samples.
+
+Extra keys of the N=1 line (measured after the timed region, never part of `value`):
+  sfwd            the north-star S-fwd batch (640x480 x 64 samples, forward) with its own roofline
+                  and the oracle's CPU rate at 64 samples
+  faithful_n1000  the room0 Mapper iteration at its real size (N = 1,000 rays), replayed from a
+                  captured HIP graph (pnr.mapping.MapGraph), and N = 5,000 (C4/C5)
+  fp32            the same S-map step with fp32-MFMA decoder arithmetic
+  gather_roofline the neural-point gather (A15) on its HBM roofline
+N>1 lines add `fixed_global_batch`: the 307,200-ray batch split over the N ranks.
 
 Data: synthetic.  Decoder = the trained room0 weights committed as a golden fixture
 (tests/golden/weights.npz, from the reference's own checkpoint) -- random init if absent; rays
 from room0 pose gt_c2w_list[1000] through ScanNet-style 640x480 intrinsics; gt depth U[0.05,0.6]
 with 10% zeros; gt colour U[0,1]; seed 0 + rank.
 
-Multi-GPU (torchrun, one process per GPU, RCCL): every rank maps its own R rays (weak
-scaling); per step one scalar all_reduce(MAX) (global far clamp) and one 891 KB gradient
-all_reduce(SUM).  Rank 0 prints ONE JSON line.
+Multi-GPU (torchrun, one process per GPU, RCCL): every rank maps its own R rays (weak scaling;
+`--global-batch B` splits B rays over the ranks instead: strong scaling); per step one scalar
+all_reduce(MAX) (global far clamp, read on the device) and one 891 KB gradient all_reduce(SUM).
+Rank 0 prints ONE JSON line.
 """
 import argparse
 import json
@@ -176,39 +189,66 @@ def gather_roofline(dev, voxel=0.001, k=8, reps=5, feat_dtype='float32'):
             'bytes_per_launch': byt}
 
 
-def cpu_baseline(bound, pose, params, workload, n_rays=2048, reps=3, gpu_render=None):
+def cpu_threads():
+    """Threads of the CPU baseline: torch's intra-op pool (OMP_NUM_THREADS = this host's CPU share,
+    16 on the GPU box), capped at the physical cores psutil reports."""
+    n = torch.get_num_threads()
+    try:
+        import psutil
+        n = min(n, psutil.cpu_count(logical=False) or n)
+    except ImportError:
+        pass
+    return max(1, n)
+
+
+def cpu_baseline(bound, pose, params, workload, gpu_render=None, reps=5):
     """The oracle (oracle/ref_render.py, a bit-exact restatement of the reference CPU path pinned
-    by tests/test_oracle_golden.py) timed on this host: bounded sample, median of `reps`.
-    `gpu_render(ro, rd, gt) -> (depth, colour)` renders the same rays on the measured HIP path
-    with the initial weights; the leg then reports the metric's PSNR condition on them."""
+    by tests/test_oracle_golden.py) timed on this host on a bounded sample, median of `reps` after
+    one warm-up, at the physical-core thread count and at 1 thread.  `gpu_render(ro,
+    rd, gt) -> (depth, colour)` renders the same rays on the measured HIP path with the initial
+    weights; the leg then reports the metric's PSNR condition on them."""
     from oracle import ref_render as ref
-    cores = torch.get_num_threads()
-    ro, rd, gt, col = [t.cpu() for t in synth_batch(n_rays, 0, pose, 'cpu', seed=7)]
-    p = {k: v.clone().requires_grad_(workload == 'map') for k, v in params.items()}
-    opt = torch.optim.Adam(list(p.values()), lr=2e-4) if workload == 'map' else None
+    cores = cpu_threads()
+    prev = torch.get_num_threads()
+    # rays per sample: ~1-3 s per timed step at each thread count
+    sizes = {'map': (2048, 256), 'fwd': (8192, 1024)}[workload]
 
-    def step():
-        if workload == 'map':
-            opt.zero_grad()
-            d, v, c = ref.render_batch_ray(p, rd, ro, bound, gt_depth=gt)
-            sig = ref.regulation(p, rd, ro, gt, bound)
-            ref.mapping_loss(d, c, gt, col, sig).backward()
-            opt.step()
-        else:
-            with torch.no_grad():
-                ref.render_batch_ray(p, rd, ro, bound, n_samples=64, n_importance=0)
+    def rate(n_rays, threads):
+        torch.set_num_threads(threads)
+        ro, rd, gt, col = [t.cpu() for t in synth_batch(n_rays, 0, pose, 'cpu', seed=7)]
+        p = {k: v.clone().requires_grad_(workload == 'map') for k, v in params.items()}
+        opt = torch.optim.Adam(list(p.values()), lr=2e-4) if workload == 'map' else None
 
-    step()
-    ts = []
-    for _ in range(reps):
-        t0 = time.perf_counter()
+        def step():
+            if workload == 'map':
+                opt.zero_grad()
+                d, v, c = ref.render_batch_ray(p, rd, ro, bound, gt_depth=gt)
+                sig = ref.regulation(p, rd, ro, gt, bound)
+                ref.mapping_loss(d, c, gt, col, sig).backward()
+                opt.step()
+            else:
+                with torch.no_grad():
+                    ref.render_batch_ray(p, rd, ro, bound, n_samples=64, n_importance=0)
+
         step()
-        ts.append(time.perf_counter() - t0)
-    t = float(np.median(ts))
-    out = {'value': round(n_rays / t, 1), 'unit': 'rays/s', 'cores': cores, 'kind': 'port',
-           'sample': f'{workload} step on {n_rays} rays, oracle (torch CPU restatement of src/utils/Renderer.py), '
-                     f'median of {reps} after 1 warm-up, {cores} threads'}
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            step()
+            ts.append(time.perf_counter() - t0)
+        return n_rays / float(np.median(ts))
+
+    v_all = rate(sizes[0], cores)
+    v_one = rate(sizes[1], 1)
+    torch.set_num_threads(prev)
+    what = {'map': 'map step (render + regulation + L1 losses + backward + Adam)',
+            'fwd': 'render_batch_ray forward, 64 samples'}[workload]
+    out = {'value': round(v_all, 1), 'unit': 'rays/s', 'cores': cores, 'kind': 'port',
+           'sample': f'{what} on {sizes[0]} rays ({cores} threads) and {sizes[1]} rays (1 thread), oracle (torch '
+                     f'CPU restatement of src/utils/Renderer.py), median of {reps} after 1 warm-up',
+           'value_1thread': round(v_one, 1)}
     if gpu_render is not None:
+        ro, rd, gt, col = [t.cpu() for t in synth_batch(2048, 0, pose, 'cpu', seed=7)]
         with torch.no_grad():
             if workload == 'map':
                 d_r, _, c_r = ref.render_batch_ray(params, rd, ro, bound, gt_depth=gt)
@@ -217,10 +257,149 @@ def cpu_baseline(bound, pose, params, workload, n_rays=2048, reps=3, gpu_render=
         d_g, c_g = gpu_render(ro, rd, gt if workload == 'map' else None)
         rel = ((d_g.double() - d_r.double()).abs() / d_r.double().abs().clamp_min(1e-12)).max().item()
         out['parity'] = {'psnr_db': round(ref.psnr(c_g, c_r), 2), 'depth_max_rel': float(f'{rel:.3g}'),
-                         'rays': n_rays,
+                         'rays': 2048,
                          'what': 'PSNR of the HIP render vs the oracle render of the same rays (initial weights); '
                                  'the metric\'s PSNR delta vs GT <= 0.1 dB holds when this exceeds PSNR(ref, GT) '
                                  '+ 39 dB (SURVEY.md 8(d))'}
+    return out
+
+
+def timed(step, steps, warmup, ddp, lib):
+    """W untimed steps, then exactly K steps between barrier + device syncs; wall seconds (max over
+    ranks) and the libpnr kernel timings (hipEvents on each launch's stream) of the K steps."""
+    from pnr._lib import timing_read
+    for _ in range(warmup):
+        step()
+    ddp.barrier()
+    torch.cuda.synchronize()
+    lib.pnr_timing_enable(1)
+    for kind in range(6):
+        timing_read(kind)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    ddp.barrier()
+    el = time.perf_counter() - t0
+    lib.pnr_timing_enable(0)
+    kt = {'mlp_fwd': timing_read(0), 'mlp_bwd': timing_read(1), 'wgrad': timing_read(3), 'gather': timing_read(4),
+          'gather_bwd': timing_read(5)}
+    kt = {k: v for k, v in kt.items() if v[0] > 0}
+    if ddp.world > 1:
+        t = torch.tensor([el], device='cuda', dtype=torch.float64)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        el = float(t.item())
+    return el, kt
+
+
+def kernel_roofline(kt, prec, el_s, traffic_units=True):
+    """Roofline of the dominant hand-written MLP kernel (fused forward or delta chain), per launch:
+    algorithmic fp32-equivalent FLOP per point x points per launch / mean launch time."""
+    best = None
+    for name, (launches, ms, units) in kt.items():
+        if name not in ('mlp_fwd', 'mlp_bwd'):
+            continue
+        fl = FLOP_PER_POINT_FWD if name == 'mlp_fwd' else FLOP_PER_POINT_BWD
+        # the delta chain is fp32 in the fp32 mode and the f16x3 split in every other mode
+        kprec = prec if name == 'mlp_fwd' else ('fp32' if prec == 'fp32' else 'f16x3')
+        kname = ('k_mlp_fwd16' if prec != 'fp32' else 'k_mlp_fwd') if name == 'mlp_fwd' else \
+            ('k_mlp_bwd16' if prec != 'fp32' else 'k_mlp_bwd')
+        cand = {'kernel': kname, 'launches': launches, 'prec': kprec, 'peak': ALGO_PEAK_TF[kprec],
+                'avg_ms': ms / launches, 'share_of_step': ms / (el_s * 1e3), 'units': units / launches,
+                'achieved': fl * units / launches / (ms / launches * 1e-3) / 1e12, '_ms': ms}
+        if best is None or ms > best['_ms']:
+            best = cand
+    if best is None:
+        return None
+    tkey = {'k_mlp_fwd': 'k_mlp_fwd_train', 'k_mlp_fwd16': 'k_mlp_fwd16_train', 'k_mlp_bwd': 'k_mlp_bwd',
+            'k_mlp_bwd16': 'k_mlp_bwd16'}
+    traffic = pmc_traffic(tkey[best['kernel']], best['units']) if traffic_units else None
+    return {'bound': 'mfma', 'achieved': round(best['achieved'], 2), 'peak': round(best['peak'], 1),
+            'unit': 'TFLOP/s', 'frac': round(best['achieved'] / best['peak'], 4), 'traffic': traffic,
+            'kernel': best['kernel'], 'avg_launch_ms': round(best['avg_ms'], 3), 'launches': best['launches'],
+            'kernel_share_of_step': round(best['share_of_step'], 3),
+            'flop_basis': 'algorithmic fp32-equivalent FLOP (443,438 fwd / 442,880 bwd per point); peak = '
+                          + ('fp32 MFMA 157.3 TF' if best['prec'] == 'fp32' else
+                             'f16/bf16 MFMA 2.5 PF dense / 3 products per fp32 product'
+                             if best['prec'] != 'bf16' else 'bf16 MFMA 2.5 PF dense')}
+
+
+DTYPE = {'fp32': 'fp32 (fp32 MFMA forward, delta chain and weight gradients)',
+         'f16x3': 'fp32-class f16x3 throughout: forward, delta chain (per-point power-of-two scaled) and weight-'
+                  'gradient GEMMs (on fp32-stored operands) all split every operand into 2 f16 parts (22 '
+                  'significant bits), 3 MFMA products, fp32 accumulation; dWo/dB fp32 FMA',
+         'bf16x3': 'bf16x3 split forward (16 significant bits); f16x3 backward as the default',
+         'bf16': 'bf16 MFMA forward (fp32 accumulate); f16x3 backward as the default'}
+
+
+def make_decoder(pnr, cfg, params, dev):
+    dec = pnr.get_model(cfg, nice=False)
+    if params is not None:
+        dec.load_state_dict(params)
+    return dec.to(dev)
+
+
+def map_step_fn(pnr, renderer, dec, cfg, ro, rd, gt, col, dev, ddp=None, points=None, graph=False):
+    from pnr.mapping import MapStep, MapGraph
+    n = ro.shape[0]
+    ns = cfg['rendering']['N_samples']
+    mstep = MapStep(renderer, dec, lr=cfg['mapping']['imap_decoders_lr'], w_color_loss=cfg['mapping']['w_color_loss'],
+                    ddp=ddp, points=points)
+    if graph:
+        mgraph = MapGraph(mstep, ro, rd, gt, col, torch.rand((n, ns), device=dev))
+
+        def step():  # the same iteration, replayed; a fresh regulation jitter drawn per step
+            mgraph(ro, rd, gt, col, torch.rand((n, ns), device=dev))
+        return step
+
+    def step():
+        mstep(ro, rd, gt, col, torch.rand((n, ns), device=dev))
+    return step
+
+
+def sfwd_extra(pnr, plib, slam, params, bound, pose, dev, ddp, lib, steps=10, cpu=True):
+    """S-fwd: render_batch_ray forward over the 640x480 batch at 64 stratified
+    samples, no importance, gt_depth None; roofline of k_mlp_fwd16 (eval) and the oracle CPU rate."""
+    import copy
+    cfg = copy.deepcopy(pnr.ROOM0_CFG)
+    cfg['rendering']['N_samples'], cfg['rendering']['N_importance'] = 64, 0
+    r = pnr.Renderer(cfg, None, slam)
+    dec = make_decoder(pnr, cfg, params, dev)
+    ro, rd, _, _ = synth_batch(W * H, 0, pose, dev)
+
+    def step():
+        with torch.no_grad():
+            r.render_batch_ray({}, dec, rd, ro, dev, 'color', gt_depth=None)
+    el, kt = timed(step, steps, 2, ddp, lib)
+    prec = plib.DEFAULT_PRECISION
+    out = {'workload': 'S-fwd: render_batch_ray forward, 640x480 rays x 64 stratified samples, gt_depth None',
+           'value': round(W * H * steps / el, 1), 'unit': 'rays/s', 'ms_per_step': round(el / steps * 1e3, 3),
+           'steps': steps, 'roofline': kernel_roofline(kt, prec, el, traffic_units=False)}
+    if out['roofline'] is not None:
+        out['roofline']['kernel'] += ' (eval, no activation saves)'
+    if cpu and params is not None:
+        def gpu_render(ro_c, rd_c, gt_c):
+            with torch.no_grad():
+                d, _, c = r.render_batch_ray({}, dec, rd_c.to(dev), ro_c.to(dev), dev, 'color', gt_depth=None)
+            return d.cpu(), c.cpu()
+        out['cpu_baseline'] = cpu_baseline(bound, pose, params, 'fwd', gpu_render=gpu_render)
+        out['speedup_vs_cpu'] = round(out['value'] / out['cpu_baseline']['value'], 1)
+    return out
+
+
+def faithful_extra(pnr, slam, params, pose, dev, ddp, lib, sizes=(1000, 5000), steps=50):
+    """The Mapper iteration at its real batch sizes (room0: mapping.pixels = 1,000; ScanNet /
+    Apartment: 5,000), replayed from a captured HIP graph."""
+    out = {}
+    for n in sizes:
+        cfg = pnr.ROOM0_CFG
+        r = pnr.Renderer(cfg, None, slam)
+        dec = make_decoder(pnr, cfg, params, dev)
+        ro, rd, gt, col = synth_batch(n, 0, pose, dev)
+        step = map_step_fn(pnr, r, dec, cfg, ro, rd, gt, col, dev, graph=True)
+        el, _ = timed(step, steps, 3, ddp, lib)
+        out[f'n{n}'] = {'ms_per_iter': round(el / steps * 1e3, 4), 'rays_per_s': round(n * steps / el, 1),
+                        'graph': True, 'iters': steps}
     return out
 
 
@@ -230,13 +409,15 @@ def main():
     ap.add_argument('--steps', type=int, default=5)
     ap.add_argument('--warmup', type=int, default=2)
     ap.add_argument('--workload', choices=['map', 'fwd', 'map-points'], default='map')
-    ap.add_argument('--rays', type=int, default=W * H, help='rays per GPU per step')
+    ap.add_argument('--rays', type=int, default=W * H, help='rays per GPU per step (weak scaling)')
+    ap.add_argument('--global-batch', type=int, default=None,
+                    help='fixed global batch split over the ranks (strong scaling; SURVEY.md 8(e))')
     ap.add_argument('--graph', action='store_true',
-                    help='replay the mapping iteration from a captured HIP graph (pnr.mapping.MapGraph; '
-                         'single GPU, for the latency-bound faithful batches N=1000 / 5000)')
+                    help='replay the mapping iteration from a captured HIP graph (pnr.mapping.MapGraph)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-gather', action='store_true', help='skip the point-gather roofline line')
-    ap.add_argument('--precision', default=None, help="decoder forward matmuls: fp32 | f16x3 (default) | bf16x3 | bf16")
+    ap.add_argument('--no-extras', action='store_true', help='skip sfwd / faithful_n1000 / fp32 extras')
+    ap.add_argument('--precision', default=None, help="decoder matmuls: f16x3 (default) | fp32 | bf16x3 | bf16")
     ap.add_argument('--feat-dtype', default='float32', choices=['float32', 'float16'],
                     help='neural-point feature storage (map-points workload and the gather line; C5: float16)')
     args = ap.parse_args()
@@ -244,8 +425,6 @@ def main():
     import pnr
     from pnr import _lib as plib
     from pnr import dist as pdist
-    from pnr._lib import timing_read
-    from pnr.mapping import MapStep
     if args.precision is not None:
         plib.precision_code(args.precision)
         plib.DEFAULT_PRECISION = args.precision
@@ -264,6 +443,13 @@ def main():
         cfg = copy.deepcopy(cfg)
         cfg['rendering']['N_samples'], cfg['rendering']['N_importance'] = 64, 0
     renderer = pnr.Renderer(cfg, None, slam)
+    ddp = pdist.DataParallel()
+    strong = args.global_batch is not None
+    if strong:  # this rank's contiguous share of one global batch
+        a, b = pdist.shard_bounds(args.global_batch, rank, world)
+        n = b - a
+    else:
+        n = args.rays
     points = None
     if args.workload == 'map-points':
         # the neural-point decoder: trained base weights + fresh fc_c, points on
@@ -273,100 +459,64 @@ def main():
         sd.update(params)
         dec.load_state_dict(sd)
         dec = dec.to(dev)
-        xyz, feats, _, (ro, rd, gt) = neural_point_scene(dev, n_rays=args.rays, seed=rank)
+        xyz, feats, _, (ro, rd, gt) = neural_point_scene(dev, n_rays=n, seed=rank)
         points = pnr.NeuralPoints(xyz, feats, mode='idw', radius=0.002, k=8, feat_dtype=args.feat_dtype).to(dev)
-        col = torch.rand((args.rays, 3), device=dev, generator=torch.Generator(device=dev).manual_seed(rank))
+        col = torch.rand((n, 3), device=dev, generator=torch.Generator(device=dev).manual_seed(rank))
     else:
-        dec = pnr.get_model(cfg, nice=False)
-        if params is not None:
-            dec.load_state_dict(params)
-        dec = dec.to(dev)
-        ro, rd, gt, col = synth_batch(args.rays, rank, pose, dev)
-    ddp = pdist.DataParallel()
-    n = args.rays
+        dec = make_decoder(pnr, cfg, params, dev)
+        if strong:  # the global batch drawn once (seed 0), this rank's slice
+            ro, rd, gt, col = [t[a:b].contiguous() for t in synth_batch(args.global_batch, 0, pose, dev)]
+        else:
+            ro, rd, gt, col = synth_batch(n, rank, pose, dev)
 
     if args.workload in ('map', 'map-points'):
-        mstep = MapStep(renderer, dec, lr=cfg['mapping']['imap_decoders_lr'],
-                        w_color_loss=cfg['mapping']['w_color_loss'], ddp=ddp if world > 1 else None,
-                        points=points)
-
-        def step():
-            t_rand = torch.rand((n, cfg['rendering']['N_samples']), device=dev)
-            mstep(ro, rd, gt, col, t_rand)
-
-        if args.graph and world == 1 and points is None:
-            from pnr.mapping import MapGraph
-            mgraph = MapGraph(mstep, ro, rd, gt, col, torch.rand((n, cfg['rendering']['N_samples']), device=dev))
-
-            def step():  # noqa: F811  (the same iteration, replayed; a fresh jitter drawn per step)
-                t_rand = torch.rand((n, cfg['rendering']['N_samples']), device=dev)
-                mgraph(ro, rd, gt, col, t_rand)
+        step = map_step_fn(pnr, renderer, dec, cfg, ro, rd, gt, col, dev, ddp=ddp if world > 1 else None,
+                           points=points, graph=args.graph and points is None)
     else:
         def step():
             with torch.no_grad():
                 renderer.render_batch_ray({}, dec, rd, ro, dev, 'color', gt_depth=None)
 
-    for _ in range(args.warmup):
-        step()
-    ddp.barrier()
-    torch.cuda.synchronize()
-    lib.pnr_timing_enable(1)
-    for kind in range(6):
-        timing_read(kind)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    ddp.barrier()
-    el = time.perf_counter() - t0
-    lib.pnr_timing_enable(0)
-    kt = {'mlp_fwd': timing_read(0), 'mlp_bwd': timing_read(1), 'wgrad': timing_read(3)}
-    if points is not None:
-        kt.update({'gather': timing_read(4), 'gather_bwd': timing_read(5)})
-    t = torch.tensor([el], device=dev, dtype=torch.float64)
-    if world > 1:
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-    el = float(t.item())
+    el, kt = timed(step, args.steps, args.warmup, ddp, lib)
     ms_per_step = el / args.steps * 1e3
-    value = n * world / (el / args.steps)
+    total = args.global_batch if strong else n * world
+    value = total / (el / args.steps)
+    roofline = kernel_roofline(kt, prec, el, traffic_units=args.workload == 'map')
+    if renderer.status(dev):
+        raise FloatingPointError('bench: the f16x3 forward met a value outside the f16 range (PNR_STATUS_F16_RANGE)')
 
-    # roofline of the dominant hand-written kernel (fused MLP fwd or delta chain), per launch
-    best = None
-    for name, (launches, ms, units) in kt.items():
-        if launches == 0 or name not in ('mlp_fwd', 'mlp_bwd'):
-            continue
-        fl = FLOP_PER_POINT_FWD if name == 'mlp_fwd' else FLOP_PER_POINT_BWD
-        # the delta chain is fp32 in the fp32 mode and the bf16x3 split in every other mode
-        kprec = prec if name == 'mlp_fwd' else ('fp32' if prec == 'fp32' else 'bf16x3')
-        kname = ('k_mlp_fwd16' if prec != 'fp32' else 'k_mlp_fwd') if name == 'mlp_fwd' else \
-            ('k_mlp_bwd16' if prec != 'fp32' else 'k_mlp_bwd')
-        cand = {'kernel': kname,
-                'launches': launches, 'prec': kprec, 'peak': ALGO_PEAK_TF[kprec],
-                'avg_ms': ms / launches, 'share_of_step': ms / (el * 1e3), 'units': units / launches,
-                'achieved': fl * units / launches / (ms / launches * 1e-3) / 1e12}
-        if best is None or ms > best['_ms']:
-            best = dict(cand, _ms=ms)
-    roofline = None
-    if best is not None:
-        tkey = {'k_mlp_fwd': 'k_mlp_fwd_train', 'k_mlp_fwd16': 'k_mlp_fwd16_train', 'k_mlp_bwd': 'k_mlp_bwd',
-                'k_mlp_bwd16': 'k_mlp_bwd16'}
-        traffic = pmc_traffic(tkey[best['kernel']], best['units']) if args.workload == 'map' else None
-        roofline = {'bound': 'mfma', 'achieved': round(best['achieved'], 2), 'peak': round(best['peak'], 1),
-                    'unit': 'TFLOP/s', 'frac': round(best['achieved'] / best['peak'], 4), 'traffic': traffic,
-                    'kernel': best['kernel'], 'avg_launch_ms': round(best['avg_ms'], 3),
-                    'launches': best['launches'], 'kernel_share_of_step': round(best['share_of_step'], 3),
-                    'flop_basis': 'algorithmic fp32-equivalent FLOP (443,438 fwd / 442,880 bwd per point); peak = '
-                                  + ('fp32 MFMA 157.3 TF' if best['prec'] == 'fp32' else
-                                     'f16/bf16 MFMA 2.5 PF dense / 3 products per fp32 product'
-                                     if best['prec'] != 'bf16' else 'bf16 MFMA 2.5 PF dense')}
+    extras = {}
+    if not args.no_extras and args.workload == 'map' and not strong:
+        if world > 1:
+            # the fixed-global-batch (strong-scaling) form of the same step: 307,200 rays over the ranks
+            ga, gb = pdist.shard_bounds(W * H, rank, world)
+            sro, srd, sgt, scol = [t[ga:gb].contiguous() for t in synth_batch(W * H, 0, pose, dev)]
+            sdec = make_decoder(pnr, cfg, params, dev)
+            sstep = map_step_fn(pnr, pnr.Renderer(cfg, None, slam), sdec, cfg, sro, srd, sgt, scol, dev, ddp=ddp)
+            sel, _ = timed(sstep, args.steps, args.warmup, ddp, lib)
+            extras['fixed_global_batch'] = {'global_batch': W * H, 'rays_per_gpu': gb - ga, 'scaling': 'strong',
+                                            'ms_per_step': round(sel / args.steps * 1e3, 3),
+                                            'value': round(W * H * args.steps / sel, 1), 'unit': 'rays/s'}
+        elif params is not None:
+            extras['sfwd'] = sfwd_extra(pnr, plib, slam, params, bound, pose, dev, ddp, lib,
+                                        cpu=not args.no_cpu_baseline)
+            extras['faithful_n1000'] = faithful_extra(pnr, slam, params, pose, dev, ddp, lib)
+            if prec != 'fp32':
+                saved = plib.DEFAULT_PRECISION
+                plib.DEFAULT_PRECISION = 'fp32'
+                fdec = make_decoder(pnr, cfg, params, dev)
+                fstep = map_step_fn(pnr, pnr.Renderer(cfg, None, slam), fdec, cfg, ro, rd, gt, col, dev)
+                fel, fkt = timed(fstep, 3, 1, ddp, lib)
+                plib.DEFAULT_PRECISION = saved
+                extras['fp32'] = {'value': round(n * 3 / fel, 1), 'unit': 'rays/s',
+                                  'ms_per_step': round(fel / 3 * 1e3, 3), 'steps': 3, 'dtype': DTYPE['fp32'],
+                                  'roofline': kernel_roofline(fkt, 'fp32', fel, traffic_units=False)}
 
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu_baseline and params is not None and args.workload != 'map-points':
             def gpu_render(ro_c, rd_c, gt_c):
-                d0 = pnr.get_model(cfg, nice=False)
-                d0.load_state_dict(params)
-                d0 = d0.to(dev)
+                d0 = make_decoder(pnr, cfg, params, dev)
                 with torch.no_grad():
                     d, _, c = renderer.render_batch_ray({}, d0, rd_c.to(dev), ro_c.to(dev), dev, 'color',
                                                         gt_depth=None if gt_c is None else gt_c.to(dev))
@@ -379,26 +529,22 @@ def main():
                                  'fc_c injection, feature + decoder Adam'}[args.workload]
         out = {
             'metric': METRIC, 'value': round(value, 1), 'unit': 'rays/s', 'n_gpus': world, 'steps': args.steps,
-            'warmup': args.warmup, 'ms_per_step': round(ms_per_step, 3), 'higher_is_better': True, 'scaling': 'weak',
-            'vs_baseline': None,
-            'dtype': {'fp32': 'fp32',
-                      'f16x3': 'fp32-class: f16x3 split MFMA forward, bf16x3 split delta chain (fp32 accumulate); '
-                               'weight gradients f16 MFMA on f16-stored activations / scaled-f16 deltas',
-                      'bf16x3': 'bf16x3 split MFMA forward and delta chain (fp32 accumulate); weight gradients f16 MFMA '
-                                'on f16-stored activations / scaled-f16 deltas',
-                      'bf16': 'bf16 MFMA forward (fp32 accumulate), bf16x3 delta chain; weight gradients f16 MFMA'}[prec],
+            'warmup': args.warmup, 'ms_per_step': round(ms_per_step, 3), 'higher_is_better': True,
+            'scaling': 'strong' if strong else 'weak', 'vs_baseline': None,
+            'dtype': DTYPE[prec],
             'data': 'synthetic (640x480 ScanNet-intrinsics rays at room0 pose 1000, U[0.05,0.6] gt depth, trained '
                     'room0 decoder fixture)',
             'config': {'workload': wl_name,
-                       'rays_per_gpu': n, 'global_batch': n * world, 'samples_per_ray': samples,
+                       'rays_per_gpu': n, 'global_batch': total, 'samples_per_ray': samples,
                        'parallelism': f'dp{world}', 'decoder_precision': prec,
-                       'graph': bool(args.graph and world == 1 and args.workload == 'map'),
+                       'graph': bool(args.graph and args.workload == 'map'),
                        **({'point_features': args.feat_dtype} if args.workload == 'map-points' else {})},
             'roofline': roofline, 'cpu_baseline': cpu,
             'kernels': {k: {'launches': v[0], 'ms': round(v[1], 3), 'units': v[2]} for k, v in kt.items()},
         }
         if cpu is not None:
             out['speedup_vs_cpu'] = round(value / cpu['value'], 1)
+        out.update(extras)
         if world == 1 and not args.no_gather and params is not None and args.workload != 'fwd':
             # the neural-point gather on its own roofline, after the timed region
             out['gather_roofline'] = gather_roofline(dev, feat_dtype=args.feat_dtype)

@@ -158,14 +158,18 @@ class MapGraph:
     overhead rivals the GPU time.  Replaying the captured step removes it.  The graph owns static
     input buffers (rays, gt depth / colour and the regulation jitter t_rand): each call copies the
     batch in, replays, and returns the loss tensor (overwritten by the next call).  Capture needs a
-    fixed batch shape, the single-GPU step (ddp=None) and Adam's device step counter
-    (`Adam.use_device_step`).  `warmup` ordinary steps run first on the given batch (torch requires
-    work on a side stream before a capture); they are real optimisation steps.
+    fixed batch shape and Adam's device step counter (`Adam.use_device_step`).  A data-parallel
+    step (ddp) is captured with its collectives when the process group is RCCL ('nccl'): the far
+    clamp is all-reduced and read on the device (far_mode 2), so the step has no host sync; gloo
+    collectives cannot be captured.  `warmup` ordinary steps run first on the given batch (torch
+    requires work on a side stream before a capture); they are real optimisation steps.
     """
 
     def __init__(self, mstep: MapStep, rays_o, rays_d, gt_depth, gt_color, t_rand, warmup=2):
-        if mstep.ddp is not None:
-            raise NotImplementedError('pnr.MapGraph: capture of the data-parallel step (RCCL) is not supported')
+        if mstep.ddp is not None and mstep.ddp.world > 1:
+            import torch.distributed as dist
+            if dist.get_backend(mstep.ddp.group) != 'nccl':
+                raise NotImplementedError('pnr.MapGraph: only RCCL (nccl) collectives can be captured in a graph')
         self.mstep = mstep
         dev = rays_o.device
         self.inputs = [t.detach().clone() for t in (rays_o, rays_d, gt_depth, gt_color, t_rand)]
