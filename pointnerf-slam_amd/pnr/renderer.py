@@ -71,6 +71,9 @@ class _Feat:
         self.params = tensors[:_lib.N_PARAMS]
         self.fc = tensors[_lib.N_PARAMS:_lib.N_PARAMS + _lib.N_FC_PARAMS] if pts is not None else ()
         self.keep = []
+        # grad mode of the CALLER (inside Function.forward it is always off, and needs_input_grad
+        # only reflects requires_grad): an eval call under no_grad saves no activations
+        self.train = torch.is_grad_enabled()
 
     def attach(self, prm, g_feats=None, g_fc=None):
         if self.pts is None:
@@ -80,12 +83,18 @@ class _Feat:
         prm.points = ctypes.pointer(s)
 
     def grads(self, dev, needs):
-        """Zeroed fc_c / feature grad buffers (or Nones) matching the extra autograd inputs."""
+        """Zeroed fc_c / feature grad buffers matching the extra autograd inputs (7 + 11 decoder
+        tensors, then 8 fc_c tensors, then the point features), or None where autograd needs no
+        gradient: the C ABI then skips the fc_c weight-gradient GEMMs (g_fc NULL) or the feature
+        atomics (g_feats NULL), e.g. in the Tracker's camera-only backward."""
         if self.pts is None:
             return None, None, []
-        g_fc = [torch.zeros(t.shape, device=dev, dtype=torch.float32) for t in self.fc]
-        g_feats = torch.zeros_like(self.pts.feats)
-        return g_feats, g_fc, [*g_fc, g_feats]
+        base = 7 + _lib.N_PARAMS
+        g_fc = None
+        if any(needs[base:base + _lib.N_FC_PARAMS]):
+            g_fc = [torch.zeros(t.shape, device=dev, dtype=torch.float32) for t in self.fc]
+        g_feats = torch.zeros_like(self.pts.feats) if needs[base + _lib.N_FC_PARAMS] else None
+        return g_feats, g_fc, [*(g_fc or [None] * _lib.N_FC_PARAMS), g_feats]
 
 
 def _param_grads(ctx, dev):
@@ -107,7 +116,7 @@ class _RenderFn(torch.autograd.Function):
         dev = rays_o.device
         packed = packer.image(feat.params)
         feat.attach(prm)
-        need = any(ctx.needs_input_grad)  # (inside forward grad mode is off; ask autograd)
+        need = feat.train and any(ctx.needs_input_grad)  # (inside forward grad mode is off)
         prm.save_for_backward = 1 if need else 0
         prm.need_ray_grads = 1 if (ctx.needs_input_grad[3] or ctx.needs_input_grad[4]) else 0
         if isinstance(far_clamp, torch.Tensor):  # device value (sharded batch): no host round trip
@@ -165,7 +174,7 @@ class _RegulationFn(torch.autograd.Function):
         dev = rays_o.device
         packed = packer.image(feat.params)
         feat.attach(prm)
-        need = any(ctx.needs_input_grad)  # (inside forward grad mode is off; ask autograd)
+        need = feat.train and any(ctx.needs_input_grad)  # (inside forward grad mode is off)
         prm.save_for_backward = 1 if need else 0
         prm.need_ray_grads = 1 if (ctx.needs_input_grad[3] or ctx.needs_input_grad[4]) else 0
         ws = torch.empty(lib.pnr_regulation_workspace_bytes(ctypes_ref(prm), n), dtype=torch.uint8, device=dev)

@@ -99,15 +99,18 @@ class TrackStep:
 
     def loss(self, camera_tensor, gt_color, gt_depth, batch_size):
         dec = self.decoder
-        req = [p.requires_grad for p in dec.parameters()]
-        for p in dec.parameters():
+        # the Tracker optimises the camera only (src/Tracker.py:870-874): decoder weights and point
+        # features take no gradient (no weight-gradient GEMMs, no feature atomics)
+        frozen = list(dec.parameters()) + [v.feats for v in self.c.values() if hasattr(v, 'feats')]
+        req = [p.requires_grad for p in frozen]
+        for p in frozen:
             p.requires_grad_(False)
         try:
             c2w = get_camera_from_tensor(camera_tensor)
             ro, rd, gd, gc = self.samples(c2w, gt_depth, gt_color, batch_size)
             d, v, col = self.renderer.render_batch_ray(self.c, dec, rd, ro, rd.device, 'color', gt_depth=gd)
         finally:
-            for p, q in zip(dec.parameters(), req):
+            for p, q in zip(frozen, req):
                 p.requires_grad_(q)
         v = v.detach()
         if self.handle_dynamic:

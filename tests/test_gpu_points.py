@@ -365,3 +365,32 @@ def test_map_step_sharded_features_single_rank(pnr_mod, dev):
     assert out[0][0][0] == out[1][0][0]  # the first forward precedes any update
     assert abs(out[0][0][1] - out[1][0][1]) <= 1e-6 * abs(out[0][0][1])
     close(out[1][1], out[0][1], 1e-6 * out[0][1].abs().max().item(), 'parameters after 2 steps')
+
+
+def test_track_step_with_points_leaves_features_alone(pnr_mod, dev):
+    """The Tracker optimises the camera only (src/Tracker.py:870-874): a TrackStep over a
+    neural-point decoder produces the camera gradient and leaves the point features' and the
+    decoder's .grad untouched (no feature atomics, no fc_c weight-gradient GEMMs)."""
+    scene = load_golden('scene.npz')
+    bound = torch.from_numpy(scene['bound'])
+    _, _, _, xyz, feats = surface_cloud(dev, seed=9)
+    params = RP.init_fc_c(golden_params('trained'), seed=4)
+    pts = pnr_mod.NeuralPoints(xyz.to(dev), feats.to(dev), mode='idw', radius=0.04, k=8).to(dev)
+    dec = pnr_mod.MLP(name='color', dim=3, c_dim=32, color=True, skips=[], n_blocks=4, hidden_size=256)
+    dec.load_state_dict({k: v.clone() for k, v in params.items()})
+    dec = dec.to(dev)
+    import types
+    H, W = 68, 120
+    slam = types.SimpleNamespace(bound=bound, H=H, W=W, fx=60., fy=60., cx=59.5, cy=33.5)
+    r = pnr_mod.Renderer(pnr_mod.ROOM0_CFG, None, slam)
+    c2w = torch.from_numpy(scene['poses'][2]).float()
+    gd = torch.full((H, W), 0.3, device=dev)
+    gc = torch.rand((H, W, 3), generator=torch.Generator().manual_seed(3)).to(dev)
+    step = pnr_mod.TrackStep(r, dec, c={'points_color': pts}, ignore_edge_W=10, ignore_edge_H=10)
+    ct = pnr_mod.get_tensor_from_camera(c2w).to(dev).requires_grad_(True)
+    loss = step.loss(ct, gc, gd, 0)
+    loss.backward()
+    assert ct.grad is not None and torch.isfinite(ct.grad).all() and ct.grad.abs().sum() > 0
+    assert pts.feats.grad is None
+    assert all(p.grad is None for p in dec.parameters())
+    assert pts.feats.requires_grad and all(p.requires_grad for p in dec.parameters())

@@ -131,46 +131,67 @@ def test_mlp_grads_elementwise_vs_oracle(precision, pnr_mod, dev, trained_params
 
 
 def test_map_steps_follow_fp32_trajectory(pnr_mod, dev, scene):
-    """50 MapStep iterations on fresh 2,048-ray batches (same rays, gt and regulation jitter for
-    both modes): the f16x3 loss trajectory stays on the fp32 one and the weights end close."""
+    """50 Mapper iterations (MapStep: render + regulation + L1 losses + backward + Adam, lr 2e-4) on
+    fresh 1,024-ray batches, from the trained decoder, in fp32 and in f16x3 -- and the same 50 steps
+    of the reference arithmetic on the CPU (the oracle + torch.optim.Adam: float32 torch, what
+    src/Mapper.py:507-662 runs).  Rounding differences flip discrete decisions (ReLU masks at ~0
+    pre-activations, the signs of the L1 terms) and Adam normalises every element's gradient, so
+    no two float32 orders follow identical weight trajectories; the f16x3 mode must stay as close to
+    the reference's trajectory as the fp32 mode does (losses and weights)."""
+    from oracle import ref_render as ref
     from pnr.mapping import MapStep
     params = golden_params('trained')
+    bound = scene['bound_t']
     g = torch.Generator().manual_seed(11)
-    n, steps = 2048, 50
+    n, steps, lr = 1024, 50, 2e-4
     batches = []
     for s in range(steps):
         c2w = torch.from_numpy(scene['poses'][s % 4]).float()
         i = torch.randint(0, 1200, (n,), generator=g).float()
         j = torch.randint(0, 680, (n,), generator=g).float()
-        batches.append((c2w, i, j, torch.rand(n, generator=g) * 0.4 + 0.15, torch.rand((n, 3), generator=g),
+        ro, rd = ref.rays_from_uv(i, j, c2w, 600., 600., 599.5, 339.5)
+        batches.append((ro.reshape(-1, 3).contiguous(), rd.reshape(-1, 3).contiguous(),
+                        torch.rand(n, generator=g) * 0.4 + 0.15, torch.rand((n, 3), generator=g),
                         torch.rand((n, 32), generator=g)))
+    # the reference arithmetic on the CPU
+    torch.set_num_threads(max(1, min(16, torch.get_num_threads())))
+    pr = {k: v.clone().requires_grad_(True) for k, v in params.items()}
+    opt = torch.optim.Adam(list(pr.values()), lr=lr)
+    l_ref = []
+    for ro, rd, gt, col, tr in batches:
+        opt.zero_grad()
+        d, v, c = ref.render_batch_ray(pr, rd, ro, bound, gt_depth=gt)
+        sig = ref.regulation(pr, rd, ro, gt, bound, t_rand=tr)
+        loss = ref.mapping_loss(d, c, gt, col, sig)
+        loss.backward()
+        opt.step()
+        l_ref.append(loss.item())
+    from pnr.decoder import PARAM_ORDER
+    w_ref = torch.cat([pr[k].detach().reshape(-1) for k in PARAM_ORDER])
+    l_ref = np.array(l_ref)
     runs = {}
-    for prec in ('fp32', 'fp32_again', 'f16x3'):
+    for prec in ('fp32', 'f16x3'):
         dec = _decoder(pnr_mod, params, dev)
-        r = _renderer(pnr_mod, scene, prec.split('_')[0])
-        ms = MapStep(r, dec, lr=2e-4, w_color_loss=0.05)
-        losses = []
-        for c2w, i, j, gt, col, tr in batches:
-            ro, rd = pnr_mod.get_rays_from_uv(i.to(dev), j.to(dev), c2w.to(dev), 680, 1200, 600., 600., 599.5,
-                                             339.5, dev)
-            losses.append(float(ms(ro, rd, gt.to(dev), col.to(dev), tr.to(dev))))
+        r = _renderer(pnr_mod, scene, prec)
+        ms = MapStep(r, dec, lr=lr, w_color_loss=0.05)
+        losses = [float(ms(ro.to(dev), rd.to(dev), gt.to(dev), col.to(dev), tr.to(dev)))
+                  for ro, rd, gt, col, tr in batches]
         runs[prec] = (np.array(losses), ms.flat.data.detach().cpu().clone())
         assert r.status(dev) == 0
-    (l32, w32), (l32b, w32b), (l16, w16) = runs['fp32'], runs['fp32_again'], runs['f16x3']
-    rel = np.abs(l16 - l32) / np.abs(l32)
-    rel_self = np.abs(l32b - l32) / np.abs(l32)
-    # Adam normalises each element's gradient, so an element whose gradient is ~0 can take a
-    # different +-lr step between two summation orders (the weight-gradient GEMMs flush with float
-    # atomics: two fp32 runs already differ): compare the f16x3 drift with fp32's own
-    thr = 1e-3 * 2e-4 * steps
-    dw, dw_self = (w16 - w32).abs(), (w32b - w32).abs()
-    frac, frac_self = (dw > thr).float().mean().item(), (dw_self > thr).float().mean().item()
-    print('loss %.4f -> %.4f; f16x3 vs fp32: loss rel max %.2e, weights > %.0e: %.4f | fp32 vs fp32 rerun: '
-          'loss rel max %.2e, weights: %.4f' % (l32[0], l32[-1], rel.max(), thr, frac, rel_self.max(), frac_self))
-    assert l32[-1] < l32[0]
-    assert rel.max() < 1e-4, rel
-    assert dw.max().item() <= steps * 2 * 2e-4
-    assert frac <= max(3 * frac_self, 0.03), (frac, frac_self)
+    thr = 1e-3 * lr * steps
+    stats = {}
+    for prec, (l, w) in runs.items():
+        rel = np.abs(l - l_ref) / np.abs(l_ref)
+        dw = (w - w_ref).abs()
+        stats[prec] = (rel.max(), (dw > thr).float().mean().item(), dw.max().item())
+        print(f'{prec:6s} vs reference CPU: loss rel max {rel.max():.2e}, weights beyond {thr:.0e}: '
+              f'{stats[prec][1]:.4f}, max |dw| {stats[prec][2]:.2e}')
+    print(f'reference loss {l_ref[0]:.3f} -> {l_ref[-1]:.3f}')
+    assert l_ref[-1] < l_ref[0]
+    (r32, f32, m32), (r16, f16, m16) = stats['fp32'], stats['f16x3']
+    assert r16 <= max(3 * r32, 2e-5), (r16, r32)
+    assert f16 <= max(1.5 * f32, 0.02), (f16, f32)
+    assert m16 <= steps * 2 * lr
 
 
 def test_f16_range_status(pnr_mod, dev, scene):
