@@ -24,6 +24,15 @@ __device__ __forceinline__ void glds16(const float* gsrc, uint32_t lds_byte) {
                : "=&s"(keep) : "v"(gsrc), "s"(lds_byte) : "memory");
 }
 
+// Same DMA with a wave-uniform 64-bit base in SGPRs and the lane's 32-bit byte offset in a VGPR
+// (the saddr form): a loop that stages many pieces keeps ONE offset VGPR instead of a 64-bit
+// address pair per piece (hoisted out of a persistent tile loop, those pairs spilled).
+__device__ __forceinline__ void glds16s(const void* sbase, uint32_t voff, uint32_t lds_byte) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(voff), "s"(sbase), "s"(lds_byte) : "memory");
+}
+
 __device__ __forceinline__ uint32_t lds_addr(const float* p) {
   return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) float*)p;
 }

@@ -194,6 +194,10 @@ struct BfState {
   Frag<PR> F[R];       // fragment ring (one 32-row output tile of the current / next step each)
   Frag<PR> FC;         // feature-branch fragments of the step's epilogue tile
   float vmax;          // max |value| split into f16 parts so far (f16 range check)
+  int sb;              // ring slot of step 0 of this tile (persistent kernels: the ring runs on)
+#if defined(PNR_EXP_TIMELINE)
+  bool tick;
+#endif
   int64_t col, mask_word0;
   bool valid, inside;
 };
@@ -250,11 +254,12 @@ __device__ __forceinline__ void mfma_frag(const Frag<PR>& F, const T (&act)[Prec
 }
 
 #if defined(PNR_EXP_TIMELINE)
-// experiment: s_memtime timeline of one steady-state workgroup (wave 0 .. 3, lane 0)
+// experiment: s_memtime timeline of one steady-state tile (S.tick: workgroup 7, its 6th tile;
+// wave 0 .. 3, lane 0)
 extern __device__ unsigned long long g_pnr_dbg[4][48];
 #define PNR_TICK(i)                                                                     \
   do {                                                                                  \
-    if (blockIdx.x == 2000 && (threadIdx.x & 63) == 0)                                  \
+    if (S.tick && (threadIdx.x & 63) == 0)                                              \
       g_pnr_dbg[threadIdx.x >> 6][(i)] = __builtin_amdgcn_s_memtime();                  \
   } while (0)
 #else
@@ -271,20 +276,27 @@ struct BfFwd {
   using V8 = typename Prec<PR>::V8;
   static constexpr int kRing = (HASC && SAVE) ? 3 : 4, kPf = kRing - 1;
   using St = BfState<PR, kRing>;
+  // Persistent kernels (no feature branch): a workgroup loops over 128-point tiles and the weight
+  // stream runs on across tiles -- the last steps of tile i prefetch the first steps of tile i+1
+  // into the ring, so no tile waits for its first weights (the non-persistent kernel paid the
+  // DMA latency in every workgroup's first three steps: ~4k cycles each against ~2.7k).  Step g of
+  // tile i sits in ring slot (g + sb) % kNbuf, sb = i kSteps % kNbuf (continuous numbering).
+  static constexpr bool PST = !HASC;
 
-  // issue the DMA of step g into its ring slot (wave-uniform, lane-linear 4 KiB pieces)
+  // issue the DMA of step g into its ring slot (wave-uniform, lane-linear 4 KiB pieces); in the
+  // persistent kernels steps g >= kSteps are the next tile's steps g - kSteps
   template <int g>
-  static __device__ __forceinline__ void stage_step(const BfFwdArgs& a, const char* lds) {
-    if constexpr (g < G::kSteps) {
+  static __device__ __forceinline__ void stage_step(const BfFwdArgs& a, const char* lds, int sb) {
+    if constexpr (g < G::kSteps || (PST && g < 2 * G::kSteps)) {
+      constexpr int st = g < G::kSteps ? g : g - G::kSteps;
       const int w = wave_id(), lane = threadIdx.x & 63;
-      const uint32_t slot = lds_addr(reinterpret_cast<const float*>(lds + (g % G::kNbuf) * G::kSlot)) + w * 1024;
-      const char* src = a.wmain + G::main_off(g) + w * 1024 + lane * 16;
+      const uint32_t slot =
+          lds_addr(reinterpret_cast<const float*>(lds + ((g + sb) % G::kNbuf) * G::kSlot)) + w * 1024;
+      const uint32_t voff = lane * 16;
+      const char* src = a.wmain + G::main_off(st) + w * 1024;  // wave-uniform (SGPRs)
 #pragma unroll
-      for (int i = 0; i < G::main_n(g); ++i)
-        glds16(reinterpret_cast<const float*>(src + i * 4096), slot + i * 4096);
-      if constexpr (G::fc_n(g) > 0)
-        glds16(reinterpret_cast<const float*>(a.wfc + (int64_t)(g - 2) * 4096 + w * 1024 + lane * 16),
-               slot + G::kMainH);
+      for (int i = 0; i < G::main_n(st); ++i) glds16s(src + i * 4096, voff, slot + i * 4096);
+      if constexpr (G::fc_n(st) > 0) glds16s(a.wfc + (int64_t)(st - 2) * 4096 + w * 1024, voff, slot + G::kMainH);
     }
   }
 
@@ -417,7 +429,7 @@ struct BfFwd {
   // VMEM ops issued after DMA(i) and before the wait of barrier B_i (i >= 1, in step i-1)
   __host__ __device__ static constexpr int younger_b(int i) {
     int n = 0;
-    for (int j = i + 1; j <= i + kD - 1 && j < G::kSteps; ++j) n += G::n_glds(j);
+    for (int j = i + 1; j <= i + kD - 1; ++j) n += j < G::kSteps ? G::n_glds(j) : (PST ? G::n_glds(j - G::kSteps) : 0);
     if (SAVE) {
       int first = 0;  // first step whose stores all follow the DMA
       if (i >= kD && i - kD >= 1) {
@@ -439,14 +451,14 @@ struct BfFwd {
     return n + (SAVE ? kFwdPrologueStores : 0);
   }
 
-  static __device__ __forceinline__ const char* slot_of(const char* lds, int g) {
-    return lds + (g % G::kNbuf) * G::kSlot;
+  static __device__ __forceinline__ const char* slot_of(const char* lds, int g, int sb) {
+    return lds + ((g + sb) % G::kNbuf) * G::kSlot;
   }
 
   // next step's fragment tile k (issued after its barrier)
   template <int g, int k>
   static __device__ __forceinline__ void next_frag(St& S, const char* lds) {
-    if constexpr (k < nt(g)) load_frag<PR>(slot_of(lds, g) + k * 2 * NP * 1024, S.F[(ring(g) + k) % kRing]);
+    if constexpr (k < nt(g)) load_frag<PR>(slot_of(lds, g, S.sb) + k * 2 * NP * 1024, S.F[(ring(g) + k) % kRing]);
   }
   // next step's epilogue constants
   template <int g>
@@ -478,7 +490,7 @@ struct BfFwd {
       constexpr int SET = CL & 1;
       constexpr int SHIFT = shift(g);  // that tile is produced by group 0 of this step
       constexpr int b = ring(g);
-      const char* slot = slot_of(lds, g);
+      const char* slot = slot_of(lds, g, S.sb);
       if constexpr (HASC && CONV && T == clamp_t(1, g)) load_frag<PR>(slot + G::kMainH, S.FC);
       if constexpr (HASC && CONV && T == clamp_t(3, g)) preload_fc<CL, CT>(S, lds);
       if constexpr (T + kPf < NT) load_frag<PR>(slot + (T + kPf) * 2 * NP * 1024, S.F[(b + T + kPf) % kRing]);
@@ -502,7 +514,7 @@ struct BfFwd {
           sync_chunk<0>();
 #else
           sync_chunk<younger_b(g + 1)>();
-          stage_step<g + 1 + kD>(a, lds);
+          stage_step<g + 1 + kD>(a, lds, S.sb);
 #endif
         }
         if constexpr (T == next_grp(g, 0)) next_frag<g + 1, 0>(S, lds);
@@ -518,11 +530,16 @@ struct BfFwd {
   template <int g>
   static __device__ __forceinline__ void step(const BfFwdArgs& a, St& S, const char* lds) {
     if constexpr (g < G::kSteps) {
-      // both accumulator sets live in the 256 AGPRs for the whole kernel; out / f stay in VGPRs
+      // both accumulator sets live in the 256 AGPRs for the whole kernel; out / f stay in VGPRs.
+      // Step 0 only DEFINES them ("=a"): read there, a persistent kernel's tiles would carry the
+      // previous tile's registers around the loop (256 AGPRs live across its tail: spills)
 #pragma unroll
       for (int st = 0; st < 2; ++st)
 #pragma unroll
-        for (int t = 0; t < 8; ++t) asm volatile("" : "+a"(S.acc[st][t]));
+        for (int t = 0; t < 8; ++t) {
+          if constexpr (g == 0) asm volatile("" : "=a"(S.acc[st][t]));
+          else asm volatile("" : "+a"(S.acc[st][t]));
+        }
       if constexpr (fwd_layer(g) == 0) {
         group<g, 0>(a, S, lds, S.ft[fwd_kc(g)]);
       } else {
@@ -545,7 +562,7 @@ struct BfFwd {
   template <int g>
   static __device__ __forceinline__ void prologue(const BfFwdArgs& a, const char* lds) {
     if constexpr (g < kD) {
-      stage_step<g>(a, lds);
+      stage_step<g>(a, lds, 0);
       prologue<g + 1>(a, lds);
     }
   }
@@ -556,7 +573,7 @@ struct BfFwd {
     sync_chunk<0>();
 #else
     sync_chunk<younger_b0()>();
-    stage_step<kD>(a, lds);
+    stage_step<kD>(a, lds, S.sb);
 #endif
     next_frag<0, 0>(S, lds);
     next_frag<0, 1>(S, lds);
@@ -567,15 +584,16 @@ struct BfFwd {
   // ---- output layer on the VALU (no feature branch) ------------------------------------------
   // out[i] (+)= sum over this lane's 16 units of h4 tile t of Wo[i][u] h4[u] (fp32 FMAs; Wo fp32
   // in LDS after the main raw table).  Units of register r: 32 t + perm(r, hh).
+  // wo: this lane's 32-bit LDS address of Wo (see out_layer)
   template <int t>
-  static __device__ __forceinline__ void out_dot(const St& S, const char* lds, float (&o)[4]) {
-    const int hh = (threadIdx.x >> 5) & 1;
-    const float* wo = raw_lds(lds) + kRawBytes / 4;
+  static __device__ __forceinline__ void out_dot(const St& S, uint32_t wo, float (&o)[4]) {
+    typedef float v4f __attribute__((ext_vector_type(4)));
+    using lds_f4 = const __attribute__((address_space(3))) v4f;
 #pragma unroll
     for (int q = 0; q < 4; ++q)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const float4 w = *reinterpret_cast<const float4*>(wo + i * kHidden + 32 * t + 8 * q + 4 * hh);
+        const v4f w = *reinterpret_cast<lds_f4*>((uintptr_t)(wo + 4 * (i * kHidden + 32 * t + 8 * q)));
         o[i] = __builtin_fmaf(w.x, S.v[4 * q + 0], o[i]);
         o[i] = __builtin_fmaf(w.y, S.v[4 * q + 1], o[i]);
         o[i] = __builtin_fmaf(w.z, S.v[4 * q + 2], o[i]);
@@ -584,7 +602,8 @@ struct BfFwd {
   }
   // h4 tile t: bias + ReLU (+ mask bits, f16 save), then its share of the output layer
   template <int t>
-  static __device__ __forceinline__ void out_tile(const BfFwdArgs& a, St& S, const char* lds, float (&o)[4]) {
+  static __device__ __forceinline__ void out_tile(const BfFwdArgs& a, St& S, const char* lds, uint32_t wo,
+                                                  float (&o)[4]) {
     if constexpr (t < 8) {
       if constexpr (t > 0) {  // tile 0 was converted by the last hidden step (S.v holds it)
         preload<3, t>(S, lds);
@@ -600,45 +619,36 @@ struct BfFwd {
                                        4 * hh) = make_float4(S.v[4 * q], S.v[4 * q + 1], S.v[4 * q + 2], S.v[4 * q + 3]);
         }
       }
-      out_dot<t>(S, lds, o);
-      out_tile<t + 1>(a, S, lds, o);
+      out_dot<t>(S, wo, o);
+      out_tile<t + 1>(a, S, lds, wo, o);
     }
   }
   static __device__ __forceinline__ void out_layer(const BfFwdArgs& a, St& S, const char* lds, float (&o)[4]) {
     o[0] = o[1] = o[2] = o[3] = 0.f;
-    out_tile<0>(a, S, lds, o);
+    // Wo lies above 64 KiB of LDS, past ds_read's 16-bit offset field: from a generic pointer every
+    // read got its own address VGPR, which a persistent kernel hoists out of its tile loop (and
+    // spills).  One opaque per-tile base, constant offsets folded into the instructions.
+    uint32_t wo = lds_addr(raw_lds(lds) + kRawBytes / 4) + 16 * ((threadIdx.x >> 5) & 1);
+    asm volatile("" : "+v"(wo));
+    out_tile<0>(a, S, lds, wo, o);
 #pragma unroll
     for (int i = 0; i < 4; ++i) o[i] += __shfl_xor(o[i], 32);  // the other lane half's 128 units
   }
 };
 
+// one 128-point tile of k_mlp_fwd16 (it: the workgroup's tile count so far, sb: its ring slot base)
 template <int PR, bool HASC, bool SAVE>
-__global__ __launch_bounds__(256, 1) void k_mlp_fwd16(BfFwdArgs a, int mode) {
+static __device__ __forceinline__ void fwd16_tile(const BfFwdArgs& a, int mode, const char* lds, int64_t tile,
+                                                 int it, int sb) {
   using K = BfFwd<PR, HASC, SAVE>;
-  extern __shared__ __attribute__((aligned(16))) char lds[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, hh = lane >> 5, j = lane & 31;
-  const int64_t p = (int64_t)blockIdx.x * 128 + wave * 32 + j;
-
-  // raw tables (biases, Fourier B, scales; + fc raw) then the first kDist steps, all by LDS-DMA
-  {
-    const int w = wave_id();
-    const uint32_t rbase = lds_addr(K::raw_lds(lds)) + w * 1024;
-#pragma unroll
-    for (int i = 0; i < (int)(kRawBytes / 4096); ++i)
-      glds16(reinterpret_cast<const float*>(a.raw + i * 4096 + w * 1024 + lane * 16), rbase + i * 4096);
-    if (HASC) {
-#pragma unroll
-      for (int i = 0; i < (int)(kFcRawBytes / 4096); ++i)
-        glds16(reinterpret_cast<const float*>(a.fcraw + i * 4096 + w * 1024 + lane * 16),
-               rbase + kRawBytes + i * 4096);
-    } else {  // Wo for the VALU output layer
-      glds16(reinterpret_cast<const float*>(a.raw + kRawBytes + w * 1024 + lane * 16), rbase + kRawBytes);
-    }
-  }
-  PNR_TICK(0);
-  K::template prologue<0>(a, lds);
-
+  const int64_t p = tile * 128 + wave * 32 + j;
   typename K::St S;
+  S.sb = sb;
+#if defined(PNR_EXP_TIMELINE)
+  S.tick = blockIdx.x == 7 && it == 5;
+#endif
+  PNR_TICK(0);
   S.valid = p < a.P;
   float x0 = 0.f, x1 = 0.f, x2 = 0.f;
   bool inside = false;
@@ -652,7 +662,7 @@ __global__ __launch_bounds__(256, 1) void k_mlp_fwd16(BfFwdArgs a, int mode) {
   }
   S.inside = inside;
   S.col = a.save.p0 + p;
-  S.mask_word0 = ((a.save.p0 + (int64_t)blockIdx.x * 128) / 32 + wave_id()) * 64;
+  S.mask_word0 = ((a.save.p0 + tile * 128) / 32 + wave_id()) * 64;
   S.mw[0] = S.mw[1] = S.mw[2] = S.mw[3] = 0u;
   S.vmax = 0.f;
   if (HASC) {
@@ -673,8 +683,9 @@ __global__ __launch_bounds__(256, 1) void k_mlp_fwd16(BfFwdArgs a, int mode) {
   // no accumulator zero fill: the first input tile of every layer starts its tiles from 0 (ZERO in
   // mfma_frag), and nothing reads a tile before that (256 v_accvgpr_mov saved per workgroup)
 
-  // Fourier features: the raw tables must have landed (they are older than the step DMAs)
-  sync_chunk<K::prologue_glds()>();
+  // Fourier features: the raw tables must have landed (they are older than the step DMAs; later
+  // tiles of a persistent workgroup read them long after)
+  if (it == 0) sync_chunk<K::prologue_glds()>();
   {
     const float* FB = K::raw_lds(lds) + kRawFB;
 #pragma unroll
@@ -724,6 +735,46 @@ __global__ __launch_bounds__(256, 1) void k_mlp_fwd16(BfFwdArgs a, int mode) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) o[i] += bo[i];
     reinterpret_cast<float4*>(a.raw_out)[p] = make_float4(o[0], o[1], o[2], S.inside ? o[3] : 100.f);
+  }
+}
+
+template <int PR, bool HASC, bool SAVE>
+__global__ __launch_bounds__(256, 1) void k_mlp_fwd16(BfFwdArgs a, int mode) {
+  using K = BfFwd<PR, HASC, SAVE>;
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int lane = threadIdx.x & 63;
+
+  // raw tables (biases, Fourier B, scales; + fc raw) then the first kDist steps, all by LDS-DMA
+  {
+    const int w = wave_id();
+    const uint32_t rbase = lds_addr(K::raw_lds(lds)) + w * 1024;
+#pragma unroll
+    for (int i = 0; i < (int)(kRawBytes / 4096); ++i)
+      glds16(reinterpret_cast<const float*>(a.raw + i * 4096 + w * 1024 + lane * 16), rbase + i * 4096);
+    if (HASC) {
+#pragma unroll
+      for (int i = 0; i < (int)(kFcRawBytes / 4096); ++i)
+        glds16(reinterpret_cast<const float*>(a.fcraw + i * 4096 + w * 1024 + lane * 16),
+               rbase + kRawBytes + i * 4096);
+    } else {  // Wo for the VALU output layer
+      glds16(reinterpret_cast<const float*>(a.raw + kRawBytes + w * 1024 + lane * 16), rbase + kRawBytes);
+    }
+  }
+  K::template prologue<0>(a, lds);
+  // persistent kernels loop over tiles (grid <= CUs); the others run one tile per workgroup with no
+  // loop at all (a loop, even one that runs once, costs the register allocator ~100 spills here)
+  if constexpr (K::PST) {
+    const int64_t ntiles = (a.P + 127) / 128;
+    int sb = 0, it = 0;
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x, ++it) {
+      fwd16_tile<PR, HASC, SAVE>(a, mode, lds, tile, it, sb);
+      sb = (sb + K::G::kSteps) % K::G::kNbuf;
+    }
+    // the last tile's prefetch of a next tile (always issued: fixed wait counts) must land in the
+    // workgroup's LDS before it exits
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  } else {
+    fwd16_tile<PR, HASC, SAVE>(a, mode, lds, blockIdx.x, 0, 0);
   }
 }
 

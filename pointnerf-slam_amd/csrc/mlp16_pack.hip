@@ -273,7 +273,20 @@ int launch_mlp_fwd_bf(int prec, const float* packed, const PointSrc& src, int mo
   const bool sv = save != nullptr;
   if (save) a.save = *save;
   else a.save = SaveArgs{nullptr, nullptr, nullptr, nullptr, 0, 0};
-  const dim3 grid((unsigned)((P + 127) / 128));
+  // one workgroup per 128-point tile; the persistent kernels (no feature branch) loop over tiles
+  // on at most one workgroup per CU
+  int64_t nwg = (P + 127) / 128;
+  if (!hasc) {
+    static const int ncu = [] {
+      int dev = 0, n = 0;
+      if (hipGetDevice(&dev) != hipSuccess ||
+          hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+        n = 256;
+      return n;
+    }();
+    nwg = nwg < ncu ? nwg : ncu;
+  }
+  const dim3 grid((unsigned)nwg);
   TimingScope ts(kTimeMlpFwd, P, st);
   switch (prec) {
     case PNR_PREC_BF16X3: return launch_fwd16_bf16x3(mode, grid, st, a, hasc, sv);
