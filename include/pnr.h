@@ -62,9 +62,9 @@ enum {
  * into every hidden layer: h = relu(W h + b) + fc_c[i](c) (decoder.py:196-197).
  * Search structure: a spatial hash of cubic cells (edge `cell`, corner `origin`) into
  * 2^table_bits buckets, bucket-sorted copies of the positions; built on the device by
- * pnr_points_build into the caller's `index` buffer.  `cell` must be >= 2 * radius (IDW) or
- * >= 2 * max(spacing) (TRILINEAR): the search visits the 2x2x2 cells covering [p - reach, p + reach]
- * (a margin of ~1e-3 relative absorbs float rounding). */
+ * pnr_points_build into the caller's `index` buffer.  `cell` must be >= 2 * radius * (1 + 2^-9)
+ * (IDW) or >= 2 * max(spacing) * (1 + 2^-9) (TRILINEAR): the search visits the 2x2x2 cells
+ * covering [p - reach, p + reach], and the margin absorbs the f32 rounding of cell coordinates. */
 enum { PNR_GATHER_IDW = 0, PNR_GATHER_TRILINEAR = 1 };
 
 /* Arithmetic of the decoder matmuls (build-defined; the reference runs torch fp32 matmuls).

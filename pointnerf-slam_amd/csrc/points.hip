@@ -24,6 +24,8 @@
 //                   (v_min/v_max_f64, 2 VALU per stage); normalised weights, then the feature sum
 //                   with 8 lanes per sample.
 //   k_gather_bwd    dL/df_i += w_k dL/dc (float atomics) and dL/dp through the weights.
+#include <mutex>
+
 #include "pnr_internal.h"
 
 namespace pnr {
@@ -882,26 +884,46 @@ __global__ __launch_bounds__(256) void k_gather_bwd(GatherBwdArgs a) {
 // ---------------------------------------------------------------------------------------------
 // Launchers
 // ---------------------------------------------------------------------------------------------
+// cell >= 2 reach (1 + 2^-9): the search widens the reach by 2^-10 (+ 5 ulp of the cell coordinate)
+// and its half-cell masks only cover the 2x2x2 probe block, so the widened reach must stay <= half a
+// cell; at cell == 2 reach a neighbour on the block edge could be dropped by f32 rounding
+// (pnr.NeuralPoints applies the same bound)
+constexpr float kCellMargin = 1.0f + 1.0f / 512.0f;
 static bool points_ok(const pnr_points& pts) {
   const float reach = pts.mode == PNR_GATHER_IDW
                           ? pts.radius
                           : fmaxf(pts.spacing[0], fmaxf(pts.spacing[1], pts.spacing[2]));
   return pts.n_points >= 0 && pts.k >= 1 && pts.k <= PNR_MAX_K && pts.table_bits >= 10 && pts.table_bits <= 24 &&
          pts.index && (pts.mode == PNR_GATHER_IDW || pts.mode == PNR_GATHER_TRILINEAR) && reach > 0.f &&
-         pts.cell >= 2.0f * reach && (pts.n_points == 0 || (pts.xyz && pts.feats));
+         pts.cell >= 2.0f * reach * kCellMargin && (pts.n_points == 0 || (pts.xyz && pts.feats));
 }
 
 // persistent grid = the blocks of `kern` resident at once (a later wave of blocks would run as a
-// tail), at most `tasks`; queried once per kernel
+// tail), at most `tasks`; queried once per (kernel, block size, device): template variants of one
+// kernel share a function-pointer type, so the cache is keyed by the pointer itself
 template <typename K>
 static unsigned resident_grid(K kern, int block, int64_t tasks) {
-  static int resident = 0;
-  if (!resident) {
-    int dev = 0, cus = 0, per = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kern, block, 0);
-    resident = (cus > 0 && per > 0) ? cus * per : 2048;
+  struct Entry {
+    const void* kern;
+    int block, dev, resident;
+  };
+  static Entry cache[64];
+  static int n_cache = 0;
+  static std::mutex mu;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  int resident = 0;
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    for (int i = 0; i < n_cache; ++i)
+      if (cache[i].kern == (const void*)kern && cache[i].block == block && cache[i].dev == dev) resident = cache[i].resident;
+    if (!resident) {
+      int cus = 0, per = 0;
+      (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kern, block, 0);
+      resident = (cus > 0 && per > 0) ? cus * per : 2048;
+      if (n_cache < 64) cache[n_cache++] = Entry{(const void*)kern, block, dev, resident};
+    }
   }
   return (unsigned)(tasks < resident ? tasks : resident);
 }

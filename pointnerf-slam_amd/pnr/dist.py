@@ -47,6 +47,16 @@ class DataParallel:
         self.group = group
         self.shard_points = bool(shard_points)
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self._bufs = {}  # padded send / receive buffers of the sharded feature update, reused per step
+
+    def _buf(self, name, n, like):
+        """A cached device buffer of n words (allocated once per shape / dtype / device)."""
+        key = (name, n, like.dtype, like.device)
+        b = self._bufs.get(key)
+        if b is None:
+            b = torch.zeros(n, dtype=like.dtype, device=like.device)
+            self._bufs[key] = b
+        return b
 
     def global_far_clamp(self, gt_depth_local):
         """max(1.2 * gt) over every rank's rays (Renderer.py:112), as a one-element float32 device
@@ -86,10 +96,10 @@ class DataParallel:
         if self.world == 1:
             return a, b
         buf = seg
-        if per * self.world != n:
-            buf = torch.zeros(per * self.world, dtype=seg.dtype, device=seg.device)
+        if per * self.world != n:  # the padded tail stays zero: only [:n] is ever written
+            buf = self._buf('rs_in', per * self.world, seg)
             buf[:n].copy_(seg)
-        out = torch.empty(per, dtype=seg.dtype, device=seg.device)
+        out = self._buf('rs_out', per, seg)
         dist.reduce_scatter_tensor(out, buf, op=dist.ReduceOp.SUM, group=self.group)
         seg[a:b].copy_(out[:b - a])
         return a, b
@@ -100,9 +110,9 @@ class DataParallel:
         a, b, per = self.feature_shard(n)
         if self.world == 1:
             return seg
-        mine = torch.zeros(per, dtype=seg.dtype, device=seg.device)
+        mine = self._buf('ag_in', per, seg)  # words past b - a stay zero (the last rank's padding)
         mine[:b - a].copy_(seg[a:b])
-        out = torch.empty(per * self.world, dtype=seg.dtype, device=seg.device)
+        out = self._buf('ag_out', per * self.world, seg)
         dist.all_gather_into_tensor(out, mine, group=self.group)
         seg.copy_(out[:n])
         return seg

@@ -54,9 +54,10 @@ class NeuralPoints(nn.Module):
         reach = self.radius if mode == 'idw' else max(self.spacing)
         # the search probes the 2x2x2 cells covering [p - reach, p + reach]: cell >= 2 reach, with a
         # margin so that float rounding of the cell coordinates never misses a neighbour
-        self.cell = float(cell) if cell is not None else 2.0 * reach * (1.0 + 1e-3)
-        if self.cell < 2.0 * reach * (1.0 + 1e-4):
-            raise ValueError('pnr.NeuralPoints: cell must be >= 2 x the neighbourhood reach (+1e-4)')
+        # (points.hip kCellMargin: the search's widened reach must stay within half a cell)
+        self.cell = float(cell) if cell is not None else 2.0 * reach * (1.0 + 4e-3)
+        if self.cell < 2.0 * reach * (1.0 + 2.0 ** -9):
+            raise ValueError('pnr.NeuralPoints: cell must be >= 2 x the neighbourhood reach x (1 + 2^-9)')
         if origin is None:
             origin = (xyz.min(0).values - self.cell).tolist() if M > 0 else [0.0, 0.0, 0.0]
         self.origin = [float(v) for v in origin]

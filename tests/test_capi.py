@@ -109,5 +109,14 @@ def test_point_queries_and_arg_errors(lib):
     pts.k, pts.table_bits, pts.cell = 9, 12, 0.1           # k > PNR_MAX_K
     assert L.pnr_point_gather(ctypes.byref(pts), None, 0, None, None, None, None, 0, None) == -1
     assert L.pnr_point_gather_workspace_bytes(1000) >= 16000
+    # the cell-size bound at its limit (points.hip kCellMargin): cell = 2 radius is refused, a cell
+    # just above 2 radius (1 + 2^-9) is accepted (P = 0: no compute, no device access)
+    edge = _lib.Points()
+    edge.mode, edge.k, edge.table_bits, edge.radius, edge.n_points = 0, 8, 12, 0.05, 0
+    edge.index = ctypes.c_void_p(16)
+    edge.cell = 0.1
+    assert L.pnr_point_gather(ctypes.byref(edge), None, 0, None, None, None, None, 0, None) == -1
+    edge.cell = 0.1 * (1 + 2.0 ** -8)
+    assert L.pnr_point_gather(ctypes.byref(edge), None, 0, None, None, None, None, 0, None) == 0
     assert L.pnr_points_build(None, None) == -1
     assert L.pnr_eval_points_c(None, None, None, None, 3, None, None, 0, None) == -1

@@ -172,7 +172,7 @@ def test_gather_bucket_beyond_65535_points(pnr_mod, dev):
     gen = torch.Generator().manual_seed(22)
     n = 70_000
     radius = 0.01
-    cell = 2 * radius * 1.001
+    cell = 2 * radius * 1.003
     xyz = 0.1 + torch.rand((n, 3), generator=gen) * (cell * 0.98)
     xyz = xyz + 0.001 * cell  # strictly inside one cell of the grid anchored at `origin`
     feats = torch.randn((n, 32), generator=gen) * 0.5
