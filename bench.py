@@ -139,11 +139,13 @@ def neural_point_scene(dev, voxel=0.001, n_rays=W * H, seed=0):
     return xyz, feats, p, (o.float().contiguous(), d.float().contiguous(), gt.float().contiguous())
 
 
-def gather_bytes(n_samples, n_nb_total, k, save=True, feat_bytes=128):
-    """Algorithmic bytes of one pnr_point_gather (with the 8 probes made): per
-    sample 24 B point + 8 x 8 B bucket headers + 128 B c (+ k x 8 B idx/weight saves), per
-    neighbour 4 B idx + 12 B xyz + 128 B features (64 B with float16 features)."""
-    return n_samples * (24 + 8 * 8 + 128 + (k * 8 if save else 0)) + n_nb_total * (4 + 12 + feat_bytes)
+def gather_bytes(n_samples, n_probed, n_nb_total, k, save=True, feat_bytes=128):
+    """Algorithmic bytes of one pnr_point_gather: per sample 24 B point + 128 B c
+    (+ k x 8 B idx/weight saves); 8 x 8 B bucket headers only for the `n_probed` samples whose probe
+    block is occupied (the others stop at one L2-resident filter bit); per neighbour 4 B idx + 12 B
+    xyz + 128 B features (64 B with float16 features)."""
+    return (n_samples * (24 + 128 + (k * 8 if save else 0)) + n_probed * 8 * 8 +
+            n_nb_total * (4 + 12 + feat_bytes))
 
 
 def gather_roofline(dev, voxel=0.001, k=8, reps=5, feat_dtype='float32'):
@@ -169,6 +171,9 @@ def gather_roofline(dev, voxel=0.001, k=8, reps=5, feat_dtype='float32'):
     run()
     torch.cuda.synchronize()
     nb = int((idx >= 0).sum().item())
+    # samples on the search's work list: the 64 sub-list counters at the head of the workspace
+    # (csrc/points.hip WorkList: counter r at int32 offset 32 r)
+    probed = int(ws[:64 * 32 * 4].view(torch.int32)[::32].sum().item())
     lib.pnr_timing_enable(1)
     timing_read(4)
     for _ in range(reps):
@@ -177,7 +182,7 @@ def gather_roofline(dev, voxel=0.001, k=8, reps=5, feat_dtype='float32'):
     lib.pnr_timing_enable(0)
     launches, ms, _ = timing_read(4)
     avg = ms / launches
-    byt = gather_bytes(P, nb, k, feat_bytes=64 if feat_dtype == 'float16' else 128)
+    byt = gather_bytes(P, probed, nb, k, feat_bytes=64 if feat_dtype == 'float16' else 128)
     gbs = byt / (avg * 1e-3) / 1e9
     return {'bound': 'hbm', 'achieved': round(gbs, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
             'frac': round(gbs / HBM_PEAK_GBS, 4),
@@ -185,8 +190,10 @@ def gather_roofline(dev, voxel=0.001, k=8, reps=5, feat_dtype='float32'):
             'traffic': pmc_traffic('k_gather', P) if feat_dtype == 'float32' else None,
             'kernel': 'k_gather_probe+k_gather_search',
             'avg_launch_ms': round(avg, 3), 'launches': launches, 'samples': P, 'points': int(xyz.shape[0]),
-            'neighbours_per_sample': round(nb / P, 3), 'radius': 2 * voxel, 'k': k, 'point_features': feat_dtype,
-            'bytes_per_launch': byt}
+            'neighbours_per_sample': round(nb / P, 3), 'probed_samples': probed, 'radius': 2 * voxel, 'k': k,
+            'point_features': feat_dtype, 'bytes_per_launch': byt,
+            'byte_basis': 'per sample 24 B point + 128 B c + k x 8 B idx/weight; 8 x 8 B bucket headers per '
+                          'probed sample (occupied probe block); per neighbour 4 + 12 + 128 B'}
 
 
 def cpu_threads():

@@ -83,7 +83,8 @@ enum { PNR_GATHER_IDW = 0, PNR_GATHER_TRILINEAR = 1 };
  * Backward of every mode but PNR_PREC_FP32 (which runs fp32 MFMA throughout): the delta chain is
  * f16x3 with an exact per-point power-of-two scale (any gradient magnitude), and the weight-gradient
  * GEMMs dW0..dW3, dWc are f16x3 on fp32-stored activations and deltas (per-wave power-of-two scale of
- * the deltas); dWo and dB are fp32 FMA reductions.  Every GEMM of the backward thus carries >= 22
+ * the deltas; delta4 = (Wo^T g_out) masked is not stored but rebuilt in fp32 FMAs inside the dW3
+ * GEMM); dWo and dB are fp32 FMA reductions.  Every GEMM of the backward thus carries >= 22
  * significant bits per operand and accumulates in fp32. */
 enum { PNR_PREC_FP32 = 0, PNR_PREC_BF16X3 = 1, PNR_PREC_BF16 = 2, PNR_PREC_F16X3 = 3 };
 

@@ -238,8 +238,13 @@ int mlp_backward_core(int prec, const float* packed, const SaveArgs& sv, int64_t
       const float* ep = sv.eP + p0 * kFourierPad;
       // output layer: dWo (4x256) += g_out^T h4 ; dbo += colsum(g_out)
       rc = launch_wgrad_out16(b.g_out + p0 * 4, hp + 3 * hstride, C, grads[9], grads[10], st);
-      // hidden layers: dW_l += delta_{l+1}^T h_l  (W3: delta4.h3, W2: delta3.h2, W1: delta2.h1)
-      for (int l = 3; l >= 1 && rc == 0; --l)
+      // hidden layers: dW_l += delta_{l+1}^T h_l  (W3: delta4.h3, W2: delta3.h2, W1: delta2.h1); delta4
+      // is not stored by k_mlp_bwd16 (rank 4: rebuilt from g_out and the h4 masks inside the GEMM)
+      const WgradSyn syn{reinterpret_cast<const float4*>(b.g_out + p0 * 4), sv.masks + 3 * (sv.ld / 32) * 64, p0 / 32,
+                         packed + packed_raw_wo_offset()};
+      if (rc == 0)
+        rc = launch_wgrad16(kWgradOutDelta, nullptr, hp + 2 * hstride, C, C, grads[7], kHidden, grads[8], st, &syn);
+      for (int l = 2; l >= 1 && rc == 0; --l)
         rc = launch_wgrad16(kWgradHidden, b.dP + l * dstride, hp + (l - 1) * hstride, C, C, grads[1 + 2 * l],
                             kHidden, grads[2 + 2 * l], st);
       // first layer: dW0 (256x93) += delta1^T e ; db0

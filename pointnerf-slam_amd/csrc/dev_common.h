@@ -33,6 +33,20 @@ __device__ __forceinline__ void glds16s(const void* sbase, uint32_t voff, uint32
                : "=&s"(keep) : "v"(voff), "s"(sbase), "s"(lds_byte) : "memory");
 }
 
+// 16-B store of a training save (activations, deltas), read back only by a later kernel.
+// PNR_SAVE_SC1: write-through (sc1) -- the line is dropped from the XCD's L2 instead of kept
+// (MI355X_MICROARCH.md "stores of each flavour"), so the save stream does not evict the weight
+// images the LDS-DMA ring re-reads.
+__device__ __forceinline__ void save16(float* p, float4 v) {
+#if defined(PNR_SAVE_SC1)
+  typedef float v4f __attribute__((ext_vector_type(4)));
+  const v4f x = {v.x, v.y, v.z, v.w};
+  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(x) : "memory");
+#else
+  *reinterpret_cast<float4*>(p) = v;
+#endif
+}
+
 __device__ __forceinline__ uint32_t lds_addr(const float* p) {
   return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) float*)p;
 }

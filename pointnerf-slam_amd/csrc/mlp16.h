@@ -128,7 +128,11 @@ __host__ __device__ constexpr int fwd_ct(int g) {
 }
 // activation-save stores one wave issues in step g (SAVE): 4 h quads + the mask words after tile 7
 __host__ __device__ constexpr int fwd_stores(int g) { return fwd_conv(g) ? 4 + (fwd_ct(g) == 7 ? 1 : 0) : 0; }
+#if defined(PNR_EXP_NOSTORE)  // experiment: no h / e saves (timing bound only)
+constexpr int kFwdPrologueStores = 1;
+#else
 constexpr int kFwdPrologueStores = 13;  // e tiles (3 x 4 quads) + x
+#endif
 
 template <int NP, bool HASC, bool SAVE = false>
 struct BfGeo {
@@ -349,9 +353,17 @@ struct BfFwd {
       }
     }
   }
+  // fp32 save address of this lane's unit quad (t, q) of h_L: point-major row S.col
+  static __device__ __forceinline__ float* h_save(const BfFwdArgs& a, const St& S, int L, int t, int q) {
+    const int lane = threadIdx.x & 63;
+#if defined(PNR_EXP_LINSAVE)  // experiment: ideal store shape (1 KB contiguous per instruction), wrong layout
+    return a.save.hP + ((int64_t)L * a.save.ld + S.col - (lane & 31)) * kHidden + (t * 4 + q) * 256 + lane * 4;
+#else
+    return a.save.hP + ((int64_t)L * a.save.ld + S.col) * kHidden + 32 * t + 8 * q + 4 * (lane >> 5);
+#endif
+  }
   template <int L, int t, int q>
   static __device__ __forceinline__ void conv2(const BfFwdArgs& a, St& S, const char* lds) {
-    const int lane = threadIdx.x & 63, hh = lane >> 5;
     if constexpr (HASC) {
       const float4 b = S.bcq[q];
       const float b4[4] = {b.x, b.y, b.z, b.w};
@@ -359,9 +371,12 @@ struct BfFwd {
 #pragma unroll
       for (int i = 0; i < 4; ++i) S.v[4 * q + i] += (F16 ? S.f[4 * q + i] * inv : S.f[4 * q + i]) + b4[i];
     }
+#if !defined(PNR_EXP_NOSTORE)
     if constexpr (SAVE)  // fp32 activation save (pnr_internal.h SaveArgs)
-      *reinterpret_cast<float4*>(a.save.hP + ((int64_t)L * a.save.ld + S.col) * kHidden + 32 * t + 8 * q + 4 * hh) =
-          make_float4(S.v[4 * q], S.v[4 * q + 1], S.v[4 * q + 2], S.v[4 * q + 3]);
+#else
+    if constexpr (false)
+#endif
+      save16(h_save(a, S, L, t, q), make_float4(S.v[4 * q], S.v[4 * q + 1], S.v[4 * q + 2], S.v[4 * q + 3]));
     S.vmax = fmaxf(S.vmax, fmaxf(fmaxf(fabsf(S.v[4 * q]), fabsf(S.v[4 * q + 1])),
                                  fmaxf(fabsf(S.v[4 * q + 2]), fabsf(S.v[4 * q + 3]))));
     split_quad<PR>(S.v + 4 * q, q, S.nxt);
@@ -417,7 +432,9 @@ struct BfFwd {
   __host__ __device__ static constexpr int stores_grp(int g, int T) {
     if (!SAVE || !fwd_conv(g)) return 0;
     int n = 0;
+#if !defined(PNR_EXP_NOSTORE)
     for (int q = 0; q < 4; ++q) n += clamp_t(4 + q, g) == T ? 1 : 0;
+#endif
     if (fwd_ct(g) == 7 && clamp_t(3 + shift(g), g) == T) ++n;
     return n;
   }
@@ -611,12 +628,14 @@ struct BfFwd {
         conv1<3, t, 1>(a, S, S.acc[1][t], lds);
         conv1<3, t, 2>(a, S, S.acc[1][t], lds);
         conv1<3, t, 3>(a, S, S.acc[1][t], lds);
+#if !defined(PNR_EXP_NOSTORE)
         if constexpr (SAVE) {
-          const int hh = (threadIdx.x >> 5) & 1;
+#else
+        if constexpr (false) {
+#endif
 #pragma unroll
           for (int q = 0; q < 4; ++q)
-            *reinterpret_cast<float4*>(a.save.hP + ((int64_t)3 * a.save.ld + S.col) * kHidden + 32 * t + 8 * q +
-                                       4 * hh) = make_float4(S.v[4 * q], S.v[4 * q + 1], S.v[4 * q + 2], S.v[4 * q + 3]);
+            save16(h_save(a, S, 3, t, q), make_float4(S.v[4 * q], S.v[4 * q + 1], S.v[4 * q + 2], S.v[4 * q + 3]));
         }
       }
       out_dot<t>(S, wo, o);
@@ -703,11 +722,15 @@ static __device__ __forceinline__ void fwd16_tile(const BfFwdArgs& a, int mode, 
         }
         v[r] = k < kFourier ? fourier_sc<false>(arg) : 0.f;
       }
+#if !defined(PNR_EXP_NOSTORE)
       if constexpr (SAVE) {
+#else
+      if constexpr (false) {
+#endif
         float* row = a.save.eP + S.col * kFourierPad + 32 * t + 4 * hh;
 #pragma unroll
         for (int q = 0; q < 4; ++q)
-          *reinterpret_cast<float4*>(row + 8 * q) = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+          save16(row + 8 * q, make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]));
       }
       split_tile<PR>(v, S.ft[t]);
     }

@@ -295,4 +295,6 @@ int launch_mlp_fwd_bf(int prec, const float* packed, const PointSrc& src, int mo
   }
 }
 
+int64_t packed_raw_wo_offset() { return kOffRaw + kRawWo; }
+
 }  // namespace pnr

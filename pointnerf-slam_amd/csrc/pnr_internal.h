@@ -172,6 +172,8 @@ int launch_mlp_bwd(const float* packed, const BwdArgs& a, int64_t P, hipStream_t
 int launch_mlp_bwd_bf(const float* packed, const BwdArgs& a, int64_t P, hipStream_t st);
 
 int launch_pack(const RawParams& rp, float* packed, hipStream_t st);
+// float offset of Wo [4][256] fp32 in the packed buffer (the raw table's copy, mlp16.h kRawWo)
+int64_t packed_raw_wo_offset();
 int launch_fc_pack(const float* const* fc, float* out, hipStream_t st);
 
 // bf16 split forward (mlp_bf.hip): images appended to the fp32 images in the same buffers
@@ -223,14 +225,25 @@ int launch_gather_bwd(const pnr_points& pts, const PointSrc* src, int mode, cons
                       bool gp_accum, void* ws, size_t ws_bytes, hipStream_t st);
 
 // weight-gradient GEMM shapes (wgrad.hip): C[MA][NB] += A[K][WA]^T B[K][WB]
-enum WgradKind : int { kWgradHidden = 0, kWgradFirst = 1, kWgradOut = 2, kWgradFourier = 3, kWgradFc = 4 };
+enum WgradKind : int {
+  kWgradHidden = 0, kWgradFirst = 1, kWgradOut = 2, kWgradFourier = 3, kWgradFc = 4,
+  kWgradOutDelta = 5  // split precisions: dW3 = delta4^T h3 with delta4 rebuilt from g_out (WgradSyn)
+};
+// kWgradOutDelta: delta4 = (Wo^T g_out) * [h4 > 0] is not stored by the delta chain; the GEMM
+// rebuilds it per element from the chunk's g_out rows, the forward's h4 mask words and Wo
+struct WgradSyn {
+  const float4* g_out;  // [K] chunk-local
+  const uint4* masks;   // layer-4 mask words (SaveArgs::masks + 3 x ld / 32 x 64)
+  int64_t mgrp0;        // saved row of A row 0, / 32
+  const float* wo;      // Wo [4][256] fp32
+};
 int launch_wgrad(int kind, const float* A, int ma, const float* B, int nb, int64_t K, float* C, int64_t ldc,
                  float* bias, hipStream_t st);
 // split precisions (wgrad16.hip): kWgradHidden / kWgradFirst / kWgradFc as f16x3 GEMMs on fp32
 // operands (A = deltas or dL/dh [K][256], B = activations / Fourier features / point features
 // [K][WB]; B rows >= kb_rows are not read), dWo and dB as fp32 FMA reductions
 int launch_wgrad16(int kind, const float* A, const float* B, int64_t K, int64_t kb_rows, float* C, int64_t ldc,
-                   float* bias, hipStream_t st);
+                   float* bias, hipStream_t st, const WgradSyn* syn = nullptr);
 int launch_wgrad_out16(const float* g_out, const float* h4, int64_t K, float* C, float* bias, hipStream_t st);
 int launch_wgrad_fourier16(const float4* xP, const float* garg, int64_t K, float* C, hipStream_t st);
 

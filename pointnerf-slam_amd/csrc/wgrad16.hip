@@ -45,7 +45,7 @@ template <int NTB, int WB>
 struct Wx3 {
   static constexpr int kThreads = 512;                   // 8 waves, 2 per SIMD
   static constexpr int kPlane = NTB * kTileB;            // one plane (hi or lo) of a B tile
-  static constexpr int kSlot = 2 * kPlane;
+  static constexpr int kSlot = 2 * kPlane + 512;         // + the tile's 32 g_out rows (SYN)
   static constexpr int kLds = 2 * kSlot;                 // double-buffered
   static constexpr int kC4 = WB / 4;                     // float4 per B row
   static constexpr int kB4 = 32 * kC4;                   // float4 per B tile
@@ -62,23 +62,43 @@ struct WxArgs {
   float* C;
   int64_t ldc;
   float* bias;
+  // SYN (dW3 = delta4^T h3): A is not read but rebuilt per element from the rank-4 product
+  // delta4 = (Wo^T g_out) * [h4 > 0] -- the forward's ReLU mask words of h4 and the tile's g_out
+  const float4* g_out;   // [K] chunk-local rows (zero past the real points)
+  const uint4* masks;    // layer-4 mask words [ld / 32][64] (k_mlp_fwd16 layout)
+  int64_t mgrp0;         // mask group of A row 0 (saved row / 32)
+  const float* wo;       // Wo [4][256] fp32
 };
 
 template <int NTB, int WB>
 struct WxRegs {
-  float a[16];                                 // A element (k-step s, j) -> a[8s + j]
+  float a[16];                                 // A element (k-step s, j) -> a[8s + j]  (SYN: mask words)
   float4 b[Wx3<NTB, WB>::kBPer];
+  float4 go;                                   // SYN: g_out row k0 + tid (threads < 32)
 };
 
-template <int NTB, int WB>
+template <int NTB, int WB, bool SYN>
 __device__ __forceinline__ void wx_load(const WxArgs& a, int64_t k0, WxRegs<NTB, WB>& R) {
   using Cfg = Wx3<NTB, WB>;
   const int tid = threadIdx.x, lane = tid & 63;
-  const float* Ab = a.A + (k0 + 8 * (lane >> 5)) * 256 + 32 * wave_id() + (lane & 31);
+  if constexpr (SYN) {
+    // mask word of unit u = 32w + (lane & 31) for the lane's 16 points 8 hh + 16 s + j of the
+    // 32-point group: uint4 (point + 32 ((u >> 2) & 1)), component u >> 6 (k_mlp_fwd16 conv1)
+    const int u = 32 * wave_id() + (lane & 31);
+    const uint32_t* mw = reinterpret_cast<const uint32_t*>(a.masks + (a.mgrp0 + k0 / 32) * 64 + 32 * ((u >> 2) & 1)) +
+                         (u >> 6);
 #pragma unroll
-  for (int s = 0; s < 2; ++s)
+    for (int s = 0; s < 2; ++s)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) R.a[8 * s + j] = Ab[(16 * s + j) * 256];
+      for (int j = 0; j < 8; ++j) R.a[8 * s + j] = __uint_as_float(mw[(8 * (lane >> 5) + 16 * s + j) * 4]);
+    if (tid < 32) R.go = a.g_out[k0 + tid];
+  } else {
+    const float* Ab = a.A + (k0 + 8 * (lane >> 5)) * 256 + 32 * wave_id() + (lane & 31);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) R.a[8 * s + j] = Ab[(16 * s + j) * 256];
+  }
 #pragma unroll
   for (int i = 0; i < Cfg::kBPer; ++i) {
     const int q = tid + Cfg::kThreads * i;
@@ -90,11 +110,12 @@ __device__ __forceinline__ void wx_load(const WxArgs& a, int64_t k0, WxRegs<NTB,
   }
 }
 
-// B tile -> hi / lo f16 planes of `slot`
-template <int NTB, int WB>
+// B tile -> hi / lo f16 planes of `slot` (SYN: + the tile's g_out rows after them)
+template <int NTB, int WB, bool SYN>
 __device__ __forceinline__ void wx_stage_b(const WxRegs<NTB, WB>& R, char* slot) {
   using Cfg = Wx3<NTB, WB>;
   const int tid = threadIdx.x;
+  if (SYN && tid < 32) reinterpret_cast<float4*>(slot + 2 * Cfg::kPlane)[tid] = R.go;
 #pragma unroll
   for (int i = 0; i < Cfg::kBPer; ++i) {
     const int q = tid + Cfg::kThreads * i;
@@ -129,7 +150,7 @@ __device__ __forceinline__ f16x8 tr_frag(const char* img, int T, int s) {
   return r;
 }
 
-template <int NTB, int WB>
+template <int NTB, int WB, bool SYN>
 __global__ __launch_bounds__(512, 1) void k_wgrad16(WxArgs a) {
   using Cfg = Wx3<NTB, WB>;
   extern __shared__ __attribute__((aligned(16))) char lds[];
@@ -147,10 +168,31 @@ __global__ __launch_bounds__(512, 1) void k_wgrad16(WxArgs a) {
   float cs = 0.f;          // fp32 row sums of A (bias) for row 32w + (lane & 31), this lane's points
   float sc = 0x1p60f;      // running scale of A (wave-uniform, <= 2^60 as pt_scale); lowered by a tile
   WxRegs<NTB, WB> R;
-  if (ntile > 0) wx_load<NTB, WB>(a, kb, R);
+  float wo[4];             // SYN: Wo[:, u] of this lane's unit, and its mask bit
+  int mbit = 0;
+  if constexpr (SYN) {
+    const int u = 32 * w + (lane & 31);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) wo[i] = a.wo[i * kHidden + u];
+    mbit = ((u >> 5) & 1) * 16 + ((u >> 3) & 3) * 4 + (u & 3);
+  }
+  if (ntile > 0) wx_load<NTB, WB, SYN>(a, kb, R);
   for (int64_t t = 0; t < ntile; ++t) {
     char* slot = lds + (t & 1) * Cfg::kSlot;
-    wx_stage_b<NTB, WB>(R, slot);
+    wx_stage_b<NTB, WB, SYN>(R, slot);
+    if constexpr (SYN) {
+      // delta4 = (Wo^T g_out) masked, fp32 FMAs (the tile's g_out rows from LDS, broadcast reads)
+      __syncthreads();
+      const float4* go = reinterpret_cast<const float4*>(slot + 2 * Cfg::kPlane) + 8 * hh;
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float4 g = go[16 * s + j];
+          const float d = __builtin_fmaf(wo[3], g.w, __builtin_fmaf(wo[2], g.z, __builtin_fmaf(wo[1], g.y, wo[0] * g.x)));
+          R.a[8 * s + j] = ((__float_as_uint(R.a[8 * s + j]) >> mbit) & 1u) ? d : 0.f;
+        }
+    }
     float m = 0.f;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
@@ -180,7 +222,7 @@ __global__ __launch_bounds__(512, 1) void k_wgrad16(WxArgs a) {
       }
     {  // next tile into the (now free) registers; the last tile is re-read (keeps the loop uniform)
       const int64_t tn = t + 1 < ntile ? t + 1 : t;
-      wx_load<NTB, WB>(a, kb + 32 * tn, R);
+      wx_load<NTB, WB, SYN>(a, kb + 32 * tn, R);
     }
     __syncthreads();  // planes of tile t written; every wave is done with the slot of tile t - 2
     const char* ph = slot;
@@ -208,10 +250,10 @@ __global__ __launch_bounds__(512, 1) void k_wgrad16(WxArgs a) {
   if (a.bias && hh == 0) atomicAdd(a.bias + 32 * w + lane, cs);
 }
 
-template <int NTB, int WB>
+template <int NTB, int WB, bool SYN = false>
 static int launch_k(const WxArgs& a, hipStream_t st) {
   using Cfg = Wx3<NTB, WB>;
-  auto kern = k_wgrad16<NTB, WB>;
+  auto kern = k_wgrad16<NTB, WB, SYN>;
   static const bool attr = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                                                Cfg::kLds) == hipSuccess;
   if (!attr) return PNR_E_ARG;
@@ -222,7 +264,7 @@ static int launch_k(const WxArgs& a, hipStream_t st) {
 // kind: kWgradHidden (B [K][256]), kWgradFirst (B [K][96], 93 columns) or kWgradFc (B [K][32]);
 // K is rounded up to 32 (the A rows up to it exist and carry zero deltas)
 int launch_wgrad16(int kind, const float* A, const float* B, int64_t K, int64_t kb_rows, float* C, int64_t ldc,
-                   float* bias, hipStream_t st) {
+                   float* bias, hipStream_t st, const WgradSyn* syn) {
   if (K <= 0) return 0;
   if (kb_rows <= 0) return PNR_E_ARG;
   K = (K + 31) / 32 * 32;
@@ -233,9 +275,17 @@ int launch_wgrad16(int kind, const float* A, const float* B, int64_t K, int64_t 
   nwg = nwg < 4 ? 4 : (nwg > 256 ? 256 : nwg);
   int64_t ks = (K + nwg - 1) / nwg;
   ks = (ks + 31) / 32 * 32;
-  WxArgs a{A, B, 256, K, kb_rows, ks, C, ldc, bias};
+  WxArgs a{A, B, 256, K, kb_rows, ks, C, ldc, bias, nullptr, nullptr, 0, nullptr};
   TimingScope ts(kTimeWgrad, K, st);
   if (kind == kWgradHidden) return launch_k<8, 256>(a, st);
+  if (kind == kWgradOutDelta) {  // dW3 += delta4^T h3, delta4 rebuilt from g_out and the h4 masks
+    if (!syn || !syn->g_out || !syn->masks || !syn->wo) return PNR_E_ARG;
+    a.g_out = syn->g_out;
+    a.masks = syn->masks;
+    a.mgrp0 = syn->mgrp0;
+    a.wo = syn->wo;
+    return launch_k<8, 256, true>(a, st);
+  }
   if (kind == kWgradFc) {  // dWc_l (256 x 32) += gH_l^T c
     a.nb = kCDim;
     return launch_k<1, 32>(a, st);

@@ -83,7 +83,7 @@ def main():
         print('phases (wave-cycles, share of total):', ', '.join(f'{n} {ph[i]:.3e} ({ph[i] / tot:.2f})' for i, n in enumerate(names[:6])),
               f'rounds {ph[6]}, trips {ph[7]}, cycles/round {ph[5] / max(ph[6], 1):.0f}')
     avg = ms / launches
-    byt = gather_bytes(P, nb, args.k)
+    byt = gather_bytes(P, n_work, nb, args.k)
     gbs = byt / (avg * 1e-3) / 1e9
     # backward (feature grads + position grads)
     gf = torch.zeros_like(feats)
