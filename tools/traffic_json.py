@@ -1,7 +1,7 @@
 """Per-unit HBM traffic (profiles/r*_traffic.json, read by bench.py pmc_traffic) from a
 tools/prof_bench.sh traffic directory.
 
-  python tools/traffic_json.py <gpurun_out/prof_<tag>_traffic> <out.json> [source note]
+  python tools/traffic_json.py <gpurun_out/prof_<tag>_traffic> <out.json> [source note] [--mlp-points=N]
 
 Per kernel family, the mean over its launches of (2 x FETCH_SIZE + WRITE_SIZE) bytes divided by the
 units of that launch (tools/traffic.py documents the counter units and the gfx950 FETCH correction):
@@ -46,8 +46,10 @@ def family(name):
 
 
 def main():
-    d, dst = sys.argv[1], sys.argv[2]
-    note = sys.argv[3] if len(sys.argv) > 3 else ''
+    args = [a for a in sys.argv[1:] if not a.startswith('--mlp-points=')]
+    mlp_pts = [int(a.split('=')[1]) for a in sys.argv[1:] if a.startswith('--mlp-points=')]
+    d, dst = args[0], args[1]
+    note = args[2] if len(args) > 2 else ''
     pl = per_launch(d)
     acc = collections.defaultdict(lambda: [0.0, 0.0, 0])  # fetch, write, units
     for c, per in pl.items():
@@ -65,6 +67,13 @@ def main():
         for (name, grid), vals in per.items():
             if family(name) == 'k_gather_search':
                 acc['k_gather'][0 if c == 'FETCH_SIZE' else 1] += sum(vals)
+    # persistent MLP kernels run one workgroup per CU: their grid says nothing about the points, so
+    # --mlp-points=N (the run's training points, the same for the forward and the delta chain)
+    # replaces the grid-derived unit count of both families
+    if mlp_pts:
+        for fam in ('k_mlp_fwd16_train', 'k_mlp_bwd16'):
+            if fam in acc:
+                acc[fam][2] = mlp_pts[0]
     res = {'source': note}
     for fam, (f, w, u) in sorted(acc.items()):
         if u <= 0:
