@@ -235,20 +235,20 @@ int mlp_backward_core(int prec, const float* packed, const SaveArgs& sv, int64_t
     if (!grads) {  // no decoder weight gradients (the Tracker's camera-only backward)
     } else if (split) {  // f16x3 GEMMs on the fp32 saves (h / e by k_mlp_fwd16, deltas by k_mlp_bwd16)
       const float* hp = sv.hP + p0 * kHidden;
-      const float* ep = sv.eP + p0 * kFourierPad;
       // output layer: dWo (4x256) += g_out^T h4 ; dbo += colsum(g_out)
       rc = launch_wgrad_out16(b.g_out + p0 * 4, hp + 3 * hstride, C, grads[9], grads[10], st);
       // hidden layers: dW_l += delta_{l+1}^T h_l  (W3: delta4.h3, W2: delta3.h2, W1: delta2.h1); delta4
       // is not stored by k_mlp_bwd16 (rank 4: rebuilt from g_out and the h4 masks inside the GEMM)
       const WgradSyn syn{reinterpret_cast<const float4*>(b.g_out + p0 * 4), sv.masks + 3 * (sv.ld / 32) * 64, p0 / 32,
-                         packed + packed_raw_wo_offset()};
+                         packed + packed_raw_wo_offset(), sv.xP + p0, packed + kOffFB};
       if (rc == 0)
         rc = launch_wgrad16(kWgradOutDelta, nullptr, hp + 2 * hstride, C, C, grads[7], kHidden, grads[8], st, &syn);
       for (int l = 2; l >= 1 && rc == 0; --l)
         rc = launch_wgrad16(kWgradHidden, b.dP + l * dstride, hp + (l - 1) * hstride, C, C, grads[1 + 2 * l],
                             kHidden, grads[2 + 2 * l], st);
-      // first layer: dW0 (256x93) += delta1^T e ; db0
-      if (rc == 0) rc = launch_wgrad16(kWgradFirst, b.dP, ep, C, C, grads[1], kFourier, grads[2], st);
+      // first layer: dW0 (256x93) += delta1^T e ; db0 -- e = sin(x@B) recomputed from the saved x
+      // (k_mlp_fwd16 saves no e)
+      if (rc == 0) rc = launch_wgrad16(kWgradFirstX, b.dP, nullptr, C, C, grads[1], kFourier, grads[2], st, &syn);
     } else {
       const float* hp = sv.hP + p0 * kHidden;
       rc = launch_wgrad(kWgradOut, b.g_out + p0 * 4, 4, hp + 3 * hstride, kHidden, C, grads[9], kHidden, grads[10],

@@ -14,7 +14,8 @@
 // of 64 cycles for the same depth).
 //
 // Training saves (SAVE) are fp32 in every precision: the weight-gradient GEMMs (wgrad16.hip) split
-// them into hi/lo f16 parts themselves, so the backward stays fp32-class.  Every value the forward
+// them into hi/lo f16 parts themselves, so the backward stays fp32-class.  x and h1..h4 are saved;
+// the Fourier features e = sin(x@B) are recomputed by the dW0 GEMM from x.  Every value the forward
 // splits into f16 parts (hidden activations, features) is checked against the f16 range: a value
 // >= 65504 would turn into inf; the kernel then ORs PNR_STATUS_F16_RANGE into *status (when given).
 //
@@ -128,11 +129,7 @@ __host__ __device__ constexpr int fwd_ct(int g) {
 }
 // activation-save stores one wave issues in step g (SAVE): 4 h quads + the mask words after tile 7
 __host__ __device__ constexpr int fwd_stores(int g) { return fwd_conv(g) ? 4 + (fwd_ct(g) == 7 ? 1 : 0) : 0; }
-#if defined(PNR_EXP_NOSTORE)  // experiment: no h / e saves (timing bound only)
-constexpr int kFwdPrologueStores = 1;
-#else
-constexpr int kFwdPrologueStores = 13;  // e tiles (3 x 4 quads) + x
-#endif
+constexpr int kFwdPrologueStores = 1;  // x (e is not saved: kWgradFirstX recomputes it)
 
 template <int NP, bool HASC, bool SAVE = false>
 struct BfGeo {
@@ -722,16 +719,7 @@ static __device__ __forceinline__ void fwd16_tile(const BfFwdArgs& a, int mode, 
         }
         v[r] = k < kFourier ? fourier_sc<false>(arg) : 0.f;
       }
-#if !defined(PNR_EXP_NOSTORE)
-      if constexpr (SAVE) {
-#else
-      if constexpr (false) {
-#endif
-        float* row = a.save.eP + S.col * kFourierPad + 32 * t + 4 * hh;
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-          save16(row + 8 * q, make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]));
-      }
+      // no e save: the dW0 GEMM recomputes sin(x@B) from the saved x (wgrad16.hip kWgradFirstX)
       split_tile<PR>(v, S.ft[t]);
     }
     if (SAVE && hh == 0) a.save.xP[S.col] = make_float4(x0, x1, x2, inside ? 1.f : 0.f);

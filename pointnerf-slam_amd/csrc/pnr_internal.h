@@ -227,7 +227,8 @@ int launch_gather_bwd(const pnr_points& pts, const PointSrc* src, int mode, cons
 // weight-gradient GEMM shapes (wgrad.hip): C[MA][NB] += A[K][WA]^T B[K][WB]
 enum WgradKind : int {
   kWgradHidden = 0, kWgradFirst = 1, kWgradOut = 2, kWgradFourier = 3, kWgradFc = 4,
-  kWgradOutDelta = 5  // split precisions: dW3 = delta4^T h3 with delta4 rebuilt from g_out (WgradSyn)
+  kWgradOutDelta = 5,  // split precisions: dW3 = delta4^T h3 with delta4 rebuilt from g_out (WgradSyn)
+  kWgradFirstX = 6     // split precisions: dW0 = delta1^T e with e = sin(x@B) recomputed (WgradSyn xP, fb)
 };
 // kWgradOutDelta: delta4 = (Wo^T g_out) * [h4 > 0] is not stored by the delta chain; the GEMM
 // rebuilds it per element from the chunk's g_out rows, the forward's h4 mask words and Wo
@@ -236,6 +237,8 @@ struct WgradSyn {
   const uint4* masks;   // layer-4 mask words (SaveArgs::masks + 3 x ld / 32 x 64)
   int64_t mgrp0;        // saved row of A row 0, / 32
   const float* wo;      // Wo [4][256] fp32
+  const float4* xP;     // kWgradFirstX: saved inputs of the chunk rows
+  const float* fb;      // kWgradFirstX: Fourier B padded [3][96] (packed + kOffFB)
 };
 int launch_wgrad(int kind, const float* A, int ma, const float* B, int nb, int64_t K, float* C, int64_t ldc,
                  float* bias, hipStream_t st);

@@ -68,16 +68,20 @@ struct WxArgs {
   const uint4* masks;    // layer-4 mask words [ld / 32][64] (k_mlp_fwd16 layout)
   int64_t mgrp0;         // mask group of A row 0 (saved row / 32)
   const float* wo;       // Wo [4][256] fp32
+  // FOUR (dW0 = delta1^T e): B = e = sin(x@B) is not read but recomputed from the saved inputs, by
+  // the forward's own arithmetic (bit-identical e)
+  const float4* xP;      // [K] saved MLP inputs (x0, x1, x2, inside), chunk rows
+  const float* fb;       // Fourier B padded [3][96]
 };
 
 template <int NTB, int WB>
 struct WxRegs {
   float a[16];                                 // A element (k-step s, j) -> a[8s + j]  (SYN: mask words)
-  float4 b[Wx3<NTB, WB>::kBPer];
+  float4 b[Wx3<NTB, WB>::kBPer];               // FOUR: the B row's point x (the values come in stage)
   float4 go;                                   // SYN: g_out row k0 + tid (threads < 32)
 };
 
-template <int NTB, int WB, bool SYN>
+template <int NTB, int WB, bool SYN, bool FOUR>
 __device__ __forceinline__ void wx_load(const WxArgs& a, int64_t k0, WxRegs<NTB, WB>& R) {
   using Cfg = Wx3<NTB, WB>;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -105,14 +109,15 @@ __device__ __forceinline__ void wx_load(const WxArgs& a, int64_t k0, WxRegs<NTB,
     if (Cfg::kB4 % Cfg::kThreads == 0 || q < Cfg::kB4) {  // wave-uniform
       int64_t row = k0 + q / Cfg::kC4;
       row = row < a.kb_rows ? row : a.kb_rows - 1;
-      R.b[i] = *reinterpret_cast<const float4*>(a.B + row * WB + 4 * (q % Cfg::kC4));
+      if constexpr (FOUR) R.b[i] = a.xP[row];
+      else R.b[i] = *reinterpret_cast<const float4*>(a.B + row * WB + 4 * (q % Cfg::kC4));
     }
   }
 }
 
 // B tile -> hi / lo f16 planes of `slot` (SYN: + the tile's g_out rows after them)
-template <int NTB, int WB, bool SYN>
-__device__ __forceinline__ void wx_stage_b(const WxRegs<NTB, WB>& R, char* slot) {
+template <int NTB, int WB, bool SYN, bool FOUR>
+__device__ __forceinline__ void wx_stage_b(const WxRegs<NTB, WB>& R, char* slot, const float (&fbr)[Wx3<NTB, WB>::kBPer][3][4]) {
   using Cfg = Wx3<NTB, WB>;
   const int tid = threadIdx.x;
   if (SYN && tid < 32) reinterpret_cast<float4*>(slot + 2 * Cfg::kPlane)[tid] = R.go;
@@ -121,7 +126,21 @@ __device__ __forceinline__ void wx_stage_b(const WxRegs<NTB, WB>& R, char* slot)
     const int q = tid + Cfg::kThreads * i;
     if (Cfg::kB4 % Cfg::kThreads == 0 || q < Cfg::kB4) {
       const int r = q / Cfg::kC4, c = 4 * (q % Cfg::kC4);
-      const float v[4] = {R.b[i].x, R.b[i].y, R.b[i].z, R.b[i].w};
+      float v[4] = {R.b[i].x, R.b[i].y, R.b[i].z, R.b[i].w};
+      if constexpr (FOUR) {  // e[c + e] = sin(x @ B[:, c + e]), as k_mlp_fwd16's prologue computes it
+        const float x0 = R.b[i].x, x1 = R.b[i].y, x2 = R.b[i].z;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float arg;
+          {
+#pragma clang fp contract(off)
+            arg = x0 * fbr[i][0][e];
+            arg = __builtin_fmaf(x1, fbr[i][1][e], arg);
+            arg = __builtin_fmaf(x2, fbr[i][2][e], arg);
+          }
+          v[e] = c + e < kFourier ? fourier_sc<false>(arg) : 0.f;
+        }
+      }
       f16x4 hi, lo;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -150,7 +169,7 @@ __device__ __forceinline__ f16x8 tr_frag(const char* img, int T, int s) {
   return r;
 }
 
-template <int NTB, int WB, bool SYN>
+template <int NTB, int WB, bool SYN, bool FOUR>
 __global__ __launch_bounds__(512, 1) void k_wgrad16(WxArgs a) {
   using Cfg = Wx3<NTB, WB>;
   extern __shared__ __attribute__((aligned(16))) char lds[];
@@ -176,10 +195,18 @@ __global__ __launch_bounds__(512, 1) void k_wgrad16(WxArgs a) {
     for (int i = 0; i < 4; ++i) wo[i] = a.wo[i * kHidden + u];
     mbit = ((u >> 5) & 1) * 16 + ((u >> 3) & 3) * 4 + (u & 3);
   }
-  if (ntile > 0) wx_load<NTB, WB, SYN>(a, kb, R);
+  float fbr[Cfg::kBPer][3][4];  // FOUR: Fourier B of this thread's 4 columns (fixed over the tiles)
+#pragma unroll
+  for (int i = 0; i < Cfg::kBPer; ++i)
+#pragma unroll
+    for (int d = 0; d < 3; ++d)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        fbr[i][d][e] = FOUR ? a.fb[d * kFourierPad + 4 * ((threadIdx.x + Cfg::kThreads * i) % Cfg::kC4) + e] : 0.f;
+  if (ntile > 0) wx_load<NTB, WB, SYN, FOUR>(a, kb, R);
   for (int64_t t = 0; t < ntile; ++t) {
     char* slot = lds + (t & 1) * Cfg::kSlot;
-    wx_stage_b<NTB, WB, SYN>(R, slot);
+    wx_stage_b<NTB, WB, SYN, FOUR>(R, slot, fbr);
     if constexpr (SYN) {
       // delta4 = (Wo^T g_out) masked, fp32 FMAs (the tile's g_out rows from LDS, broadcast reads)
       __syncthreads();
@@ -222,7 +249,7 @@ __global__ __launch_bounds__(512, 1) void k_wgrad16(WxArgs a) {
       }
     {  // next tile into the (now free) registers; the last tile is re-read (keeps the loop uniform)
       const int64_t tn = t + 1 < ntile ? t + 1 : t;
-      wx_load<NTB, WB, SYN>(a, kb + 32 * tn, R);
+      wx_load<NTB, WB, SYN, FOUR>(a, kb + 32 * tn, R);
     }
     __syncthreads();  // planes of tile t written; every wave is done with the slot of tile t - 2
     const char* ph = slot;
@@ -250,10 +277,10 @@ __global__ __launch_bounds__(512, 1) void k_wgrad16(WxArgs a) {
   if (a.bias && hh == 0) atomicAdd(a.bias + 32 * w + lane, cs);
 }
 
-template <int NTB, int WB, bool SYN = false>
+template <int NTB, int WB, bool SYN = false, bool FOUR = false>
 static int launch_k(const WxArgs& a, hipStream_t st) {
   using Cfg = Wx3<NTB, WB>;
-  auto kern = k_wgrad16<NTB, WB, SYN>;
+  auto kern = k_wgrad16<NTB, WB, SYN, FOUR>;
   static const bool attr = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                                                Cfg::kLds) == hipSuccess;
   if (!attr) return PNR_E_ARG;
@@ -275,7 +302,7 @@ int launch_wgrad16(int kind, const float* A, const float* B, int64_t K, int64_t 
   nwg = nwg < 4 ? 4 : (nwg > 256 ? 256 : nwg);
   int64_t ks = (K + nwg - 1) / nwg;
   ks = (ks + 31) / 32 * 32;
-  WxArgs a{A, B, 256, K, kb_rows, ks, C, ldc, bias, nullptr, nullptr, 0, nullptr};
+  WxArgs a{A, B, 256, K, kb_rows, ks, C, ldc, bias, nullptr, nullptr, 0, nullptr, nullptr, nullptr};
   TimingScope ts(kTimeWgrad, K, st);
   if (kind == kWgradHidden) return launch_k<8, 256>(a, st);
   if (kind == kWgradOutDelta) {  // dW3 += delta4^T h3, delta4 rebuilt from g_out and the h4 masks
@@ -293,6 +320,13 @@ int launch_wgrad16(int kind, const float* A, const float* B, int64_t K, int64_t 
   if (kind == kWgradFirst) {
     a.nb = kFourier;
     return launch_k<3, 96>(a, st);
+  }
+  if (kind == kWgradFirstX) {  // dW0 (256 x 93) += delta1^T sin(x@B): e recomputed from x
+    if (!syn || !syn->xP || !syn->fb) return PNR_E_ARG;
+    a.nb = kFourier;
+    a.xP = syn->xP;
+    a.fb = syn->fb;
+    return launch_k<3, 96, false, true>(a, st);
   }
   return PNR_E_ARG;
 }
