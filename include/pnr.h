@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define PNR_ABI_VERSION 7
+#define PNR_ABI_VERSION 8
 #define PNR_N_PARAMS 11
 #define PNR_MAX_SAMPLES 64      /* N_samples + N_importance per ray */
 #define PNR_C_DIM 32            /* neural-point feature width (decoder.py:122-125 fc_c input) */
@@ -128,7 +128,12 @@ typedef struct pnr_render_params {
   double far_clamp;         /* used when far_mode == 1                                 */
   float t_vals[PNR_MAX_SAMPLES];   /* torch.linspace(0,1,n_samples) float32           */
   float u_vals[PNR_MAX_SAMPLES];   /* torch.linspace(0,1,n_importance) float32        */
-  int32_t save_for_backward;       /* keep MLP activations in the workspace for pnr_render_bwd */
+  int32_t save_for_backward;       /* 1: keep MLP activations in the workspace for pnr_render_bwd;
+                                      2 (ABI 8): keep only the ReLU masks and inputs -- the backward
+                                      then computes NO decoder / fc_c weight gradients (grads and
+                                      g_fc must be NULL: the Tracker's camera-only backward); the
+                                      split precisions skip the 4 KB/point activation stores
+                                      (PNR_PREC_FP32 saves everything either way) */
   int32_t need_ray_grads;          /* backward also produces dL/drays_o, dL/drays_d (tracking) */
   const pnr_points* points;        /* neural-point features, NULL = the reference decoder (c_dim=0) */
   int32_t precision;               /* PNR_PREC_* of the decoder matmuls                           */

@@ -127,12 +127,21 @@ struct RenderWS {
   size_t gws_bytes;
 };
 
-SaveArgs carve_save(Carver& c, int64_t ld) {
+// What the forward keeps for the backward: 0 nothing, 1 every activation, 2 the ReLU masks and the
+// inputs only (save_for_backward 2: no weight gradients will be asked for; implemented for the
+// default PNR_PREC_F16X3 -- the other precisions save everything)
+int save_mode(const pnr_render_params* prm) {
+  if (!prm->save_for_backward) return 0;
+  return (prm->save_for_backward == 2 && prm->precision == PNR_PREC_F16X3) ? 2 : 1;
+}
+
+SaveArgs carve_save(Carver& c, int64_t ld, bool acts = true) {
   SaveArgs s{};
   s.ld = ld;
   s.p0 = 0;
-  s.eP = c.take<float>(kFourierPad * ld);
-  s.hP = c.take<float>((size_t)4 * kHidden * ld);
+  // mode 2: hP = eP = NULL, which tells the split forward to store masks and inputs only
+  s.eP = acts ? c.take<float>(kFourierPad * ld) : nullptr;
+  s.hP = acts ? c.take<float>((size_t)4 * kHidden * ld) : nullptr;
   s.xP = c.take<float4>(ld);
   s.masks = c.take<uint4>((size_t)4 * (ld / 32) * 64);
   return s;
@@ -149,7 +158,7 @@ RenderWS carve_render(const pnr_render_params* prm, int64_t n, void* ws, size_t*
   w.far = c.take<double>(n);
   w.pc_pad = pad128(n * prm->n_samples);
   w.ld = w.pc_pad + pad128(n * prm->n_importance);
-  if (prm->save_for_backward) w.save = carve_save(c, w.ld);
+  if (prm->save_for_backward) w.save = carve_save(c, w.ld, save_mode(prm) == 1);
   if (prm->points) {
     w.c = c.take<float>((size_t)w.ld * kCDim);
     w.nidx = c.take<int32_t>((size_t)w.ld * prm->points->k);
@@ -505,6 +514,8 @@ int pnr_render_bwd(const pnr_render_params* prm, const float* packed, const floa
   if (grads)  // NULL: no decoder weight gradients
     for (int i = 0; i < PNR_N_PARAMS; ++i)
       if (!grads[i]) return PNR_E_ARG;
+  // a masks-only forward (save_for_backward 2) kept no activations to form weight gradients from
+  if (save_mode(prm) == 2 && (grads || (prm->points && prm->points->g_fc))) return PNR_E_ARG;
   if (prm->need_ray_grads && (!g_rays_o || !g_rays_d)) return PNR_E_ARG;
   size_t need = 0, bneed = 0;
   RenderWS w = carve_render(prm, n, workspace, &need);
@@ -553,7 +564,7 @@ RegWS carve_reg(const pnr_render_params* prm, int64_t n, void* ws, size_t* bytes
   const int64_t P = n * prm->n_samples;
   w.z = c.take<float>(P);
   w.raw = c.take<float>(P * 4);
-  if (prm->save_for_backward) w.save = carve_save(c, pad128(P));
+  if (prm->save_for_backward) w.save = carve_save(c, pad128(P), save_mode(prm) == 1);
   if (prm->points) {
     w.c = c.take<float>((size_t)pad128(P) * kCDim);
     w.nidx = c.take<int32_t>((size_t)pad128(P) * prm->points->k);
@@ -626,6 +637,8 @@ int pnr_regulation_bwd(const pnr_render_params* prm, const float* packed, const 
   if (grads)  // NULL: no decoder weight gradients
     for (int i = 0; i < PNR_N_PARAMS; ++i)
       if (!grads[i]) return PNR_E_ARG;
+  // a masks-only forward (save_for_backward 2) kept no activations to form weight gradients from
+  if (save_mode(prm) == 2 && (grads || (prm->points && prm->points->g_fc))) return PNR_E_ARG;
   if (prm->need_ray_grads && (!g_rays_o || !g_rays_d || !rays_d)) return PNR_E_ARG;
   size_t need = 0, bneed = 0;
   RegWS w = carve_reg(prm, n, workspace, &need);

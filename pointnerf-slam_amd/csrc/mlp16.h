@@ -269,11 +269,15 @@ extern __device__ unsigned long long g_pnr_dbg[4][48];
   } while (0)
 #endif
 
-template <int PR, bool HASC, bool SAVE>
+// SV: 0 no saves (eval), 1 masks + inputs + activations (training), 2 masks + inputs only (a
+// backward with no weight gradients: the Tracker's camera-only step; PNR_PREC_F16X3 only)
+template <int PR, bool HASC, int SV>
 struct BfFwd {
+  static constexpr bool SAVE = SV != 0;   // ReLU masks + inputs
+  static constexpr bool SAVEH = SV == 1;  // + h1..h4
   static constexpr int NP = Prec<PR>::NP;
   static constexpr bool F16 = Prec<PR>::F16;
-  using G = BfGeo<NP, HASC, SAVE>;
+  using G = BfGeo<NP, HASC, SV != 0>;
   using V8 = typename Prec<PR>::V8;
   static constexpr int kRing = (HASC && SAVE) ? 3 : 4, kPf = kRing - 1;
   using St = BfState<PR, kRing>;
@@ -369,7 +373,7 @@ struct BfFwd {
       for (int i = 0; i < 4; ++i) S.v[4 * q + i] += (F16 ? S.f[4 * q + i] * inv : S.f[4 * q + i]) + b4[i];
     }
 #if !defined(PNR_EXP_NOSTORE)
-    if constexpr (SAVE)  // fp32 activation save (pnr_internal.h SaveArgs)
+    if constexpr (SAVEH)  // fp32 activation save (pnr_internal.h SaveArgs)
 #else
     if constexpr (false)
 #endif
@@ -430,7 +434,8 @@ struct BfFwd {
     if (!SAVE || !fwd_conv(g)) return 0;
     int n = 0;
 #if !defined(PNR_EXP_NOSTORE)
-    for (int q = 0; q < 4; ++q) n += clamp_t(4 + q, g) == T ? 1 : 0;
+    if (SAVEH)
+      for (int q = 0; q < 4; ++q) n += clamp_t(4 + q, g) == T ? 1 : 0;
 #endif
     if (fwd_ct(g) == 7 && clamp_t(3 + shift(g), g) == T) ++n;
     return n;
@@ -626,7 +631,7 @@ struct BfFwd {
         conv1<3, t, 2>(a, S, S.acc[1][t], lds);
         conv1<3, t, 3>(a, S, S.acc[1][t], lds);
 #if !defined(PNR_EXP_NOSTORE)
-        if constexpr (SAVE) {
+        if constexpr (SAVEH) {
 #else
         if constexpr (false) {
 #endif
@@ -653,10 +658,11 @@ struct BfFwd {
 };
 
 // one 128-point tile of k_mlp_fwd16 (it: the workgroup's tile count so far, sb: its ring slot base)
-template <int PR, bool HASC, bool SAVE>
+template <int PR, bool HASC, int SV>
 static __device__ __forceinline__ void fwd16_tile(const BfFwdArgs& a, int mode, const char* lds, int64_t tile,
                                                  int it, int sb) {
-  using K = BfFwd<PR, HASC, SAVE>;
+  using K = BfFwd<PR, HASC, SV>;
+  constexpr bool SAVE = K::SAVE;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, hh = lane >> 5, j = lane & 31;
   const int64_t p = tile * 128 + wave * 32 + j;
   typename K::St S;
@@ -749,9 +755,9 @@ static __device__ __forceinline__ void fwd16_tile(const BfFwdArgs& a, int mode, 
   }
 }
 
-template <int PR, bool HASC, bool SAVE>
+template <int PR, bool HASC, int SV>
 __global__ __launch_bounds__(256, 1) void k_mlp_fwd16(BfFwdArgs a, int mode) {
-  using K = BfFwd<PR, HASC, SAVE>;
+  using K = BfFwd<PR, HASC, SV>;
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int lane = threadIdx.x & 63;
 
@@ -778,26 +784,26 @@ __global__ __launch_bounds__(256, 1) void k_mlp_fwd16(BfFwdArgs a, int mode) {
     const int64_t ntiles = (a.P + 127) / 128;
     int sb = 0, it = 0;
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x, ++it) {
-      fwd16_tile<PR, HASC, SAVE>(a, mode, lds, tile, it, sb);
+      fwd16_tile<PR, HASC, SV>(a, mode, lds, tile, it, sb);
       sb = (sb + K::G::kSteps) % K::G::kNbuf;
     }
     // the last tile's prefetch of a next tile (always issued: fixed wait counts) must land in the
     // workgroup's LDS before it exits
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   } else {
-    fwd16_tile<PR, HASC, SAVE>(a, mode, lds, blockIdx.x, 0, 0);
+    fwd16_tile<PR, HASC, SV>(a, mode, lds, blockIdx.x, 0, 0);
   }
 }
 
 // per-precision launchers (mlp16_fwd_*.hip), dispatched by launch_mlp_fwd_bf (mlp16_pack.hip)
-int launch_fwd16_f16x3(int mode, dim3 grid, hipStream_t st, const BfFwdArgs& a, bool hasc, bool save);
-int launch_fwd16_bf16x3(int mode, dim3 grid, hipStream_t st, const BfFwdArgs& a, bool hasc, bool save);
-int launch_fwd16_bf16(int mode, dim3 grid, hipStream_t st, const BfFwdArgs& a, bool hasc, bool save);
+int launch_fwd16_f16x3(int mode, dim3 grid, hipStream_t st, const BfFwdArgs& a, bool hasc, int save);
+int launch_fwd16_bf16x3(int mode, dim3 grid, hipStream_t st, const BfFwdArgs& a, bool hasc, int save);
+int launch_fwd16_bf16(int mode, dim3 grid, hipStream_t st, const BfFwdArgs& a, bool hasc, int save);
 
-template <int PR, bool HASC, bool SAVE>
+template <int PR, bool HASC, int SV>
 static int launch16s(int mode, dim3 grid, hipStream_t st, const BfFwdArgs& a) {
   const size_t lds = BfGeo<Prec<PR>::NP, HASC>::kLds;
-  auto kern = k_mlp_fwd16<PR, HASC, SAVE>;
+  auto kern = k_mlp_fwd16<PR, HASC, SV>;
   static const bool attr = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                                                (int)lds) == hipSuccess;
   if (!attr) return PNR_E_ARG;
@@ -805,9 +811,14 @@ static int launch16s(int mode, dim3 grid, hipStream_t st, const BfFwdArgs& a) {
   return hip_status(hipGetLastError());
 }
 template <int PR>
-static int launch16(int mode, dim3 grid, hipStream_t st, const BfFwdArgs& a, bool hasc, bool save) {
-  if (hasc) return save ? launch16s<PR, true, true>(mode, grid, st, a) : launch16s<PR, true, false>(mode, grid, st, a);
-  return save ? launch16s<PR, false, true>(mode, grid, st, a) : launch16s<PR, false, false>(mode, grid, st, a);
+static int launch16(int mode, dim3 grid, hipStream_t st, const BfFwdArgs& a, bool hasc, int save) {
+  if (save == 2) {  // masks + inputs only: instantiated for the default precision (capi save_mode)
+    if constexpr (PR == PNR_PREC_F16X3)
+      return hasc ? launch16s<PR, true, 2>(mode, grid, st, a) : launch16s<PR, false, 2>(mode, grid, st, a);
+    return PNR_E_ARG;
+  }
+  if (hasc) return save ? launch16s<PR, true, 1>(mode, grid, st, a) : launch16s<PR, true, 0>(mode, grid, st, a);
+  return save ? launch16s<PR, false, 1>(mode, grid, st, a) : launch16s<PR, false, 0>(mode, grid, st, a);
 }
 
 }  // namespace pnr

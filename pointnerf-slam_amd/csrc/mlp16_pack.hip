@@ -270,7 +270,8 @@ int launch_mlp_fwd_bf(int prec, const float* packed, const PointSrc& src, int mo
   a.P = P;
   a.raw_out = raw;
   a.status = status;
-  const bool sv = save != nullptr;
+  // 0 no saves, 1 masks + inputs + activations, 2 masks + inputs (hP NULL: no weight gradients)
+  const int sv = save == nullptr ? 0 : (save->hP != nullptr ? 1 : 2);
   if (save) a.save = *save;
   else a.save = SaveArgs{nullptr, nullptr, nullptr, nullptr, 0, 0};
   // one workgroup per 128-point tile; the persistent kernels (no feature branch) loop over tiles

@@ -24,7 +24,7 @@ PRECISIONS = {'fp32': 0, 'bf16x3': 1, 'bf16': 2, 'f16x3': 3}
 # f16x3: fp32-class forward AND backward (every GEMM on 22-bit split operands with fp32
 # accumulation; tests/test_gpu_parity.py runs every case under fp32 and f16x3 at the same tolerances)
 DEFAULT_PRECISION = os.environ.get('PNR_PRECISION', 'f16x3')
-ABI_VERSION = 7
+ABI_VERSION = 8
 STATUS_F16_RANGE = 1  # include/pnr.h PNR_STATUS_F16_RANGE
 
 

@@ -107,6 +107,14 @@ def _param_grads(ctx, dev):
     return grads, _lib.PtrArray(*[g.data_ptr() for g in grads])
 
 
+def _save_mode(ctx):
+    """pnr_render_params.save_for_backward: 1 keeps every activation; 2 (ABI 8) keeps the ReLU masks
+    and inputs only, when no decoder or fc_c tensor (autograd inputs 7 .. 7 + 11 + 8) needs a
+    gradient -- the Tracker's camera-only backward forms no weight gradient, so the forward skips
+    the activation stores."""
+    return 1 if any(ctx.needs_input_grad[7:7 + _lib.N_PARAMS + _lib.N_FC_PARAMS]) else 2
+
+
 class _RenderFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, prm_bytes, packer, feat, rays_o, rays_d, gt_depth, far_clamp, *tensors):
@@ -117,7 +125,7 @@ class _RenderFn(torch.autograd.Function):
         packed = packer.image(feat.params)
         feat.attach(prm)
         need = feat.train and any(ctx.needs_input_grad)  # (inside forward grad mode is off)
-        prm.save_for_backward = 1 if need else 0
+        prm.save_for_backward = _save_mode(ctx) if need else 0
         prm.need_ray_grads = 1 if (ctx.needs_input_grad[3] or ctx.needs_input_grad[4]) else 0
         if isinstance(far_clamp, torch.Tensor):  # device value (sharded batch): no host round trip
             far_clamp = far_clamp.reshape(-1)[:1].float().contiguous()
@@ -175,7 +183,7 @@ class _RegulationFn(torch.autograd.Function):
         packed = packer.image(feat.params)
         feat.attach(prm)
         need = feat.train and any(ctx.needs_input_grad)  # (inside forward grad mode is off)
-        prm.save_for_backward = 1 if need else 0
+        prm.save_for_backward = _save_mode(ctx) if need else 0
         prm.need_ray_grads = 1 if (ctx.needs_input_grad[3] or ctx.needs_input_grad[4]) else 0
         ws = torch.empty(lib.pnr_regulation_workspace_bytes(ctypes_ref(prm), n), dtype=torch.uint8, device=dev)
         sigma = torch.empty(n * prm.n_samples, dtype=torch.float32, device=dev)

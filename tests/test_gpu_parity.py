@@ -64,7 +64,7 @@ def close(a, b, rtol, atol, what):
 
 def test_library_info(pnr_mod):
     lib = pnr_mod.library()
-    assert lib.pnr_abi_version() == 7
+    assert lib.pnr_abi_version() == 8
     assert lib.pnr_mlp_packed_floats() > 0
 
 
@@ -157,6 +157,28 @@ def test_tracking_ray_grads_golden(pnr_mod, dev, scene):
     for name, t, key in (('rays_o', ro, 'trk_grad_rays_o'), ('rays_d', rd, 'trk_grad_rays_d')):
         gref = G[key]
         close(t.grad, gref, 0, 5e-3 * np.abs(gref).max(), name)
+
+
+def test_masks_only_save_equals_full_save_ray_grads(pnr_mod, dev, scene):
+    """ABI 8 save_for_backward = 2 (decoder frozen: the Tracker's step): the forward keeps only the
+    ReLU masks and inputs, and the ray gradients equal those of a full-save forward whose decoder
+    gradients are requested too (same kernels on the same values: bit-identical)."""
+    G = load_golden('grads.npz')
+    r = make_renderer(pnr_mod, scene)
+    gt = torch.from_numpy(G['map_gt_depth']).to(dev)
+    out = {}
+    for frozen in (True, False):
+        dec = make_decoder(pnr_mod, golden_params('trained'), dev)
+        for p_ in dec.parameters():
+            p_.requires_grad_(not frozen)
+        ro = torch.from_numpy(G['map_rays_o']).to(dev).requires_grad_(True)
+        rd = torch.from_numpy(G['map_rays_d']).to(dev).requires_grad_(True)
+        d, v, c = r.render_batch_ray({}, dec, rd, ro, dev, 'color', gt_depth=gt)
+        (d.sum() + 0.5 * c.sum() + v.sum()).backward()
+        out[frozen] = (ro.grad.clone(), rd.grad.clone(), d.detach().clone())
+        assert all((p_.grad is None) == frozen for p_ in dec.parameters())
+    for a, b in zip(out[True], out[False]):
+        assert torch.equal(a, b)
 
 
 def test_render_img_golden(pnr_mod, dev, scene):
