@@ -331,6 +331,39 @@ def kernel_roofline(kt, prec, el_s, traffic_units=True):
                              if best['prec'] != 'bf16' else 'bf16 MFMA 2.5 PF dense')}
 
 
+def kernel_table(kt, prec, el_s, steps):
+    """Every timed MLP kernel family of the step on its MFMA roofline (algorithmic fp32-equivalent
+    FLOP / measured time; the split modes against 833 TF, fp32 against 157.3 TF), with the MFMA-busy
+    fraction of the newest committed rocprofv3 PMC pass (profiles/r*_mfma_busy_map.json)."""
+    import glob
+    busy = {}
+    files = sorted(glob.glob(os.path.join(REPO, 'profiles', 'r*_mfma_busy_map.json')))
+    if files:
+        for k, v in json.load(open(files[-1])).get('kernels', {}).items():
+            busy[k] = v.get('mfma_busy_frac')
+    peak = ALGO_PEAK_TF['fp32' if prec == 'fp32' else 'f16x3']
+    out = {}
+    for name, fl, kname in (('mlp_fwd', FLOP_PER_POINT_FWD, 'k_mlp_fwd16 (training, saves)'),
+                            ('mlp_bwd', FLOP_PER_POINT_BWD, 'k_mlp_bwd16 (delta chain)'),
+                            ('wgrad', 443430, 'k_wgrad16 + k_wgrad_skinny (all weight gradients)')):
+        if name not in kt:
+            continue
+        launches, ms, units = kt[name]
+        # wgrad units count each layer's launch over its K points: 6 launches per chunk
+        pts = units / 6 if name == 'wgrad' else units
+        tf = fl * pts / (ms * 1e-3) / 1e12
+        out[kname] = {'achieved_tf': round(tf, 1), 'peak_tf': round(peak, 1), 'frac': round(tf / peak, 4),
+                      'ms_per_step': round(ms / steps, 3),
+                      'share_of_step': round(ms / (el_s * 1e3), 3)}
+    pm = {'k_mlp_fwd16 (training, saves)': ('void pnr::k_mlp_fwd16<3, false, 1>', 'void pnr::k_mlp_fwd16<3, false, true>'),
+          'k_mlp_bwd16 (delta chain)': ('void pnr::k_mlp_bwd16<false>',)}
+    for k, names in pm.items():
+        for b in names:
+            if k in out and b in busy:
+                out[k]['mfma_busy_pmc'] = busy[b]
+    return out
+
+
 DTYPE = {'fp32': 'fp32 (fp32 MFMA forward, delta chain and weight gradients)',
          'f16x3': 'fp32-class f16x3 throughout: forward, delta chain (per-point power-of-two scaled) and weight-'
                   'gradient GEMMs (on fp32-stored operands) all split every operand into 2 f16 parts (22 '
@@ -547,6 +580,7 @@ def main():
                        'graph': bool(args.graph and args.workload == 'map'),
                        **({'point_features': args.feat_dtype} if args.workload == 'map-points' else {})},
             'roofline': roofline, 'cpu_baseline': cpu,
+            'kernel_rooflines': kernel_table(kt, prec, el, args.steps) if args.workload != 'fwd' else None,
             'kernels': {k: {'launches': v[0], 'ms': round(v[1], 3), 'units': v[2]} for k, v in kt.items()},
         }
         if cpu is not None:
