@@ -12,6 +12,13 @@
 `track_frame` is the per-frame loop of Tracker.run (:860-921): Adam on the camera tensor (or
 on T and quad separately, lr and 0.2 lr), keeping the minimum-loss candidate.
 
+Data parallel (`TrackStep(ddp=pnr.dist.DataParallel())`): every rank draws the
+same pixel set (weak depth: deterministic; random pixels: pass the same-seeded `generator` on every
+rank) and renders its contiguous shard of it; the batch-global far clamp is an all_reduce(MAX)
+read on the device, the dynamic-object median (handle_dynamic) runs over the all-gathered
+residuals, and the camera gradient and the loss are all_reduce(SUM)ed before the camera Adam
+step -- the loss is a sum over pixels, so every rank then takes the single-process step.
+
 The rays are built on the device by `pnr_rays_from_uv`.  `_RaysFromUV`
 carries the gradient to the 3x4 pose: dL/dR = g_dᵀ·dirs and dL/dt = Σ g_o, the exact adjoint
 of rays_d = Σ_c dirs_c R[:, c] and rays_o = t.  The decoder's parameters get no gradient:
@@ -23,6 +30,7 @@ import torch
 
 from . import _lib
 from .common import get_camera_from_tensor, select_uv_indices
+from .dist import shard_bounds
 
 
 class _RaysFromUV(torch.autograd.Function):
@@ -66,8 +74,10 @@ def rays_from_uv(i, j, c2w34, fx, fy, cx, cy):
 class TrackStep:
     def __init__(self, renderer, decoder, c=None, w_color_loss=0.5, use_color_in_tracking=True,
                  depth_supervision=True, handle_dynamic=False, weak_depth=True, ignore_edge_W=100,
-                 ignore_edge_H=100, generator=None):
+                 ignore_edge_H=100, generator=None, ddp=None):
         self.renderer = renderer
+        self.ddp = ddp if (ddp is not None and ddp.world > 1) else None
+        self.rays_fn = rays_from_uv  # (i, j, c2w34, fx, fy, cx, cy) -> rays_o, rays_d
         self.decoder = decoder
         self.c = {} if c is None else c
         self.w_color = w_color_loss
@@ -91,11 +101,28 @@ class TrackStep:
             idx = torch.nonzero(depth > 0.01).reshape(-1)
         else:
             idx = select_uv_indices(depth.numel(), n, depth.device, self.generator)
+        if self.ddp is not None:  # this rank's contiguous shard of the (identical) global pixel set
+            import torch.distributed as dist
+            a, b = shard_bounds(idx.numel(), dist.get_rank(self.ddp.group), self.ddp.world)
+            idx = idx[a:b]
         w = W1 - W0
         i = (idx % w + W0).float()
         j = (torch.div(idx, w, rounding_mode='floor') + H0).float()
-        ro, rd = rays_from_uv(i, j, c2w, r.fx, r.fy, r.cx, r.cy)
+        ro, rd = self.rays_fn(i, j, c2w, r.fx, r.fy, r.cx, r.cy)
         return ro, rd, depth[idx], color[idx]
+
+    def _global_median(self, t):
+        """torch.median over every rank's values (the lower median, as torch.median)."""
+        import torch.distributed as dist
+        n = torch.tensor([t.numel()], device=t.device, dtype=torch.int64)
+        ns = [torch.zeros_like(n) for _ in range(self.ddp.world)]
+        dist.all_gather(ns, n, group=self.ddp.group)
+        m = int(max(int(x) for x in ns))
+        buf = torch.zeros(m, device=t.device, dtype=t.dtype)
+        buf[:t.numel()] = t
+        outs = [torch.zeros_like(buf) for _ in range(self.ddp.world)]
+        dist.all_gather(outs, buf, group=self.ddp.group)
+        return torch.cat([o[:int(k)] for o, k in zip(outs, ns)]).median()
 
     def loss(self, camera_tensor, gt_color, gt_depth, batch_size):
         dec = self.decoder
@@ -108,14 +135,17 @@ class TrackStep:
         try:
             c2w = get_camera_from_tensor(camera_tensor)
             ro, rd, gd, gc = self.samples(c2w, gt_depth, gt_color, batch_size)
-            d, v, col = self.renderer.render_batch_ray(self.c, dec, rd, ro, rd.device, 'color', gt_depth=gd)
+            fc = self.ddp.global_far_clamp(gd) if self.ddp is not None else None
+            d, v, col = self.renderer.render_batch_ray(self.c, dec, rd, ro, rd.device, 'color', gt_depth=gd,
+                                                       far_clamp=fc)
         finally:
             for p, q in zip(frozen, req):
                 p.requires_grad_(q)
         v = v.detach()
         if self.handle_dynamic:
             tmp = torch.abs(gd - d) / torch.sqrt(v + 1e-10)
-            mask = (tmp < 10 * tmp.median()) & (gd > 0)
+            med = self._global_median(tmp.detach()) if self.ddp is not None else tmp.median()
+            mask = (tmp < 10 * med) & (gd > 0)
         else:
             mask = gd > 0
         if not self.depth_supervision:
@@ -129,9 +159,15 @@ class TrackStep:
         optimizer.zero_grad()
         loss = self.loss(camera_tensor, gt_color, gt_depth, batch_size)
         loss.backward()
+        if self.ddp is not None:  # the pixel-sum loss: summed camera gradients = the full-batch step
+            for grp in optimizer.param_groups:
+                for p in grp['params']:
+                    if p.grad is not None:
+                        self.ddp.allreduce_(p.grad)
+            loss = self.ddp.allreduce_(loss.detach().reshape(1).clone())
         optimizer.step()
         optimizer.zero_grad()
-        return loss.item()
+        return float(loss.reshape(-1)[0].item())
 
 
 def track_frame(step: TrackStep, camera_tensor, gt_color, gt_depth, iters, cam_lr, batch_size,

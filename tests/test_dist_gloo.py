@@ -160,3 +160,80 @@ def test_sharded_feature_update_equals_dense():
         p.join(timeout=60)
     assert all(ok for _, ok, _ in res), res
     assert [r[2] for r in res] == [(0, 1602), (1602, 3203)]
+
+
+class _OracleRenderer:
+    """CPU stand-in for pnr.Renderer in the data-parallel Tracker test: the oracle render of
+    src/utils/Renderer.py with the renderer's far_clamp extension (the sharding logic under test is
+    TrackStep's, not the HIP kernels')."""
+
+    def __init__(self, params, bound, H, W, fx, fy, cx, cy):
+        self.params, self.bound = params, bound
+        self.H, self.W, self.fx, self.fy, self.cx, self.cy = H, W, fx, fy, cx, cy
+
+    def render_batch_ray(self, c, decoders, rays_d, rays_o, device, stage, gt_depth=None, far_clamp=None):
+        from oracle import ref_render as ref
+        fc = None if far_clamp is None else float(far_clamp.reshape(-1)[0])
+        return ref.render_batch_ray(self.params, rays_d, rays_o, self.bound, gt_depth=gt_depth, far_clamp=fc)
+
+
+def _track_case(ddp, handle_dynamic):
+    """One TrackStep (optimize_cam_in_batch) on a synthetic 12x16 weak-depth frame; returns the
+    loss and the camera tensor after the Adam step."""
+    from oracle import ref_render as ref
+    from pnr.common import get_tensor_from_camera
+    from pnr.tracking import TrackStep
+    S = load_golden('scene.npz')
+    bound = torch.from_numpy(S['bound'])
+    g = torch.Generator().manual_seed(3)
+    H, W = 12, 16
+    depth = torch.rand((H, W), generator=g) * 0.5 + 0.3
+    depth[torch.rand((H, W), generator=g) < 0.2] = 0.0  # weak depth: these pixels are left out
+    color = torch.rand((H, W, 3), generator=g)
+    r = _OracleRenderer(golden_params('trained'), bound, H, W, 12., 12., 7.5, 5.5)
+    step = TrackStep(r, torch.nn.Module(), ignore_edge_W=0, ignore_edge_H=0, handle_dynamic=handle_dynamic,
+                     ddp=ddp)
+    step.rays_fn = lambda i, j, c2w, fx, fy, cx, cy: [t.reshape(-1, 3) for t in
+                                                      ref.rays_from_uv(i, j, c2w, fx, fy, cx, cy)]
+    cam = get_tensor_from_camera(torch.from_numpy(S['poses'][1]).float()).requires_grad_(True)
+    opt = torch.optim.Adam([cam], lr=1e-3)
+    loss = step(cam, color, depth, H * W, opt)
+    return loss, cam.detach().clone()
+
+
+def _track_worker(rank, world, port, q, handle_dynamic):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    sys.path.insert(0, REPO)
+    sys.path.insert(0, os.path.join(REPO, 'pointnerf-slam_amd'))
+    torch.set_num_threads(1)
+    from pnr import dist as pdist
+    pdist.init(backend='gloo')
+    loss, cam = _track_case(pdist.DataParallel(), handle_dynamic)
+    q.put((rank, loss, cam.numpy()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('handle_dynamic', [False, True])
+def test_dp_tracking_step_matches_single_process(handle_dynamic):
+    """TrackStep(ddp=DataParallel()) at world size 2 (pixel batches shard, the pose
+    gradient is all-reduced): each rank renders half of the weak-depth pixel set with the global
+    far clamp (and the global dynamic-object median); the all-reduced loss and the camera after
+    the Adam step equal the single-process step's."""
+    torch.set_num_threads(2)
+    loss1, cam1 = _track_case(None, handle_dynamic)
+    world = 2
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_track_worker, args=(r, world, port, q, handle_dynamic)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=300) for _ in range(world))
+    for p in ps:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    for _, loss, cam in res:
+        assert abs(loss - loss1) <= 1e-5 * abs(loss1)
+        np.testing.assert_allclose(cam, cam1.numpy(), rtol=0, atol=1e-7)
