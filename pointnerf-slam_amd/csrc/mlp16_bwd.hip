@@ -224,9 +224,14 @@ struct BfBwd {
   static __device__ __forceinline__ void conv2(const BwdArgs& a, St& S) {
     constexpr int li = 3 - CC;
     const uint32_t wd = t < 2 ? S.m[li].x : t < 4 ? S.m[li].y : t < 6 ? S.m[li].z : S.m[li].w;
+    // ReLU derivative: the bit sign-extended to an all-ones / zero word (v_bfe_i32) ANDed into the
+    // value -- 2 VALU per value where the bit test + compare + select took 3
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-      if (!((wd >> ((t & 1) * 16 + 4 * q + i)) & 1u)) S.v[4 * q + i] = 0.f;
+    for (int i = 0; i < 4; ++i) {
+      const int bit = (t & 1) * 16 + 4 * q + i;
+      const int m = (int)(wd << (31 - bit)) >> 31;
+      S.v[4 * q + i] = __int_as_float(__float_as_int(S.v[4 * q + i]) & m);
+    }
     // fp32 delta for the weight-gradient GEMMs (delta4 = chain 0's: not stored, kWgradOutDelta)
 #if !defined(PNR_EXP_NOSTORE)
     if constexpr (CC != 0)
