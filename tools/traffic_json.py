@@ -32,8 +32,9 @@ def per_launch(d):
 
 
 def family(name):
-    if 'k_mlp_fwd16<' in name:
-        return 'k_mlp_fwd16_train' if name.split('>')[0].endswith('true') else 'k_mlp_fwd16_eval'
+    if 'k_mlp_fwd16<' in name:  # last template argument: save mode (true / 1 training, 2 masks only)
+        sv = name.split('>')[0].split(',')[-1].strip()
+        return {'true': 'k_mlp_fwd16_train', '1': 'k_mlp_fwd16_train', '2': 'k_mlp_fwd16_masks'}.get(sv, 'k_mlp_fwd16_eval')
     if 'k_mlp_bwd16<' in name:
         return 'k_mlp_bwd16'
     if 'k_mlp_fwd<' in name and 'true' in name.split('>')[0]:
