@@ -135,8 +135,16 @@ class MapStep:
     def __call__(self, rays_o, rays_d, gt_depth, gt_color, t_rand=None):
         self.flat.zero_grad()
         far_clamp = self.ddp.global_far_clamp(gt_depth) if self.ddp is not None else None
-        loss = self.loss(rays_o, rays_d, gt_depth, gt_color, t_rand, far_clamp)
-        loss.backward()
+        # the render / regulation backwards add straight into the flat gradient buffer (renderer
+        # _direct): the parameters' .grad are views of it, zeroed just above
+        for p in self.flat.params:
+            p._pnr_direct = True
+        try:
+            loss = self.loss(rays_o, rays_d, gt_depth, gt_color, t_rand, far_clamp)
+            loss.backward()
+        finally:
+            for p in self.flat.params:
+                p._pnr_direct = False
         if self.ddp is not None and self.shard:
             self.ddp.allreduce_(self.flat.grad[:self.n_dec])
             self.ddp.reduce_scatter_(self.flat.grad[self.n_dec:])

@@ -90,11 +90,29 @@ class _Feat:
         if self.pts is None:
             return None, None, []
         base = 7 + _lib.N_PARAMS
-        g_fc = None
+        g_fc, out_fc = None, [None] * _lib.N_FC_PARAMS
         if any(needs[base:base + _lib.N_FC_PARAMS]):
-            g_fc = [torch.zeros(t.shape, device=dev, dtype=torch.float32) for t in self.fc]
-        g_feats = torch.zeros_like(self.pts.feats) if needs[base + _lib.N_FC_PARAMS] else None
-        return g_feats, g_fc, [*(g_fc or [None] * _lib.N_FC_PARAMS), g_feats]
+            if _direct(self.fc):  # MapStep: accumulate into the flat gradient buffer (see _direct)
+                g_fc = [t.grad for t in self.fc]
+            else:
+                g_fc = [torch.zeros(t.shape, device=dev, dtype=torch.float32) for t in self.fc]
+                out_fc = g_fc
+        g_feats, out_feats = None, None
+        if needs[base + _lib.N_FC_PARAMS]:
+            if _direct([self.pts.feats]):
+                g_feats = self.pts.feats.grad
+            else:
+                g_feats = out_feats = torch.zeros_like(self.pts.feats)
+        return g_feats, g_fc, [*out_fc, out_feats]
+
+
+def _direct(tensors):
+    """True while a MapStep accumulates straight into these tensors' .grad (views of its flat
+    gradient buffer, zeroed at the step's start): the kernels then add into them and autograd
+    gets None -- no per-call zeroed buffers and no autograd accumulation kernels (22 fills and
+    22 adds of a mapping iteration, a sixth of its launches at the faithful N = 1,000)."""
+    return len(tensors) > 0 and all(getattr(t, '_pnr_direct', False) and t.grad is not None and
+                                    t.grad.is_contiguous() for t in tensors)
 
 
 def _param_grads(ctx, dev):
@@ -103,6 +121,8 @@ def _param_grads(ctx, dev):
     launch).  The decoder tensors are autograd inputs 7..17 of both Functions."""
     if not any(ctx.needs_input_grad[7:7 + _lib.N_PARAMS]):
         return [None] * _lib.N_PARAMS, None
+    if _direct(ctx.feat.params):
+        return [None] * _lib.N_PARAMS, _lib.PtrArray(*[p.grad.data_ptr() for p in ctx.feat.params])
     grads = [torch.zeros(s, device=dev, dtype=torch.float32) for s in _GRAD_SHAPES]
     return grads, _lib.PtrArray(*[g.data_ptr() for g in grads])
 
