@@ -180,6 +180,8 @@ struct BwdWS {
   float* gargP;   // [C][96]
   float* gH;      // [4][C][256]  features only: dL/dh_l
   float* g_c;     // [P][32]      features only: dL/dc
+  float* part;    // weight-gradient partial tiles (wgrad16.hip two-phase flush)
+  float* part_bias;
   void* gws;      // features only: gather-backward work list
   size_t gws_bytes;
   int64_t C;
@@ -195,6 +197,8 @@ BwdWS carve_bwd(int64_t P, int64_t n, void* ws, size_t* bytes, bool feat = false
   b.g_nrm = c.take<float>(n);
   b.dP = c.take<float>((size_t)4 * kHidden * b.C);
   b.gargP = c.take<float>(kFourierPad * b.C);
+  b.part = c.take<float>(kWgradPartFloats);
+  b.part_bias = c.take<float>(kWgradPartBiasFloats);
   if (feat) {
     b.gH = c.take<float>((size_t)4 * kHidden * b.C);
     b.g_c = c.take<float>((size_t)P * kCDim);
@@ -249,12 +253,12 @@ int mlp_backward_core(int prec, const float* packed, const SaveArgs& sv, int64_t
       // hidden layers: dW_l += delta_{l+1}^T h_l  (W3: delta4.h3, W2: delta3.h2, W1: delta2.h1); delta4
       // is not stored by k_mlp_bwd16 (rank 4: rebuilt from g_out and the h4 masks inside the GEMM)
       const WgradSyn syn{reinterpret_cast<const float4*>(b.g_out + p0 * 4), sv.masks + 3 * (sv.ld / 32) * 64, p0 / 32,
-                         packed + packed_raw_wo_offset(), sv.xP + p0, packed + kOffFB};
+                         packed + packed_raw_wo_offset(), sv.xP + p0, packed + kOffFB, b.part, b.part_bias};
       if (rc == 0)
         rc = launch_wgrad16(kWgradOutDelta, nullptr, hp + 2 * hstride, C, C, grads[7], kHidden, grads[8], st, &syn);
       for (int l = 2; l >= 1 && rc == 0; --l)
         rc = launch_wgrad16(kWgradHidden, b.dP + l * dstride, hp + (l - 1) * hstride, C, C, grads[1 + 2 * l],
-                            kHidden, grads[2 + 2 * l], st);
+                            kHidden, grads[2 + 2 * l], st, &syn);
       // first layer: dW0 (256x93) += delta1^T e ; db0 -- e = sin(x@B) recomputed from the saved x
       // (k_mlp_fwd16 saves no e)
       if (rc == 0) rc = launch_wgrad16(kWgradFirstX, b.dP, nullptr, C, C, grads[1], kFourier, grads[2], st, &syn);
@@ -278,9 +282,12 @@ int mlp_backward_core(int prec, const float* packed, const SaveArgs& sv, int64_t
     if (rc) return rc;
     // feature branch: dWc_l (256x32) += (dL/dh_l)^T c ; dbc_l += colsum(dL/dh_l)
     if (fb && fb->g_fc && split) {  // f16x3 GEMMs: dL/dh from k_mlp_bwd16, the fp32 features
+      WgradSyn fsyn{};
+      fsyn.part = b.part;
+      fsyn.part_bias = b.part_bias;
       for (int l = 0; l < 4 && rc == 0; ++l)
         rc = launch_wgrad16(kWgradFc, b.gH + l * dstride, fb->c + p0 * kCDim, C, C, fb->g_fc[2 * l], kCDim,
-                            fb->g_fc[2 * l + 1], st);
+                            fb->g_fc[2 * l + 1], st, &fsyn);
     } else if (fb && fb->g_fc) {
       for (int l = 0; l < 4 && rc == 0; ++l)
         rc = launch_wgrad(kWgradFc, b.gH + l * dstride, kHidden, fb->c + p0 * kCDim, kCDim, C, fb->g_fc[2 * l], kCDim,

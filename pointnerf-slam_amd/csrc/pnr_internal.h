@@ -239,7 +239,14 @@ struct WgradSyn {
   const float* wo;      // Wo [4][256] fp32
   const float4* xP;     // kWgradFirstX: saved inputs of the chunk rows
   const float* fb;      // kWgradFirstX: Fourier B padded [3][96] (packed + kOffFB)
+  // every split kind: per-workgroup partial tiles instead of float atomics, then one reduce launch
+  // (kWgradPartFloats + kWgradPartBiasFloats of scratch; NULL = atomics)
+  float* part;
+  float* part_bias;
 };
+constexpr int kWgradMaxWg = 256;
+constexpr int64_t kWgradPartFloats = (int64_t)kWgradMaxWg * 256 * 256;
+constexpr int64_t kWgradPartBiasFloats = (int64_t)kWgradMaxWg * 256;
 int launch_wgrad(int kind, const float* A, int ma, const float* B, int nb, int64_t K, float* C, int64_t ldc,
                  float* bias, hipStream_t st);
 // split precisions (wgrad16.hip): kWgradHidden / kWgradFirst / kWgradFc as f16x3 GEMMs on fp32

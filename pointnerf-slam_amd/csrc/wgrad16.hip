@@ -72,6 +72,8 @@ struct WxArgs {
   // the forward's own arithmetic (bit-identical e)
   const float4* xP;      // [K] saved MLP inputs (x0, x1, x2, inside), chunk rows
   const float* fb;       // Fourier B padded [3][96]
+  float* part;           // non-null: [grid][256][NTB 32] partial tiles + part_bias [grid][256]
+  float* part_bias;      //   (plain stores; k_wgrad_reduce sums them into C / bias)
 };
 
 template <int NTB, int WB>
@@ -265,6 +267,19 @@ __global__ __launch_bounds__(512, 1) void k_wgrad16(WxArgs a) {
       }
   }
   const float inv = 1.f / sc;
+  if (a.part) {
+    // two-phase flush: this workgroup's tile with plain stores (each instruction two 128-B row
+    // segments), summed by k_wgrad_reduce.  Float atomics run at one 256-B wave-instruction per
+    // ~50 ns per CU: a 256 x 256 tile took ~51 us per workgroup, the whole launch at small K.
+    float* P = a.part + (int64_t)blockIdx.x * 256 * (NTB * 32);
+#pragma unroll
+    for (int y = 0; y < NTB; ++y)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) P[(32 * w + perm(r, hh)) * (NTB * 32) + 32 * y + (lane & 31)] = acc[y][r] * inv;
+    cs += __shfl_xor(cs, 32);
+    if (a.bias && hh == 0) a.part_bias[(int64_t)blockIdx.x * 256 + 32 * w + lane] = cs;
+    return;
+  }
   // C[32w + perm(r,hh)][32y + (lane&31)] += acc / sc
 #pragma unroll
   for (int y = 0; y < NTB; ++y) {
@@ -277,6 +292,27 @@ __global__ __launch_bounds__(512, 1) void k_wgrad16(WxArgs a) {
   if (a.bias && hh == 0) atomicAdd(a.bias + 32 * w + lane, cs);
 }
 
+// C[row][col] += sum over the grid's partial tiles (col < nb), bias[row] += sum of the partial
+// bias rows; one thread per output element, the partials read coalesced
+__global__ __launch_bounds__(256) void k_wgrad_reduce(const float* __restrict__ part, const float* __restrict__ pbias,
+                                                      int nwg, int wb, int nb, float* __restrict__ C, int64_t ldc,
+                                                      float* __restrict__ bias) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  const int row = i / wb, col = i % wb;
+  if (i < 256 * wb && col < nb) {
+    float s = 0.f;
+#pragma unroll 8
+    for (int k = 0; k < nwg; ++k) s += part[(int64_t)k * 256 * wb + i];
+    C[(int64_t)row * ldc + col] += s;
+  }
+  if (bias && i < 256) {
+    float s = 0.f;
+#pragma unroll 8
+    for (int k = 0; k < nwg; ++k) s += pbias[(int64_t)k * 256 + i];
+    bias[i] += s;
+  }
+}
+
 template <int NTB, int WB, bool SYN = false, bool FOUR = false>
 static int launch_k(const WxArgs& a, hipStream_t st) {
   using Cfg = Wx3<NTB, WB>;
@@ -284,7 +320,11 @@ static int launch_k(const WxArgs& a, hipStream_t st) {
   static const bool attr = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                                                Cfg::kLds) == hipSuccess;
   if (!attr) return PNR_E_ARG;
-  hipLaunchKernelGGL(kern, dim3((unsigned)((a.K + a.ks - 1) / a.ks)), dim3(Cfg::kThreads), Cfg::kLds, st, a);
+  const int nwg = (int)((a.K + a.ks - 1) / a.ks);
+  hipLaunchKernelGGL(kern, dim3((unsigned)nwg), dim3(Cfg::kThreads), Cfg::kLds, st, a);
+  if (a.part)
+    hipLaunchKernelGGL(k_wgrad_reduce, dim3((unsigned)((256 * NTB * 32 + 255) / 256)), dim3(256), 0, st, a.part,
+                       a.part_bias, nwg, NTB * 32, a.nb, a.C, a.ldc, a.bias);
   return hip_status(hipGetLastError());
 }
 
@@ -295,14 +335,18 @@ int launch_wgrad16(int kind, const float* A, const float* B, int64_t K, int64_t 
   if (K <= 0) return 0;
   if (kb_rows <= 0) return PNR_E_ARG;
   K = (K + 31) / 32 * 32;
-  // split-K: each workgroup flushes its whole C tile (256 KB of float atomics for a hidden layer,
-  // ~0.2 us of the chip's atomic rate) and spends ~1 us per 32-point tile, so the time
-  // (K / 32 / n) + n * 0.2 is least at n = sqrt(5 K / 32); at most one workgroup per CU
+  // split-K over at most one workgroup per CU.  Atomic flush (no partials buffer): each workgroup
+  // adds its whole C tile (256 KB of float atomics for a hidden layer) and spends ~1 us per
+  // 32-point tile, n = sqrt(5 K / 32).  Two-phase flush (the backward's scratch): plain stores of
+  // the tile + k_wgrad_reduce, >= 8 tiles per workgroup
+  const bool two_phase = syn && syn->part && syn->part_bias;
   int64_t nwg = (int64_t)sqrt(5.0 * (double)K / 32.0);
-  nwg = nwg < 4 ? 4 : (nwg > 256 ? 256 : nwg);
+  if (two_phase) nwg = (K / 32 + 7) / 8;  // >= 8 tiles per workgroup: the flush no longer dominates
+  nwg = nwg < 4 ? 4 : (nwg > kWgradMaxWg ? kWgradMaxWg : nwg);
   int64_t ks = (K + nwg - 1) / nwg;
   ks = (ks + 31) / 32 * 32;
-  WxArgs a{A, B, 256, K, kb_rows, ks, C, ldc, bias, nullptr, nullptr, 0, nullptr, nullptr, nullptr};
+  WxArgs a{A, B, 256, K, kb_rows, ks, C, ldc, bias, nullptr, nullptr, 0, nullptr, nullptr, nullptr,
+           two_phase ? syn->part : nullptr, two_phase ? syn->part_bias : nullptr};
   TimingScope ts(kTimeWgrad, K, st);
   if (kind == kWgradHidden) return launch_k<8, 256>(a, st);
   if (kind == kWgradOutDelta) {  // dW3 += delta4^T h3, delta4 rebuilt from g_out and the h4 masks
