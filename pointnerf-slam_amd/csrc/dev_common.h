@@ -64,7 +64,11 @@ __device__ __forceinline__ void stage(const float*& sp, float* dst, int nfloats)
 // reading the buffer that the next stage() overwrites.
 template <int N>
 __device__ __forceinline__ void sync_chunk() {
+#if defined(PNR_EXP_NOWAIT)  // experiment: barrier without the DMA wait (races on LDS: timing only)
+  asm volatile("s_barrier" ::: "memory");
+#else
   asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
+#endif
 }
 
 // sin / cos for the Fourier features of the split-precision kernels (decoder.py:26-30).  OCML's
