@@ -69,6 +69,18 @@ struct BwdGeo {
     return clamp_t(t > sync_t(g) ? t : sync_t(g), g);
   }
   __host__ __device__ static constexpr bool bnd(int g) { return bwd_conv(g) && bwd_conv_tile(g) == 0; }
+  // group of a step with nt groups in which conversion piece q runs: phase 1 (conv1) and phase 2
+  // (conv2, the delta store).  Without the feature branch the phases alternate (stores in every
+  // other group: the save stream is spread over the step); with it phase 1 must finish by the
+  // feature-branch product in group 5, so the phases run in groups 0-3 and 4-7
+  __host__ __device__ static constexpr int grp1(int q, int shift, int n) {
+    const int t = HASC ? q + shift : 2 * q + shift;
+    return t < n - 1 ? t : n - 1;
+  }
+  __host__ __device__ static constexpr int grp2(int q, int shift, int n) {
+    const int t = HASC ? 4 + q : 2 * q + 1 + shift;
+    return t < n - 1 ? t : n - 1;
+  }
   // delta (+ dL/dh) quad stores issued in group T of step g (conv_pieces placement)
   __host__ __device__ static constexpr int stores_grp(int g, int T) {
 #if defined(PNR_EXP_NOSTORE)
@@ -79,7 +91,7 @@ struct BwdGeo {
     int n = 0;
     // conv2 stores no delta4 (chain 0: kWgradOutDelta rebuilds it); conv1's dL/dh (features) stays
     const bool d = bwd_conv_chain(g) != 0;
-    for (int q = 0; q < 4; ++q) n += (HASC && clamp_t(q, g) == T ? 1 : 0) + (d && clamp_t(4 + q, g) == T ? 1 : 0);
+    for (int q = 0; q < 4; ++q) n += (HASC && grp1(q, 0, nt(g)) == T ? 1 : 0) + (d && grp2(q, 0, nt(g)) == T ? 1 : 0);
     return n;
   }
   __host__ __device__ static constexpr int stores_rng(int g, int t0, int t1) {
@@ -246,19 +258,24 @@ struct BfBwd {
   static __device__ __forceinline__ void conv_pieces(const BwdArgs& a, St& S, const Frag<PR>& FC) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const int t1 = (q + SHIFT) < NT - 1 ? (q + SHIFT) : NT - 1;
-      if (t1 == T) {
+      if (G::grp1(q, SHIFT, NT) == T) {
         if (q == 0) conv1<CC, t, 0>(a, S);
         if (q == 1) conv1<CC, t, 1>(a, S);
         if (q == 2) conv1<CC, t, 2>(a, S);
         if (q == 3) conv1<CC, t, 3>(a, S);
       }
+      if (!HASC && G::grp2(q, SHIFT, NT) == T) {  // alternating phases: piece q's phase 2 right after
+        if (q == 0) conv2<CC, t, 0>(a, S);
+        if (q == 1) conv2<CC, t, 1>(a, S);
+        if (q == 2) conv2<CC, t, 2>(a, S);
+        if (q == 3) conv2<CC, t, 3>(a, S);
+      }
     }
     if constexpr (HASC && T == (5 < NT - 1 ? 5 : NT - 1)) mfma_frag<PR, false>(FC, S.tmp, S.gc);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const int t2 = (4 + q) < NT - 1 ? (4 + q) : NT - 1;
-      if (t2 == T) {
+      const int t2 = G::grp2(q, SHIFT, NT);
+      if (HASC && t2 == T) {
         if (q == 0) conv2<CC, t, 0>(a, S);
         if (q == 1) conv2<CC, t, 1>(a, S);
         if (q == 2) conv2<CC, t, 2>(a, S);
