@@ -280,6 +280,20 @@ struct BfFwd {
   using G = BfGeo<NP, HASC, SV != 0>;
   using V8 = typename Prec<PR>::V8;
   static constexpr int kRing = (HASC && SAVE) ? 3 : 4, kPf = kRing - 1;
+  // group of a step with nt groups that runs epilogue piece q: phase 1 (conv1) and phase 2 (conv2,
+  // the activation save).  The training kernel without the feature branch alternates the phases,
+  // one save every other MFMA group (the save stream spread over the step, as in k_mlp_bwd16);
+  // otherwise phase 1 runs in groups SHIFT..3+SHIFT and phase 2 in 4..7 (the feature branch's
+  // product lands in group 3)
+  static constexpr bool ALT = !HASC && SAVEH;
+  __host__ __device__ static constexpr int grp1(int q, int shift, int n) {
+    const int t = ALT ? 2 * q + shift : q + shift;
+    return t < n - 1 ? t : n - 1;
+  }
+  __host__ __device__ static constexpr int grp2(int q, int shift, int n) {
+    const int t = ALT ? 2 * q + 1 + shift : 4 + q;
+    return t < n - 1 ? t : n - 1;
+  }
   using St = BfState<PR, kRing>;
   // Persistent kernels (no feature branch): a workgroup loops over 128-point tiles and the weight
   // stream runs on across tiles -- the last steps of tile i prefetch the first steps of tile i+1
@@ -388,8 +402,7 @@ struct BfFwd {
   static __device__ __forceinline__ void conv_pieces(const BfFwdArgs& a, St& S, const char* lds) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const int t1 = (q + SHIFT) < NT - 1 ? (q + SHIFT) : NT - 1;
-      if (t1 == T) {
+      if (grp1(q, SHIFT, NT) == T) {
         if (q == 0) conv1<L, t, 0>(a, S, S.acc[SET][t], lds);
         if (q == 1) conv1<L, t, 1>(a, S, S.acc[SET][t], lds);
         if (q == 2) conv1<L, t, 2>(a, S, S.acc[SET][t], lds);
@@ -398,8 +411,7 @@ struct BfFwd {
     }
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const int t2 = (4 + q) < NT - 1 ? (4 + q) : NT - 1;
-      if (t2 == T) {
+      if (grp2(q, SHIFT, NT) == T) {
         if (q == 0) conv2<L, t, 0>(a, S, lds);
         if (q == 1) conv2<L, t, 1>(a, S, lds);
         if (q == 2) conv2<L, t, 2>(a, S, lds);
@@ -435,9 +447,9 @@ struct BfFwd {
     int n = 0;
 #if !defined(PNR_EXP_NOSTORE)
     if (SAVEH)
-      for (int q = 0; q < 4; ++q) n += clamp_t(4 + q, g) == T ? 1 : 0;
+      for (int q = 0; q < 4; ++q) n += grp2(q, shift(g), nt(g)) == T ? 1 : 0;
 #endif
-    if (fwd_ct(g) == 7 && clamp_t(3 + shift(g), g) == T) ++n;
+    if (fwd_ct(g) == 7 && grp1(3, shift(g), nt(g)) == T) ++n;  // the mask words (conv1, tile 7, q 3)
     return n;
   }
   __host__ __device__ static constexpr int stores_rng(int g, int t0, int t1) {  // groups [t0, t1]
