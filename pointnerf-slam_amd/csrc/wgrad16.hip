@@ -293,23 +293,27 @@ __global__ __launch_bounds__(512, 1) void k_wgrad16(WxArgs a) {
 }
 
 // C[row][col] += sum over the grid's partial tiles (col < nb), bias[row] += sum of the partial
-// bias rows; one thread per output element, the partials read coalesced
+// bias rows; one thread per output element and slice of the partials (blockIdx.y: kReduceSlices
+// slices, so a thread chains at most nwg / kReduceSlices dependent loads), the partials read
+// coalesced, each slice's sum added with one float atomic per element
+constexpr int kReduceSlices = 8;
 __global__ __launch_bounds__(256) void k_wgrad_reduce(const float* __restrict__ part, const float* __restrict__ pbias,
                                                       int nwg, int wb, int nb, float* __restrict__ C, int64_t ldc,
                                                       float* __restrict__ bias) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   const int row = i / wb, col = i % wb;
-  if (i < 256 * wb && col < nb) {
+  const int k0 = (int)((int64_t)nwg * blockIdx.y / gridDim.y), k1 = (int)((int64_t)nwg * (blockIdx.y + 1) / gridDim.y);
+  if (i < 256 * wb && col < nb && k1 > k0) {
     float s = 0.f;
 #pragma unroll 8
-    for (int k = 0; k < nwg; ++k) s += part[(int64_t)k * 256 * wb + i];
-    C[(int64_t)row * ldc + col] += s;
+    for (int k = k0; k < k1; ++k) s += part[(int64_t)k * 256 * wb + i];
+    atomicAdd(C + (int64_t)row * ldc + col, s);
   }
-  if (bias && i < 256) {
+  if (bias && i < 256 && k1 > k0) {
     float s = 0.f;
 #pragma unroll 8
-    for (int k = 0; k < nwg; ++k) s += pbias[(int64_t)k * 256 + i];
-    bias[i] += s;
+    for (int k = k0; k < k1; ++k) s += pbias[(int64_t)k * 256 + i];
+    atomicAdd(bias + i, s);
   }
 }
 
@@ -323,8 +327,9 @@ static int launch_k(const WxArgs& a, hipStream_t st) {
   const int nwg = (int)((a.K + a.ks - 1) / a.ks);
   hipLaunchKernelGGL(kern, dim3((unsigned)nwg), dim3(Cfg::kThreads), Cfg::kLds, st, a);
   if (a.part)
-    hipLaunchKernelGGL(k_wgrad_reduce, dim3((unsigned)((256 * NTB * 32 + 255) / 256)), dim3(256), 0, st, a.part,
-                       a.part_bias, nwg, NTB * 32, a.nb, a.C, a.ldc, a.bias);
+    hipLaunchKernelGGL(k_wgrad_reduce,
+                       dim3((unsigned)((256 * NTB * 32 + 255) / 256), (unsigned)(nwg < kReduceSlices ? nwg : kReduceSlices)),
+                       dim3(256), 0, st, a.part, a.part_bias, nwg, NTB * 32, a.nb, a.C, a.ldc, a.bias);
   return hip_status(hipGetLastError());
 }
 
