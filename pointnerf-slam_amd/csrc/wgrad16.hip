@@ -80,7 +80,7 @@ template <int NTB, int WB>
 struct WxRegs {
   float a[16];                                 // A element (k-step s, j) -> a[8s + j]  (SYN: mask words)
   float4 b[Wx3<NTB, WB>::kBPer];               // FOUR: the B row's point x (the values come in stage)
-  float4 go;                                   // SYN: g_out row k0 + tid (threads < 32)
+  float4 go;                                   // SYN: g_out row k0 + 32 + tid (threads < 32): the NEXT tile's
 };
 
 template <int NTB, int WB, bool SYN, bool FOUR>
@@ -97,7 +97,10 @@ __device__ __forceinline__ void wx_load(const WxArgs& a, int64_t k0, WxRegs<NTB,
     for (int s = 0; s < 2; ++s)
 #pragma unroll
       for (int j = 0; j < 8; ++j) R.a[8 * s + j] = __uint_as_float(mw[(8 * (lane >> 5) + 16 * s + j) * 4]);
-    if (tid < 32) R.go = a.g_out[k0 + tid];
+    if (tid < 32) {  // one tile ahead (staged into the other slot, read after the next barrier)
+      const int64_t row = k0 + 32 + tid;
+      R.go = a.g_out[row < a.K ? row : a.K - 1];
+    }
   } else {
     const float* Ab = a.A + (k0 + 8 * (lane >> 5)) * 256 + 32 * wave_id() + (lane & 31);
 #pragma unroll
@@ -117,12 +120,13 @@ __device__ __forceinline__ void wx_load(const WxArgs& a, int64_t k0, WxRegs<NTB,
   }
 }
 
-// B tile -> hi / lo f16 planes of `slot` (SYN: + the tile's g_out rows after them)
+// B tile -> hi / lo f16 planes of `slot` (SYN: + the next tile's g_out rows into the other slot)
 template <int NTB, int WB, bool SYN, bool FOUR>
-__device__ __forceinline__ void wx_stage_b(const WxRegs<NTB, WB>& R, char* slot, const float (&fbr)[Wx3<NTB, WB>::kBPer][3][4]) {
+__device__ __forceinline__ void wx_stage_b(const WxRegs<NTB, WB>& R, char* slot, char* next_slot,
+                                           const float (&fbr)[Wx3<NTB, WB>::kBPer][3][4]) {
   using Cfg = Wx3<NTB, WB>;
   const int tid = threadIdx.x;
-  if (SYN && tid < 32) reinterpret_cast<float4*>(slot + 2 * Cfg::kPlane)[tid] = R.go;
+  if (SYN && tid < 32) reinterpret_cast<float4*>(next_slot + 2 * Cfg::kPlane)[tid] = R.go;
 #pragma unroll
   for (int i = 0; i < Cfg::kBPer; ++i) {
     const int q = tid + Cfg::kThreads * i;
@@ -206,12 +210,18 @@ __global__ __launch_bounds__(512, 1) void k_wgrad16(WxArgs a) {
       for (int e = 0; e < 4; ++e)
         fbr[i][d][e] = FOUR ? a.fb[d * kFourierPad + 4 * ((threadIdx.x + Cfg::kThreads * i) % Cfg::kC4) + e] : 0.f;
   if (ntile > 0) wx_load<NTB, WB, SYN, FOUR>(a, kb, R);
+  if (SYN && ntile > 0) {  // the first tile's g_out rows; later tiles' are staged one tile ahead
+    if (threadIdx.x < 32) reinterpret_cast<float4*>(lds + 2 * Cfg::kPlane)[threadIdx.x] = a.g_out[kb + threadIdx.x];
+    __syncthreads();
+  }
   for (int64_t t = 0; t < ntile; ++t) {
     char* slot = lds + (t & 1) * Cfg::kSlot;
-    wx_stage_b<NTB, WB, SYN, FOUR>(R, slot, fbr);
+    // g_out rows of tile t + 1 go to the other slot: their last reader (synth of tile t - 1) ran
+    // before the previous barrier
+    wx_stage_b<NTB, WB, SYN, FOUR>(R, slot, lds + ((t + 1) & 1) * Cfg::kSlot, fbr);
     if constexpr (SYN) {
-      // delta4 = (Wo^T g_out) masked, fp32 FMAs (the tile's g_out rows from LDS, broadcast reads)
-      __syncthreads();
+      // delta4 = (Wo^T g_out) masked, fp32 FMAs (the tile's g_out rows from LDS, staged before the
+      // previous barrier; broadcast reads)
       const float4* go = reinterpret_cast<const float4*>(slot + 2 * Cfg::kPlane) + 8 * hh;
 #pragma unroll
       for (int s = 0; s < 2; ++s)
