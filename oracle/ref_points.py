@@ -149,6 +149,24 @@ def mlp_forward_c(params: Params, p: torch.Tensor, c: torch.Tensor) -> torch.Ten
     return F.linear(h, params['output_linear.weight'], params['output_linear.bias'])
 
 
+def mlp_forward_c_cr(params: Params, p: torch.Tensor, c: torch.Tensor) -> torch.Tensor:
+    """mlp_forward_c with every hidden, fc_c and output GEMM CORRECTLY ROUNDED (float64 sums, each
+    layer's output rounded to float32; in the backward each layer's input gradient, and dL/dc =
+    sum_l Wc_l^T dL/dh_l, rounded likewise).  The yardstick for fp32-class feature-branch gradients
+    (tests/golden/make_grads_cr.py), like ref_render.mlp_forward_cr for the c_dim = 0 decoder."""
+    from .ref_render import _RoundF32
+    x = p.reshape(-1, 3).float()
+    h = torch.sin(x @ params['embedder._B'])
+    cd = c.double()
+    for li in range(N_LAYERS):
+        a = F.relu(F.linear(h.double(), params[f'pts_linears.{li}.weight'].double(),
+                            params[f'pts_linears.{li}.bias'].double()))
+        a = a + F.linear(cd, params[f'fc_c.{li}.weight'].double(), params[f'fc_c.{li}.bias'].double())
+        h = _RoundF32.apply(a)
+    return _RoundF32.apply(F.linear(h.double(), params['output_linear.weight'].double(),
+                                    params['output_linear.bias'].double()))
+
+
 def eval_points_c(params: Params, p: torch.Tensor, bound: torch.Tensor, points: dict) -> torch.Tensor:
     """src/utils/Renderer.py:23-61 with the neural-point features: raw (P,4) f32, density := 100
     outside the bound.  `points` = dict(xyz, feats, mode, radius, spacing, k, eps)."""

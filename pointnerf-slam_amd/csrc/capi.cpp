@@ -9,8 +9,8 @@
 // output, so the fine pass gathers them from the coarse results through the sort order.
 //
 // Backward: compositing backward -> per point dL/draw -> (chunks of <= kBwdChunk points)
-// delta chain kernel (mlp.hip) -> split-K weight-gradient MFMA GEMMs (wgrad.hip, atomically
-// accumulated) -> optional ray gradients.
+// delta chain kernel (mlp.hip) -> split-K weight-gradient MFMA GEMMs (wgrad.hip / wgrad16.hip,
+// per-workgroup partial tiles summed in a fixed order: deterministic) -> optional ray gradients.
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -135,12 +135,13 @@ int save_mode(const pnr_render_params* prm) {
   return (prm->save_for_backward == 2 && prm->precision == PNR_PREC_F16X3) ? 2 : 1;
 }
 
-SaveArgs carve_save(Carver& c, int64_t ld, bool acts = true) {
+SaveArgs carve_save(Carver& c, int64_t ld, int prec, bool acts = true) {
   SaveArgs s{};
   s.ld = ld;
   s.p0 = 0;
-  // mode 2: hP = eP = NULL, which tells the split forward to store masks and inputs only
-  s.eP = acts ? c.take<float>(kFourierPad * ld) : nullptr;
+  // mode 2: hP = eP = NULL, which tells the split forward to store masks and inputs only; e is saved
+  // by the fp32 forward only (the split dW0 GEMM recomputes it from x)
+  s.eP = acts && prec == PNR_PREC_FP32 ? c.take<float>(kFourierPad * ld) : nullptr;
   s.hP = acts ? c.take<float>((size_t)4 * kHidden * ld) : nullptr;
   s.xP = c.take<float4>(ld);
   s.masks = c.take<uint4>((size_t)4 * (ld / 32) * 64);
@@ -158,7 +159,7 @@ RenderWS carve_render(const pnr_render_params* prm, int64_t n, void* ws, size_t*
   w.far = c.take<double>(n);
   w.pc_pad = pad128(n * prm->n_samples);
   w.ld = w.pc_pad + pad128(n * prm->n_importance);
-  if (prm->save_for_backward) w.save = carve_save(c, w.ld, save_mode(prm) == 1);
+  if (prm->save_for_backward) w.save = carve_save(c, w.ld, prm->precision, save_mode(prm) == 1);
   if (prm->points) {
     w.c = c.take<float>((size_t)w.ld * kCDim);
     w.nidx = c.take<int32_t>((size_t)w.ld * prm->points->k);
@@ -187,7 +188,8 @@ struct BwdWS {
   int64_t C;
 };
 
-BwdWS carve_bwd(int64_t P, int64_t n, void* ws, size_t* bytes, bool feat = false) {
+// wgrad: weight gradients may be asked for (the partial tiles of the weight-gradient GEMMs)
+BwdWS carve_bwd(int64_t P, int64_t n, void* ws, size_t* bytes, bool feat, bool wgrad) {
   Carver c(ws);
   BwdWS b{};
   b.C = P < kBwdChunk ? ((P + 127) / 128) * 128 : kBwdChunk;
@@ -197,8 +199,10 @@ BwdWS carve_bwd(int64_t P, int64_t n, void* ws, size_t* bytes, bool feat = false
   b.g_nrm = c.take<float>(n);
   b.dP = c.take<float>((size_t)4 * kHidden * b.C);
   b.gargP = c.take<float>(kFourierPad * b.C);
-  b.part = c.take<float>(kWgradPartFloats);
-  b.part_bias = c.take<float>(kWgradPartBiasFloats);
+  if (wgrad) {
+    b.part = c.take<float>(kWgradPartFloats);
+    b.part_bias = c.take<float>(kWgradPartBiasFloats);
+  }
   if (feat) {
     b.gH = c.take<float>((size_t)4 * kHidden * b.C);
     b.g_c = c.take<float>((size_t)P * kCDim);
@@ -249,7 +253,7 @@ int mlp_backward_core(int prec, const float* packed, const SaveArgs& sv, int64_t
     } else if (split) {  // f16x3 GEMMs on the fp32 saves (h / e by k_mlp_fwd16, deltas by k_mlp_bwd16)
       const float* hp = sv.hP + p0 * kHidden;
       // output layer: dWo (4x256) += g_out^T h4 ; dbo += colsum(g_out)
-      rc = launch_wgrad_out16(b.g_out + p0 * 4, hp + 3 * hstride, C, grads[9], grads[10], st);
+      rc = launch_wgrad_out16(b.g_out + p0 * 4, hp + 3 * hstride, C, grads[9], grads[10], b.part, b.part_bias, st);
       // hidden layers: dW_l += delta_{l+1}^T h_l  (W3: delta4.h3, W2: delta3.h2, W1: delta2.h1); delta4
       // is not stored by k_mlp_bwd16 (rank 4: rebuilt from g_out and the h4 masks inside the GEMM)
       const WgradSyn syn{reinterpret_cast<const float4*>(b.g_out + p0 * 4), sv.masks + 3 * (sv.ld / 32) * 64, p0 / 32,
@@ -265,20 +269,20 @@ int mlp_backward_core(int prec, const float* packed, const SaveArgs& sv, int64_t
     } else {
       const float* hp = sv.hP + p0 * kHidden;
       rc = launch_wgrad(kWgradOut, b.g_out + p0 * 4, 4, hp + 3 * hstride, kHidden, C, grads[9], kHidden, grads[10],
-                        st);
+                        b.part, b.part_bias, st);
       for (int l = 3; l >= 1 && rc == 0; --l)
         rc = launch_wgrad(kWgradHidden, b.dP + l * dstride, kHidden, hp + (l - 1) * hstride, kHidden, C,
-                          grads[1 + 2 * l], kHidden, grads[2 + 2 * l], st);
+                          grads[1 + 2 * l], kHidden, grads[2 + 2 * l], b.part, b.part_bias, st);
       if (rc == 0)
         rc = launch_wgrad(kWgradFirst, b.dP, kHidden, sv.eP + p0 * kFourierPad, kFourier, C, grads[1], kFourier,
-                          grads[2], st);
+                          grads[2], b.part, b.part_bias, st);
     }
     if (rc) return rc;
     // Fourier: dB (3x93) += x^T g_arg   (x rows are float4 (x0,x1,x2,inside): 3 of 4 used)
     if (grads)
-      rc = split ? launch_wgrad_fourier16(sv.xP + p0, b.gargP, C, grads[0], st)
+      rc = split ? launch_wgrad_fourier16(sv.xP + p0, b.gargP, C, grads[0], b.part, st)
                  : launch_wgrad(kWgradFourier, reinterpret_cast<const float*>(sv.xP + p0), 3, b.gargP, kFourier, C,
-                                grads[0], kFourier, nullptr, st);
+                                grads[0], kFourier, nullptr, b.part, b.part_bias, st);
     if (rc) return rc;
     // feature branch: dWc_l (256x32) += (dL/dh_l)^T c ; dbc_l += colsum(dL/dh_l)
     if (fb && fb->g_fc && split) {  // f16x3 GEMMs: dL/dh from k_mlp_bwd16, the fp32 features
@@ -291,7 +295,7 @@ int mlp_backward_core(int prec, const float* packed, const SaveArgs& sv, int64_t
     } else if (fb && fb->g_fc) {
       for (int l = 0; l < 4 && rc == 0; ++l)
         rc = launch_wgrad(kWgradFc, b.gH + l * dstride, kHidden, fb->c + p0 * kCDim, kCDim, C, fb->g_fc[2 * l], kCDim,
-                          fb->g_fc[2 * l + 1], st);
+                          fb->g_fc[2 * l + 1], b.part, b.part_bias, st);
     }
     if (rc) return rc;
   }
@@ -383,7 +387,7 @@ int pnr_eval_points_f32(const float* packed, const float* p, int64_t P, const do
 size_t pnr_mlp_train_workspace_bytes(int64_t P) {
   if (P < 0) return 0;
   Carver c(nullptr);
-  carve_save(c, pad128(P));
+  carve_save(c, pad128(P), PNR_PREC_FP32);
   return c.off;
 }
 
@@ -392,7 +396,7 @@ int pnr_mlp_fwd_train(const float* packed, const float* p, int64_t P, float* raw
   if (!packed || P < 0 || (P > 0 && (!p || !raw_out || !ws))) return PNR_E_ARG;
   if (P == 0) return PNR_OK;
   Carver c(ws);
-  SaveArgs sv = carve_save(c, pad128(P));
+  SaveArgs sv = carve_save(c, pad128(P), precision);
   if (ws_bytes < c.off) return PNR_E_WORKSPACE;
   PointSrc s{};
   s.pts = p;
@@ -403,7 +407,7 @@ int pnr_mlp_fwd_train(const float* packed, const float* p, int64_t P, float* raw
 size_t pnr_mlp_bwd_workspace_bytes(int64_t P) {
   if (P < 0) return 0;
   size_t b = 0;
-  carve_bwd(pad128(P), 1, nullptr, &b);
+  carve_bwd(pad128(P), 1, nullptr, &b, false, true);
   return b;
 }
 
@@ -414,9 +418,9 @@ int pnr_mlp_bwd(const float* packed, int64_t P, const float* g_raw, float* const
   for (int i = 0; i < PNR_N_PARAMS; ++i)
     if (!grads[i]) return PNR_E_ARG;
   Carver c(ws);
-  SaveArgs sv = carve_save(c, pad128(P));
+  SaveArgs sv = carve_save(c, pad128(P), precision);
   size_t bneed = 0;
-  BwdWS b = carve_bwd(sv.ld, 1, bwd_ws, &bneed);
+  BwdWS b = carve_bwd(sv.ld, 1, bwd_ws, &bneed, false, true);
   if (ws_bytes < c.off || bwd_bytes < bneed) return PNR_E_WORKSPACE;
   hipStream_t st = (hipStream_t)stream;
   if (hipMemsetAsync(b.g_out, 0, (size_t)sv.ld * 16, st) != hipSuccess) return (int)hipGetLastError();
@@ -505,7 +509,7 @@ size_t pnr_render_bwd_workspace_bytes(const pnr_render_params* prm, int64_t n_ra
   if (!valid_prm(prm) || n_rays < 0) return 0;
   size_t b = 0;
   carve_bwd(pad128(n_rays * prm->n_samples) + pad128(n_rays * prm->n_importance), n_rays, nullptr, &b,
-            prm->points != nullptr);
+            prm->points != nullptr, save_mode(prm) != 2);
   return b;
 }
 
@@ -529,7 +533,7 @@ int pnr_render_bwd(const pnr_render_params* prm, const float* packed, const floa
   const int S = prm->n_samples, I = prm->n_importance;
   const int64_t ld = w.save.ld;
   const pnr_points* pts = prm->points;
-  BwdWS b = carve_bwd(ld, n, bwd_ws, &bneed, pts != nullptr);
+  BwdWS b = carve_bwd(ld, n, bwd_ws, &bneed, pts != nullptr, save_mode(prm) != 2);
   if (ws_bytes < need || bwd_bytes < bneed) return PNR_E_WORKSPACE;
   hipStream_t st = (hipStream_t)stream;
   const double* zi = w.z + n * S;
@@ -571,7 +575,7 @@ RegWS carve_reg(const pnr_render_params* prm, int64_t n, void* ws, size_t* bytes
   const int64_t P = n * prm->n_samples;
   w.z = c.take<float>(P);
   w.raw = c.take<float>(P * 4);
-  if (prm->save_for_backward) w.save = carve_save(c, pad128(P), save_mode(prm) == 1);
+  if (prm->save_for_backward) w.save = carve_save(c, pad128(P), prm->precision, save_mode(prm) == 1);
   if (prm->points) {
     w.c = c.take<float>((size_t)pad128(P) * kCDim);
     w.nidx = c.take<int32_t>((size_t)pad128(P) * prm->points->k);
@@ -628,7 +632,7 @@ int pnr_regulation_fwd(const pnr_render_params* prm, const float* packed, const 
 size_t pnr_regulation_bwd_workspace_bytes(const pnr_render_params* prm, int64_t n_rays) {
   if (!valid_prm(prm) || n_rays < 0) return 0;
   size_t b = 0;
-  carve_bwd(pad128(n_rays * prm->n_samples), n_rays, nullptr, &b, prm->points != nullptr);
+  carve_bwd(pad128(n_rays * prm->n_samples), n_rays, nullptr, &b, prm->points != nullptr, save_mode(prm) != 2);
   return b;
 }
 
@@ -652,7 +656,7 @@ int pnr_regulation_bwd(const pnr_render_params* prm, const float* packed, const 
   const int64_t P = n * prm->n_samples;
   const int64_t ld = w.save.ld;
   const pnr_points* pts = prm->points;
-  BwdWS b = carve_bwd(ld, n, bwd_ws, &bneed, pts != nullptr);
+  BwdWS b = carve_bwd(ld, n, bwd_ws, &bneed, pts != nullptr, save_mode(prm) != 2);
   if (ws_bytes < need || bwd_bytes < bneed) return PNR_E_WORKSPACE;
   hipStream_t st = (hipStream_t)stream;
   if (hipMemsetAsync(b.g_out, 0, (size_t)ld * 16, st) != hipSuccess) return (int)hipGetLastError();
@@ -731,7 +735,7 @@ int pnr_mlp_fwd_train_c(const float* packed, const float* fc_packed, const float
   if (!packed || !fc_packed || P < 0 || (P > 0 && (!p || !c || !raw_out || !ws))) return PNR_E_ARG;
   if (P == 0) return PNR_OK;
   Carver cv(ws);
-  SaveArgs sv = carve_save(cv, pad128(P));
+  SaveArgs sv = carve_save(cv, pad128(P), precision);
   if (ws_bytes < cv.off) return PNR_E_WORKSPACE;
   PointSrc s{};
   s.pts = p;
@@ -742,7 +746,7 @@ int pnr_mlp_fwd_train_c(const float* packed, const float* fc_packed, const float
 size_t pnr_mlp_bwd_workspace_bytes_c(int64_t P) {
   if (P < 0) return 0;
   size_t b = 0;
-  carve_bwd(pad128(P), 1, nullptr, &b, true);
+  carve_bwd(pad128(P), 1, nullptr, &b, true, true);
   return b;
 }
 
@@ -756,9 +760,9 @@ int pnr_mlp_bwd_c(const float* packed, const float* fc_packed, const float* c, i
   for (int i = 0; i < PNR_N_FC_PARAMS; ++i)
     if (!g_fc[i]) return PNR_E_ARG;
   Carver cv(ws);
-  SaveArgs sv = carve_save(cv, pad128(P));
+  SaveArgs sv = carve_save(cv, pad128(P), precision);
   size_t bneed = 0;
-  BwdWS b = carve_bwd(sv.ld, 1, bwd_ws, &bneed, true);
+  BwdWS b = carve_bwd(sv.ld, 1, bwd_ws, &bneed, true, true);
   if (ws_bytes < cv.off || bwd_bytes < bneed) return PNR_E_WORKSPACE;
   hipStream_t st = (hipStream_t)stream;
   if (hipMemsetAsync(b.g_out, 0, (size_t)sv.ld * 16, st) != hipSuccess) return (int)hipGetLastError();

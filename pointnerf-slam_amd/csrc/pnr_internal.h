@@ -239,23 +239,28 @@ struct WgradSyn {
   const float* wo;      // Wo [4][256] fp32
   const float4* xP;     // kWgradFirstX: saved inputs of the chunk rows
   const float* fb;      // kWgradFirstX: Fourier B padded [3][96] (packed + kOffFB)
-  // every split kind: per-workgroup partial tiles instead of float atomics, then one reduce launch
-  // (kWgradPartFloats + kWgradPartBiasFloats of scratch; NULL = atomics)
+  // every kind: per-workgroup partial tiles (kWgradPartFloats + kWgradPartBiasFloats of scratch),
+  // added into C / bias in a fixed order by k_part_reduce -- no float atomics, deterministic
   float* part;
   float* part_bias;
 };
-constexpr int kWgradMaxWg = 256;
+constexpr int kWgradMaxWg = 512;    // fp32 k_wgrad grid cap
+constexpr int kWgrad16MaxWg = 256;  // split k_wgrad16 grid cap
 constexpr int64_t kWgradPartFloats = (int64_t)kWgradMaxWg * 256 * 256;
 constexpr int64_t kWgradPartBiasFloats = (int64_t)kWgradMaxWg * 256;
+// C[r][c] += sum_g part[g][r pw + c] (r < nr, c < nb), bias[r] += sum_g pbias[g][r]: fixed order
+int launch_part_reduce(const float* part, const float* pbias, int nwg, int nr, int pw, int nb, float* C, int64_t ldc,
+                       float* bias, hipStream_t st);
 int launch_wgrad(int kind, const float* A, int ma, const float* B, int nb, int64_t K, float* C, int64_t ldc,
-                 float* bias, hipStream_t st);
+                 float* bias, float* part, float* part_bias, hipStream_t st);
 // split precisions (wgrad16.hip): kWgradHidden / kWgradFirst / kWgradFc as f16x3 GEMMs on fp32
 // operands (A = deltas or dL/dh [K][256], B = activations / Fourier features / point features
 // [K][WB]; B rows >= kb_rows are not read), dWo and dB as fp32 FMA reductions
 int launch_wgrad16(int kind, const float* A, const float* B, int64_t K, int64_t kb_rows, float* C, int64_t ldc,
                    float* bias, hipStream_t st, const WgradSyn* syn = nullptr);
-int launch_wgrad_out16(const float* g_out, const float* h4, int64_t K, float* C, float* bias, hipStream_t st);
-int launch_wgrad_fourier16(const float4* xP, const float* garg, int64_t K, float* C, hipStream_t st);
+int launch_wgrad_out16(const float* g_out, const float* h4, int64_t K, float* C, float* bias, float* part,
+                       float* part_bias, hipStream_t st);
+int launch_wgrad_fourier16(const float4* xP, const float* garg, int64_t K, float* C, float* part, hipStream_t st);
 
 inline int hip_status(hipError_t e) { return e == hipSuccess ? 0 : (int)e; }
 

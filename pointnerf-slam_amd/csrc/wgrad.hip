@@ -8,8 +8,8 @@
 // point-major operand is one contiguous block (32 x MA floats), copied linearly into LDS with
 // 16-B loads/stores (register double-buffering); the MFMA operand reads of that [k][u] image are
 // conflict-free (lanes read consecutive units).  The whole MA x NB partial stays in accumulator
-// registers (v_mfma_f32_32x32x2_f32, exact fp32) and is added into C with one float atomic per
-// element at the end.
+// registers (v_mfma_f32_32x32x2_f32, exact fp32) and is stored as this workgroup's partial tile;
+// k_part_reduce (wgrad16.hip) adds the partials into C in a fixed order (deterministic).
 //
 // Used for (src/conv_onet/models/decoder.py:149-159 parameters):
 //   dW3 = delta4^T h3, dW2 = delta3^T h2, dW1 = delta2^T h1     MA = NB = 256
@@ -48,9 +48,9 @@ struct WgradArgs {
   int nb;          // valid columns of B (columns of C)
   int64_t K;
   int64_t ks;      // points per workgroup (multiple of kKT)
-  float* C;
-  int64_t ldc;
-  float* bias;     // optional column sums of A
+  float* part;     // [grid][ma][NT 32] partial tiles
+  float* pbias;    // [grid][ma] partial column sums of A (bias non-null)
+  bool bias;
 };
 
 // load one 32-point tile (rows k0.. of a [K][W] operand) as float4 per thread, zero past ke
@@ -143,46 +143,50 @@ __global__ __launch_bounds__(256, 1) void k_wgrad(WgradArgs a) {
     for (int q = 0; q < Cfg::TPW; ++q) asm volatile("" : "+a"(acc[q]));
     buf ^= 1;
   }
-  // C[32ti + perm(r,hh)][32tj + i] += acc
+  // this workgroup's partial tile: part[blk][row][32 tj + i] (rows < ma)
+  float* P = a.part + (int64_t)blockIdx.x * a.ma * (NT * 32);
 #pragma unroll
   for (int x = 0; x < Cfg::RW; ++x)
 #pragma unroll
     for (int y = 0; y < Cfg::CW; ++y) {
       const int ti = tr0 + x, tj = tc0 + y;
-      const int col = 32 * tj + i;
-      if (tj >= NT || col >= a.nb) continue;
+      if (tj >= NT) continue;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int row = 32 * ti + perm(r, hh);
-        if (row < a.ma) atomicAdd(a.C + (int64_t)row * a.ldc + col, acc[x * Cfg::CW + y][r]);
+        if (row < a.ma) P[row * (NT * 32) + 32 * tj + i] = acc[x * Cfg::CW + y][r];
       }
     }
-  if (a.bias && (int)threadIdx.x < a.ma) atomicAdd(a.bias + threadIdx.x, csum);
+  if (a.bias && (int)threadIdx.x < a.ma) a.pbias[(int64_t)blockIdx.x * a.ma + threadIdx.x] = csum;
 }
 
-// choose the K split so that the grid covers the chip ~2x
+// choose the K split so that the grid covers the chip ~2x (<= kWgradMaxWg partial tiles)
 static int64_t pick_ks(int64_t K) {
-  int64_t ks = (K + 511) / 512;
+  int64_t ks = (K + kWgradMaxWg - 1) / kWgradMaxWg;
   ks = (ks + kKT - 1) / kKT * kKT;
   if (ks < 256) ks = 256;
   return ks;
 }
 
 int launch_wgrad(int kind, const float* A, int ma, const float* B, int nb, int64_t K, float* C, int64_t ldc,
-                 float* bias, hipStream_t st) {
+                 float* bias, float* part, float* part_bias, hipStream_t st) {
   if (K <= 0) return 0;
-  WgradArgs a{A, ma, B, nb, K, pick_ks(K), C, ldc, bias};
-  const dim3 grid((unsigned)((K + a.ks - 1) / a.ks)), block(256);
+  if (!part || !part_bias) return PNR_E_ARG;
+  WgradArgs a{A, ma, B, nb, K, pick_ks(K), part, part_bias, bias != nullptr};
+  const int nwg = (int)((K + a.ks - 1) / a.ks);
+  const dim3 grid((unsigned)nwg), block(256);
   TimingScope ts(kTimeWgrad, K, st);
+  int nt;
   switch (kind) {
-    case kWgradHidden: hipLaunchKernelGGL((k_wgrad<8, 8, 256, 256>), grid, block, 0, st, a); break;
-    case kWgradFirst: hipLaunchKernelGGL((k_wgrad<8, 3, 256, 96>), grid, block, 0, st, a); break;
-    case kWgradOut: hipLaunchKernelGGL((k_wgrad<1, 8, 4, 256>), grid, block, 0, st, a); break;
-    case kWgradFourier: hipLaunchKernelGGL((k_wgrad<1, 3, 4, 96>), grid, block, 0, st, a); break;
-    case kWgradFc: hipLaunchKernelGGL((k_wgrad<8, 1, 256, 32>), grid, block, 0, st, a); break;
+    case kWgradHidden: nt = 8; hipLaunchKernelGGL((k_wgrad<8, 8, 256, 256>), grid, block, 0, st, a); break;
+    case kWgradFirst: nt = 3; hipLaunchKernelGGL((k_wgrad<8, 3, 256, 96>), grid, block, 0, st, a); break;
+    case kWgradOut: nt = 8; hipLaunchKernelGGL((k_wgrad<1, 8, 4, 256>), grid, block, 0, st, a); break;
+    case kWgradFourier: nt = 3; hipLaunchKernelGGL((k_wgrad<1, 3, 4, 96>), grid, block, 0, st, a); break;
+    case kWgradFc: nt = 1; hipLaunchKernelGGL((k_wgrad<8, 1, 256, 32>), grid, block, 0, st, a); break;
     default: return PNR_E_ARG;
   }
-  return hip_status(hipGetLastError());
+  const int rc = hip_status(hipGetLastError());
+  return rc ? rc : launch_part_reduce(part, part_bias, nwg, ma, 32 * nt, nb, C, ldc, bias, st);
 }
 
 }  // namespace pnr

@@ -22,7 +22,8 @@
 // The GEMM moves 2 x 4 B per point and unit and is HBM-bound (the kernel streams 64 KB per 32-point
 // tile at ~3 flops per byte of f16 MFMA work).  K (points) is split over workgroups of 8 waves
 // (2 per SIMD, one workgroup per CU); wave w owns output rows [32w, 32w + 32) for the whole K range
-// in NTB accumulator tiles and flushes them with one float atomic per element at the end.
+// in NTB accumulator tiles and stores them (x 1 / scale) as this workgroup's partial tile, which
+// k_part_reduce adds into C in a fixed order (deterministic).
 //  - A: each wave reads its own 32 columns straight into registers in MFMA operand order (lane l:
 //    column 32w + (l & 31), points 16s + 8(l >> 5) + j): two 128-B lines per load instruction.
 //  - B: shared by the 8 waves; the block loads a 32 x WB tile with 16-B loads, splits it and writes
@@ -276,55 +277,71 @@ __global__ __launch_bounds__(512, 1) void k_wgrad16(WxArgs a) {
         acc[y] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[s], bh, acc[y], 0, 0, 0);
       }
   }
+  // two-phase flush: this workgroup's tile with plain stores (each instruction two 128-B row
+  // segments), summed in a fixed order by k_part_reduce.  (Float atomics ran at one 256-B
+  // wave-instruction per ~50 ns per CU -- a 256 x 256 tile took ~51 us per workgroup -- and left the
+  // summation order to the scheduler.)
   const float inv = 1.f / sc;
-  if (a.part) {
-    // two-phase flush: this workgroup's tile with plain stores (each instruction two 128-B row
-    // segments), summed by k_wgrad_reduce.  Float atomics run at one 256-B wave-instruction per
-    // ~50 ns per CU: a 256 x 256 tile took ~51 us per workgroup, the whole launch at small K.
-    float* P = a.part + (int64_t)blockIdx.x * 256 * (NTB * 32);
+  float* P = a.part + (int64_t)blockIdx.x * 256 * (NTB * 32);
 #pragma unroll
-    for (int y = 0; y < NTB; ++y)
+  for (int y = 0; y < NTB; ++y)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) P[(32 * w + perm(r, hh)) * (NTB * 32) + 32 * y + (lane & 31)] = acc[y][r] * inv;
-    cs += __shfl_xor(cs, 32);
-    if (a.bias && hh == 0) a.part_bias[(int64_t)blockIdx.x * 256 + 32 * w + lane] = cs;
-    return;
-  }
-  // C[32w + perm(r,hh)][32y + (lane&31)] += acc / sc
-#pragma unroll
-  for (int y = 0; y < NTB; ++y) {
-    const int col = 32 * y + (lane & 31);
-    if (col >= a.nb) continue;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) atomicAdd(a.C + (int64_t)(32 * w + perm(r, hh)) * a.ldc + col, acc[y][r] * inv);
-  }
+    for (int r = 0; r < 16; ++r) P[(32 * w + perm(r, hh)) * (NTB * 32) + 32 * y + (lane & 31)] = acc[y][r] * inv;
   cs += __shfl_xor(cs, 32);
-  if (a.bias && hh == 0) atomicAdd(a.bias + 32 * w + lane, cs);
+  if (a.bias && hh == 0) a.part_bias[(int64_t)blockIdx.x * 256 + 32 * w + lane] = cs;
 }
 
-// C[row][col] += sum over the grid's partial tiles (col < nb), bias[row] += sum of the partial
-// bias rows; one thread per output element and slice of the partials (blockIdx.y: kReduceSlices
-// slices, so a thread chains at most nwg / kReduceSlices dependent loads), the partials read
-// coalesced, each slice's sum added with one float atomic per element
-constexpr int kReduceSlices = 8;
-__global__ __launch_bounds__(256) void k_wgrad_reduce(const float* __restrict__ part, const float* __restrict__ pbias,
-                                                      int nwg, int wb, int nb, float* __restrict__ C, int64_t ldc,
-                                                      float* __restrict__ bias) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  const int row = i / wb, col = i % wb;
-  const int k0 = (int)((int64_t)nwg * blockIdx.y / gridDim.y), k1 = (int)((int64_t)nwg * (blockIdx.y + 1) / gridDim.y);
-  if (i < 256 * wb && col < nb && k1 > k0) {
-    float s = 0.f;
-#pragma unroll 8
-    for (int k = k0; k < k1; ++k) s += part[(int64_t)k * 256 * wb + i];
-    atomicAdd(C + (int64_t)row * ldc + col, s);
+// Deterministic reduction of per-workgroup partials (every weight-gradient GEMM flushes this way):
+//   C[r][c] += sum_{g < nwg} part[g][r pw + c]    (r < nr, c < nb)
+//   bias[r] += sum_{g < nwg} pbias[g][r]          (r < nr; bias non-null)
+// A block owns 64 consecutive elements; wave v of its 8 sums the partials g = v, v + 8, v + 16, ...
+// in that order (two chains, even and odd steps, added at the end), the 8 wave sums are added in
+// wave order through LDS and wave 0 updates C with a plain read-modify-write (one owner per
+// element).  The summation order is a function of nwg alone: no float atomics, so two runs (eager
+// or graph-replayed) give identical bits.
+constexpr int kRedWaves = 8;
+__global__ __launch_bounds__(64 * kRedWaves) void k_part_reduce(const float* __restrict__ part,
+                                                                const float* __restrict__ pbias, int nwg, int nr,
+                                                                int pw, int nb, float* __restrict__ C, int64_t ldc,
+                                                                float* __restrict__ bias) {
+  __shared__ float red[kRedWaves][64];
+  const int lane = threadIdx.x & 63, v = threadIdx.x >> 6;
+  const int64_t E = (int64_t)nr * pw;
+  const int64_t nmain = (E + 63) / 64;
+  const bool is_bias = (int64_t)blockIdx.x >= nmain;
+  const int64_t e = (is_bias ? (int64_t)blockIdx.x - nmain : (int64_t)blockIdx.x) * 64 + lane;
+  const float* src = is_bias ? pbias : part;
+  const int64_t stride = is_bias ? nr : E;
+  const bool ok = is_bias ? (bias != nullptr && e < nr) : (e < E && (int)(e % pw) < nb);
+  float s0 = 0.f, s1 = 0.f;
+  if (ok) {
+    int g = v;
+#pragma unroll 4
+    for (; g + kRedWaves < nwg; g += 2 * kRedWaves) {
+      s0 += src[(int64_t)g * stride + e];
+      s1 += src[(int64_t)(g + kRedWaves) * stride + e];
+    }
+    if (g < nwg) s0 += src[(int64_t)g * stride + e];
   }
-  if (bias && i < 256 && k1 > k0) {
-    float s = 0.f;
-#pragma unroll 8
-    for (int k = k0; k < k1; ++k) s += pbias[(int64_t)k * 256 + i];
-    atomicAdd(bias + i, s);
+  red[v][lane] = s0 + s1;
+  __syncthreads();
+  if (v == 0 && ok) {
+    float s = red[0][lane];
+#pragma unroll
+    for (int i = 1; i < kRedWaves; ++i) s += red[i][lane];
+    if (is_bias) bias[e] += s;
+    else C[(e / pw) * ldc + e % pw] += s;
   }
+}
+
+int launch_part_reduce(const float* part, const float* pbias, int nwg, int nr, int pw, int nb, float* C, int64_t ldc,
+                       float* bias, hipStream_t st) {
+  if (nwg <= 0) return 0;
+  const int64_t nmain = ((int64_t)nr * pw + 63) / 64;
+  const int64_t nbias = bias ? (nr + 63) / 64 : 0;
+  hipLaunchKernelGGL(k_part_reduce, dim3((unsigned)(nmain + nbias)), dim3(64 * kRedWaves), 0, st, part, pbias, nwg,
+                     nr, pw, nb, C, ldc, bias);
+  return hip_status(hipGetLastError());
 }
 
 template <int NTB, int WB, bool SYN = false, bool FOUR = false>
@@ -336,11 +353,8 @@ static int launch_k(const WxArgs& a, hipStream_t st) {
   if (!attr) return PNR_E_ARG;
   const int nwg = (int)((a.K + a.ks - 1) / a.ks);
   hipLaunchKernelGGL(kern, dim3((unsigned)nwg), dim3(Cfg::kThreads), Cfg::kLds, st, a);
-  if (a.part)
-    hipLaunchKernelGGL(k_wgrad_reduce,
-                       dim3((unsigned)((256 * NTB * 32 + 255) / 256), (unsigned)(nwg < kReduceSlices ? nwg : kReduceSlices)),
-                       dim3(256), 0, st, a.part, a.part_bias, nwg, NTB * 32, a.nb, a.C, a.ldc, a.bias);
-  return hip_status(hipGetLastError());
+  const int rc = hip_status(hipGetLastError());
+  return rc ? rc : launch_part_reduce(a.part, a.part_bias, nwg, 256, NTB * 32, a.nb, a.C, a.ldc, a.bias, st);
 }
 
 // kind: kWgradHidden (B [K][256]), kWgradFirst (B [K][96], 93 columns) or kWgradFc (B [K][32]);
@@ -350,18 +364,15 @@ int launch_wgrad16(int kind, const float* A, const float* B, int64_t K, int64_t 
   if (K <= 0) return 0;
   if (kb_rows <= 0) return PNR_E_ARG;
   K = (K + 31) / 32 * 32;
-  // split-K over at most one workgroup per CU.  Atomic flush (no partials buffer): each workgroup
-  // adds its whole C tile (256 KB of float atomics for a hidden layer) and spends ~1 us per
-  // 32-point tile, n = sqrt(5 K / 32).  Two-phase flush (the backward's scratch): plain stores of
-  // the tile + k_wgrad_reduce, >= 8 tiles per workgroup
-  const bool two_phase = syn && syn->part && syn->part_bias;
-  int64_t nwg = (int64_t)sqrt(5.0 * (double)K / 32.0);
-  if (two_phase) nwg = (K / 32 + 7) / 8;  // >= 8 tiles per workgroup: the flush no longer dominates
-  nwg = nwg < 4 ? 4 : (nwg > kWgradMaxWg ? kWgradMaxWg : nwg);
+  // split-K over at most one workgroup per CU, >= 8 tiles per workgroup (the flush of the partial
+  // tile no longer dominates); the partials go to the backward's scratch (WgradSyn part/part_bias)
+  if (!syn || !syn->part || !syn->part_bias) return PNR_E_ARG;
+  int64_t nwg = (K / 32 + 7) / 8;
+  nwg = nwg < 4 ? 4 : (nwg > kWgrad16MaxWg ? kWgrad16MaxWg : nwg);
   int64_t ks = (K + nwg - 1) / nwg;
   ks = (ks + 31) / 32 * 32;
-  WxArgs a{A, B, 256, K, kb_rows, ks, C, ldc, bias, nullptr, nullptr, 0, nullptr, nullptr, nullptr,
-           two_phase ? syn->part : nullptr, two_phase ? syn->part_bias : nullptr};
+  WxArgs a{A, B, 256, K, kb_rows, ks, C, ldc, bias, nullptr, nullptr, 0, nullptr, nullptr, nullptr, syn->part,
+           syn->part_bias};
   TimingScope ts(kTimeWgrad, K, st);
   if (kind == kWgradHidden) return launch_k<8, 256>(a, st);
   if (kind == kWgradOutDelta) {  // dW3 += delta4^T h3, delta4 rebuilt from g_out and the h4 masks
@@ -395,15 +406,17 @@ int launch_wgrad16(int kind, const float* A, const float* B, int64_t K, int64_t 
 // A fp32 rows of 4 (float4: g_out, or x = (x0, x1, x2, inside) with M = 3), B fp32 rows of WB.
 //   dWo (4 x 256) = g_out^T h4 (+ dbo)       dB (3 x 93) = x^T g_arg
 // A block streams its K range: thread (r, c) = (tid / CPR, tid % CPR) loads 32 B (8 columns) of row
-// r and the row's float4 of A, keeping 4 x 8 partial sums; the rows are then reduced through LDS and
-// flushed with one atomic per output element per block.
+// r and the row's float4 of A, keeping 4 x 8 partial sums; the RPI row groups are then added in
+// row-group order through LDS and the block's M x N sums go to the partials (part[block][m N + n],
+// pbias[block][m]) that k_part_reduce adds into C / bias in a fixed order.
 template <int WB>
 __global__ __launch_bounds__(256) void k_wgrad_skinny(const float4* __restrict__ A, const float* __restrict__ B,
-                                                      int64_t K, int64_t ks, int M, int N, float* __restrict__ C,
-                                                      int64_t ldc, float* __restrict__ bias) {
+                                                      int64_t K, int64_t ks, int M, int N, float* __restrict__ part,
+                                                      float* __restrict__ pbias) {
   constexpr int CPR = WB / 8;          // threads per row (32 for 256, 12 for 96)
   constexpr int RPI = 256 / CPR;       // rows per iteration (8 or 21)
-  __shared__ float red[4][256 + 8];
+  __shared__ float red[RPI][4][WB];
+  __shared__ float redb[RPI][4];
   const int tid = threadIdx.x;
   const int r = tid / CPR, c = tid % CPR;
   const bool act = r < RPI;
@@ -442,49 +455,61 @@ __global__ __launch_bounds__(256) void k_wgrad_skinny(const float4* __restrict__
         }
       }
     }
-  }
-  // reduce the RPI row groups: column n = 8c + j
-  for (int m = 0; m < 4; ++m) {
-    for (int i = tid; i < 256 + 8; i += 256) red[m][i] = 0.f;
-  }
-  __syncthreads();
-  if (act) {
 #pragma unroll
     for (int m = 0; m < 4; ++m)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) atomicAdd(&red[m][8 * c + j], acc[m][j]);  // LDS atomics
+      for (int j = 0; j < 8; ++j) red[r][m][8 * c + j] = acc[m][j];
     if (c == 0)
 #pragma unroll
-      for (int m = 0; m < 4; ++m) atomicAdd(&red[m][256 + 4], bs[m]);
+      for (int m = 0; m < 4; ++m) redb[r][m] = bs[m];
   }
   __syncthreads();
-  for (int i = tid; i < 4 * N; i += 256) {
+  for (int i = tid; i < M * N; i += 256) {
     const int m = i / N, n = i % N;
-    if (m < M) atomicAdd(C + (int64_t)m * ldc + n, red[m][n]);
+    float s = red[0][m][n];
+#pragma unroll
+    for (int q = 1; q < RPI; ++q) s += red[q][m][n];
+    part[(int64_t)blockIdx.x * M * N + i] = s;
   }
-  if (bias && tid < M) atomicAdd(bias + tid, red[tid][256 + 4]);
+  if (pbias && tid < M) {
+    float s = redb[0][tid];
+#pragma unroll
+    for (int q = 1; q < RPI; ++q) s += redb[q][tid];
+    pbias[(int64_t)blockIdx.x * M + tid] = s;
+  }
+}
+
+static int skinny_blocks(int64_t K, int64_t* ks) {
+  *ks = (K + 1023) / 1024;
+  if (*ks < 256) *ks = 256;
+  return (int)((K + *ks - 1) / *ks);
 }
 
 // dWo (4 x 256) += g_out^T h4, dbo += colsum(g_out)
-int launch_wgrad_out16(const float* g_out, const float* h4, int64_t K, float* C, float* bias, hipStream_t st) {
+int launch_wgrad_out16(const float* g_out, const float* h4, int64_t K, float* C, float* bias, float* part,
+                       float* part_bias, hipStream_t st) {
   if (K <= 0) return 0;
-  int64_t ks = (K + 1023) / 1024;
-  if (ks < 256) ks = 256;
+  if (!part || !part_bias) return PNR_E_ARG;
+  int64_t ks;
+  const int nb = skinny_blocks(K, &ks);
   TimingScope ts(kTimeWgrad, K, st);
-  hipLaunchKernelGGL(k_wgrad_skinny<256>, dim3((unsigned)((K + ks - 1) / ks)), dim3(256), 0, st,
-                     reinterpret_cast<const float4*>(g_out), h4, K, ks, 4, kHidden, C, (int64_t)kHidden, bias);
-  return hip_status(hipGetLastError());
+  hipLaunchKernelGGL(k_wgrad_skinny<256>, dim3((unsigned)nb), dim3(256), 0, st, reinterpret_cast<const float4*>(g_out),
+                     h4, K, ks, 4, kHidden, part, bias ? part_bias : nullptr);
+  const int rc = hip_status(hipGetLastError());
+  return rc ? rc : launch_part_reduce(part, part_bias, nb, 4, kHidden, kHidden, C, (int64_t)kHidden, bias, st);
 }
 
 // dB (3 x 93) += x^T g_arg: x rows float4 (x0, x1, x2, inside), g_arg fp32 [K][96]
-int launch_wgrad_fourier16(const float4* xP, const float* garg, int64_t K, float* C, hipStream_t st) {
+int launch_wgrad_fourier16(const float4* xP, const float* garg, int64_t K, float* C, float* part, hipStream_t st) {
   if (K <= 0) return 0;
-  int64_t ks = (K + 1023) / 1024;
-  if (ks < 256) ks = 256;
+  if (!part) return PNR_E_ARG;
+  int64_t ks;
+  const int nb = skinny_blocks(K, &ks);
   TimingScope ts(kTimeWgrad, K, st);
-  hipLaunchKernelGGL(k_wgrad_skinny<96>, dim3((unsigned)((K + ks - 1) / ks)), dim3(256), 0, st, xP, garg, K, ks,
-                     3, kFourier, C, (int64_t)kFourier, nullptr);
-  return hip_status(hipGetLastError());
+  hipLaunchKernelGGL(k_wgrad_skinny<96>, dim3((unsigned)nb), dim3(256), 0, st, xP, garg, K, ks, 3, kFourier, part,
+                     nullptr);
+  const int rc = hip_status(hipGetLastError());
+  return rc ? rc : launch_part_reduce(part, nullptr, nb, 3, kFourier, kFourier, C, (int64_t)kFourier, nullptr, st);
 }
 
 }  // namespace pnr

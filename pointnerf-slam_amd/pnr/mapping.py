@@ -12,8 +12,12 @@ join the same buffer (features last, with their own learning rate: a second Adam
 tail of the buffer), still one all-reduce per step -- or, with DataParallel(shard_points=True), a
 reduce-scatter of the feature tail, Adam on the owned feature range and an all-gather.  `ddp`
 (pnr.dist.DataParallel) adds the cross-GPU gradient all-reduce and the
-global far clamp; without it the step is single-GPU and bit-identical to the reference order of
-operations of a 1-process Mapper.
+global far clamp; without it the step is single-GPU.  The step is deterministic: every weight-
+gradient GEMM stores per-workgroup partial tiles that one reduction adds in a fixed order (no float
+atomics), so a replay or a rerun reproduces it bit for bit.  It is not the reference's float32
+summation order (no GPU sum is); tests/test_gpu_precision.py holds it to the correctly-rounded
+gradient.  The point-feature gradient (neural points) is scattered with float atomics and is the
+one part whose bits depend on scheduling.
 """
 from __future__ import annotations
 

@@ -45,11 +45,21 @@ def main():
     lt = torch.tensor(local_losses, device=dev, dtype=torch.float64)
     torch.distributed.all_reduce(lt)  # the global loss = sum of the shards' losses (sums, A14)
     w_dp = ms.flat.data.detach().cpu().clone()
+    # every rank holds the same weights, bit for bit (Adam on identical all-reduced gradients)
+    wmax, wmin = ms.flat.data.detach().clone(), ms.flat.data.detach().clone()
+    torch.distributed.all_reduce(wmax, op=torch.distributed.ReduceOp.MAX)
+    torch.distributed.all_reduce(wmin, op=torch.distributed.ReduceOp.MIN)
+    ranks_identical = bool(torch.equal(wmax, wmin))
     if rank == 0:
         dec1 = bench.make_decoder(pnr, pnr.ROOM0_CFG, params, dev)
         ms1 = MapStep(pnr.Renderer(pnr.ROOM0_CFG, None, slam), dec1, lr=2e-4, w_color_loss=0.05)
         full = [float(ms1(ro, rd, gt, col, t)) for t in t_rands]
         w1 = ms1.flat.data.detach().cpu().clone()
+        # the 1-process step is deterministic: a second run gives identical bits
+        dec2 = bench.make_decoder(pnr, pnr.ROOM0_CFG, params, dev)
+        ms2 = MapStep(pnr.Renderer(pnr.ROOM0_CFG, None, slam), dec2, lr=2e-4, w_color_loss=0.05)
+        full2 = [float(ms2(ro, rd, gt, col, t)) for t in t_rands]
+        rerun_identical = full2 == full and torch.equal(ms2.flat.data.detach().cpu(), w1)
         dw = (w_dp - w1).abs()
         loss_rel = [abs(x - y) / abs(y) for x, y in zip(lt.tolist(), full)]
         res = {'world': world, 'backend': torch.distributed.get_backend(), 'global_batch': n,
@@ -57,12 +67,16 @@ def main():
                'loss_dp': lt.tolist(), 'loss_1proc': full, 'loss_rel_diff': loss_rel,
                'weights_max_abs_diff': float(dw.max()),
                'weights_frac_beyond_1e-5_rel': float((dw > 1e-7 + 1e-5 * w1.abs()).float().mean()),
-               'far_clamp': 'device (far_mode 2), all_reduce MAX', 'precision': pnr._lib.DEFAULT_PRECISION}
+               'far_clamp': 'device (far_mode 2), all_reduce MAX', 'precision': pnr._lib.DEFAULT_PRECISION,
+               'ranks_bitwise_identical': ranks_identical, 'one_process_rerun_bitwise_identical': rerun_identical}
         print(json.dumps(res), flush=True)
         if len(sys.argv) > 1:
             json.dump(res, open(sys.argv[1], 'w'), indent=1)
-        # step 1 starts from the same weights: the losses agree to summation order; Adam then moves
-        # near-zero-gradient elements by up to lr per step (the 2-process sum is a different order)
+        assert ranks_identical and rerun_identical, res
+        # step 1 starts from the same weights: the losses agree to summation order (each rank sums
+        # its own half of the points, then the all-reduce adds the halves: a different association
+        # of the same float32 terms than the 1-process sum); Adam then moves near-zero-gradient
+        # elements by up to lr per step
         assert loss_rel[0] < 1e-6, loss_rel
         assert max(loss_rel) < 1e-4, loss_rel
         assert float(dw.max()) <= steps * 2 * 2e-4 and res['weights_frac_beyond_1e-5_rel'] < 0.01, res

@@ -48,15 +48,23 @@ def main():
     torch.cuda.set_device(dev)
     ddp = pdist.DataParallel()
     l_dp, ct_dp = run(pnr, ddp, dev)
+    cmax, cmin = ct_dp.clone().to(dev), ct_dp.clone().to(dev)
+    torch.distributed.all_reduce(cmax, op=torch.distributed.ReduceOp.MAX)
+    torch.distributed.all_reduce(cmin, op=torch.distributed.ReduceOp.MIN)
+    ranks_identical = bool(torch.equal(cmax, cmin))  # the camera Adam runs on the all-reduced gradient
     if rank == 0:
         l1, ct1 = run(pnr, None, dev)
+        l2, ct2 = run(pnr, None, dev)
+        rerun_identical = l1 == l2 and torch.equal(ct1, ct2)
         rel = [abs(x - y) / abs(y) for x, y in zip(l_dp, l1)]
         res = {'world': world, 'backend': torch.distributed.get_backend(), 'iters': len(l1), 'loss_dp': l_dp,
                'loss_1proc': l1, 'loss_rel_diff': rel, 'camera_max_abs_diff': float((ct_dp - ct1).abs().max()),
-               'precision': pnr._lib.DEFAULT_PRECISION}
+               'precision': pnr._lib.DEFAULT_PRECISION, 'ranks_bitwise_identical': ranks_identical,
+               'one_process_rerun_bitwise_identical': rerun_identical}
         print(json.dumps(res), flush=True)
         if len(sys.argv) > 1:
             json.dump(res, open(sys.argv[1], 'w'), indent=1)
+        assert ranks_identical and rerun_identical, res
         assert rel[0] < 1e-6 and max(rel) < 1e-4, rel
         assert res['camera_max_abs_diff'] < 1e-5, res
         print('DP_TRACK_CHECK_OK', flush=True)
