@@ -154,9 +154,9 @@ def mlp_forward_c_cr(params: Params, p: torch.Tensor, c: torch.Tensor) -> torch.
     layer's output rounded to float32; in the backward each layer's input gradient, and dL/dc =
     sum_l Wc_l^T dL/dh_l, rounded likewise).  The yardstick for fp32-class feature-branch gradients
     (tests/golden/make_grads_cr.py), like ref_render.mlp_forward_cr for the c_dim = 0 decoder."""
-    from .ref_render import _RoundF32
+    from .ref_render import _RoundF32, fourier_arg_cr
     x = p.reshape(-1, 3).float()
-    h = torch.sin(x @ params['embedder._B'])
+    h = torch.sin(fourier_arg_cr(x, params['embedder._B']))
     cd = c.double()
     for li in range(N_LAYERS):
         a = F.relu(F.linear(h.double(), params[f'pts_linears.{li}.weight'].double(),
@@ -167,13 +167,14 @@ def mlp_forward_c_cr(params: Params, p: torch.Tensor, c: torch.Tensor) -> torch.
                                     params['output_linear.bias'].double()))
 
 
-def eval_points_c(params: Params, p: torch.Tensor, bound: torch.Tensor, points: dict) -> torch.Tensor:
+def eval_points_c(params: Params, p: torch.Tensor, bound: torch.Tensor, points: dict, cr: bool = False) -> torch.Tensor:
     """src/utils/Renderer.py:23-61 with the neural-point features: raw (P,4) f32, density := 100
-    outside the bound.  `points` = dict(xyz, feats, mode, radius, spacing, k, eps)."""
+    outside the bound.  `points` = dict(xyz, feats, mode, radius, spacing, k, eps).  cr: the decoder
+    GEMMs correctly rounded (mlp_forward_c_cr; test yardstick)."""
     c = point_gather(p, points['xyz'], points['feats'], points.get('mode', 'idw'),
                      points.get('radius', 0.0), points.get('spacing'), points.get('k', 8),
                      points.get('eps', 1e-6))
-    ret = mlp_forward_c(params, p, c).clone()
+    ret = (mlp_forward_c_cr if cr else mlp_forward_c)(params, p, c).clone()
     mask = inside_bound(p.reshape(-1, 3), bound)
     ret[~mask, 3] = OUT_OF_BOUND_SIGMA
     return ret

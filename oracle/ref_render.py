@@ -154,15 +154,38 @@ class _RoundF32(torch.autograd.Function):
         return g.double()
 
 
+class _FourierArgCR(torch.autograd.Function):
+    """x @ B in the reference's float32 arithmetic (decoder.py:26-30: the same float32 argument as
+    the reference), with the backward's two GEMMs -- dL/dB = x^T g over all points and dL/dx =
+    g B^T -- summed in float64 and rounded to float32 (correctly rounded, like every other GEMM of
+    mlp_forward_cr)."""
+
+    @staticmethod
+    def forward(ctx, x, B):
+        ctx.save_for_backward(x, B)
+        return x @ B
+
+    @staticmethod
+    def backward(ctx, g):
+        x, B = ctx.saved_tensors
+        gd = g.double()
+        return (gd @ B.double().t()).float(), (x.double().t() @ gd).float()
+
+
+def fourier_arg_cr(x: torch.Tensor, B: torch.Tensor) -> torch.Tensor:
+    return _FourierArgCR.apply(x, B)
+
+
 def mlp_forward_cr(params: Params, p: torch.Tensor) -> torch.Tensor:
     """mlp_forward with every GEMM CORRECTLY ROUNDED: the hidden and output layers sum in float64
     and round each layer's output (and, in the backward, each layer's input gradient) to float32;
-    the Fourier argument x @ B stays the reference's float32 product (decoder.py:26-30).  Not the
+    the Fourier argument x @ B stays the reference's float32 product (decoder.py:26-30), its
+    backward GEMMs (dL/dB, dL/dx) are correctly rounded too (fourier_arg_cr).  Not the
     reference's arithmetic -- its float32 sums carry their own rounding -- but the same function
     without summation-order noise: the yardstick for fp32-class gradients
     (tests/golden/make_grads_cr.py)."""
     x = p.reshape(-1, 3).float()
-    h = torch.sin(x @ params['embedder._B'])
+    h = torch.sin(fourier_arg_cr(x, params['embedder._B']))
     for li in range(N_LAYERS):
         h = _RoundF32.apply(F.relu(F.linear(h.double(), params[f'pts_linears.{li}.weight'].double(),
                                             params[f'pts_linears.{li}.bias'].double())))

@@ -11,8 +11,9 @@ with fresh fc_c layers (src/conv_onet/models/decoder.py:122-125), a camera at th
 Parity: rays through the HIP path vs the oracle (oracle/ref_points.py gather + oracle/ref_render.py)
 over the points near those rays (a superset of every sample's neighbourhood: exact) -- the render,
 and the gradient of one MapStep (Mapper loss with regulation, src/Mapper.py:623-655) w.r.t. every
-decoder / fc_c tensor and the point features, elementwise (rtol 1e-3, atol 2e-5 max|g|: the float32
-oracle's own rounding) for f16x3; bf16 to 5% in norm.  f16x3 is
+decoder / fc_c tensor and the point features, elementwise for f16x3: rtol 1e-3 with atol
+(1e-6 + d32) max|g| against the correctly-rounded gradient (oracle.ref_points.mlp_forward_c_cr),
+d32 = the float32 oracle's own distance from it; bf16 to 5% in norm.  f16x3 is
 held to the fp32 tolerances of tests/test_gpu_parity.py.  bf16 (8 significant bits per operand)
 is held to PSNR(bf16 HIP render, fp32 oracle render) > 45 dB and depth within 3e-2 relative: it
 does NOT meet the metric's 0.1 dB PSNR clause (that needs ~70 dB); f16x3 does.
@@ -140,13 +141,17 @@ def map_grad_parity(pnr, ms, params, bound, xyz, feats, ro, rd, gt, radius, prec
     torch.cuda.synchronize()
     far = float(((bound[:, 1] - bound[:, 0]) ** 2).sum().sqrt()) * 2
     sub = near_ray_points(xyz, ro, rd, far, 2 * radius)
-    ref_p = {k: v.clone().requires_grad_(True) for k, v in params.items()}
-    fr = feats[sub].clone().requires_grad_(True)
-    pdict = dict(xyz=xyz[sub], feats=fr, mode='idw', radius=radius, k=8, eps=1e-6)
-    ev = lambda q: RP.eval_points_c(ref_p, q, bound, pdict)  # noqa: E731
-    d, v, c = RR.render_batch_ray(ref_p, rd, ro, bound, gt_depth=gt, eval_fn=ev)
-    sig = RR.regulation(ref_p, rd, ro, gt, bound, t_rand=t_rand, eval_fn=ev)
-    RR.mapping_loss(d, c, gt, col, sig).backward()
+    refs = {}
+    for cr in (False, True):
+        ref_p = {k: v.clone().requires_grad_(True) for k, v in params.items()}
+        fr = feats[sub].clone().requires_grad_(True)
+        pdict = dict(xyz=xyz[sub], feats=fr, mode='idw', radius=radius, k=8, eps=1e-6)
+        ev = lambda q, ref_p=ref_p, pdict=pdict, cr=cr: RP.eval_points_c(ref_p, q, bound, pdict, cr=cr)  # noqa: E731
+        d, v, c = RR.render_batch_ray(ref_p, rd, ro, bound, gt_depth=gt, eval_fn=ev)
+        sig = RR.regulation(ref_p, rd, ro, gt, bound, t_rand=t_rand, eval_fn=ev)
+        RR.mapping_loss(d, c, gt, col, sig).backward()
+        refs[cr] = {k: t.grad for k, t in ref_p.items()}
+        refs[cr]['feats'] = fr.grad
     got = {}
     off = 0
     from pnr.decoder import PARAM_ORDER, FC_ORDER
@@ -154,20 +159,21 @@ def map_grad_parity(pnr, ms, params, bound, xyz, feats, ro, rd, gt, radius, prec
         got[name] = ms.flat.grad[off:off + t.numel()].view_as(t).cpu()
         off += t.numel()
     got['feats'] = ms.flat.grad[off:].view(-1, 32).cpu()[sub]
-    refs = {k: ref_p[k].grad for k in got if k != 'feats'}
-    refs['feats'] = fr.grad
-    assert float(refs['feats'].abs().max()) > 0, 'the rays must reach neural points'
-    for k, gr in refs.items():
-        a, b = got[k].numpy(), gr.numpy()
-        scale = max(np.abs(b).max(), 1e-30)
+    assert float(refs[False]['feats'].abs().max()) > 0, 'the rays must reach neural points'
+    for k in got:
+        a, b, bcr = got[k].numpy(), refs[False][k].numpy(), refs[True][k].numpy()
         if precision == 'bf16':  # 8-bit operands: a norm bound only
             rel = np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30)
             print(f'{precision} {k}: |g - g_oracle| / |g_oracle| = {rel:.2e}')
             assert rel < 5e-2, (k, rel)
-        else:
-            viol = np.abs(a - b) / (1e-3 * np.abs(b) + 2e-5 * scale)
-            print(f'{precision} {k}: worst |g - g_oracle| / (rtol |g| + atol) = {viol.max():.3f}')
-            np.testing.assert_allclose(a, b, rtol=1e-3, atol=2e-5 * scale, err_msg=k)
+            continue
+        # elementwise: rtol 1e-3, atol (1e-6 + d32) max|g_cr| vs the correctly-rounded gradient
+        scale = max(np.abs(bcr).max(), 1e-30)
+        d32 = np.abs(b - bcr).max() / scale
+        atol = (1e-6 + d32) * scale
+        viol = np.abs(a - bcr) / (1e-3 * np.abs(bcr) + atol)
+        print(f'{precision} {k}: d32 {d32:.2e}, worst |g - g_cr| / (rtol |g_cr| + atol) = {viol.max():.3f}')
+        np.testing.assert_allclose(a, bcr, rtol=1e-3, atol=atol, err_msg=k)
 
 
 def oracle_render(params, bound, xyz, feats, ro, rd, gt, radius):
@@ -276,10 +282,11 @@ def test_c5_apartment_1m_points_f16(pnr_mod, dev):
     # gradient of one Mapper iteration on the 96 rays (gt = the fp32 render) vs the oracle on the
     # f16-rounded features
     r = pnr_mod.Renderer(pnr_mod.ROOM0_CFG, None, slam)
-    pts_g = pnr_mod.NeuralPoints(xyz.to(dev), feats.to(dev), mode='idw', radius=0.008, k=8,
+    # (a 3 cm radius: the rays' samples sit near the decoder's surfaces, not the synthetic walls)
+    pts_g = pnr_mod.NeuralPoints(xyz.to(dev), feats.to(dev), mode='idw', radius=0.03, k=8,
                                  feat_dtype='float16').to(dev)
     ms = MapStep(r, make_decoder(pnr_mod, params, dev, 'f16x3'), points=pts_g, feat_lr=1e-3)
-    map_grad_parity(pnr_mod, ms, params, bound, xyz, feats16, ro, rd, d.float(), 0.008, 'f16x3', seed=8)
+    map_grad_parity(pnr_mod, ms, params, bound, xyz, feats16, ro, rd, d.float(), 0.03, 'f16x3', seed=8)
     # Mapper iterations at 5,000 pixels with the 1M f16-feature cloud
     g = torch.Generator().manual_seed(5)
     pix = torch.randint(0, 720 * 1280, (5000,), generator=g)

@@ -4,11 +4,13 @@ the CPU oracle (oracle/ref_points.py) and the reference's grid_sample decoder fi
 (tests/golden/points_c32.npz).
 
 Tolerances: gather idx exact; c / weights 1e-5 * max; raw 2e-5 * max; depth / colour 1e-4 rel
-(north_star).  Gradients of the reference's grid decoder (points_c32.npz): ELEMENTWISE, rtol 1e-3
-with atol 1e-6 * max|g| against the correctly-rounded gradient (tests/golden/grads_cr.npz `pts/*`)
-and atol (1e-6 + golden_vs_cr) * max|g| against the reference's float32 gradient.  Render /
-regulation with IDW features vs the float32 oracle: elementwise rtol 1e-3, atol 2e-5 * max|g| (the
-oracle's own float32 rounding, no correctly-rounded yardstick for these).
+(north_star).  Gradients ELEMENTWISE (grad_elementwise): rtol 1e-3 with atol (1e-6 + d32) * max|g|
+against the correctly-rounded gradient (every decoder / fc_c GEMM and the Fourier backward summed in
+float64 and rounded, oracle.ref_points.mlp_forward_c_cr), d32 = the float32 gradient's own distance
+from it (max |g_f32 - g_cr| / max |g_cr|), and rtol 1e-3 with atol (1e-6 + d32) * max|g| against
+the float32 gradient.  For the reference's grid decoder (points_c32.npz) the correctly-rounded
+gradient is the fixture tests/golden/grads_cr.npz `pts/*` and the float32 one the reference's own;
+for the IDW render / regulation / tracking cases both are the oracle's, formed in the test.
 """
 import numpy as np
 import pytest
@@ -44,16 +46,17 @@ def pnr_mod():
     return pnr
 
 
-def grad_elementwise(g, cr, f32, rel_f32, what, rtol=1e-3, atol=1e-6):
-    """|g - g_cr| <= rtol |g_cr| + atol max|g_cr| and |g - g_f32| <= rtol |g_f32| + (atol + rel_f32) max|g_f32|
-    elementwise (g_f32 = the reference's float32 gradient, rel_f32 * max from the correctly-rounded one)."""
+def grad_elementwise(g, cr, f32, what, rel_f32=None, rtol=1e-3, atol=1e-6):
+    """|g - g_cr| <= rtol |g_cr| + (atol + d32) max|g_cr| and |g - g_f32| <= rtol |g_f32| + (atol + d32)
+    max|g_f32| elementwise, d32 = rel_f32 or max |g_f32 - g_cr| / max |g_cr|."""
     g = g.detach().cpu().numpy() if isinstance(g, torch.Tensor) else np.asarray(g)
-    refs = ((cr, atol, 'correctly rounded'),) if cr is not None else ()
-    for ref, a_rel, tag in refs + ((f32, atol + float(rel_f32), 'float32'),):
-        ref = np.asarray(ref)
-        a = a_rel * max(np.abs(ref).max(), 1e-30)
+    cr, f32 = (t.detach().cpu().numpy() if isinstance(t, torch.Tensor) else np.asarray(t) for t in (cr, f32))
+    scale = max(np.abs(cr).max(), 1e-30)
+    d32 = float(rel_f32) if rel_f32 is not None else float(np.abs(f32 - cr).max() / scale)
+    for ref, tag in ((cr, 'correctly rounded'), (f32, 'float32')):
+        a = (atol + d32) * max(np.abs(ref).max(), 1e-30)
         viol = np.abs(g - ref) / (rtol * np.abs(ref) + a)
-        print(f'{what} vs {tag}: worst |g - g_ref| / (rtol |g_ref| + atol) = {viol.max():.3f}')
+        print(f'{what} vs {tag} (d32 {d32:.2e}): worst |g - g_ref| / (rtol |g_ref| + atol) = {viol.max():.3f}')
         np.testing.assert_allclose(g, ref, rtol=rtol, atol=a, err_msg=f'{what} vs {tag}')
 
 
@@ -61,11 +64,6 @@ def close(a, b, atol, what, rtol=0.0):
     a = a.detach().cpu().numpy() if isinstance(a, torch.Tensor) else np.asarray(a)
     b = b.detach().cpu().numpy() if isinstance(b, torch.Tensor) else np.asarray(b)
     np.testing.assert_allclose(a, b, rtol=rtol, atol=atol, err_msg=what)
-
-
-# the float32 oracle's own summation-order rounding (a different order than any GPU sum), the absolute
-# floor (x max|g|) of the elementwise comparisons against it where no correctly-rounded gradient exists
-ORACLE_F32 = 2e-5
 
 
 def grid_setup(pnr, dev):
@@ -170,10 +168,10 @@ def test_decoder_c32_matches_reference(pnr_mod, dev):
     (raw * torch.from_numpy(g['g_raw']).to(dev)).sum().backward()
     CR = load_golden('grads_cr.npz')
     for k, t in dec.named_parameters():
-        grad_elementwise(t.grad, CR[f'pts/grad/{k}'], g['grad/' + k], CR[f'golden_vs_cr/pts/{k}'], k)
+        grad_elementwise(t.grad, CR[f'pts/grad/{k}'], g['grad/' + k], k, CR[f'golden_vs_cr/pts/{k}'])
     ref = RP.grid_features(torch.from_numpy(g['grad_grid'])).numpy()
-    grad_elementwise(pts.feats.grad, CR['pts/grad_feats'], ref, CR['golden_vs_cr/pts/grad_feats'], 'dL/dgrid')
-    grad_elementwise(p.grad, CR['pts/grad_p'], g['grad_p'], CR['golden_vs_cr/pts/grad_p'], 'dL/dp')
+    grad_elementwise(pts.feats.grad, CR['pts/grad_feats'], ref, 'dL/dgrid', CR['golden_vs_cr/pts/grad_feats'])
+    grad_elementwise(p.grad, CR['pts/grad_p'], g['grad_p'], 'dL/dp', CR['golden_vs_cr/pts/grad_p'])
 
 
 def test_fc_weight_scale_covers_every_weight(pnr_mod, dev):
@@ -235,19 +233,23 @@ def test_render_with_points_matches_oracle(pnr_mod, dev, mode):
     loss = (d - gt.to(dev).double()).abs().sum() + 0.05 * (col * gc_).sum() + 1e-3 * v.sum()
     loss.backward()
 
-    ref_p = {k: t.clone().requires_grad_(True) for k, t in params.items()}
-    fr = feats.clone().requires_grad_(True)
-    pdict = dict(xyz=xyz, feats=fr, mode=mode, radius=0.04, spacing=[0.03] * 3, k=8, eps=1e-6)
-    ev = lambda q: RP.eval_points_c(ref_p, q, bound, pdict)  # noqa: E731
-    dr, vr, cr = RR.render_batch_ray(ref_p, rd, ro, bound, gt_depth=gt, eval_fn=ev)
-    lr = (dr - gt.double()).abs().sum() + 0.05 * (cr * gc_.cpu()).sum() + 1e-3 * vr.sum()
-    lr.backward()
-    close(d, dr, 0, 'depth', rtol=1e-4)
-    close(col, cr, 2e-5, 'rgb', rtol=1e-4)
-    close(v, vr, 1e-8, 'var', rtol=2e-3)
+    refs = {}
+    for cr_ in (False, True):
+        ref_p = {k: t.clone().requires_grad_(True) for k, t in params.items()}
+        fr = feats.clone().requires_grad_(True)
+        pdict = dict(xyz=xyz, feats=fr, mode=mode, radius=0.04, spacing=[0.03] * 3, k=8, eps=1e-6)
+        ev = lambda q: RP.eval_points_c(ref_p, q, bound, pdict, cr=cr_)  # noqa: E731
+        dr, vr, cr = RR.render_batch_ray(ref_p, rd, ro, bound, gt_depth=gt, eval_fn=ev)
+        lr = (dr - gt.double()).abs().sum() + 0.05 * (cr * gc_.cpu()).sum() + 1e-3 * vr.sum()
+        lr.backward()
+        refs[cr_] = ({k: t.grad for k, t in ref_p.items()}, fr.grad)
+        if not cr_:
+            close(d, dr, 0, 'depth', rtol=1e-4)
+            close(col, cr, 2e-5, 'rgb', rtol=1e-4)
+            close(v, vr, 1e-8, 'var', rtol=2e-3)
     for k, t in dec.named_parameters():
-        grad_elementwise(t.grad, None, ref_p[k].grad.numpy(), ORACLE_F32, k)
-    grad_elementwise(pts.feats.grad, None, fr.grad.numpy(), ORACLE_F32, 'dL/dfeats')
+        grad_elementwise(t.grad, refs[True][0][k], refs[False][0][k], k)
+    grad_elementwise(pts.feats.grad, refs[True][1], refs[False][1], 'dL/dfeats')
 
 
 def test_tracking_ray_grads_with_points(pnr_mod, dev):
@@ -267,14 +269,17 @@ def test_tracking_ray_grads_with_points(pnr_mod, dev):
     rdd = rd.to(dev).requires_grad_(True)
     d, v, col = r.render_batch_ray({'points_color': pts}, dec, rdd, rod, dev, 'color', gt_depth=gt.to(dev))
     ((d - gt.to(dev).double()).abs() / torch.sqrt(v.detach() + 1e-10)).sum().backward()
-    ror = ro.clone().requires_grad_(True)
-    rdr = rd.clone().requires_grad_(True)
-    pdict = dict(xyz=xyz, feats=feats, mode='idw', radius=0.04, k=8, eps=1e-6)
-    ev = lambda q: RP.eval_points_c(params, q, bound, pdict)  # noqa: E731
-    dr, vr, _ = RR.render_batch_ray(params, rdr, ror, bound, gt_depth=gt, eval_fn=ev)
-    ((dr - gt.double()).abs() / torch.sqrt(vr.detach() + 1e-10)).sum().backward()
-    grad_elementwise(rod.grad, None, ror.grad.numpy(), ORACLE_F32, 'dL/drays_o')
-    grad_elementwise(rdd.grad, None, rdr.grad.numpy(), ORACLE_F32, 'dL/drays_d')
+    refs = {}
+    for cr_ in (False, True):
+        ror = ro.clone().requires_grad_(True)
+        rdr = rd.clone().requires_grad_(True)
+        pdict = dict(xyz=xyz, feats=feats, mode='idw', radius=0.04, k=8, eps=1e-6)
+        ev = lambda q: RP.eval_points_c(params, q, bound, pdict, cr=cr_)  # noqa: E731
+        dr, vr, _ = RR.render_batch_ray(params, rdr, ror, bound, gt_depth=gt, eval_fn=ev)
+        ((dr - gt.double()).abs() / torch.sqrt(vr.detach() + 1e-10)).sum().backward()
+        refs[cr_] = (ror.grad, rdr.grad)
+    grad_elementwise(rod.grad, refs[True][0], refs[False][0], 'dL/drays_o')
+    grad_elementwise(rdd.grad, refs[True][1], refs[False][1], 'dL/drays_d')
 
 
 def test_regulation_with_points(pnr_mod, dev):
@@ -292,16 +297,20 @@ def test_regulation_with_points(pnr_mod, dev):
     r = make_renderer(pnr_mod, bound)
     s = r.regulation({'points_color': pts}, dec, rd.to(dev), ro.to(dev), gt.to(dev), dev, t_rand=t_rand.to(dev))
     s.abs().sum().backward()
-    ref_p = {k: t.clone().requires_grad_(True) for k, t in params.items()}
-    fr = feats.clone().requires_grad_(True)
-    pdict = dict(xyz=xyz, feats=fr, mode='idw', radius=0.05, k=8, eps=1e-6)
-    sr = RR.regulation(ref_p, rd, ro, gt, bound, t_rand=t_rand,
-                       eval_fn=lambda q: RP.eval_points_c(ref_p, q, bound, pdict))
-    sr.abs().sum().backward()
-    close(s, sr, 2e-5 * sr.abs().max().item(), 'sigma')
-    grad_elementwise(pts.feats.grad, None, fr.grad.numpy(), ORACLE_F32, 'dL/dfeats')
+    refs = {}
+    for cr_ in (False, True):
+        ref_p = {k: t.clone().requires_grad_(True) for k, t in params.items()}
+        fr = feats.clone().requires_grad_(True)
+        pdict = dict(xyz=xyz, feats=fr, mode='idw', radius=0.05, k=8, eps=1e-6)
+        sr = RR.regulation(ref_p, rd, ro, gt, bound, t_rand=t_rand,
+                           eval_fn=lambda q: RP.eval_points_c(ref_p, q, bound, pdict, cr=cr_))
+        sr.abs().sum().backward()
+        refs[cr_] = ({k: t.grad for k, t in ref_p.items()}, fr.grad)
+        if not cr_:
+            close(s, sr, 2e-5 * sr.abs().max().item(), 'sigma')
+    grad_elementwise(pts.feats.grad, refs[True][1], refs[False][1], 'dL/dfeats')
     for k, t in dec.named_parameters():
-        grad_elementwise(t.grad, None, ref_p[k].grad.numpy(), ORACLE_F32, k)
+        grad_elementwise(t.grad, refs[True][0][k], refs[False][0][k], k)
 
 
 def test_gather_f16_features_equal_rounded_fp32(pnr_mod, dev):

@@ -104,7 +104,7 @@ def _elementwise(g, cr, f32, what):
     atol = (1e-6 + d32) * scale
     viol = np.abs(g - cr) / (1e-3 * np.abs(cr) + atol)
     print(f'{what}: float32 oracle vs cr {d32:.2e} max; worst |g - g_cr| / (rtol |g_cr| + atol) = {viol.max():.3f}')
-    np.testing.assert_allclose(g, cr, rtol=1e-3, atol=atol, err_msg=what)
+    return viol.max()
 
 
 def test_c4_scannet_map_step(pnr_mod, dev, scannet, precision):
@@ -137,10 +137,12 @@ def test_c4_scannet_map_step(pnr_mod, dev, scannet, precision):
     assert abs(loss - refs['f32'][0]) <= 1e-5 * abs(refs['f32'][0])
     from pnr.decoder import PARAM_ORDER
     off = 0
+    worst = {}
     for k, t in zip(PARAM_ORDER, ms.flat.params):
         gk = ms.flat.grad[off:off + t.numel()].view_as(t)
         off += t.numel()
-        _elementwise(gk, refs['cr'][1][k], refs['f32'][1][k], f'{precision} C4 map grad {k}')
+        worst[k] = _elementwise(gk, refs['cr'][1][k], refs['f32'][1][k], f'{precision} C4 map grad {k}')
+    assert max(worst.values()) <= 1.0, worst
 
 
 def test_c4_scannet_track_step(pnr_mod, dev, scannet, precision):
@@ -180,7 +182,7 @@ def test_c4_scannet_track_step(pnr_mod, dev, scannet, precision):
         refs[tag] = (lr_.item(), ctr.grad.numpy().copy())
     print(f'C4 track loss: HIP {float(loss):.6f}, oracle {refs["f32"][0]:.6f}')
     assert abs(float(loss) - refs['f32'][0]) <= 1e-4 * abs(refs['f32'][0])
-    _elementwise(ct.grad, refs['cr'][1], refs['f32'][1], f'{precision} C4 camera tensor grad')
+    assert _elementwise(ct.grad, refs['cr'][1], refs['f32'][1], f'{precision} C4 camera tensor grad') <= 1.0
     # the per-frame loop at the config's lr: 20 iterations from the perturbed pose
     best, _, losses = pnr_mod.track_frame(step_for(12), ct0.to(dev), gc, gd, 20, TRACK_LR, TRACK_PIXELS)
     print(f'C4 tracking losses {losses[0]:.4f} -> {min(losses):.4f}')
