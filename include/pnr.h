@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define PNR_ABI_VERSION 8
+#define PNR_ABI_VERSION 9
 #define PNR_N_PARAMS 11
 #define PNR_MAX_SAMPLES 64      /* N_samples + N_importance per ray */
 #define PNR_C_DIM 32            /* neural-point feature width (decoder.py:122-125 fc_c input) */
@@ -258,13 +258,35 @@ int pnr_adam_step_dev(float* p, const float* g, float* m, float* v, int64_t n, f
                       float beta2, float eps, const int32_t* step_count, void* stream);
 int pnr_step_advance(int32_t* step_count, void* stream);
 
+/* Mapper loss terms and their gradients (src/Mapper.py:628-655, the loss of Mapper.optimize_map
+ * built from render_batch_ray's depth / colour and regulation's sigma), in one pass (ABI 9):
+ *   *loss   = sum_{i<n, gt_depth_i > 0} |gt_depth_i - depth_i| + w_color sum_{i<n} |gt_color_i - color_i|_1
+ *           + w_reg sum_{j<n_sigma} |sigma_j|                                          (float64)
+ *   g_depth = -sign(gt_depth - depth) [gt_depth > 0]  (float64, n)
+ *   g_color = -w_color sign(gt_color - color)         (float32, n x 3)
+ *   g_sigma = w_reg sign(sigma)                       (float32, n_sigma)
+ * sign(0) = 0 as torch's abs backward.  Either part may be empty (n = 0 or n_sigma = 0, its
+ * pointers NULL).  The sum has a fixed order (deterministic).  workspace:
+ * pnr_map_loss_workspace_bytes() bytes of device scratch.  Replaces the ~20 elementwise / reduction
+ * launches the torch form of the loss and its autograd backward cost per iteration. */
+size_t pnr_map_loss_workspace_bytes(void);
+int pnr_map_loss(const float* gt_depth, const double* depth, const float* gt_color, const float* color, int64_t n,
+                 float w_color, const float* sigma, int64_t n_sigma, float w_reg, double* loss, double* g_depth,
+                 float* g_color, float* g_sigma, void* workspace, void* stream);
+
 /* ---- diagnostics (not on the reference API) ----------------------------------------------- */
 /* Kernel timing: while enabled, every launch of the timed kernels is bracketed by hipEvents on
  * its own stream.  pnr_timing_read synchronises those events and returns, for `kernel`
- * (0 = fused MLP forward k_mlp_fwd, 1 = MLP delta-chain k_mlp_bwd, 2 = ray kernels, 3 = weight-
- * gradient GEMMs k_wgrad, units = points of the K dimension), the launch
- * count, the summed device milliseconds and the summed number of points (MLP) or rays processed,
- * then clears that kernel's record.  Process-global, mutex-protected; off by default. */
+ *   0 = fused MLP forward (k_mlp_fwd / k_mlp_fwd16), units = points
+ *   1 = MLP delta chain (k_mlp_bwd / k_mlp_bwd16), units = points
+ *   2 = ray kernels, units = rays
+ *   3 = weight-gradient GEMMs (k_wgrad / k_wgrad16 / k_wgrad_skinny, each with its fixed-order
+ *       partial reduction k_part_reduce), units = points of the K dimension
+ *   4 = neural-point gather (pnr_point_gather and the render's gathers: probe, group scan /
+ *       scatter and search as one bracket), units = samples
+ *   5 = neural-point gather backward (k_gather_bwd_probe + k_gather_bwd), units = samples
+ * the launch count, the summed device milliseconds and the summed units, then clears that
+ * kernel's record.  Process-global, mutex-protected; off by default. */
 int pnr_timing_enable(int on);
 int pnr_timing_read(int kernel, int64_t* launches, double* ms, int64_t* units);
 

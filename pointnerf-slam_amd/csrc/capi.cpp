@@ -45,6 +45,8 @@ int launch_adam(float*, const float*, float*, float*, int64_t, float, float, flo
 int launch_adam_dev(float*, const float*, float*, float*, int64_t, float, float, float, float, const int32_t*,
                     hipStream_t);
 int launch_step_advance(int32_t*, hipStream_t);
+int launch_map_loss(const float*, const double*, const float*, const float*, int64_t, float, const float*, int64_t,
+                    float, double*, double*, double*, float*, float*, hipStream_t);
 
 }  // namespace pnr
 
@@ -62,6 +64,21 @@ std::vector<TimedLaunch> g_tl[kTimeKinds];
 }  // namespace
 
 namespace pnr {
+int device_cu_count() {
+  static std::mutex mu;
+  static int cached[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0) dev = 0;
+  const int slot = dev < 64 ? dev : 63;
+  std::lock_guard<std::mutex> g(mu);
+  if (cached[slot] <= 0) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cached[slot] = n;
+  }
+  return cached[slot];
+}
+
 TimingScope::TimingScope(int k, int64_t u, hipStream_t s) : st(s), kind(k), units(u) {
   bool on;
   {
@@ -806,6 +823,18 @@ int pnr_adam_step_dev(float* p, const float* g, float* m, float* v, int64_t n, f
                       float eps, const int32_t* step_count, void* stream) {
   if (n < 0 || !step_count || (n > 0 && (!p || !g || !m || !v))) return PNR_E_ARG;
   return launch_adam_dev(p, g, m, v, n, lr, beta1, beta2, eps, step_count, (hipStream_t)stream);
+}
+
+size_t pnr_map_loss_workspace_bytes(void) { return 256 * sizeof(double); }
+
+int pnr_map_loss(const float* gt_depth, const double* depth, const float* gt_color, const float* color, int64_t n,
+                 float w_color, const float* sigma, int64_t n_sigma, float w_reg, double* loss, double* g_depth,
+                 float* g_color, float* g_sigma, void* workspace, void* stream) {
+  if (n < 0 || n_sigma < 0 || !loss || !workspace) return PNR_E_ARG;
+  if (n > 0 && (!gt_depth || !depth || !gt_color || !color || !g_depth || !g_color)) return PNR_E_ARG;
+  if (n_sigma > 0 && (!sigma || !g_sigma)) return PNR_E_ARG;
+  return launch_map_loss(gt_depth, depth, gt_color, color, n, w_color, sigma, n_sigma, w_reg,
+                         static_cast<double*>(workspace), loss, g_depth, g_color, g_sigma, (hipStream_t)stream);
 }
 
 int pnr_step_advance(int32_t* step_count, void* stream) {

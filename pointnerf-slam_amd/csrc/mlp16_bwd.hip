@@ -558,13 +558,7 @@ static int launch_bwd16(const float* packed, const BwdArgs& a, int64_t P, hipStr
   // at most one workgroup per CU
   int64_t nwg = (P + 127) / 128;
   if (BfBwd<HASC>::PST) {
-    static const int ncu = [] {
-      int dev = 0, n = 0;
-      if (hipGetDevice(&dev) != hipSuccess ||
-          hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
-        n = 256;
-      return n;
-    }();
+    const int ncu = device_cu_count();
     nwg = nwg < ncu ? nwg : ncu;
   }
   hipLaunchKernelGGL(kern, dim3((unsigned)nwg), dim3(256), lds, st, packed, a, P);

@@ -278,13 +278,7 @@ int launch_mlp_fwd_bf(int prec, const float* packed, const PointSrc& src, int mo
   // on at most one workgroup per CU
   int64_t nwg = (P + 127) / 128;
   if (!hasc) {
-    static const int ncu = [] {
-      int dev = 0, n = 0;
-      if (hipGetDevice(&dev) != hipSuccess ||
-          hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
-        n = 256;
-      return n;
-    }();
+    const int ncu = device_cu_count();
     nwg = nwg < ncu ? nwg : ncu;
   }
   const dim3 grid((unsigned)nwg);

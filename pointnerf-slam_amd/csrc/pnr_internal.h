@@ -264,6 +264,10 @@ int launch_wgrad_fourier16(const float4* xP, const float* garg, int64_t K, float
 
 inline int hip_status(hipError_t e) { return e == hipSuccess ? 0 : (int)e; }
 
+// compute units of the current device (cached per device; 256 if the query fails): the grid cap of
+// the persistent kernels
+int device_cu_count();
+
 
 // Diagnostics: bracket a launch with hipEvents when pnr_timing_enable(1) (capi.cpp).
 enum TimedKernel : int {

@@ -10,19 +10,23 @@
 // collision flag}, one 16-B sub-cell end-offset table per bucket, and an occupancy filter (one
 // bit per hashed probe-block base cell).
 //
-// Gather, two passes:
+// Gather (launch_gather), the samples grouped by probe block:
 //   k_gather_probe  one thread per sample row: coalesced zero fill of the block's output rows,
-//                   occupancy-filter test of the sample's 2x2x2 probe block; samples that may have
-//                   neighbours go to a work list (one atomic per wave, 64 sub-lists).  Free space -- most of a
-//                   ray -- costs one L2-resident bit load.
-//   k_gather_search persistent blocks over the work list (grid = resident blocks), one thread per
-//                   sample: 8 bucket headers and sub-cell tables (foreign buckets of a hash collision
-//                   are skipped by their key); per probe cell one span from the first to the last
-//                   sub-cell (half-cell) the reach box touches, the spans compacted into the
-//                   thread's LDS row and scanned by ONE flat candidate loop (uniform exit, next span
-//                   read ahead); a branch-free top-k network on packed (d2, index) float64 keys
-//                   (v_min/v_max_f64, 2 VALU per stage); normalised weights, then the feature sum
-//                   with 8 lanes per sample.
+//                   occupancy-filter test of the sample's 2x2x2 probe block; a sample that may have
+//                   neighbours takes a slot in its block's group (one counter per group-table entry,
+//                   the block's base cell hashed) and goes to a work list (one atomic per wave, 64
+//                   sub-lists).  Free space -- most of a ray -- costs one L2-resident bit load.
+//   k_scan_*        exclusive scan of the group counts -> group start offsets.
+//   k_group_scatter work items -> the grouped list (group start + slot): the samples of one probe
+//                   block are contiguous.
+//   k_gather_search persistent waves over 64-item chunks of the grouped list.  Per probe block in
+//                   the chunk (usually one or two): lanes 0..7 load the 8 bucket headers, the wave
+//                   stages the block's candidate points into LDS with coalesced loads (one global
+//                   round trip per 64 candidates, shared by every sample of the block), then every
+//                   lane of the block scans the staged list by broadcast LDS reads; the top-k network
+//                   on packed (d2, index) float64 keys (v_min/v_max_f64, 2 VALU per stage) runs only
+//                   for candidates that some lane keeps (ballot).  Normalised weights, then the
+//                   feature sum with 8 lanes per sample.
 //   k_gather_bwd    dL/df_i += w_k dL/dc (float atomics) and dL/dp through the weights.
 #include <mutex>
 
@@ -369,6 +373,7 @@ struct WorkList {
   uint32_t* cnt;   // [kLists * 32], counter r at cnt[32 r]
   float4* items;   // [kLists][cap]
   int64_t cap;     // per sub-list capacity
+  int2* aux;       // [kLists][cap] (group, slot in the group) of each item, or null
 };
 
 static int64_t wl_cap(int64_t rows) {
@@ -381,10 +386,49 @@ static WorkList wl_view(void* ws, int64_t rows) {
   w.cnt = static_cast<uint32_t*>(ws);
   w.items = reinterpret_cast<float4*>(static_cast<char*>(ws) + kLists * 32 * 4);
   w.cap = wl_cap(rows);
+  w.aux = nullptr;
   return w;
 }
 
-__device__ __forceinline__ void wl_append(const WorkList& wl, bool has, const float4& item) {
+// Group table of the forward gather: G = 2^gbits counters, one per hashed probe-block base cell
+// (a few blocks may share an entry; the search separates them), sized from the sample count
+static int group_bits(int64_t P) {
+  int b = 10;
+  while (b < 22 && (1ll << b) < P / 32) ++b;
+  return b;
+}
+struct GroupView {
+  WorkList wl;       // items + aux
+  int32_t* gcnt;     // [G]
+  int32_t* gstart;   // [G + 1]
+  int32_t* scratch;  // scan scratch
+  float4* grouped;   // [P] items in group order
+  int gbits;
+};
+static GroupView group_view(void* ws, int64_t P, size_t* bytes) {
+  GroupView v{};
+  char* b = static_cast<char*>(ws);
+  size_t off = 0;
+  auto take = [&](size_t n) {
+    char* p = b ? b + off : nullptr;
+    off += a256(n);
+    return p;
+  };
+  char* wl = take(wl_bytes(P));
+  v.wl = wl_view(wl, P);
+  v.wl.aux = reinterpret_cast<int2*>(take((size_t)kLists * v.wl.cap * 8));
+  v.gbits = group_bits(P);
+  const int64_t G = 1ll << v.gbits;
+  v.gcnt = reinterpret_cast<int32_t*>(take((size_t)G * 4));
+  v.gstart = reinterpret_cast<int32_t*>(take((size_t)(G + 1) * 4));
+  v.scratch = reinterpret_cast<int32_t*>(take((size_t)scan_scratch_ints(G) * 4));
+  v.grouped = reinterpret_cast<float4*>(take((size_t)(P > 0 ? P : 1) * 16));
+  if (bytes) *bytes = off;
+  return v;
+}
+
+__device__ __forceinline__ void wl_append(const WorkList& wl, bool has, const float4& item,
+                                          int2 aux = make_int2(0, 0)) {
   const uint64_t m = __ballot(has);
   if (m == 0) return;
   const int lane = threadIdx.x & 63;
@@ -393,7 +437,11 @@ __device__ __forceinline__ void wl_append(const WorkList& wl, bool has, const fl
   uint32_t base = 0;
   if (lane == leader) base = atomicAdd(wl.cnt + r * 32, (uint32_t)__popcll(m));
   base = __shfl(base, leader);
-  if (has) wl.items[(int64_t)r * wl.cap + base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = item;
+  if (has) {
+    const int64_t at = (int64_t)r * wl.cap + base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+    wl.items[at] = item;
+    if (wl.aux) wl.aux[at] = aux;
+  }
 }
 
 struct GatherArgs {
@@ -415,6 +463,10 @@ struct GatherArgs {
   int32_t* idx;          // (rows, k) or null
   float* w;              // (rows, k) or null
   WorkList wl;           // (x, y, z, sample row bits) of the samples that may have neighbours
+  int32_t* gcnt;         // [G] samples per group (probe block base cell hashed with gmask)
+  const int32_t* gstart; // [G + 1] group start offsets in `grouped`; gstart[G] = all items
+  float4* grouped;       // the work items in group order
+  uint32_t gmask;        // G - 1
 };
 
 // Pass 1, one thread per sample row: the occupancy bit of each sample's probe block; the hits go
@@ -428,15 +480,20 @@ __global__ __launch_bounds__(256) void k_gather_probe(GatherArgs a) {
   const int64_t p = r0 + threadIdx.x;
   float x0 = 0.f, x1 = 0.f, x2 = 0.f;
   bool has = false;
+  int bx = 0, by = 0, bz = 0;
   if (p < a.P) {
     bool inside;
     load_point<SRC>(a.src, p, x0, x1, x2, inside);
-    int bx, by, bz;
     base_cell(x0, a.g.o0, a.g.inv, bx);
     base_cell(x1, a.g.o1, a.g.inv, by);
     base_cell(x2, a.g.o2, a.g.inv, bz);
     const uint32_t bit = cell_hash(bx, by, bz, a.g.omask);
     has = (a.occ[bit >> 5] >> (bit & 31u)) & 1u;
+  }
+  int2 gs = make_int2(0, 0);  // (group, slot in the group)
+  if (has) {
+    gs.x = (int)cell_hash(bx, by, bz, a.gmask);
+    gs.y = atomicAdd(a.gcnt + gs.x, 1);
   }
   s_has[threadIdx.x] = has ? 1 : 0;
   __syncthreads();
@@ -461,34 +518,17 @@ __global__ __launch_bounds__(256) void k_gather_probe(GatherArgs a) {
       }
     }
   }
-  wl_append(a.wl, has, make_float4(x0, x1, x2, __int_as_float((int)p)));
+  wl_append(a.wl, has, make_float4(x0, x1, x2, __int_as_float((int)p)), gs);
 }
 
-// Pass 2, persistent blocks over the work list, one thread per sample.  A thread's non-empty
-// probe ranges (own bucket whole; colliding bucket with a per-point cell test; foreign bucket not
-// at all) are compacted into its LDS row, so the candidate loop is ONE flat loop over all of them
-// (trip count = the wave's largest candidate total) with the next range read ahead.  Top-k is a
-// branch-free insertion network on (d2, index) keys packed into positive doubles (their order is
-// the lexicographic one): v_min_f64 / v_max_f64 by inline asm, 2 VALU per stage (the builtins add
-// an IEEE canonicalisation per operand).  The feature sum then runs 8 lanes per sample, 4 feature
-// rows in flight per lane.
-// end offset of sub-cell k (0..7) in a bucket's sub table (8 x u16)
-__device__ __forceinline__ int sub_end(const int4& sb, int k) {
-  const int w = k < 2 ? sb.x : (k < 4 ? sb.y : (k < 6 ? sb.z : sb.w));
-  return (int)(((uint32_t)w >> (16 * (k & 1))) & 0xFFFFu);
-}
-// per axis: bits 2c+h (c = block cell 0/1, h = half) of the half-cells that [u - rho', u + rho']
-// touches, u = (x - o) * inv as in cell_coord and b = the block's first cell
-__device__ __forceinline__ uint32_t half_mask(float x, float o, float inv, float rho, int b) {
-  PNR_FP_STRICT
-  float u = (x - o) * inv;
-  u = fminf(fmaxf(u, -1.0e9f), 1.0e9f);
-  const float r = rho + fabsf(u) * 6.0e-7f;
-  const int lo = (int)floorf(2.0f * (u - r)) - 2 * b, hi = (int)floorf(2.0f * (u + r)) - 2 * b;
-  uint32_t m = 0;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) m |= (lo <= k && k <= hi) ? (1u << k) : 0u;
-  return m;
+// work items -> the grouped list: grouped[gstart[group] + slot]
+__global__ __launch_bounds__(256) void k_group_scatter(GatherArgs a) {
+  const int r = (int)(blockIdx.x % kLists);
+  const int64_t i = (int64_t)(blockIdx.x / kLists) * 256 + threadIdx.x;
+  if (i >= (int64_t)a.wl.cnt[r * 32]) return;
+  const int64_t at = (int64_t)r * a.wl.cap + i;
+  const int2 gs = a.wl.aux[at];
+  a.grouped[a.gstart[gs.x] + gs.y] = a.wl.items[at];
 }
 
 // one network stage: key <- min(key, kn), return max(key, kn); key is updated in place (a tied
@@ -499,117 +539,124 @@ __device__ __forceinline__ double kstage(double& key, double kn) {
   return hi;
 }
 
-// One wave per search block: a round's barriers then never hold a finished wave behind the
-// block's slowest one.  1.25 -> 1.20 ms per gather against 256-thread blocks (128: 1.22 ms;
-// profiles/r01g_gather_occupancy_ablation.txt).
-#ifndef PNR_SEARCH_BLOCK
-#define PNR_SEARCH_BLOCK 64
-#endif
-constexpr int kSearchBlock = PNR_SEARCH_BLOCK;
-union SearchLds {
-  struct {
-    int2 rng[8][kSearchBlock];      // [range][thread] (start, end): conflict-free per-thread access
-    uint8_t cell[8][kSearchBlock];  // probe cell n | 8 if the bucket collides
-  } r;
-  struct {
-    int32_t idx[kSearchBlock * PNR_MAX_K];
-    float w[kSearchBlock * PNR_MAX_K];
-    int32_t row[kSearchBlock];
-  } f;
+// Pass 2: one wave per block, persistent over 64-item chunks of the grouped list.  The samples of a
+// probe block are contiguous there, so a chunk holds one or a few blocks ("segments"): per segment
+// the 8 bucket headers are read by lanes 0..7, the block's candidates (the 8 cells' buckets: own
+// bucket whole, colliding bucket with a per-point cell test, foreign bucket not at all) are staged
+// into LDS kCandBatch at a time by coalesced loads, and every lane of the segment scans them by
+// broadcast LDS reads.  Against a thread per sample walking its own candidates through global
+// memory, a candidate costs one global load per block instead of one per sample.
+constexpr int kCandBatch = 128;
+struct SearchLds {
+  float4 cand[kCandBatch];   // staged candidate points (x, y, z, index bits)
+  uint8_t tag[kCandBatch];   // probe cell n | 8 if its bucket collides
+  int32_t idx[64 * PNR_MAX_K];
+  float w[64 * PNR_MAX_K];
+  int32_t row[64];
 };
 
-// One search round of a block: thread tid searches work item `wk` (x, y, z, row bits) when `has`;
-// block-uniform call (it holds barriers).
+#ifndef PNR_SEARCH_WAVES
+#define PNR_SEARCH_WAVES 7
+#endif
 template <int KER>
-__device__ __forceinline__ void search_round(const GatherArgs& a, SearchLds& L, const float4 wk, const bool has) {
+__global__ __launch_bounds__(64, PNR_SEARCH_WAVES) void k_gather_search(GatherArgs a) {
   PNR_FP_STRICT
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, gq = lane >> 3, q = lane & 7;
+  __shared__ SearchLds L;
+  const int lane = threadIdx.x, gq = lane >> 3, q = lane & 7;
   const double kInf = __longlong_as_double(0x7FF0000000000000ll);
-  {
-    double key[PNR_MAX_K];
-#pragma unroll
-    for (int t = 0; t < PNR_MAX_K; ++t) key[t] = kInf;
+  const int64_t n_items = a.gstart[(int64_t)a.gmask + 1];
+  const int64_t nchunk = (n_items + 63) / 64;
+  for (int64_t chunk = blockIdx.x; chunk < nchunk; chunk += gridDim.x) {
+    const int64_t it = chunk * 64 + lane;
+    const bool has = it < n_items;
     float x0 = 0.f, x1 = 0.f, x2 = 0.f;
-    int row = -1, bx = 0, by = 0, bz = 0, nr = 0;
-    __syncthreads();  // the previous task's feature phase is done with the LDS
+    int row = -1, bx = 0, by = 0, bz = 0;
     if (has) {
+      const float4 wk = a.grouped[it];
       x0 = wk.x; x1 = wk.y; x2 = wk.z;
       row = __float_as_int(wk.w);
       base_cell(x0, a.g.o0, a.g.inv, bx);
       base_cell(x1, a.g.o1, a.g.inv, by);
       base_cell(x2, a.g.o2, a.g.inv, bz);
-      // half-cells (block-relative, 0..3 per axis) that the reach box [u - rho, u + rho] touches;
-      // the margin (2^-10 of rho + 5 ulp of u) covers the f32 rounding of both sides' coordinates
-      const uint32_t am0 = half_mask(x0, a.g.o0, a.g.inv, a.rho0, bx);
-      const uint32_t am1 = half_mask(x1, a.g.o1, a.g.inv, a.rho1, by);
-      const uint32_t am2 = half_mask(x2, a.g.o2, a.g.inv, a.rho2, bz);
-#pragma unroll
-      for (int n0 = 0; n0 < 8; n0 += 4) {  // 4 bucket headers + sub-cell tables in flight at a time
-        int4 h[4], sb[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int n = n0 + u;
-          const uint32_t bk = cell_hash(bx + (n & 1), by + ((n >> 1) & 1), bz + (n >> 2), a.g.mask);
-          h[u] = a.hdr[bk];
-          sb[u] = a.sub[bk];
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int n = n0 + u;
-          const int cx = bx + (n & 1), cy = by + ((n >> 1) & 1), cz = bz + (n >> 2);
-          const uint64_t hk = (uint64_t)(uint32_t)h[u].z | ((uint64_t)(uint32_t)h[u].w << 32);
-          const bool coll = (hk & kCollision) != 0;
-          const bool own = (hk & ~kCollision) == cell_key(cx, cy, cz);
-          // this cell's wanted sub-cells (x fastest) and the one span from the first to the last
-          const uint32_t xm = (am0 >> (2 * (n & 1))) & 3u, ym = (am1 >> (2 * ((n >> 1) & 1))) & 3u,
-                         zm = (am2 >> (2 * (n >> 2))) & 3u;
-          const uint32_t plane = ((ym & 1u) ? xm : 0u) | ((ym & 2u) ? xm << 2 : 0u);
-          const uint32_t m = ((zm & 1u) ? plane : 0u) | ((zm & 2u) ? plane << 4 : 0u);
-          int s0 = h[u].x, s1 = h[u].y;
-          if (m != 0u && (((uint32_t)sb[u].w >> 16) != 0xFFFFu)) {  // an ordered bucket: the span only
-            const int f = __ffs((int)m) - 1, l = 31 - __clz((int)m);
-            s0 = h[u].x + (f == 0 ? 0 : sub_end(sb[u], f - 1));
-            s1 = h[u].x + sub_end(sb[u], l);
-          }
-          if ((coll || own) && m != 0u && s1 > s0) {
-            L.r.rng[nr][tid] = make_int2(s0, s1);
-            L.r.cell[nr][tid] = (uint8_t)(n | (coll ? 8 : 0));
-            ++nr;
-          }
-        }
-      }
     }
-    // flat candidate loop over the nr ranges; uniform over the wave (finished lanes insert +inf, a
-    // no-op), so the key registers are updated in place with no copies at the loop head
-    int jj = 0, je = 0, cf = 0, k = 0;
-    int2 nx = nr > 0 ? L.r.rng[0][tid] : make_int2(0, 0);
-    while (true) {
-      const bool act = jj < je || k < nr;
-      if (__ballot(act) == 0) break;
-      double kn = kInf;
-      if (act) {
-        if (jj >= je) {
-          jj = nx.x;
-          je = nx.y;
-          cf = L.r.cell[k][tid];
-          ++k;
-          if (k < nr) nx = L.r.rng[k][tid];  // read ahead
-        }
-        const float4 qv = a.sorted[jj++];
-        const float d0 = x0 - qv.x, d1 = x1 - qv.y, d2 = x2 - qv.z;
-        const float dd = (d0 * d0 + d1 * d1) + d2 * d2;
-        bool ok;
-        if (KER == PNR_GATHER_IDW) ok = dd <= a.r2;
-        else ok = fabsf(d0) < a.h0 && fabsf(d1) < a.h1 && fabsf(d2) < a.h2;
-        if (cf & 8) {  // colliding bucket: the point must lie in this probe cell
-          ok = ok && cell_coord(qv.x, a.g.o0, a.g.inv) == bx + (cf & 1) &&
-               cell_coord(qv.y, a.g.o1, a.g.inv) == by + ((cf >> 1) & 1) &&
-               cell_coord(qv.z, a.g.o2, a.g.inv) == bz + ((cf >> 2) & 1);
-        }
-        if (ok) kn = pack_key(dd, __float_as_int(qv.w));
-      }
+    double key[PNR_MAX_K];
 #pragma unroll
-      for (int t = 0; t < PNR_MAX_K; ++t) kn = kstage(key[t], kn);
+    for (int t = 0; t < PNR_MAX_K; ++t) key[t] = kInf;
+    uint64_t pending = __ballot(has);
+    while (pending) {  // one segment (= probe block) per trip, wave-uniform
+      const int leader = __ffsll((unsigned long long)pending) - 1;
+      const int lbx = __builtin_amdgcn_readlane(bx, leader), lby = __builtin_amdgcn_readlane(by, leader),
+                lbz = __builtin_amdgcn_readlane(bz, leader);
+      const bool member = ((pending >> lane) & 1ull) && bx == lbx && by == lby && bz == lbz;
+      pending &= ~__ballot(member);
+      // the 8 probe cells' candidate ranges, lane n < 8 for cell n
+      int s0 = 0, len = 0, fl = 0;
+      if (lane < 8) {
+        const int cx = lbx + (lane & 1), cy = lby + ((lane >> 1) & 1), cz = lbz + (lane >> 2);
+        const int4 h = a.hdr[cell_hash(cx, cy, cz, a.g.mask)];
+        const uint64_t hk = (uint64_t)(uint32_t)h.z | ((uint64_t)(uint32_t)h.w << 32);
+        const bool coll = (hk & kCollision) != 0;
+        const bool own = (hk & ~kCollision) == cell_key(cx, cy, cz);
+        if (coll || own) {
+          s0 = h.x;
+          len = h.y - h.x;
+        }
+        fl = lane | (coll ? 8 : 0);
+      }
+      int incl = len;  // inclusive scan over lanes 0..7
+#pragma unroll
+      for (int d = 1; d < 8; d <<= 1) {
+        const int t = __shfl_up(incl, d);
+        if (lane >= d) incl += t;
+      }
+      int cs[8], ce[8], cb[8], cf[8];  // wave-uniform: list start / end, bucket start, tag per cell
+#pragma unroll
+      for (int n = 0; n < 8; ++n) {
+        ce[n] = __builtin_amdgcn_readlane(incl, n);
+        cs[n] = ce[n] - __builtin_amdgcn_readlane(len, n);
+        cb[n] = __builtin_amdgcn_readlane(s0, n);
+        cf[n] = __builtin_amdgcn_readlane(fl, n);
+      }
+      const int total = ce[7];
+      for (int base = 0; base < total; base += kCandBatch) {
+        const int cnt = total - base < kCandBatch ? total - base : kCandBatch;
+#pragma unroll
+        for (int j = lane; j < kCandBatch; j += 64) {
+          if (j < cnt) {
+            const int g = base + j;
+            int src = 0, tg = 0;
+#pragma unroll
+            for (int n = 0; n < 8; ++n) {
+              const bool in = g >= cs[n] && g < ce[n];
+              src = in ? cb[n] + (g - cs[n]) : src;
+              tg = in ? cf[n] : tg;
+            }
+            L.cand[j] = a.sorted[src];
+            L.tag[j] = (uint8_t)tg;
+          }
+        }
+        __syncthreads();
+        for (int j = 0; j < cnt; ++j) {
+          const float4 qv = L.cand[j];
+          const float d0 = x0 - qv.x, d1 = x1 - qv.y, d2 = x2 - qv.z;
+          const float dd = (d0 * d0 + d1 * d1) + d2 * d2;
+          bool ok;
+          if (KER == PNR_GATHER_IDW) ok = dd <= a.r2;
+          else ok = fabsf(d0) < a.h0 && fabsf(d1) < a.h1 && fabsf(d2) < a.h2;
+          ok = ok && member;
+          const int tg = L.tag[j];
+          if (tg & 8) {  // colliding bucket: the point must lie in this probe cell
+            ok = ok && cell_coord(qv.x, a.g.o0, a.g.inv) == lbx + (tg & 1) &&
+                 cell_coord(qv.y, a.g.o1, a.g.inv) == lby + ((tg >> 1) & 1) &&
+                 cell_coord(qv.z, a.g.o2, a.g.inv) == lbz + ((tg >> 2) & 1);
+          }
+          if (__ballot(ok) == 0) continue;  // nobody keeps it: the network would be a no-op
+          double kn = ok ? pack_key(dd, __float_as_int(qv.w)) : kInf;
+#pragma unroll
+          for (int t = 0; t < PNR_MAX_K; ++t) kn = kstage(key[t], kn);
+        }
+        __syncthreads();  // the next batch overwrites the staged list
+      }
     }
     // weights of the first k, normalised by their sequential sum (ascending distance)
     float wv_[PNR_MAX_K];
@@ -635,18 +682,17 @@ __device__ __forceinline__ void search_round(const GatherArgs& a, SearchLds& L, 
       W = W + w;
     }
     const float Wd = W > 0.f ? W : 1.0f;
-    __syncthreads();  // every thread is past its range reads: the LDS becomes the feature lists
-    L.f.row[tid] = row;
+    L.row[lane] = row;
     float wnv[PNR_MAX_K];
 #pragma unroll
     for (int t = 0; t < PNR_MAX_K; ++t) {
       const float wn = ki[t] >= 0 ? wv_[t] / Wd : 0.f;
       wnv[t] = wn;
-      L.f.idx[tid * PNR_MAX_K + t] = ki[t];
-      L.f.w[tid * PNR_MAX_K + t] = wn;
+      L.idx[lane * PNR_MAX_K + t] = ki[t];
+      L.w[lane * PNR_MAX_K + t] = wn;
     }
     if (row >= 0 && a.idx) {
-      // k = 8: the row's 8 indices and 8 weights as 16-B stores (1.37 -> 1.31 ms per gather)
+      // k = 8: the row's 8 indices and 8 weights as 16-B stores
       if (PNR_MAX_K == 8 && a.k == 8 && ((reinterpret_cast<uintptr_t>(a.idx) | reinterpret_cast<uintptr_t>(a.w)) & 15) == 0) {
         int4* i4 = reinterpret_cast<int4*>(a.idx) + (int64_t)row * 2;
         float4* w4 = reinterpret_cast<float4*>(a.w) + (int64_t)row * 2;
@@ -665,8 +711,8 @@ __device__ __forceinline__ void search_round(const GatherArgs& a, SearchLds& L, 
     // feature sum: 8 lanes per sample, lane q owns channels 4q..4q+3
 #pragma unroll 1
     for (int rr = 0; rr < 8; ++rr) {
-      const int sl = wv * 64 + rr * 8 + gq;
-      const int rw = L.f.row[sl];
+      const int sl = rr * 8 + gq;
+      const int rw = L.row[sl];
       if (rw < 0) continue;
       float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
@@ -675,14 +721,14 @@ __device__ __forceinline__ void search_round(const GatherArgs& a, SearchLds& L, 
         float4 f[4];
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
-          id[t] = L.f.idx[sl * PNR_MAX_K + t0 + t];
+          id[t] = L.idx[sl * PNR_MAX_K + t0 + t];
           f[t] = make_float4(0.f, 0.f, 0.f, 0.f);
           if (id[t] >= 0) f[t] = load_feat4(a.feats4, a.feat_half, (int64_t)id[t] * 8 + q);
         }
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
           if (id[t] >= 0) {
-            const float wn = L.f.w[sl * PNR_MAX_K + t0 + t];
+            const float wn = L.w[sl * PNR_MAX_K + t0 + t];
             acc.x = acc.x + wn * f[t].x;
             acc.y = acc.y + wn * f[t].y;
             acc.z = acc.z + wn * f[t].z;
@@ -692,30 +738,7 @@ __device__ __forceinline__ void search_round(const GatherArgs& a, SearchLds& L, 
       }
       nt_store(reinterpret_cast<float4*>(a.c) + (int64_t)rw * 8 + q, acc);  // 8 lanes: one 128-B row
     }
-  }
-}
-
-// Pass 2: persistent blocks over the probe's work list, one search round per kSearchBlock-item chunk.
-template <int KER>
-// The search is latency-bound: 7 waves per SIMD (72 VGPRs, one 8-B spill) instead of the 6 its
-// free allocation gives: 1.31 -> 1.25 ms per gather.  8 waves (64 VGPRs, 11 spills) measured the
-// same as 7; 8 header loads in flight instead of 4 cost 2 waves of occupancy and took 1.49 ms
-// (profiles/r01g_gather_occupancy_ablation.txt).
-#ifndef PNR_SEARCH_WAVES
-#define PNR_SEARCH_WAVES 7
-#endif
-__global__ __launch_bounds__(kSearchBlock, PNR_SEARCH_WAVES) void k_gather_search(GatherArgs a) {
-  __shared__ SearchLds L;
-  const int64_t nchunk = (a.wl.cap + kSearchBlock - 1) / kSearchBlock;
-  for (int64_t task = blockIdx.x; task < kLists * nchunk; task += gridDim.x) {
-    const int r = (int)(task % kLists);
-    const int64_t j0 = task / kLists * kSearchBlock;
-    const int64_t n_work = (int64_t)a.wl.cnt[r * 32];
-    if (j0 >= n_work) continue;  // uniform over the block
-    const int64_t i = j0 + threadIdx.x;
-    const bool has = i < n_work;
-    const float4 wk = has ? a.wl.items[r * a.wl.cap + i] : make_float4(0.f, 0.f, 0.f, 0.f);
-    search_round<KER>(a, L, wk, has);
+    __syncthreads();  // the next chunk rewrites the feature lists
   }
 }
 
@@ -937,7 +960,11 @@ static void gather_probe(int mode, dim3 grid, hipStream_t st, const GatherArgs& 
   }
 }
 
-size_t gather_workspace_bytes(int64_t P) { return wl_bytes(P > 0 ? P : 0); }
+size_t gather_workspace_bytes(int64_t P) {
+  size_t b = 0;
+  group_view(nullptr, P > 0 ? P : 0, &b);
+  return b;
+}
 
 int launch_gather(const pnr_points& pts, const PointSrc& src, int mode, int64_t P, int64_t rows, float* c,
                   int32_t* idx, float* w, void* ws, size_t ws_bytes, hipStream_t st) {
@@ -973,17 +1000,27 @@ int launch_gather(const pnr_points& pts, const PointSrc& src, int mode, int64_t 
   a.c = c;
   a.idx = idx;
   a.w = w;
-  a.wl = wl_view(ws, P);
+  GroupView gv = group_view(ws, P, nullptr);
+  a.wl = gv.wl;
+  a.gcnt = gv.gcnt;
+  a.gstart = gv.gstart;
+  a.grouped = gv.grouped;
+  a.gmask = (uint32_t)((1ll << gv.gbits) - 1);
+  const int64_t G = 1ll << gv.gbits;
   if (hipMemsetAsync(a.wl.cnt, 0, kLists * 32 * 4, st) != hipSuccess) return (int)hipGetLastError();
+  if (hipMemsetAsync(a.gcnt, 0, (size_t)G * 4, st) != hipSuccess) return (int)hipGetLastError();
   TimingScope ts(kTimeGather, P, st);
   gather_probe(mode, dim3((unsigned)((rows + 255) / 256)), st, a);
-  const int64_t tasks = kLists * ((a.wl.cap + kSearchBlock - 1) / kSearchBlock);
+  int rc = scan_exclusive(a.gcnt, gv.gstart, G, gv.scratch, st);
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_group_scatter, dim3((unsigned)(kLists * ((a.wl.cap + 255) / 256))), dim3(256), 0, st, a);
+  const int64_t tasks = (P + 63) / 64;  // upper bound on the chunks (the kernel reads the real count)
   if (pts.mode == PNR_GATHER_IDW) {
     auto kern = k_gather_search<PNR_GATHER_IDW>;
-    hipLaunchKernelGGL(kern, dim3(resident_grid(kern, kSearchBlock, tasks)), dim3(kSearchBlock), 0, st, a);
+    hipLaunchKernelGGL(kern, dim3(resident_grid(kern, 64, tasks)), dim3(64), 0, st, a);
   } else {
     auto kern = k_gather_search<PNR_GATHER_TRILINEAR>;
-    hipLaunchKernelGGL(kern, dim3(resident_grid(kern, kSearchBlock, tasks)), dim3(kSearchBlock), 0, st, a);
+    hipLaunchKernelGGL(kern, dim3(resident_grid(kern, 64, tasks)), dim3(64), 0, st, a);
   }
   return hip_status(hipGetLastError());
 }

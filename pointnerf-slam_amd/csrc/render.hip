@@ -376,6 +376,62 @@ __global__ void k_gout_sigma(const float* __restrict__ g_sigma, const float4* __
 }
 
 // ---------------------------------------------------------------------------------------------
+// Mapper loss (src/Mapper.py:628-655) and its gradient, fused: one pass over the rays / regulation
+// samples writes the gradients and a per-block partial sum, one block adds the partials in a fixed
+// order (deterministic).  Per ray: [gt > 0] |gt - depth| (float64, gt promoted) + w_color
+// sum_c |gt_c - c|; per regulation sample: w_reg |sigma|.  Gradients (torch abs: sign(x) with
+// sign(0) = 0): g_depth = -sign(gt - depth) [gt > 0], g_color = -w_color sign(gt_c - c), g_sigma =
+// w_reg sign(sigma).
+constexpr int kLossParts = 256;
+__device__ __forceinline__ double sgn(double x) { return x > 0.0 ? 1.0 : (x < 0.0 ? -1.0 : 0.0); }
+__device__ __forceinline__ float sgnf(float x) { return x > 0.f ? 1.f : (x < 0.f ? -1.f : 0.f); }
+__global__ __launch_bounds__(256) void k_map_loss(const float* __restrict__ gt, const double* __restrict__ depth,
+                                                  const float* __restrict__ gtc, const float* __restrict__ col,
+                                                  int64_t n, float w_color, const float* __restrict__ sigma,
+                                                  int64_t ns, float w_reg, double* __restrict__ part,
+                                                  double* __restrict__ g_depth, float* __restrict__ g_color,
+                                                  float* __restrict__ g_sigma) {
+  __shared__ double red[4];
+  double acc = 0.0;
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+    const float g = gt[i];
+    const double e = (double)g - depth[i];
+    const bool m = g > 0.f;
+    acc += m ? fabs(e) : 0.0;
+    g_depth[i] = m ? -sgn(e) : 0.0;
+    float cs = 0.f;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const float ec = gtc[i * 3 + c] - col[i * 3 + c];
+      cs += fabsf(ec);
+      g_color[i * 3 + c] = -w_color * sgnf(ec);
+    }
+    acc += (double)(w_color * cs);
+  }
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < ns; i += stride) {
+    const float s = sigma[i];
+    acc += (double)(w_reg * fabsf(s));
+    g_sigma[i] = w_reg * sgnf(s);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+__global__ __launch_bounds__(256) void k_map_loss_sum(const double* __restrict__ part, int parts,
+                                                      double* __restrict__ out) {
+  __shared__ double red[4];
+  double v = (int)threadIdx.x < parts ? part[threadIdx.x] : 0.0;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) out[0] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+// ---------------------------------------------------------------------------------------------
 // rays: dirs = [(i-cx)/fx, -(j-cy)/fy, -1]; rays_d = sum(dirs * c2w[:3,:3], -1); rays_o = c2w[:3,3]
 __device__ __forceinline__ void make_ray(float i, float j, float fx, float fy, float cx, float cy,
                                          const float* __restrict__ c2w, int ld, float* o, float* d) {
@@ -504,6 +560,17 @@ int launch_reg_z(const pnr_render_params& prm, const float* gt, const float* t_r
                  hipStream_t st) {
   if (n <= 0) return 0;
   hipLaunchKernelGGL(k_reg_z, dim3(nblk(n * prm.n_samples, 256)), dim3(256), 0, st, prm, gt, t_rand, n, z);
+  return hip_status(hipGetLastError());
+}
+int launch_map_loss(const float* gt, const double* depth, const float* gtc, const float* col, int64_t n,
+                    float w_color, const float* sigma, int64_t ns, float w_reg, double* part, double* loss,
+                    double* g_depth, float* g_color, float* g_sigma, hipStream_t st) {
+  const int64_t m = n > ns ? n : ns;
+  int parts = (int)((m + 1023) / 1024);
+  parts = parts < 1 ? 1 : (parts > kLossParts ? kLossParts : parts);
+  hipLaunchKernelGGL(k_map_loss, dim3(parts), dim3(256), 0, st, gt, depth, gtc, col, n, w_color, sigma, ns, w_reg,
+                     part, g_depth, g_color, g_sigma);
+  hipLaunchKernelGGL(k_map_loss_sum, dim3(1), dim3(256), 0, st, part, parts, loss);
   return hip_status(hipGetLastError());
 }
 int launch_extract_sigma(const float* raw, int64_t P, float* sigma, hipStream_t st) {

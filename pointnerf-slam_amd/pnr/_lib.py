@@ -24,7 +24,7 @@ PRECISIONS = {'fp32': 0, 'bf16x3': 1, 'bf16': 2, 'f16x3': 3}
 # f16x3: fp32-class forward AND backward (every GEMM on 22-bit split operands with fp32
 # accumulation; tests/test_gpu_parity.py runs every case under fp32 and f16x3 at the same tolerances)
 DEFAULT_PRECISION = os.environ.get('PNR_PRECISION', 'f16x3')
-ABI_VERSION = 8
+ABI_VERSION = 9
 STATUS_F16_RANGE = 1  # include/pnr.h PNR_STATUS_F16_RANGE
 
 
@@ -104,6 +104,9 @@ _SIGS = {
     'pnr_adam_step_dev': (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_float, c_float,
                                          c_float, c_float, c_void_p, c_void_p]),
     'pnr_step_advance': (ctypes.c_int, [c_void_p, c_void_p]),
+    'pnr_map_loss_workspace_bytes': (c_size_t, []),
+    'pnr_map_loss': (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_float, c_void_p, c_int64,
+                                    c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     'pnr_points_index_bytes': (c_size_t, [c_int64, c_int32]),
     'pnr_points_build': (ctypes.c_int, [PPoints, c_void_p]),
     'pnr_point_gather_workspace_bytes': (c_size_t, [c_int64]),

@@ -91,8 +91,16 @@ class Adam:
 
 
 class MapStep:
+    """One Mapper iteration.  The render and the regulation run as two independent chains: the
+    regulation's forward, loss term and backward on a side stream (its own gradient buffer), the
+    render's on the caller's stream; the chains join before the gradients are summed (render +
+    regulation, a fixed order) and Adam runs.  At the faithful batch (1,000 rays) every phase is
+    latency-bound and leaves CUs idle, so the two chains overlap.  Neither chain goes through
+    autograd: pnr.renderer.TrainPass calls the C ABI directly and pnr_map_loss forms the loss and its
+    gradient in one pass.  `overlap=False` runs both chains on the caller's stream."""
+
     def __init__(self, renderer, decoder, lr=2e-4, w_color_loss=0.05, w_reg=0.0005, ddp=None, points=None,
-                 feat_lr=None):
+                 feat_lr=None, overlap=True):
         self.renderer = renderer
         self.decoder = decoder
         self.points = points
@@ -119,6 +127,24 @@ class MapStep:
         self.w_color = w_color_loss
         self.w_reg = w_reg
         self.ddp = ddp
+        self.overlap = overlap
+        dev = self.flat.data.device
+        self.side = torch.cuda.Stream(dev) if overlap else None
+        # the regulation chain's gradient buffer (same layout as flat.grad) and its views
+        self.grad2 = torch.zeros_like(self.flat.grad) if overlap else None
+        self._views = {'main': self._split(self.flat.grad)}
+        if overlap:
+            self._views['side'] = self._split(self.grad2)
+
+    def _split(self, buf):
+        """(11 decoder, 8 fc_c or None, features or None) views of a flat-gradient-shaped buffer."""
+        views, off = [], 0
+        for p in self.flat.params:
+            views.append(buf[off:off + p.numel()].view_as(p))
+            off += p.numel()
+        if self.points is None:
+            return views, None, None
+        return views[:11], views[11:19], views[19]
 
     def _invalidate(self):
         self.decoder._packed.invalidate()
@@ -126,29 +152,51 @@ class MapStep:
             self.decoder._packed_fc.invalidate()
             self.points.invalidate_feats()  # the f16 feature copy, if any
 
-    def loss(self, rays_o, rays_d, gt_depth, gt_color, t_rand=None, far_clamp=None):
-        r, dec = self.renderer, self.decoder
-        dev = rays_o.device
-        d, _, c = r.render_batch_ray(self.c, dec, rays_d, rays_o, dev, 'color', gt_depth, far_clamp=far_clamp)
-        m = gt_depth > 0  # a masked sum, not a masked gather: no host sync, so the step can be captured
-        loss = torch.where(m, torch.abs(gt_depth - d), torch.zeros_like(d)).sum()
-        loss = loss + self.w_color * torch.abs(gt_color - c).sum()
-        sigma = r.regulation(self.c, dec, rays_d, rays_o, gt_depth, dev, 'color', t_rand=t_rand)
-        return loss + self.w_reg * torch.abs(sigma).sum()
+    def _regulation_chain(self, views, rays_o, rays_d, gt_depth, t_rand):
+        from .renderer import TrainPass, map_loss
+        reg = TrainPass(self.renderer, self.c, self.decoder, 'regulation')
+        (sigma,) = reg.forward(rays_o, rays_d, gt_depth, t_rand=t_rand)
+        loss, _, _, g_s = map_loss(None, None, None, None, 0.0, sigma=sigma, w_reg=self.w_reg)
+        reg.backward(views[0], g_fc=views[1], g_feats=views[2], g_sigma=g_s)
+        return loss
 
     def __call__(self, rays_o, rays_d, gt_depth, gt_color, t_rand=None):
+        from .renderer import TrainPass, map_loss
+        r = self.renderer
+        dev = rays_o.device
+        rays_o = rays_o.float().contiguous()
+        rays_d = rays_d.float().contiguous()
+        gt_depth = gt_depth.reshape(-1).float().contiguous()
+        gt_color = gt_color.float().contiguous()
+        if t_rand is None:
+            t_rand = torch.rand((rays_o.shape[0], r.N_samples), device=dev)
+        t_rand = t_rand.float().contiguous()
         self.flat.zero_grad()
         far_clamp = self.ddp.global_far_clamp(gt_depth) if self.ddp is not None else None
-        # the render / regulation backwards add straight into the flat gradient buffer (renderer
-        # _direct): the parameters' .grad are views of it, zeroed just above
-        for p in self.flat.params:
-            p._pnr_direct = True
-        try:
-            loss = self.loss(rays_o, rays_d, gt_depth, gt_color, t_rand, far_clamp)
-            loss.backward()
-        finally:
-            for p in self.flat.params:
-                p._pnr_direct = False
+        ren = TrainPass(r, self.c, self.decoder, 'render')
+        # the weight images, the point index and the f16 feature copy: built on this stream before the
+        # chains fork (both read them)
+        ren.packer.image(ren.feat.params)
+        if self.points is not None:
+            ren.feat.fc_owner.image(ren.feat.fc)
+            self.points.index()
+            self.points._feats_for_gather()
+        main = torch.cuda.current_stream(dev)
+        if self.overlap:
+            self.side.wait_stream(main)
+            with torch.cuda.stream(self.side):
+                self.grad2.zero_()
+                l_reg = self._regulation_chain(self._views['side'], rays_o, rays_d, gt_depth, t_rand)
+        d, _, c = ren.forward(rays_o, rays_d, gt_depth, far_clamp=far_clamp)
+        l_ren, g_d, g_c, _ = map_loss(gt_depth, d, gt_color, c, self.w_color)
+        views = self._views['main']
+        ren.backward(views[0], g_fc=views[1], g_feats=views[2], g_depth=g_d, g_rgb=g_c)
+        if self.overlap:
+            main.wait_stream(self.side)
+            self.flat.grad.add_(self.grad2)  # render + regulation gradients, a fixed order
+        else:
+            l_reg = self._regulation_chain(views, rays_o, rays_d, gt_depth, t_rand)
+        loss = l_ren + l_reg
         if self.ddp is not None and self.shard:
             self.ddp.allreduce_(self.flat.grad[:self.n_dec])
             self.ddp.reduce_scatter_(self.flat.grad[self.n_dec:])
@@ -158,8 +206,19 @@ class MapStep:
         if self.shard:
             self.ddp.all_gather_(self.flat.data[self.n_dec:])
             self.points.invalidate_feats()
-        return loss.detach()
+        return loss
 
+    def loss(self, rays_o, rays_d, gt_depth, gt_color, t_rand=None, far_clamp=None):
+        """The Mapper loss through the autograd Renderer API (src/Mapper.py:623-655): the drop-in form
+        of what __call__ computes on its fused path."""
+        r, dec = self.renderer, self.decoder
+        dev = rays_o.device
+        d, _, c = r.render_batch_ray(self.c, dec, rays_d, rays_o, dev, 'color', gt_depth, far_clamp=far_clamp)
+        m = gt_depth > 0
+        loss = torch.where(m, torch.abs(gt_depth - d), torch.zeros_like(d)).sum()
+        loss = loss + self.w_color * torch.abs(gt_color - c).sum()
+        sigma = r.regulation(self.c, dec, rays_d, rays_o, gt_depth, dev, 'color', t_rand=t_rand)
+        return loss + self.w_reg * torch.abs(sigma).sum()
 
 
 class MapGraph:

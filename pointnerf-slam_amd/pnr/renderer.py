@@ -92,27 +92,11 @@ class _Feat:
         base = 7 + _lib.N_PARAMS
         g_fc, out_fc = None, [None] * _lib.N_FC_PARAMS
         if any(needs[base:base + _lib.N_FC_PARAMS]):
-            if _direct(self.fc):  # MapStep: accumulate into the flat gradient buffer (see _direct)
-                g_fc = [t.grad for t in self.fc]
-            else:
-                g_fc = [torch.zeros(t.shape, device=dev, dtype=torch.float32) for t in self.fc]
-                out_fc = g_fc
+            g_fc = out_fc = [torch.zeros(t.shape, device=dev, dtype=torch.float32) for t in self.fc]
         g_feats, out_feats = None, None
         if needs[base + _lib.N_FC_PARAMS]:
-            if _direct([self.pts.feats]):
-                g_feats = self.pts.feats.grad
-            else:
-                g_feats = out_feats = torch.zeros_like(self.pts.feats)
+            g_feats = out_feats = torch.zeros_like(self.pts.feats)
         return g_feats, g_fc, [*out_fc, out_feats]
-
-
-def _direct(tensors):
-    """True while a MapStep accumulates straight into these tensors' .grad (views of its flat
-    gradient buffer, zeroed at the step's start): the kernels then add into them and autograd
-    gets None -- no per-call zeroed buffers and no autograd accumulation kernels (22 fills and
-    22 adds of a mapping iteration, a sixth of its launches at the faithful N = 1,000)."""
-    return len(tensors) > 0 and all(getattr(t, '_pnr_direct', False) and t.grad is not None and
-                                    t.grad.is_contiguous() for t in tensors)
 
 
 def _param_grads(ctx, dev):
@@ -121,8 +105,6 @@ def _param_grads(ctx, dev):
     launch).  The decoder tensors are autograd inputs 7..17 of both Functions."""
     if not any(ctx.needs_input_grad[7:7 + _lib.N_PARAMS]):
         return [None] * _lib.N_PARAMS, None
-    if _direct(ctx.feat.params):
-        return [None] * _lib.N_PARAMS, _lib.PtrArray(*[p.grad.data_ptr() for p in ctx.feat.params])
     grads = [torch.zeros(s, device=dev, dtype=torch.float32) for s in _GRAD_SHAPES]
     return grads, _lib.PtrArray(*[g.data_ptr() for g in grads])
 
@@ -241,6 +223,105 @@ class _RegulationFn(torch.autograd.Function):
 
 def ctypes_ref(prm):
     return ctypes.byref(prm)
+
+
+class TrainPass:
+    """One forward + backward of render_batch_ray or regulation for pnr.mapping.MapStep, without
+    autograd: the forward keeps every activation (save_for_backward = 1, no ray gradients), the
+    backward takes the upstream gradients from pnr_map_loss and adds the decoder / fc_c / point
+    feature gradients into caller-given buffers (the flat gradient views of a MapStep).  Same C ABI
+    calls as _RenderFn / _RegulationFn, minus the autograd plumbing (~20 elementwise launches of the
+    torch loss and its backward per mapping iteration)."""
+
+    def __init__(self, renderer, c, decoders, kind):
+        self.r, self.kind = renderer, kind
+        self.params = _decoder_params(decoders)
+        self.pts, fc_owner, extra = _feature_inputs(c, decoders)
+        self.feat = _Feat(self.pts, fc_owner, [*self.params, *extra])
+        self.packer = _packer(decoders)
+
+    def forward(self, rays_o, rays_d, gt_depth, t_rand=None, far_clamp=None):
+        lib = _lib.load()
+        r = self.r
+        dev = rays_o.device
+        n = rays_o.shape[0]
+        prm = r.params(n_importance=0) if self.kind == 'regulation' else r.params()
+        prm.status = r.status_word(dev).data_ptr()
+        prm.save_for_backward = 1
+        prm.need_ray_grads = 0
+        packed = self.packer.image(self.feat.params)
+        self.feat.attach(prm)
+        if isinstance(far_clamp, torch.Tensor):
+            far_clamp = far_clamp.reshape(-1)[:1].float().contiguous()
+            prm.far_mode = 2
+            prm.far_clamp_dev = far_clamp.data_ptr()
+        elif far_clamp is not None:
+            prm.far_mode = 1
+            prm.far_clamp = float(far_clamp)
+        st = _lib.stream_of(dev)
+        if self.kind == 'regulation':
+            ws = torch.empty(lib.pnr_regulation_workspace_bytes(ctypes_ref(prm), n), dtype=torch.uint8, device=dev)
+            sigma = torch.empty(n * prm.n_samples, dtype=torch.float32, device=dev)
+            _lib.check(lib.pnr_regulation_fwd(ctypes_ref(prm), _lib.ptr(packed), _lib.ptr(rays_o), _lib.ptr(rays_d),
+                                              _lib.ptr(gt_depth), _lib.ptr(t_rand), n, _lib.ptr(sigma), _lib.ptr(ws),
+                                              ws.numel(), st), 'regulation_fwd')
+            out = (sigma,)
+        else:
+            ws = torch.empty(lib.pnr_render_workspace_bytes(ctypes_ref(prm), n), dtype=torch.uint8, device=dev)
+            depth = torch.empty(n, dtype=torch.float64, device=dev)
+            var = torch.empty(n, dtype=torch.float64, device=dev)
+            rgb = torch.empty((n, 3), dtype=torch.float32, device=dev)
+            _lib.check(lib.pnr_render_fwd(ctypes_ref(prm), _lib.ptr(packed), _lib.ptr(rays_o), _lib.ptr(rays_d),
+                                          _lib.ptr(gt_depth), n, _lib.ptr(depth), _lib.ptr(var), _lib.ptr(rgb),
+                                          _lib.ptr(ws), ws.numel(), st), 'render_fwd')
+            out = (depth, var, rgb)
+        prm.points = None
+        self.prm, self.ws, self.packed, self.rays = prm, ws, packed, (rays_o, rays_d, far_clamp)
+        return out
+
+    def backward(self, grads, g_fc=None, g_feats=None, g_depth=None, g_rgb=None, g_sigma=None):
+        """grads: the 11 decoder gradient tensors to add into (contiguous float32); g_fc: the 8 fc_c
+        ones, g_feats: the point features' (with neural points)."""
+        lib = _lib.load()
+        prm, ws, packed = self.prm, self.ws, self.packed
+        rays_o, rays_d, _ = self.rays
+        dev = rays_o.device
+        n = rays_o.shape[0]
+        arr = _lib.PtrArray(*[g.data_ptr() for g in grads])
+        self.feat.attach(prm, g_feats, g_fc)
+        st = _lib.stream_of(dev)
+        if self.kind == 'regulation':
+            bws = torch.empty(lib.pnr_regulation_bwd_workspace_bytes(ctypes_ref(prm), n), dtype=torch.uint8,
+                              device=dev)
+            _lib.check(lib.pnr_regulation_bwd(ctypes_ref(prm), _lib.ptr(packed), None, _lib.ptr(rays_o),
+                                              _lib.ptr(rays_d), n, _lib.ptr(g_sigma), arr, None, None, _lib.ptr(ws),
+                                              ws.numel(), _lib.ptr(bws), bws.numel(), st), 'regulation_bwd')
+        else:
+            bws = torch.empty(lib.pnr_render_bwd_workspace_bytes(ctypes_ref(prm), n), dtype=torch.uint8, device=dev)
+            _lib.check(lib.pnr_render_bwd(ctypes_ref(prm), _lib.ptr(packed), None, _lib.ptr(rays_o), _lib.ptr(rays_d),
+                                          n, _lib.ptr(g_depth), None, _lib.ptr(g_rgb), arr, None, None, _lib.ptr(ws),
+                                          ws.numel(), _lib.ptr(bws), bws.numel(), st), 'render_bwd')
+        self.ws = self.packed = None  # release the saved activations
+
+
+def map_loss(gt_depth, depth, gt_color, color, w_color, sigma=None, w_reg=0.0):
+    """pnr_map_loss: the Mapper loss terms (src/Mapper.py:628-655) and their gradients in one pass.
+    Returns (loss float64 0-dim, g_depth, g_color, g_sigma); either part may be None."""
+    lib = _lib.load()
+    ref = depth if depth is not None else sigma
+    dev = ref.device
+    n = 0 if depth is None else depth.shape[0]
+    ns = 0 if sigma is None else sigma.numel()
+    loss = torch.empty((), dtype=torch.float64, device=dev)
+    ws = torch.empty(lib.pnr_map_loss_workspace_bytes(), dtype=torch.uint8, device=dev)
+    g_d = torch.empty(n, dtype=torch.float64, device=dev) if n else None
+    g_c = torch.empty((n, 3), dtype=torch.float32, device=dev) if n else None
+    g_s = torch.empty(ns, dtype=torch.float32, device=dev) if ns else None
+    _lib.check(lib.pnr_map_loss(_lib.ptr(gt_depth if n else None), _lib.ptr(depth), _lib.ptr(gt_color if n else None),
+                                _lib.ptr(color), n, float(w_color), _lib.ptr(sigma), ns, float(w_reg), _lib.ptr(loss),
+                                _lib.ptr(g_d), _lib.ptr(g_c), _lib.ptr(g_s), _lib.ptr(ws), _lib.stream_of(dev)),
+               'map_loss')
+    return loss, g_d, g_c, g_s
 
 
 class Renderer(object):
