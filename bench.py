@@ -17,7 +17,10 @@ Extra keys of the N=1 line (measured after the timed region, never part of `valu
   sfwd            the north-star S-fwd batch (640x480 x 64 samples, forward) with its own roofline
                   and the oracle's CPU rate at 64 samples
   faithful_n1000  the room0 Mapper iteration at its real size (N = 1,000 rays), replayed from a
-                  captured HIP graph (pnr.mapping.MapGraph), and N = 5,000 (C4/C5)
+                  captured HIP graph (pnr.mapping.MapGraph), and N = 5,000 (C4/C5), each with its
+                  fraction of the split peak and the oracle's CPU rate on the same rays
+  map_points      the neural-point Mapper iteration (A15) at 307,200 rays with its MLP roofline and
+                  the oracle's CPU rate
   fp32            the same S-map step with fp32-MFMA decoder arithmetic
   gather_roofline the neural-point gather (A15) on its HBM roofline
 N>1 lines add `fixed_global_batch`: the 307,200-ray batch split over the N ranks.
@@ -149,8 +152,9 @@ def gather_bytes(n_samples, n_probed, n_nb_total, k, save=True, feat_bytes=128):
 
 
 def gather_roofline(dev, voxel=0.001, k=8, reps=5, feat_dtype='float32'):
-    """Time the point-gather kernels (k_gather_probe + k_gather_search, hipEvents on their
-    stream) on the neural-point scene; roofline against the HBM peak."""
+    """Time the point-gather kernels (k_gather_probe, the group scan / scatter and k_gather_search,
+    hipEvents on their stream) on the neural-point scene; roofline against the HBM peak.  Then the
+    gather backward (feature gradients) against its HBM + float-atomic floor."""
     import ctypes
     import pnr
     from pnr._lib import timing_read
@@ -184,16 +188,44 @@ def gather_roofline(dev, voxel=0.001, k=8, reps=5, feat_dtype='float32'):
     avg = ms / launches
     byt = gather_bytes(P, probed, nb, k, feat_bytes=64 if feat_dtype == 'float16' else 128)
     gbs = byt / (avg * 1e-3) / 1e9
+    # backward, the Mapper's form (feature gradients only: dL/df_i += w_k dL/dc, float atomics)
+    gf = torch.zeros_like(feats)
+    gc = torch.randn_like(c)
+    sb, _ = pts.descriptor(g_feats=gf)
+    rows = int((idx[:, 0] >= 0).sum().item())
+    lib.pnr_timing_enable(1)
+    timing_read(5)
+    for _ in range(reps):
+        pnr._lib.check(lib.pnr_point_gather_bwd(ctypes.byref(sb), p.data_ptr(), P, idx.data_ptr(), w.data_ptr(),
+                                                c.data_ptr(), gc.data_ptr(), None, ws.data_ptr(), ws.numel(), st),
+                       'point_gather_bwd')
+    torch.cuda.synchronize()
+    lib.pnr_timing_enable(0)
+    bl, bms, _ = timing_read(5)
+    bavg = bms / bl
+    # per sample 4 B (its first neighbour index); per row with neighbours 128 B g_c + k x 8 B idx/w;
+    # per neighbour 128 B of feature-gradient float atomics
+    b_hbm = P * 4 + rows * (128 + k * 8)
+    b_atomic = nb * 128
+    t_floor = (b_hbm / (HBM_PEAK_GBS * 1e9) + b_atomic / 1.3e12) * 1e3
+    bwd = {'kernel': 'k_gather_bwd_probe+k_gather_bwd (feature gradients, the Mapper case)',
+           'avg_launch_ms': round(bavg, 4), 'bytes_hbm': b_hbm, 'bytes_atomic': b_atomic, 'rows': rows,
+           'achieved_gbs': round((b_hbm + b_atomic) / (bavg * 1e-3) / 1e9, 1),
+           'floor_ms': round(t_floor, 4), 'frac_of_floor': round(t_floor / bavg, 4),
+           'floor_basis': 'HBM bytes at 8 TB/s + feature-gradient atomic bytes at the 1.3 TB/s chip-wide float-'
+                          'atomic rate (MI355X_MICROARCH.md); neighbours shared with the previous row are carried, '
+                          'so fewer atomics are issued than counted'}
     return {'bound': 'hbm', 'achieved': round(gbs, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
             'frac': round(gbs / HBM_PEAK_GBS, 4),
             # PMC bytes per sample were measured on the float32-feature gather only
             'traffic': pmc_traffic('k_gather', P) if feat_dtype == 'float32' else None,
-            'kernel': 'k_gather_probe+k_gather_search',
+            'kernel': 'k_gather_probe+k_group_scatter+k_gather_search',
             'avg_launch_ms': round(avg, 3), 'launches': launches, 'samples': P, 'points': int(xyz.shape[0]),
             'neighbours_per_sample': round(nb / P, 3), 'probed_samples': probed, 'radius': 2 * voxel, 'k': k,
             'point_features': feat_dtype, 'bytes_per_launch': byt,
             'byte_basis': 'per sample 24 B point + 128 B c + k x 8 B idx/weight; 8 x 8 B bucket headers per '
-                          'probed sample (occupied probe block); per neighbour 4 + 12 + 128 B'}
+                          'probed sample (occupied probe block); per neighbour 4 + 12 + 128 B',
+            'backward': bwd}
 
 
 def cpu_threads():
@@ -427,9 +459,39 @@ def sfwd_extra(pnr, plib, slam, params, bound, pose, dev, ddp, lib, steps=10, cp
     return out
 
 
-def faithful_extra(pnr, slam, params, pose, dev, ddp, lib, sizes=(1000, 5000), steps=50):
+MAP_FLOP_PER_RAY = 115.29e6        # (32 + 3 x 44 + 3 x 32) x 443,438 per mapping iteration
+
+
+def oracle_map_rate(bound, pose, params, n, reps=3, threads=None):
+    """The oracle's Mapper iteration (render + regulation + L1 losses + backward + Adam) on n rays on
+    this host's cores, rays/s (median of `reps` after one warm-up)."""
+    from oracle import ref_render as ref
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads or cpu_threads())
+    ro, rd, gt, col = [t.cpu() for t in synth_batch(n, 0, pose, 'cpu', seed=7)]
+    p = {k: v.clone().requires_grad_(True) for k, v in params.items()}
+    opt = torch.optim.Adam(list(p.values()), lr=2e-4)
+
+    def step():
+        opt.zero_grad()
+        d, v, c = ref.render_batch_ray(p, rd, ro, bound, gt_depth=gt)
+        sig = ref.regulation(p, rd, ro, gt, bound)
+        ref.mapping_loss(d, c, gt, col, sig).backward()
+        opt.step()
+    step()
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        step()
+        ts.append(time.perf_counter() - t0)
+    torch.set_num_threads(prev)
+    return n / float(np.median(ts))
+
+
+def faithful_extra(pnr, slam, params, bound, pose, dev, ddp, lib, sizes=(1000, 5000), steps=50, cpu=True):
     """The Mapper iteration at its real batch sizes (room0: mapping.pixels = 1,000; ScanNet /
-    Apartment: 5,000), replayed from a captured HIP graph."""
+    Apartment: 5,000), replayed from a captured HIP graph; the algorithmic fraction of the split
+    peak (115.29 MFLOP per ray) and the oracle's CPU rate at the same batch."""
     out = {}
     for n in sizes:
         cfg = pnr.ROOM0_CFG
@@ -438,8 +500,82 @@ def faithful_extra(pnr, slam, params, pose, dev, ddp, lib, sizes=(1000, 5000), s
         ro, rd, gt, col = synth_batch(n, 0, pose, dev)
         step = map_step_fn(pnr, r, dec, cfg, ro, rd, gt, col, dev, graph=True)
         el, _ = timed(step, steps, 3, ddp, lib)
-        out[f'n{n}'] = {'ms_per_iter': round(el / steps * 1e3, 4), 'rays_per_s': round(n * steps / el, 1),
-                        'graph': True, 'iters': steps}
+        rate = n * steps / el
+        tf = MAP_FLOP_PER_RAY * rate / 1e12
+        peak = ALGO_PEAK_TF['f16x3']
+        e = {'ms_per_iter': round(el / steps * 1e3, 4), 'rays_per_s': round(rate, 1), 'graph': True, 'iters': steps,
+             'achieved_tflops': round(tf, 2), 'frac_of_split_peak': round(tf / peak, 4),
+             'flop_basis': '115.29 MFLOP per ray per mapping iteration (SURVEY.md 8(d)); peak 833 TF (f16 MFMA / 3)'}
+        if cpu:
+            cr = oracle_map_rate(bound, pose, params, n)
+            e['cpu_baseline'] = {'value': round(cr, 1), 'unit': 'rays/s', 'cores': cpu_threads(), 'kind': 'port',
+                                 'sample': f'the oracle Mapper iteration on the same {n} rays, median of 3 after 1 '
+                                           f'warm-up'}
+            e['speedup_vs_cpu'] = round(rate / cr, 1)
+        out[f'n{n}'] = e
+    return out
+
+
+def map_points_extra(pnr, plib, slam, params, bound, pose, dev, ddp, lib, n=W * H, steps=3, cpu=True):
+    """The neural-point Mapper iteration (--workload map-points) at 307,200 rays:
+    rays/s, the roofline of its dominant MLP kernel, the gather and gather-backward HBM rates, and the
+    oracle's CPU rate (brute-force neighbour search over the points near 32 of the rays)."""
+    dec = pnr.MLP(name='color', dim=3, c_dim=32, color=True, skips=[], n_blocks=4, hidden_size=256)
+    sd = dec.state_dict()
+    sd.update(params)
+    dec.load_state_dict(sd)
+    dec = dec.to(dev)
+    xyz, feats, _, (ro, rd, gt) = neural_point_scene(dev, n_rays=n, seed=0)
+    points = pnr.NeuralPoints(xyz, feats, mode='idw', radius=0.002, k=8).to(dev)
+    col = torch.rand((n, 3), device=dev, generator=torch.Generator(device=dev).manual_seed(0))
+    r = pnr.Renderer(pnr.ROOM0_CFG, None, slam)
+    step = map_step_fn(pnr, r, dec, pnr.ROOM0_CFG, ro, rd, gt, col, dev, points=points)
+    el, kt = timed(step, steps, 1, ddp, lib)
+    prec = plib.DEFAULT_PRECISION
+    out = {'workload': 'S-map with neural points: c_dim=32 decoder, IDW k=8 r=2 mm gather, fc_c injection, '
+                       'feature + decoder Adam', 'rays': n, 'points': int(xyz.shape[0]),
+           'value': round(n * steps / el, 1), 'unit': 'rays/s', 'ms_per_step': round(el / steps * 1e3, 3),
+           'steps': steps, 'roofline': kernel_roofline(kt, prec, el, traffic_units=False),
+           'kernels': {k: {'launches': v[0], 'ms': round(v[1], 3), 'units': v[2]} for k, v in kt.items()}}
+    if 'gather_bwd' in kt:
+        launches, ms, units = kt['gather_bwd']
+        out['gather_bwd_ms_per_step'] = round(ms / steps, 3)
+    if cpu:
+        from oracle import ref_points as RP
+        from oracle import ref_render as ref
+        m = 32
+        ro_c, rd_c, gt_c = ro[:m].cpu().double().float(), rd[:m].cpu(), gt[:m].cpu()
+        xyz_c, f_c = xyz.cpu(), feats.cpu()
+        # the points near these rays (a superset of every sample's neighbourhood)
+        far = float(gt_c.max()) * 1.2 + 0.01
+        t = torch.linspace(0, 1, 256)
+        segs = (ro_c[:, None, :] + rd_c[:, None, :] * (t[None, :, None] * far)).reshape(-1, 3)
+        keep = torch.zeros(xyz_c.shape[0], dtype=torch.bool)
+        for a in range(0, segs.shape[0], 512):
+            keep |= (torch.cdist(segs[a:a + 512], xyz_c) <= 0.004 + far / 255).any(0)
+        sub = torch.nonzero(keep).reshape(-1)
+        prm = {k: v.detach().cpu().clone().requires_grad_(True) for k, v in dec.state_dict().items()}
+        fr = f_c[sub].clone().requires_grad_(True)
+        pdict = dict(xyz=xyz_c[sub], feats=fr, mode='idw', radius=0.002, k=8, eps=1e-6)
+        ev = lambda q: RP.eval_points_c(prm, q, bound, pdict)  # noqa: E731
+        colc = col[:m].cpu()
+        torch.set_num_threads(cpu_threads())
+
+        def cstep():
+            d, v, c = ref.render_batch_ray(prm, rd_c, ro_c, bound, gt_depth=gt_c, eval_fn=ev)
+            sig = ref.regulation(prm, rd_c, ro_c, gt_c, bound, eval_fn=ev)
+            ref.mapping_loss(d, c, gt_c, colc, sig).backward()
+        cstep()
+        ts = []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            cstep()
+            ts.append(time.perf_counter() - t0)
+        cr = m / float(np.median(ts))
+        out['cpu_baseline'] = {'value': round(cr, 1), 'unit': 'rays/s', 'cores': cpu_threads(), 'kind': 'port',
+                               'sample': f'oracle Mapper loss + backward with the brute-force IDW gather on {m} of the '
+                                         f'rays over the {int(sub.numel())} points near them (no Adam), median of 3'}
+        out['speedup_vs_cpu'] = round(out['value'] / cr, 1)
     return out
 
 
@@ -540,7 +676,10 @@ def main():
         elif params is not None:
             extras['sfwd'] = sfwd_extra(pnr, plib, slam, params, bound, pose, dev, ddp, lib,
                                         cpu=not args.no_cpu_baseline)
-            extras['faithful_n1000'] = faithful_extra(pnr, slam, params, pose, dev, ddp, lib)
+            extras['faithful_n1000'] = faithful_extra(pnr, slam, params, bound, pose, dev, ddp, lib,
+                                                      cpu=not args.no_cpu_baseline)
+            extras['map_points'] = map_points_extra(pnr, plib, slam, params, bound, pose, dev, ddp, lib,
+                                                    cpu=not args.no_cpu_baseline)
             if prec != 'fp32':
                 saved = plib.DEFAULT_PRECISION
                 plib.DEFAULT_PRECISION = 'fp32'

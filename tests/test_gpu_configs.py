@@ -213,7 +213,8 @@ def test_c3_office3_200k_points(precision, pnr_mod, dev):
     pts_g = pnr_mod.NeuralPoints(xyz.to(dev), feats.to(dev), mode='idw', radius=0.01, k=8).to(dev)
     ms = MapStep(pnr_mod.Renderer(cfg, None, slam), make_decoder(pnr_mod, params, dev, precision), points=pts_g,
                  feat_lr=1e-3)
-    map_grad_parity(pnr_mod, ms, params, bound, xyz, feats, ro, rd, gt, 0.01, precision, seed=7)
+    # (gt 2% beyond the render: the depth loss's sign(gt - depth) must not hinge on rounding)
+    map_grad_parity(pnr_mod, ms, params, bound, xyz, feats, ro, rd, gt * 1.02, 0.01, precision, seed=7)
     # Mapper iterations at the config's batch (mapping.pixels = 1,000), the decoder in `precision`
     cfg = dict(pnr_mod.ROOM0_CFG)
     cfg['pnr'] = {'precision': precision}
@@ -286,7 +287,7 @@ def test_c5_apartment_1m_points_f16(pnr_mod, dev):
     pts_g = pnr_mod.NeuralPoints(xyz.to(dev), feats.to(dev), mode='idw', radius=0.03, k=8,
                                  feat_dtype='float16').to(dev)
     ms = MapStep(r, make_decoder(pnr_mod, params, dev, 'f16x3'), points=pts_g, feat_lr=1e-3)
-    map_grad_parity(pnr_mod, ms, params, bound, xyz, feats16, ro, rd, d.float(), 0.03, 'f16x3', seed=8)
+    map_grad_parity(pnr_mod, ms, params, bound, xyz, feats16, ro, rd, d.float() * 1.02, 0.03, 'f16x3', seed=8)
     # Mapper iterations at 5,000 pixels with the 1M f16-feature cloud
     g = torch.Generator().manual_seed(5)
     pix = torch.randint(0, 720 * 1280, (5000,), generator=g)

@@ -1,9 +1,10 @@
 #!/bin/bash
-# round-3 check: gather microbench, changed GPU test files, faithful-iteration kernel trace
+# round-3 check: gather microbench, the GPU test suite, faithful-iteration kernel trace
 cd /root/repo
 export TMPDIR=/tmp
 timeout -k 10 150 python -u tools/gather_bench.py > gpurun_out/gb1.log 2>&1 || { echo "gather_bench rc=$?"; exit 1; }
-timeout -k 10 900 python -u -m pytest tests/test_gpu_points.py tests/test_gpu_scannet.py tests/test_gpu_configs.py tests/test_gpu_parity.py -v --timeout 400 --timeout-method thread -p no:cacheprovider > gpurun_out/gt2.log 2>&1
+tail -3 gpurun_out/gb1.log
+timeout -k 10 1500 python -u -m pytest tests -m gpu -v --timeout 400 --timeout-method thread -p no:cacheprovider > gpurun_out/gt2.log 2>&1
 rc=$?
 echo "pytest rc=$rc"
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
