@@ -266,23 +266,54 @@ int mlp_backward_core(int prec, const float* packed, const SaveArgs& sv, int64_t
     if (rc) return rc;
     const int64_t hstride = sv.ld * kHidden;  // h_l rows of this chunk: h + l_idx * ld * 256 + p0 * 256
     const int64_t dstride = b.C * kHidden;
+    // split precisions: every GEMM of the chunk writes its own partial region, and ONE reduce launch
+    // (fixed order per element) adds them all into the gradients
+    ReduceJob jobs[kMaxReduceJobs];
+    int nj = 0;
+    float* pp = b.part;
+    float* pb = b.part_bias;
+    auto took = [&]() {
+      pp += jobs[nj].part_floats();
+      pb += jobs[nj].bias_floats();
+      ++nj;
+    };
     if (!grads) {  // no decoder weight gradients (the Tracker's camera-only backward)
     } else if (split) {  // f16x3 GEMMs on the fp32 saves (h / e by k_mlp_fwd16, deltas by k_mlp_bwd16)
       const float* hp = sv.hP + p0 * kHidden;
       // output layer: dWo (4x256) += g_out^T h4 ; dbo += colsum(g_out)
-      rc = launch_wgrad_out16(b.g_out + p0 * 4, hp + 3 * hstride, C, grads[9], grads[10], b.part, b.part_bias, st);
+      rc = launch_wgrad_out16(b.g_out + p0 * 4, hp + 3 * hstride, C, grads[9], grads[10], pp, pb, st, &jobs[nj]);
+      if (rc == 0) took();
       // hidden layers: dW_l += delta_{l+1}^T h_l  (W3: delta4.h3, W2: delta3.h2, W1: delta2.h1); delta4
       // is not stored by k_mlp_bwd16 (rank 4: rebuilt from g_out and the h4 masks inside the GEMM)
-      const WgradSyn syn{reinterpret_cast<const float4*>(b.g_out + p0 * 4), sv.masks + 3 * (sv.ld / 32) * 64, p0 / 32,
-                         packed + packed_raw_wo_offset(), sv.xP + p0, packed + kOffFB, b.part, b.part_bias};
-      if (rc == 0)
-        rc = launch_wgrad16(kWgradOutDelta, nullptr, hp + 2 * hstride, C, C, grads[7], kHidden, grads[8], st, &syn);
-      for (int l = 2; l >= 1 && rc == 0; --l)
+      WgradSyn syn{reinterpret_cast<const float4*>(b.g_out + p0 * 4), sv.masks + 3 * (sv.ld / 32) * 64, p0 / 32,
+                   packed + packed_raw_wo_offset(), sv.xP + p0, packed + kOffFB, pp, pb};
+      if (rc == 0) {
+        syn.part = pp;
+        syn.part_bias = pb;
+        rc = launch_wgrad16(kWgradOutDelta, nullptr, hp + 2 * hstride, C, C, grads[7], kHidden, grads[8], st, &syn,
+                            &jobs[nj]);
+        if (rc == 0) took();
+      }
+      for (int l = 2; l >= 1 && rc == 0; --l) {
+        syn.part = pp;
+        syn.part_bias = pb;
         rc = launch_wgrad16(kWgradHidden, b.dP + l * dstride, hp + (l - 1) * hstride, C, C, grads[1 + 2 * l],
-                            kHidden, grads[2 + 2 * l], st, &syn);
+                            kHidden, grads[2 + 2 * l], st, &syn, &jobs[nj]);
+        if (rc == 0) took();
+      }
       // first layer: dW0 (256x93) += delta1^T e ; db0 -- e = sin(x@B) recomputed from the saved x
       // (k_mlp_fwd16 saves no e)
-      if (rc == 0) rc = launch_wgrad16(kWgradFirstX, b.dP, nullptr, C, C, grads[1], kFourier, grads[2], st, &syn);
+      if (rc == 0) {
+        syn.part = pp;
+        syn.part_bias = pb;
+        rc = launch_wgrad16(kWgradFirstX, b.dP, nullptr, C, C, grads[1], kFourier, grads[2], st, &syn, &jobs[nj]);
+        if (rc == 0) took();
+      }
+      // Fourier: dB (3x93) += x^T g_arg
+      if (rc == 0) {
+        rc = launch_wgrad_fourier16(sv.xP + p0, b.gargP, C, grads[0], pp, st, &jobs[nj]);
+        if (rc == 0) took();
+      }
     } else {
       const float* hp = sv.hP + p0 * kHidden;
       rc = launch_wgrad(kWgradOut, b.g_out + p0 * 4, 4, hp + 3 * hstride, kHidden, C, grads[9], kHidden, grads[10],
@@ -293,27 +324,28 @@ int mlp_backward_core(int prec, const float* packed, const SaveArgs& sv, int64_t
       if (rc == 0)
         rc = launch_wgrad(kWgradFirst, b.dP, kHidden, sv.eP + p0 * kFourierPad, kFourier, C, grads[1], kFourier,
                           grads[2], b.part, b.part_bias, st);
+      // Fourier: dB (3x93) += x^T g_arg   (x rows are float4 (x0,x1,x2,inside): 3 of 4 used)
+      if (rc == 0)
+        rc = launch_wgrad(kWgradFourier, reinterpret_cast<const float*>(sv.xP + p0), 3, b.gargP, kFourier, C,
+                          grads[0], kFourier, nullptr, b.part, b.part_bias, st);
     }
-    if (rc) return rc;
-    // Fourier: dB (3x93) += x^T g_arg   (x rows are float4 (x0,x1,x2,inside): 3 of 4 used)
-    if (grads)
-      rc = split ? launch_wgrad_fourier16(sv.xP + p0, b.gargP, C, grads[0], b.part, st)
-                 : launch_wgrad(kWgradFourier, reinterpret_cast<const float*>(sv.xP + p0), 3, b.gargP, kFourier, C,
-                                grads[0], kFourier, nullptr, b.part, b.part_bias, st);
     if (rc) return rc;
     // feature branch: dWc_l (256x32) += (dL/dh_l)^T c ; dbc_l += colsum(dL/dh_l)
     if (fb && fb->g_fc && split) {  // f16x3 GEMMs: dL/dh from k_mlp_bwd16, the fp32 features
       WgradSyn fsyn{};
-      fsyn.part = b.part;
-      fsyn.part_bias = b.part_bias;
-      for (int l = 0; l < 4 && rc == 0; ++l)
+      for (int l = 0; l < 4 && rc == 0; ++l) {
+        fsyn.part = pp;
+        fsyn.part_bias = pb;
         rc = launch_wgrad16(kWgradFc, b.gH + l * dstride, fb->c + p0 * kCDim, C, C, fb->g_fc[2 * l], kCDim,
-                            fb->g_fc[2 * l + 1], st, &fsyn);
+                            fb->g_fc[2 * l + 1], st, &fsyn, &jobs[nj]);
+        if (rc == 0) took();
+      }
     } else if (fb && fb->g_fc) {
       for (int l = 0; l < 4 && rc == 0; ++l)
         rc = launch_wgrad(kWgradFc, b.gH + l * dstride, kHidden, fb->c + p0 * kCDim, kCDim, C, fb->g_fc[2 * l], kCDim,
                           fb->g_fc[2 * l + 1], b.part, b.part_bias, st);
     }
+    if (rc == 0) rc = launch_part_reduce_multi(jobs, nj, st);
     if (rc) return rc;
   }
   return hip_status(hipGetLastError());

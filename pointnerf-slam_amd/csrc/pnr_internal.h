@@ -246,21 +246,45 @@ struct WgradSyn {
 };
 constexpr int kWgradMaxWg = 512;    // fp32 k_wgrad grid cap
 constexpr int kWgrad16MaxWg = 256;  // split k_wgrad16 grid cap
-constexpr int64_t kWgradPartFloats = (int64_t)kWgradMaxWg * 256 * 256;
-constexpr int64_t kWgradPartBiasFloats = (int64_t)kWgradMaxWg * 256;
+constexpr int kSkinnyMaxWg = 1024;  // k_wgrad_skinny grid cap
+// split backward: every GEMM of a chunk keeps its own partial region until ONE reduce launch adds them
+// all (W3 / W2 / W1 256 x 256, W0 256 x 96, fc_c 4 x 256 x 32, Wo 4 x 256, B 3 x 93)
+constexpr int64_t kWgrad16PartFloats = (int64_t)kWgrad16MaxWg * 256 * (3 * 256 + 96 + 4 * 32) +
+                                       (int64_t)kSkinnyMaxWg * (4 * 256 + 3 * 93);
+constexpr int64_t kWgrad16PartBiasFloats = (int64_t)kWgrad16MaxWg * 256 * 8 + (int64_t)kSkinnyMaxWg * 4;
+constexpr int64_t kWgradPartFloats = kWgrad16PartFloats > (int64_t)kWgradMaxWg * 256 * 256
+                                         ? kWgrad16PartFloats : (int64_t)kWgradMaxWg * 256 * 256;
+constexpr int64_t kWgradPartBiasFloats = kWgrad16PartBiasFloats > (int64_t)kWgradMaxWg * 256
+                                             ? kWgrad16PartBiasFloats : (int64_t)kWgradMaxWg * 256;
 // C[r][c] += sum_g part[g][r pw + c] (r < nr, c < nb), bias[r] += sum_g pbias[g][r]: fixed order
 int launch_part_reduce(const float* part, const float* pbias, int nwg, int nr, int pw, int nb, float* C, int64_t ldc,
                        float* bias, hipStream_t st);
+// a deferred reduction (the GEMM launchers fill it instead of launching k_part_reduce when given one)
+struct ReduceJob {
+  const float* part;
+  const float* pbias;
+  int nwg, nr, pw, nb;
+  float* C;
+  int64_t ldc;
+  float* bias;
+  int64_t part_floats() const { return (int64_t)nwg * nr * pw; }
+  int64_t bias_floats() const { return (int64_t)nwg * nr; }
+};
+constexpr int kMaxReduceJobs = 12;
+// every job's reduction in ONE launch (blocks of a job follow the previous job's)
+int launch_part_reduce_multi(const ReduceJob* jobs, int n, hipStream_t st);
 int launch_wgrad(int kind, const float* A, int ma, const float* B, int nb, int64_t K, float* C, int64_t ldc,
                  float* bias, float* part, float* part_bias, hipStream_t st);
 // split precisions (wgrad16.hip): kWgradHidden / kWgradFirst / kWgradFc as f16x3 GEMMs on fp32
 // operands (A = deltas or dL/dh [K][256], B = activations / Fourier features / point features
 // [K][WB]; B rows >= kb_rows are not read), dWo and dB as fp32 FMA reductions
+// defer: non-null = fill the reduction job instead of launching it (launch_part_reduce_multi later)
 int launch_wgrad16(int kind, const float* A, const float* B, int64_t K, int64_t kb_rows, float* C, int64_t ldc,
-                   float* bias, hipStream_t st, const WgradSyn* syn = nullptr);
+                   float* bias, hipStream_t st, const WgradSyn* syn = nullptr, ReduceJob* defer = nullptr);
 int launch_wgrad_out16(const float* g_out, const float* h4, int64_t K, float* C, float* bias, float* part,
-                       float* part_bias, hipStream_t st);
-int launch_wgrad_fourier16(const float4* xP, const float* garg, int64_t K, float* C, float* part, hipStream_t st);
+                       float* part_bias, hipStream_t st, ReduceJob* defer = nullptr);
+int launch_wgrad_fourier16(const float4* xP, const float* garg, int64_t K, float* C, float* part, hipStream_t st,
+                           ReduceJob* defer = nullptr);
 
 inline int hip_status(hipError_t e) { return e == hipSuccess ? 0 : (int)e; }
 

@@ -334,6 +334,66 @@ __global__ __launch_bounds__(64 * kRedWaves) void k_part_reduce(const float* __r
   }
 }
 
+struct ReduceJobs {
+  ReduceJob j[kMaxReduceJobs];
+  int first[kMaxReduceJobs + 1];  // first block of each job; first[n] = grid
+  int n;
+};
+
+// every job of a backward chunk in one launch: block b belongs to the job whose block range holds it,
+// then the same fixed-order reduction as k_part_reduce
+__global__ __launch_bounds__(64 * kRedWaves) void k_part_reduce_multi(ReduceJobs J) {
+  __shared__ float red[kRedWaves][64];
+  int q = 0;
+  while (q + 1 < J.n && (int)blockIdx.x >= J.first[q + 1]) ++q;
+  const ReduceJob& jb = J.j[q];
+  const int lane = threadIdx.x & 63, v = threadIdx.x >> 6;
+  const int64_t E = (int64_t)jb.nr * jb.pw;
+  const int64_t nmain = (E + 63) / 64;
+  const int64_t blk = (int64_t)blockIdx.x - J.first[q];
+  const bool is_bias = blk >= nmain;
+  const int64_t e = (is_bias ? blk - nmain : blk) * 64 + lane;
+  const float* src = is_bias ? jb.pbias : jb.part;
+  const int64_t stride = is_bias ? jb.nr : E;
+  const bool ok = is_bias ? (jb.bias != nullptr && e < jb.nr) : (e < E && (int)(e % jb.pw) < jb.nb);
+  float s0 = 0.f, s1 = 0.f;
+  if (ok) {
+    int g = v;
+#pragma unroll 4
+    for (; g + kRedWaves < jb.nwg; g += 2 * kRedWaves) {
+      s0 += src[(int64_t)g * stride + e];
+      s1 += src[(int64_t)(g + kRedWaves) * stride + e];
+    }
+    if (g < jb.nwg) s0 += src[(int64_t)g * stride + e];
+  }
+  red[v][lane] = s0 + s1;
+  __syncthreads();
+  if (v == 0 && ok) {
+    float s = red[0][lane];
+#pragma unroll
+    for (int i = 1; i < kRedWaves; ++i) s += red[i][lane];
+    if (is_bias) jb.bias[e] += s;
+    else jb.C[(e / jb.pw) * jb.ldc + e % jb.pw] += s;
+  }
+}
+
+int launch_part_reduce_multi(const ReduceJob* jobs, int n, hipStream_t st) {
+  if (n <= 0) return 0;
+  if (n > kMaxReduceJobs) return PNR_E_ARG;
+  ReduceJobs J{};
+  int blocks = 0;
+  for (int i = 0; i < n; ++i) {
+    J.j[i] = jobs[i];
+    J.first[i] = blocks;
+    const int64_t nmain = ((int64_t)jobs[i].nr * jobs[i].pw + 63) / 64;
+    blocks += (int)(nmain + (jobs[i].bias ? (jobs[i].nr + 63) / 64 : 0));
+  }
+  J.first[n] = blocks;
+  J.n = n;
+  hipLaunchKernelGGL(k_part_reduce_multi, dim3((unsigned)blocks), dim3(64 * kRedWaves), 0, st, J);
+  return hip_status(hipGetLastError());
+}
+
 int launch_part_reduce(const float* part, const float* pbias, int nwg, int nr, int pw, int nb, float* C, int64_t ldc,
                        float* bias, hipStream_t st) {
   if (nwg <= 0) return 0;
@@ -345,7 +405,7 @@ int launch_part_reduce(const float* part, const float* pbias, int nwg, int nr, i
 }
 
 template <int NTB, int WB, bool SYN = false, bool FOUR = false>
-static int launch_k(const WxArgs& a, hipStream_t st) {
+static int launch_k(const WxArgs& a, hipStream_t st, ReduceJob* defer) {
   using Cfg = Wx3<NTB, WB>;
   auto kern = k_wgrad16<NTB, WB, SYN, FOUR>;
   static const bool attr = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -354,13 +414,18 @@ static int launch_k(const WxArgs& a, hipStream_t st) {
   const int nwg = (int)((a.K + a.ks - 1) / a.ks);
   hipLaunchKernelGGL(kern, dim3((unsigned)nwg), dim3(Cfg::kThreads), Cfg::kLds, st, a);
   const int rc = hip_status(hipGetLastError());
-  return rc ? rc : launch_part_reduce(a.part, a.part_bias, nwg, 256, NTB * 32, a.nb, a.C, a.ldc, a.bias, st);
+  if (rc) return rc;
+  if (defer) {
+    *defer = ReduceJob{a.part, a.part_bias, nwg, 256, NTB * 32, a.nb, a.C, a.ldc, a.bias};
+    return 0;
+  }
+  return launch_part_reduce(a.part, a.part_bias, nwg, 256, NTB * 32, a.nb, a.C, a.ldc, a.bias, st);
 }
 
 // kind: kWgradHidden (B [K][256]), kWgradFirst (B [K][96], 93 columns) or kWgradFc (B [K][32]);
 // K is rounded up to 32 (the A rows up to it exist and carry zero deltas)
 int launch_wgrad16(int kind, const float* A, const float* B, int64_t K, int64_t kb_rows, float* C, int64_t ldc,
-                   float* bias, hipStream_t st, const WgradSyn* syn) {
+                   float* bias, hipStream_t st, const WgradSyn* syn, ReduceJob* defer) {
   if (K <= 0) return 0;
   if (kb_rows <= 0) return PNR_E_ARG;
   K = (K + 31) / 32 * 32;
@@ -374,29 +439,29 @@ int launch_wgrad16(int kind, const float* A, const float* B, int64_t K, int64_t 
   WxArgs a{A, B, 256, K, kb_rows, ks, C, ldc, bias, nullptr, nullptr, 0, nullptr, nullptr, nullptr, syn->part,
            syn->part_bias};
   TimingScope ts(kTimeWgrad, K, st);
-  if (kind == kWgradHidden) return launch_k<8, 256>(a, st);
+  if (kind == kWgradHidden) return launch_k<8, 256>(a, st, defer);
   if (kind == kWgradOutDelta) {  // dW3 += delta4^T h3, delta4 rebuilt from g_out and the h4 masks
     if (!syn || !syn->g_out || !syn->masks || !syn->wo) return PNR_E_ARG;
     a.g_out = syn->g_out;
     a.masks = syn->masks;
     a.mgrp0 = syn->mgrp0;
     a.wo = syn->wo;
-    return launch_k<8, 256, true>(a, st);
+    return launch_k<8, 256, true>(a, st, defer);
   }
   if (kind == kWgradFc) {  // dWc_l (256 x 32) += gH_l^T c
     a.nb = kCDim;
-    return launch_k<1, 32>(a, st);
+    return launch_k<1, 32>(a, st, defer);
   }
   if (kind == kWgradFirst) {
     a.nb = kFourier;
-    return launch_k<3, 96>(a, st);
+    return launch_k<3, 96>(a, st, defer);
   }
   if (kind == kWgradFirstX) {  // dW0 (256 x 93) += delta1^T sin(x@B): e recomputed from x
     if (!syn || !syn->xP || !syn->fb) return PNR_E_ARG;
     a.nb = kFourier;
     a.xP = syn->xP;
     a.fb = syn->fb;
-    return launch_k<3, 96, false, true>(a, st);
+    return launch_k<3, 96, false, true>(a, st, defer);
   }
   return PNR_E_ARG;
 }
@@ -480,14 +545,14 @@ __global__ __launch_bounds__(256) void k_wgrad_skinny(const float4* __restrict__
 }
 
 static int skinny_blocks(int64_t K, int64_t* ks) {
-  *ks = (K + 1023) / 1024;
+  *ks = (K + kSkinnyMaxWg - 1) / kSkinnyMaxWg;
   if (*ks < 256) *ks = 256;
   return (int)((K + *ks - 1) / *ks);
 }
 
 // dWo (4 x 256) += g_out^T h4, dbo += colsum(g_out)
 int launch_wgrad_out16(const float* g_out, const float* h4, int64_t K, float* C, float* bias, float* part,
-                       float* part_bias, hipStream_t st) {
+                       float* part_bias, hipStream_t st, ReduceJob* defer) {
   if (K <= 0) return 0;
   if (!part || !part_bias) return PNR_E_ARG;
   int64_t ks;
@@ -496,11 +561,17 @@ int launch_wgrad_out16(const float* g_out, const float* h4, int64_t K, float* C,
   hipLaunchKernelGGL(k_wgrad_skinny<256>, dim3((unsigned)nb), dim3(256), 0, st, reinterpret_cast<const float4*>(g_out),
                      h4, K, ks, 4, kHidden, part, bias ? part_bias : nullptr);
   const int rc = hip_status(hipGetLastError());
-  return rc ? rc : launch_part_reduce(part, part_bias, nb, 4, kHidden, kHidden, C, (int64_t)kHidden, bias, st);
+  if (rc) return rc;
+  if (defer) {
+    *defer = ReduceJob{part, part_bias, nb, 4, kHidden, kHidden, C, (int64_t)kHidden, bias};
+    return 0;
+  }
+  return launch_part_reduce(part, part_bias, nb, 4, kHidden, kHidden, C, (int64_t)kHidden, bias, st);
 }
 
 // dB (3 x 93) += x^T g_arg: x rows float4 (x0, x1, x2, inside), g_arg fp32 [K][96]
-int launch_wgrad_fourier16(const float4* xP, const float* garg, int64_t K, float* C, float* part, hipStream_t st) {
+int launch_wgrad_fourier16(const float4* xP, const float* garg, int64_t K, float* C, float* part, hipStream_t st,
+                           ReduceJob* defer) {
   if (K <= 0) return 0;
   if (!part) return PNR_E_ARG;
   int64_t ks;
@@ -509,7 +580,12 @@ int launch_wgrad_fourier16(const float4* xP, const float* garg, int64_t K, float
   hipLaunchKernelGGL(k_wgrad_skinny<96>, dim3((unsigned)nb), dim3(256), 0, st, xP, garg, K, ks, 3, kFourier, part,
                      nullptr);
   const int rc = hip_status(hipGetLastError());
-  return rc ? rc : launch_part_reduce(part, nullptr, nb, 3, kFourier, kFourier, C, (int64_t)kFourier, nullptr, st);
+  if (rc) return rc;
+  if (defer) {
+    *defer = ReduceJob{part, nullptr, nb, 3, kFourier, kFourier, C, (int64_t)kFourier, nullptr};
+    return 0;
+  }
+  return launch_part_reduce(part, nullptr, nb, 3, kFourier, kFourier, C, (int64_t)kFourier, nullptr, st);
 }
 
 }  // namespace pnr
