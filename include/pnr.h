@@ -84,8 +84,12 @@ enum { PNR_GATHER_IDW = 0, PNR_GATHER_TRILINEAR = 1 };
  * f16x3 with an exact per-point power-of-two scale (any gradient magnitude), and the weight-gradient
  * GEMMs dW0..dW3, dWc are f16x3 on fp32-stored activations and deltas (per-wave power-of-two scale of
  * the deltas; delta4 = (Wo^T g_out) masked is not stored but rebuilt in fp32 FMAs inside the dW3
- * GEMM); dWo and dB are fp32 FMA reductions.  Every GEMM of the backward thus carries >= 22
- * significant bits per operand and accumulates in fp32. */
+ * GEMM); dWo and dB are fp32 FMA reductions.  Point features (the fc_c operand) are split under a
+ * power-of-two scale of their own in both directions (forward: per wave; dWc: per-wave running
+ * scale), so they keep 22 bits whatever their magnitude (the reference's fine-grid features have
+ * std 1e-4).  Hidden activations and Fourier features are split unscaled (|e| <= 1, activations
+ * checked < 65504): 22 bits for every value >= 2^-14, and an absolute error <= 2^-25 below that.
+ * Every GEMM accumulates in fp32. */
 enum { PNR_PREC_FP32 = 0, PNR_PREC_BF16X3 = 1, PNR_PREC_BF16 = 2, PNR_PREC_F16X3 = 3 };
 
 /* Status bits (ABI 7) the kernels OR into the caller's device word pnr_render_params.status:

@@ -39,6 +39,53 @@ from .ref_render import N_LAYERS, OUT_OF_BOUND_SIGMA, inside_bound
 Params = Dict[str, torch.Tensor]
 C_DIM = 32
 
+# ---- summation magnitudes (test yardstick) ---------------------------------------------------
+# Every gradient of the decoder parameters and of the point features is a sum over samples, g =
+# sum_p t_p.  Rounded in any order, float32 arithmetic leaves an error of order u sum_p |t_p|
+# (u = 2^-24), which a relative bound on g alone cannot express where the sum cancels (|g| <<
+# sum_p |t_p|).  While `magnitudes()` is active, mlp_forward_c and point_gather record, per
+# gradient element, M = sum_p |t_p| (|delta|^T |h| for a weight, sum |delta| for a bias, sum |w_k|
+# |dL/dc| for a feature row) by tensor hooks on the float32 oracle's graph; the GPU parity tests add
+# a floor of a few ulps of M to their elementwise tolerance.
+_MAG: Optional[Dict[str, torch.Tensor]] = None
+
+
+class magnitudes:
+    """Context manager: `with magnitudes() as m:` -- after the backward, m[name] holds M for the
+    parameter `name` (and m['feats'] for the point features), summed over every call."""
+
+    def __enter__(self):
+        global _MAG
+        _MAG = {}
+        return _MAG
+
+    def __exit__(self, *exc):
+        global _MAG
+        _MAG = None
+        return False
+
+
+def _mag_add(name: str, v: torch.Tensor) -> None:
+    m = _MAG
+    if m is None:
+        return
+    v = v.detach().double()
+    m[name] = m[name] + v if name in m else v
+
+
+def _mag_linear(out: torch.Tensor, inp: torch.Tensor, wname: str, bname: Optional[str]) -> None:
+    """out = inp W^T + b: |dL/dout|^T |inp| for W, sum |dL/dout| for b."""
+    if _MAG is None or not out.requires_grad:
+        return
+    a = inp.detach().abs().double()
+
+    def hook(g):
+        ga = g.detach().abs().double()
+        _mag_add(wname, ga.t() @ a)
+        if bname is not None:
+            _mag_add(bname, ga.sum(0))
+    out.register_hook(hook)
+
 
 def init_fc_c(params: Params, seed: int = 1, c_dim: int = C_DIM, hidden: int = 256) -> Params:
     """Add `fc_c.{i}` (nn.Linear(c_dim, hidden), decoder.py:122-125) with torch's default Linear
@@ -134,6 +181,15 @@ def point_gather(p: torch.Tensor, xyz: torch.Tensor, feats: torch.Tensor, mode: 
     c = torch.zeros(fk.shape[0], fk.shape[2], dtype=torch.float32)
     for j in range(idx.shape[1]):                                # sequential, ascending distance
         c = c + wn[:, j:j + 1] * fk[:, j]
+    if _MAG is not None and c.requires_grad:
+        wa = torch.where(idx >= 0, wn.detach().abs(), torch.zeros_like(wn)).double()
+        ic = idx.clamp(min=0).reshape(-1)
+        M = feats.shape[0]
+
+        def hook(g):  # M_feats[i] += |w_k| |dL/dc| over the samples whose neighbour k is point i
+            t = (wa[:, :, None] * g.detach().abs().double()[:, None, :]).reshape(-1, g.shape[1])
+            _mag_add('feats', torch.zeros((M, g.shape[1]), dtype=torch.float64).index_add_(0, ic, t))
+        c.register_hook(hook)
     if return_idx:
         return c, idx, wn
     return c
@@ -142,11 +198,18 @@ def point_gather(p: torch.Tensor, xyz: torch.Tensor, feats: torch.Tensor, mode: 
 def mlp_forward_c(params: Params, p: torch.Tensor, c: torch.Tensor) -> torch.Tensor:
     """decoder.py:177-203 with c_dim != 0, skips=[], color=True: h = relu(W h + b) + fc_c[i](c)."""
     x = p.reshape(-1, 3).float()
-    h = torch.sin(x @ params['embedder._B'])
+    arg = x @ params['embedder._B']
+    _mag_linear(arg, x, 'embedder._B.T', None)
+    h = torch.sin(arg)
     for li in range(N_LAYERS):
-        h = F.relu(F.linear(h, params[f'pts_linears.{li}.weight'], params[f'pts_linears.{li}.bias']))
-        h = h + F.linear(c, params[f'fc_c.{li}.weight'], params[f'fc_c.{li}.bias'])
-    return F.linear(h, params['output_linear.weight'], params['output_linear.bias'])
+        z = F.linear(h, params[f'pts_linears.{li}.weight'], params[f'pts_linears.{li}.bias'])
+        _mag_linear(z, h, f'pts_linears.{li}.weight', f'pts_linears.{li}.bias')
+        zc = F.linear(c, params[f'fc_c.{li}.weight'], params[f'fc_c.{li}.bias'])
+        _mag_linear(zc, c, f'fc_c.{li}.weight', f'fc_c.{li}.bias')
+        h = F.relu(z) + zc
+    out = F.linear(h, params['output_linear.weight'], params['output_linear.bias'])
+    _mag_linear(out, h, 'output_linear.weight', 'output_linear.bias')
+    return out
 
 
 def mlp_forward_c_cr(params: Params, p: torch.Tensor, c: torch.Tensor) -> torch.Tensor:
@@ -165,6 +228,13 @@ def mlp_forward_c_cr(params: Params, p: torch.Tensor, c: torch.Tensor) -> torch.
         h = _RoundF32.apply(a)
     return _RoundF32.apply(F.linear(h.double(), params['output_linear.weight'].double(),
                                     params['output_linear.bias'].double()))
+
+
+def magnitude_of(m: Dict[str, torch.Tensor], name: str) -> torch.Tensor:
+    """M for parameter `name` in its own shape (embedder._B is recorded transposed)."""
+    if name == 'embedder._B':
+        return m['embedder._B.T'].t()
+    return m[name]
 
 
 def eval_points_c(params: Params, p: torch.Tensor, bound: torch.Tensor, points: dict, cr: bool = False) -> torch.Tensor:

@@ -98,9 +98,11 @@ __device__ __forceinline__ float fourier_sc(float x) {
 
 // Power of two s with m s in [2^13, 2^14) (1 for m = 0, inf, NaN): the scale under which a block
 // of values with max |x| = m is split into f16 hi + lo parts (in range, 22 bits below the max).
-// s is clamped to [2^-60, 2^60]: its products with the weight-image scales (<= 2^20) and their
-// inverses stay normal fp32 numbers (a block below 2^-46 keeps ~18 bits; nothing overflows).
-constexpr int kScaleExpMax = 60;
+// s is clamped to [2^-100, 2^100]: its products with the weight-image scales (2^-20 .. 2^20, k_wscale)
+// and their inverses stay normal fp32 numbers (<= 2^120), and a block down to 2^-86 keeps 22 bits
+// (gradients of samples far behind a surface reach 1e-30: the fp32 reference keeps them, so does
+// the split path).
+constexpr int kScaleExpMax = 100;
 __device__ __forceinline__ float pt_scale(float m) {
   if (!(m > 0.f) || !(m < 3.0e38f)) return 1.f;
   int ex;

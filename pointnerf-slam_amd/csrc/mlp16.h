@@ -190,7 +190,8 @@ struct BfState {
   f32x16 f;            // feature-branch product of that tile
   float4 bq[4];        // bias quads of that tile (read from LDS at the top of the step)
   float4 bcq[4];       // fc bias quads (features)
-  float inv, finv;     // f16 weight scales of the layer / fc branch
+  float inv, finv;     // f16 weight scales of the layer / fc branch (finv: times cinv)
+  float cinv;          // 1 / s_c: the wave's feature tile is split as c s_c (f16x3; wave-uniform)
   uint32_t mw[4];      // ReLU bit words of the layer being converted
   Frag<PR> F[R];       // fragment ring (one 32-row output tile of the current / next step each)
   Frag<PR> FC;         // feature-branch fragments of the step's epilogue tile
@@ -344,7 +345,7 @@ struct BfFwd {
     const float* fr = raw_lds(lds) + kRawBytes / 4;
 #pragma unroll
     for (int q = 0; q < 4; ++q) S.bcq[q] = *reinterpret_cast<const float4*>(fr + L * 256 + 32 * t + 8 * q + 4 * hh);
-    if (F16) S.finv = fr[kFcRawInv + L];
+    if (F16) S.finv = fr[kFcRawInv + L] * S.cinv;
   }
 
   template <int L, int t, int q>
@@ -710,8 +711,23 @@ static __device__ __forceinline__ void fwd16_tile(const BfFwdArgs& a, int mode, 
         cv[8 * s + 4 * jq + 0] = v.x; cv[8 * s + 4 * jq + 1] = v.y;
         cv[8 * s + 4 * jq + 2] = v.z; cv[8 * s + 4 * jq + 3] = v.w;
       }
+    // f16x3: the wave's feature tile is split as c s_c, s_c = 2^k putting the wave's max |c| in
+    // [2^13, 2^14) (pt_scale), so the lo parts stay out of the f16 subnormals whatever the feature
+    // magnitude (the reference's fine-grid features have std 1e-4); the fc product carries s_c and
+    // finv = 2^-w / s_c undoes it exactly.  Wave-uniform (an SGPR): the training kernel with the
+    // feature branch has no VGPR to spare for a per-point scale
+    S.cinv = 1.f;
+    if constexpr (Prec<PR>::F16) {
+      float m = 0.f;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) S.vmax = fmaxf(S.vmax, fabsf(cv[r]));
+      for (int r = 0; r < 16; ++r) m = fmaxf(m, fabsf(cv[r]));
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+      const float sc = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, pt_scale(m))));
+#pragma unroll
+      for (int r = 0; r < 16; ++r) cv[r] *= sc;
+      S.cinv = 1.f / sc;
+    }
     split_tile<PR>(cv, S.ct);
   }
   // no accumulator zero fill: the first input tile of every layer starts its tiles from 0 (ZERO in

@@ -16,8 +16,11 @@
 // accumulation (the dropped Al Bl term is 2^-22 relative).  A (gradients: any magnitude) is split
 // under a per-wave running power of two sc (max |A| sc < 2^15 on every tile; when a tile needs a
 // smaller sc -- the first nonzero one does -- the accumulator is rescaled by the exact ratio).
-// B is split unscaled: activations < 65504 (the forward's PNR_STATUS_F16_RANGE check), |e| <= 1,
-// point features.  The bias row sums are fp32 sums of A.
+// B is split unscaled where its range is known (activations < 65504 by the forward's
+// PNR_STATUS_F16_RANGE check, |e| <= 1); the point features c (dWc, any magnitude: the reference's
+// fine-grid features have std 1e-4, where an unscaled lo part would sit in the f16 subnormals) are
+// split under a per-wave running power of two of their own (BSC), like A.  The bias row sums are
+// fp32 sums of A.
 //
 // The GEMM moves 2 x 4 B per point and unit and is HBM-bound (the kernel streams 64 KB per 32-point
 // tile at ~3 flops per byte of f16 MFMA work).  K (points) is split over workgroups of 8 waves
@@ -122,7 +125,11 @@ __device__ __forceinline__ void wx_load(const WxArgs& a, int64_t k0, WxRegs<NTB,
 }
 
 // B tile -> hi / lo f16 planes of `slot` (SYN: + the next tile's g_out rows into the other slot)
-template <int NTB, int WB, bool SYN, bool FOUR>
+// BSC (B = point features, WB = 32): the tile is staged in fp32, rows of kBscRow floats (16-B
+// aligned; a wave's 32-lane half reads 32 consecutive columns of one row: conflict-free)
+constexpr int kBscRow = 36;
+
+template <int NTB, int WB, bool SYN, bool FOUR, bool BSC = false>
 __device__ __forceinline__ void wx_stage_b(const WxRegs<NTB, WB>& R, char* slot, char* next_slot,
                                            const float (&fbr)[Wx3<NTB, WB>::kBPer][3][4]) {
   using Cfg = Wx3<NTB, WB>;
@@ -133,6 +140,10 @@ __device__ __forceinline__ void wx_stage_b(const WxRegs<NTB, WB>& R, char* slot,
     const int q = tid + Cfg::kThreads * i;
     if (Cfg::kB4 % Cfg::kThreads == 0 || q < Cfg::kB4) {
       const int r = q / Cfg::kC4, c = 4 * (q % Cfg::kC4);
+      if constexpr (BSC) {
+        *reinterpret_cast<float4*>(slot + (r * kBscRow + c) * 4) = R.b[i];
+        continue;
+      }
       float v[4] = {R.b[i].x, R.b[i].y, R.b[i].z, R.b[i].w};
       if constexpr (FOUR) {  // e[c + e] = sin(x @ B[:, c + e]), as k_mlp_fwd16's prologue computes it
         const float x0 = R.b[i].x, x1 = R.b[i].y, x2 = R.b[i].z;
@@ -176,8 +187,10 @@ __device__ __forceinline__ f16x8 tr_frag(const char* img, int T, int s) {
   return r;
 }
 
-template <int NTB, int WB, bool SYN, bool FOUR>
+template <int NTB, int WB, bool SYN, bool FOUR, bool BSC>
 __global__ __launch_bounds__(512, 1) void k_wgrad16(WxArgs a) {
+  static_assert(!BSC || (NTB == 1 && WB == 32 && !SYN && !FOUR), "BSC: the fc_c shape");
+  static_assert(!BSC || 32 * kBscRow * 4 <= Wx3<NTB, WB>::kSlot, "BSC tile fits the slot");
   using Cfg = Wx3<NTB, WB>;
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int lane = threadIdx.x & 63, hh = lane >> 5;
@@ -192,7 +205,8 @@ __global__ __launch_bounds__(512, 1) void k_wgrad16(WxArgs a) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[y][r] = 0.f;
   float cs = 0.f;          // fp32 row sums of A (bias) for row 32w + (lane & 31), this lane's points
-  float sc = 0x1p60f;      // running scale of A (wave-uniform, <= 2^60 as pt_scale); lowered by a tile
+  float sc = 0x1p100f;     // running scale of A (wave-uniform, <= 2^100 as pt_scale); lowered by a tile
+  float sb = 0x1p100f;     // BSC: the same for B
   WxRegs<NTB, WB> R;
   float wo[4];             // SYN: Wo[:, u] of this lane's unit, and its mask bit
   int mbit = 0;
@@ -219,7 +233,7 @@ __global__ __launch_bounds__(512, 1) void k_wgrad16(WxArgs a) {
     char* slot = lds + (t & 1) * Cfg::kSlot;
     // g_out rows of tile t + 1 go to the other slot: their last reader (synth of tile t - 1) ran
     // before the previous barrier
-    wx_stage_b<NTB, WB, SYN, FOUR>(R, slot, lds + ((t + 1) & 1) * Cfg::kSlot, fbr);
+    wx_stage_b<NTB, WB, SYN, FOUR, BSC>(R, slot, lds + ((t + 1) & 1) * Cfg::kSlot, fbr);
     if constexpr (SYN) {
       // delta4 = (Wo^T g_out) masked, fp32 FMAs (the tile's g_out rows from LDS, staged before the
       // previous barrier; broadcast reads)
@@ -265,28 +279,68 @@ __global__ __launch_bounds__(512, 1) void k_wgrad16(WxArgs a) {
       wx_load<NTB, WB, SYN, FOUR>(a, kb + 32 * tn, R);
     }
     __syncthreads();  // planes of tile t written; every wave is done with the slot of tile t - 2
-    const char* ph = slot;
-    const char* pl = slot + Cfg::kPlane;
+    if constexpr (BSC) {
+      // the lane's B operand (column lane & 31, points 16 s + 8 hh + j) from the fp32 rows, split
+      // under the wave's running B scale (lowered, with the accumulator, when this tile needs it)
+      const float* tb = reinterpret_cast<const float*>(slot) + (lane & 31);
+      float bv[16];
+      float mb = 0.f;
 #pragma unroll
-    for (int s = 0; s < 2; ++s)
+      for (int s = 0; s < 2; ++s)
 #pragma unroll
-      for (int y = 0; y < NTB; ++y) {
-        const f16x8 bh = tr_frag(ph, y, s), bl = tr_frag(pl, y, s);
-        acc[y] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[s], bh, acc[y], 0, 0, 0);
-        acc[y] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[s], bl, acc[y], 0, 0, 0);
-        acc[y] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[s], bh, acc[y], 0, 0, 0);
+        for (int j = 0; j < 8; ++j) {
+          bv[8 * s + j] = tb[(16 * s + 8 * hh + j) * kBscRow];
+          mb = fmaxf(mb, fabsf(bv[8 * s + j]));
+        }
+      if (__builtin_amdgcn_ballot_w64(mb * sb >= 32768.f) != 0) {
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) mb = fmaxf(mb, __shfl_xor(mb, o));
+        const float ns = pt_scale(mb);
+        const float r = ns / sb;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[0][i] *= r;
+        sb = ns;
       }
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        f16x8 bh, bl;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float x = bv[8 * s + j] * sb;
+          const _Float16 h = (_Float16)x;
+          bh[j] = h;
+          bl[j] = (_Float16)(x - (float)h);
+        }
+        acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[s], bh, acc[0], 0, 0, 0);
+        acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[s], bl, acc[0], 0, 0, 0);
+        acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[s], bh, acc[0], 0, 0, 0);
+      }
+    } else {
+      const char* ph = slot;
+      const char* pl = slot + Cfg::kPlane;
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int y = 0; y < NTB; ++y) {
+          const f16x8 bh = tr_frag(ph, y, s), bl = tr_frag(pl, y, s);
+          acc[y] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[s], bh, acc[y], 0, 0, 0);
+          acc[y] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[s], bl, acc[y], 0, 0, 0);
+          acc[y] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[s], bh, acc[y], 0, 0, 0);
+        }
+    }
   }
   // two-phase flush: this workgroup's tile with plain stores (each instruction two 128-B row
   // segments), summed in a fixed order by k_part_reduce.  (Float atomics ran at one 256-B
   // wave-instruction per ~50 ns per CU -- a 256 x 256 tile took ~51 us per workgroup -- and left the
   // summation order to the scheduler.)
-  const float inv = 1.f / sc;
+  // (two multiplies: 1 / (sc sb) can leave the fp32 range where each factor does not)
+  const float inv = 1.f / sc, invb = BSC ? 1.f / sb : 1.f;
   float* P = a.part + (int64_t)blockIdx.x * 256 * (NTB * 32);
 #pragma unroll
   for (int y = 0; y < NTB; ++y)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) P[(32 * w + perm(r, hh)) * (NTB * 32) + 32 * y + (lane & 31)] = acc[y][r] * inv;
+    for (int r = 0; r < 16; ++r)
+      P[(32 * w + perm(r, hh)) * (NTB * 32) + 32 * y + (lane & 31)] = BSC ? (acc[y][r] * inv) * invb : acc[y][r] * inv;
   cs += __shfl_xor(cs, 32);
   if (a.bias && hh == 0) a.part_bias[(int64_t)blockIdx.x * 256 + 32 * w + lane] = cs;
 }
@@ -404,10 +458,10 @@ int launch_part_reduce(const float* part, const float* pbias, int nwg, int nr, i
   return hip_status(hipGetLastError());
 }
 
-template <int NTB, int WB, bool SYN = false, bool FOUR = false>
+template <int NTB, int WB, bool SYN = false, bool FOUR = false, bool BSC = false>
 static int launch_k(const WxArgs& a, hipStream_t st, ReduceJob* defer) {
   using Cfg = Wx3<NTB, WB>;
-  auto kern = k_wgrad16<NTB, WB, SYN, FOUR>;
+  auto kern = k_wgrad16<NTB, WB, SYN, FOUR, BSC>;
   static const bool attr = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                                                Cfg::kLds) == hipSuccess;
   if (!attr) return PNR_E_ARG;
@@ -450,7 +504,7 @@ int launch_wgrad16(int kind, const float* A, const float* B, int64_t K, int64_t 
   }
   if (kind == kWgradFc) {  // dWc_l (256 x 32) += gH_l^T c
     a.nb = kCDim;
-    return launch_k<1, 32>(a, st, defer);
+    return launch_k<1, 32, false, false, true>(a, st, defer);
   }
   if (kind == kWgradFirst) {
     a.nb = kFourier;

@@ -97,10 +97,15 @@ class MapStep:
     regulation, a fixed order) and Adam runs.  At the faithful batch (1,000 rays) every phase is
     latency-bound and leaves CUs idle, so the two chains overlap.  Neither chain goes through
     autograd: pnr.renderer.TrainPass calls the C ABI directly and pnr_map_loss forms the loss and its
-    gradient in one pass.  `overlap=False` runs both chains on the caller's stream."""
+    gradient in one pass.  `overlap=False` runs both chains on the caller's stream; the default
+    'auto' overlaps them up to OVERLAP_MAX_RAYS rays.  Beyond that each chain fills the chip on its
+    own (the persistent MLP kernels hold every CU's LDS, so the two chains' launches only take turns)
+    and running them in order keeps each kernel's launch interval its own (bench.py times them)."""
+
+    OVERLAP_MAX_RAYS = 32768
 
     def __init__(self, renderer, decoder, lr=2e-4, w_color_loss=0.05, w_reg=0.0005, ddp=None, points=None,
-                 feat_lr=None, overlap=True):
+                 feat_lr=None, overlap='auto'):
         self.renderer = renderer
         self.decoder = decoder
         self.points = points
@@ -127,14 +132,17 @@ class MapStep:
         self.w_color = w_color_loss
         self.w_reg = w_reg
         self.ddp = ddp
+        if overlap not in (True, False, 'auto'):
+            raise ValueError(f'overlap must be True, False or "auto", not {overlap!r}')
         self.overlap = overlap
-        dev = self.flat.data.device
-        self.side = torch.cuda.Stream(dev) if overlap else None
-        # the regulation chain's gradient buffer (same layout as flat.grad) and its views
-        self.grad2 = torch.zeros_like(self.flat.grad) if overlap else None
+        self.side = None   # the side stream and the regulation chain's gradient buffer (same layout
+        self.grad2 = None  # as flat.grad) with its views: made on the first overlapped step
         self._views = {'main': self._split(self.flat.grad)}
-        if overlap:
-            self._views['side'] = self._split(self.grad2)
+
+    def _overlaps(self, n_rays):
+        if self.overlap != 'auto':
+            return bool(self.overlap)
+        return n_rays <= self.OVERLAP_MAX_RAYS
 
     def _split(self, buf):
         """(11 decoder, 8 fc_c or None, features or None) views of a flat-gradient-shaped buffer."""
@@ -182,7 +190,12 @@ class MapStep:
             self.points.index()
             self.points._feats_for_gather()
         main = torch.cuda.current_stream(dev)
-        if self.overlap:
+        overlap = self._overlaps(rays_o.shape[0])
+        if overlap and self.side is None:
+            self.side = torch.cuda.Stream(dev)
+            self.grad2 = torch.zeros_like(self.flat.grad)
+            self._views['side'] = self._split(self.grad2)
+        if overlap:
             self.side.wait_stream(main)
             with torch.cuda.stream(self.side):
                 self.grad2.zero_()
@@ -191,7 +204,7 @@ class MapStep:
         l_ren, g_d, g_c, _ = map_loss(gt_depth, d, gt_color, c, self.w_color)
         views = self._views['main']
         ren.backward(views[0], g_fc=views[1], g_feats=views[2], g_depth=g_d, g_rgb=g_c)
-        if self.overlap:
+        if overlap:
             main.wait_stream(self.side)
             self.flat.grad.add_(self.grad2)  # render + regulation gradients, a fixed order
         else:
