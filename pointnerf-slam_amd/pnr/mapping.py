@@ -61,8 +61,9 @@ class Adam:
         self.segments = segments if segments is not None else [(0, flat.numel, lr)]
         self.b1, self.b2 = betas
         self.eps = eps
-        self.m = torch.zeros_like(flat.data)
-        self.v = torch.zeros_like(flat.data)
+        # moments per segment, sized to it: a sharded feature tail holds only the owned range's m / v
+        self.mv = [(torch.zeros(n, device=flat.data.device), torch.zeros(n, device=flat.data.device))
+                   for _, n, _ in self.segments]
         self.step_count = 0
         self.step_dev = None  # int32 device counter of completed steps (graph mode)
 
@@ -75,14 +76,14 @@ class Adam:
         lib = _lib.load()
         f = self.flat
         st = _lib.stream_of(f.data.device)
-        for a, n, lr in self.segments:
+        for (a, n, lr), (m, v) in zip(self.segments, self.mv):
             if self.step_dev is not None:
-                _lib.check(lib.pnr_adam_step_dev(_lib.ptr(f.data[a:]), _lib.ptr(f.grad[a:]), _lib.ptr(self.m[a:]),
-                                                 _lib.ptr(self.v[a:]), n, lr, self.b1, self.b2, self.eps,
+                _lib.check(lib.pnr_adam_step_dev(_lib.ptr(f.data[a:]), _lib.ptr(f.grad[a:]), _lib.ptr(m),
+                                                 _lib.ptr(v), n, lr, self.b1, self.b2, self.eps,
                                                  _lib.ptr(self.step_dev), st), 'adam_step_dev')
             else:
-                _lib.check(lib.pnr_adam_step(_lib.ptr(f.data[a:]), _lib.ptr(f.grad[a:]), _lib.ptr(self.m[a:]),
-                                             _lib.ptr(self.v[a:]), n, lr, self.b1, self.b2, self.eps, self.step_count,
+                _lib.check(lib.pnr_adam_step(_lib.ptr(f.data[a:]), _lib.ptr(f.grad[a:]), _lib.ptr(m),
+                                             _lib.ptr(v), n, lr, self.b1, self.b2, self.eps, self.step_count,
                                              st), 'adam_step')
         if self.step_dev is not None:
             _lib.check(lib.pnr_step_advance(_lib.ptr(self.step_dev), st), 'step_advance')

@@ -296,7 +296,9 @@ def test_render_with_small_features_matches_oracle(pnr_mod, dev):
     ro, rd, gt, xyz, feats = surface_cloud(dev, seed=7)
     feats = feats * 2e-4
     n = 256
-    ro, rd, gt = ro[:n], rd[:n], gt[:n]
+    # (gt 2% beyond the render: with features this small the render is the golden depth to ~1e-7, and
+    # the depth loss's sign(depth - gt) would hinge on rounding)
+    ro, rd, gt = ro[:n], rd[:n], gt[:n] * 1.02
     params = RP.init_fc_c(golden_params('trained'), seed=4)
     kw = dict(mode='idw', k=8, radius=0.04, eps=1e-6)
     pts = pnr_mod.NeuralPoints(xyz.to(dev), feats.to(dev), **kw).to(dev)
