@@ -16,14 +16,11 @@
 // accumulation (the dropped Al Bl term is 2^-22 relative).  A (gradients: any magnitude) is split
 // under a per-wave running power of two sc (max |A| sc < 2^15 on every tile; when a tile needs a
 // smaller sc -- the first nonzero one does -- the accumulator is rescaled by the exact ratio).
-// B rows of the hidden layers (activations h, one row per point) are split under a per-POINT power
-// of two s_k (RSC: max_j |h[k][j]| s_k in [2^13, 2^14)) and A's column k is divided by the same s_k
-// (exact): without it a unit whose activations sit far below 1 had its lo parts in the f16
-// subnormals (absolute step 2^-24: an activation of 1e-6 kept ~5 bits).  Under s_k an activation
-// keeps 22 bits down to 2^-17 of its point's largest one, and 1e-3 relative down to ~4e-9 of it.
-// The Fourier features (|e| <= 1, dW0) are split unscaled; the point features c (dWc, any magnitude:
-// the reference's fine-grid features have std 1e-4) under a per-wave running power of two of their
-// own (BSC), like A.  The bias row sums are fp32 sums of the unscaled A.
+// B is split unscaled where its range is known (activations < 65504 by the forward's
+// PNR_STATUS_F16_RANGE check, |e| <= 1); the point features c (dWc, any magnitude: the reference's
+// fine-grid features have std 1e-4, where an unscaled lo part would sit in the f16 subnormals) are
+// split under a per-wave running power of two of their own (BSC), like A.  The bias row sums are
+// fp32 sums of A.
 //
 // The GEMM moves 2 x 4 B per point and unit and is HBM-bound (the kernel streams 64 KB per 32-point
 // tile at ~3 flops per byte of f16 MFMA work).  K (points) is split over workgroups of 8 waves
@@ -52,8 +49,7 @@ template <int NTB, int WB>
 struct Wx3 {
   static constexpr int kThreads = 512;                   // 8 waves, 2 per SIMD
   static constexpr int kPlane = NTB * kTileB;            // one plane (hi or lo) of a B tile
-  static constexpr int kSlot = 2 * kPlane + 512 + 128;   // + the tile's 32 g_out rows (SYN), 1 / s_k (RSC)
-  static constexpr int kScl = 2 * kPlane + 512;          // offset of the 32 per-point inverse scales
+  static constexpr int kSlot = 2 * kPlane + 512;         // + the tile's 32 g_out rows (SYN)
   static constexpr int kLds = 2 * kSlot;                 // double-buffered
   static constexpr int kC4 = WB / 4;                     // float4 per B row
   static constexpr int kB4 = 32 * kC4;                   // float4 per B tile
@@ -91,10 +87,10 @@ struct WxRegs {
   float4 go;                                   // SYN: g_out row k0 + 32 + tid (threads < 32): the NEXT tile's
 };
 
-// A operand of the tile at k0 (SYN: the h4 mask words)
-template <int NTB, int WB, bool SYN>
-__device__ __forceinline__ void wx_load_a(const WxArgs& a, int64_t k0, WxRegs<NTB, WB>& R) {
-  const int lane = threadIdx.x & 63;
+template <int NTB, int WB, bool SYN, bool FOUR>
+__device__ __forceinline__ void wx_load(const WxArgs& a, int64_t k0, WxRegs<NTB, WB>& R) {
+  using Cfg = Wx3<NTB, WB>;
+  const int tid = threadIdx.x, lane = tid & 63;
   if constexpr (SYN) {
     // mask word of unit u = 32w + (lane & 31) for the lane's 16 points 8 hh + 16 s + j of the
     // 32-point group: uint4 (point + 32 ((u >> 2) & 1)), component u >> 6 (k_mlp_fwd16 conv1)
@@ -105,23 +101,16 @@ __device__ __forceinline__ void wx_load_a(const WxArgs& a, int64_t k0, WxRegs<NT
     for (int s = 0; s < 2; ++s)
 #pragma unroll
       for (int j = 0; j < 8; ++j) R.a[8 * s + j] = __uint_as_float(mw[(8 * (lane >> 5) + 16 * s + j) * 4]);
+    if (tid < 32) {  // one tile ahead (staged into the other slot, read after the next barrier)
+      const int64_t row = k0 + 32 + tid;
+      R.go = a.g_out[row < a.K ? row : a.K - 1];
+    }
   } else {
     const float* Ab = a.A + (k0 + 8 * (lane >> 5)) * 256 + 32 * wave_id() + (lane & 31);
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
       for (int j = 0; j < 8; ++j) R.a[8 * s + j] = Ab[(16 * s + j) * 256];
-  }
-}
-
-// B tile at k0 (SYN: + the g_out rows of the tile after it)
-template <int NTB, int WB, bool SYN, bool FOUR>
-__device__ __forceinline__ void wx_load_b(const WxArgs& a, int64_t k0, WxRegs<NTB, WB>& R) {
-  using Cfg = Wx3<NTB, WB>;
-  const int tid = threadIdx.x;
-  if (SYN && tid < 32) {  // one tile ahead (staged into the other slot, read after the next barrier)
-    const int64_t row = k0 + 32 + tid;
-    R.go = a.g_out[row < a.K ? row : a.K - 1];
   }
 #pragma unroll
   for (int i = 0; i < Cfg::kBPer; ++i) {
@@ -140,16 +129,12 @@ __device__ __forceinline__ void wx_load_b(const WxArgs& a, int64_t k0, WxRegs<NT
 // aligned; a wave's 32-lane half reads 32 consecutive columns of one row: conflict-free)
 constexpr int kBscRow = 36;
 
-// RSC (WB = 256): a wave holds whole rows (q = tid + 512 i: row (tid >> 6) + 8 i), so the row max
-// is a wave reduction; the row is split under s_k and lane 0 writes 1 / s_k for the A side
 template <int NTB, int WB, bool SYN, bool FOUR, bool BSC = false>
 __device__ __forceinline__ void wx_stage_b(const WxRegs<NTB, WB>& R, char* slot, char* next_slot,
                                            const float (&fbr)[Wx3<NTB, WB>::kBPer][3][4]) {
   using Cfg = Wx3<NTB, WB>;
-  constexpr bool RSC = WB == 256 && !FOUR && !BSC;
   const int tid = threadIdx.x;
   if (SYN && tid < 32) reinterpret_cast<float4*>(next_slot + 2 * Cfg::kPlane)[tid] = R.go;
-  static_assert(!RSC || (Cfg::kC4 == 64 && Cfg::kB4 % Cfg::kThreads == 0), "RSC: one row per wave and i");
 #pragma unroll
   for (int i = 0; i < Cfg::kBPer; ++i) {
     const int q = tid + Cfg::kThreads * i;
@@ -160,15 +145,6 @@ __device__ __forceinline__ void wx_stage_b(const WxRegs<NTB, WB>& R, char* slot,
         continue;
       }
       float v[4] = {R.b[i].x, R.b[i].y, R.b[i].z, R.b[i].w};
-      if constexpr (RSC) {  // row r's scale: a wave max (one row at a time: registers)
-        float m = fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3])));
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
-        const float rs = pt_scale(m);
-        if ((tid & 63) == 0) reinterpret_cast<float*>(slot + Cfg::kScl)[r] = 1.f / rs;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] *= rs;
-      }
       if constexpr (FOUR) {  // e[c + e] = sin(x @ B[:, c + e]), as k_mlp_fwd16's prologue computes it
         const float x0 = R.b[i].x, x1 = R.b[i].y, x2 = R.b[i].z;
 #pragma unroll
@@ -248,11 +224,7 @@ __global__ __launch_bounds__(512, 1) void k_wgrad16(WxArgs a) {
 #pragma unroll
       for (int e = 0; e < 4; ++e)
         fbr[i][d][e] = FOUR ? a.fb[d * kFourierPad + 4 * ((threadIdx.x + Cfg::kThreads * i) % Cfg::kC4) + e] : 0.f;
-  constexpr bool RSC = WB == 256 && !FOUR && !BSC;
-  if (ntile > 0) {
-    wx_load_a<NTB, WB, SYN>(a, kb, R);
-    wx_load_b<NTB, WB, SYN, FOUR>(a, kb, R);
-  }
+  if (ntile > 0) wx_load<NTB, WB, SYN, FOUR>(a, kb, R);
   if (SYN && ntile > 0) {  // the first tile's g_out rows; later tiles' are staged one tile ahead
     if (threadIdx.x < 32) reinterpret_cast<float4*>(lds + 2 * Cfg::kPlane)[threadIdx.x] = a.g_out[kb + threadIdx.x];
     __syncthreads();
@@ -275,27 +247,12 @@ __global__ __launch_bounds__(512, 1) void k_wgrad16(WxArgs a) {
           R.a[8 * s + j] = ((__float_as_uint(R.a[8 * s + j]) >> mbit) & 1u) ? d : 0.f;
         }
     }
-#pragma unroll
-    for (int i = 0; i < 16; ++i) cs += R.a[i];
-    __builtin_amdgcn_sched_barrier(0);  // (hoisted next-tile loads overlapped the synth's registers: spills)
-    {  // next tile's B into the (now free) registers; the last tile is re-read (keeps the loop uniform)
-      const int64_t tn = t + 1 < ntile ? t + 1 : t;
-      wx_load_b<NTB, WB, SYN, FOUR>(a, kb + 32 * tn, R);
-    }
-    __syncthreads();  // planes (and 1 / s_k) of tile t written; every wave is done with tile t - 2's slot
-    if constexpr (RSC) {  // A column k / s_k: this lane's points 16 s + 8 hh + j
-      const float4* is = reinterpret_cast<const float4*>(slot + Cfg::kScl) + 2 * hh;
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const float4 u = is[4 * s], v = is[4 * s + 1];
-        const float f[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
-#pragma unroll
-        for (int j = 0; j < 8; ++j) R.a[8 * s + j] *= f[j];
-      }
-    }
     float m = 0.f;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) m = fmaxf(m, fabsf(R.a[i]));
+    for (int i = 0; i < 16; ++i) {
+      m = fmaxf(m, fabsf(R.a[i]));
+      cs += R.a[i];
+    }
     if (__builtin_amdgcn_ballot_w64(m * sc >= 32768.f) != 0) {  // this tile needs a smaller scale
 #pragma unroll
       for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
@@ -317,11 +274,11 @@ __global__ __launch_bounds__(512, 1) void k_wgrad16(WxArgs a) {
         ah[s][j] = h;
         al[s][j] = (_Float16)(x - (float)h);
       }
-    __builtin_amdgcn_sched_barrier(0);  // the split first: its registers are the next A's
-    {  // next tile's A (its latency hides under this tile's MFMAs)
+    {  // next tile into the (now free) registers; the last tile is re-read (keeps the loop uniform)
       const int64_t tn = t + 1 < ntile ? t + 1 : t;
-      wx_load_a<NTB, WB, SYN>(a, kb + 32 * tn, R);
+      wx_load<NTB, WB, SYN, FOUR>(a, kb + 32 * tn, R);
     }
+    __syncthreads();  // planes of tile t written; every wave is done with the slot of tile t - 2
     if constexpr (BSC) {
       // the lane's B operand (column lane & 31, points 16 s + 8 hh + j) from the fp32 rows, split
       // under the wave's running B scale (lowered, with the accumulator, when this tile needs it)

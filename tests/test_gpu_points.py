@@ -11,7 +11,7 @@ from it (max |g_f32 - g_cr| / max |g_cr|), and rtol 1e-3 with atol (1e-6 + d32) 
 the float32 gradient.  For the reference's grid decoder (points_c32.npz) the correctly-rounded
 gradient is the fixture tests/golden/grads_cr.npz `pts/*` and the float32 one the reference's own;
 for the IDW / trilinear render / regulation / tracking cases both are the oracle's, formed in the
-test, and up to FLIP_FRAC of the elements may reach FLIP_CAP max|g| (decision-edge samples, below).
+test, and elements may exceed the bound by up to FLIP_CAP max|g| (decision-edge samples, below).
 """
 import numpy as np
 import pytest
@@ -48,10 +48,13 @@ def pnr_mod():
 
 
 # Render / regulation / tracking with IDW or trilinear features over a random cloud: a few samples sit
-# on a decision edge (a ReLU pre-activation or a neighbour's distance within rounding of the
-# threshold), where two float32 orders take different branches; the elements those samples feed may
-# leave the fp32 floor.  At most FLIP_FRAC of a tensor's elements may, and none beyond FLIP_CAP max|g|.
-FLIP_FRAC, FLIP_CAP = 1e-2, 5e-4
+# on a decision edge (a ReLU pre-activation, a neighbour's distance or a pdf bin boundary within
+# rounding of the threshold), where two float32 orders take different branches.  A flipped sample
+# changes one rank-1 term of a weight gradient (its delta times its activations), so it can move ANY
+# fraction of the elements, each by about one sample's share: ~max|g| / n for n samples (~2.7e4 here).
+# FLIP_CAP = 5e-4 max|g| admits about a dozen such terms; the share of elements beyond the strict bound
+# is printed (it was 0-2% over the runs; it is not what a flip bounds, so it is not asserted).
+FLIP_CAP = 5e-4
 # summation-magnitude floor, in ulps (u = 2^-24) of M = sum_p |t_p|: a gradient element is a sum over
 # samples of terms that each carry a few ulps from the forward / delta chain, and the sum itself
 # rounds in a blocked order; 64 u M bounds both (an element without cancellation has M ~ |g|, where
@@ -63,8 +66,8 @@ def grad_elementwise(g, cr, f32, what, rel_f32=None, rtol=1e-3, atol=1e-6, flips
     """|g - g_cr| <= rtol |g_cr| + (atol + d32) max|g_cr| + MAG_ULPS u M and |g - g_f32| <= the same
     with g_f32 elementwise, d32 = rel_f32 or max |g_f32 - g_cr| / max |g_cr|, M = the element's
     summation magnitude sum_p |t_p| (oracle.ref_points.magnitudes; 0 when not given): the float32
-    rounding floor of a sum that cancels.  flips: FLIP_FRAC of the elements may exceed that, up to
-    FLIP_CAP max|g| (see above)."""
+    rounding floor of a sum that cancels.  flips: elements may exceed that by up to FLIP_CAP max|g|
+    (decision-edge samples, see above)."""
     g = g.detach().cpu().numpy() if isinstance(g, torch.Tensor) else np.asarray(g)
     cr, f32 = (t.detach().cpu().numpy() if isinstance(t, torch.Tensor) else np.asarray(t) for t in (cr, f32))
     mfloor = 0.0 if mag is None else MAG_ULPS * 2.0 ** -24 * np.asarray(mag)
@@ -78,7 +81,6 @@ def grad_elementwise(g, cr, f32, what, rel_f32=None, rtol=1e-3, atol=1e-6, flips
         print(f'{what} vs {tag} (d32 {d32:.2e}): worst |g - g_ref| / (rtol |g_ref| + atol) = {viol.max():.3f}, '
               f'beyond: {out:.1e}')
         if flips:
-            assert out <= FLIP_FRAC, (what, tag, out)
             np.testing.assert_array_less(np.abs(g - ref), rtol * np.abs(ref) + np.maximum(a, FLIP_CAP * m) + 1e-45,
                                          err_msg=f'{what} vs {tag}')
         else:
