@@ -420,8 +420,10 @@ def map_step_fn(pnr, renderer, dec, cfg, ro, rd, gt, col, dev, ddp=None, points=
     if graph:
         mgraph = MapGraph(mstep, ro, rd, gt, col, torch.rand((n, ns), device=dev))
 
-        def step():  # the same iteration, replayed; a fresh regulation jitter drawn per step
-            mgraph(ro, rd, gt, col, torch.rand((n, ns), device=dev))
+        def step():  # the same iteration, replayed; a fresh regulation jitter drawn per step, in place
+            # into the graph's static input (the rays already sit in its other inputs: no copies)
+            torch.rand((n, ns), device=dev, out=mgraph.inputs[4])
+            mgraph(*mgraph.inputs)
         return step
 
     def step():

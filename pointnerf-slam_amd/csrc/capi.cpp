@@ -270,6 +270,8 @@ int mlp_backward_core(int prec, const float* packed, const SaveArgs& sv, int64_t
     // (fixed order per element) adds them all into the gradients
     ReduceJob jobs[kMaxReduceJobs];
     int nj = 0;
+    Wgrad16Job gjobs[kMaxGemmJobs];
+    int ng = 0;
     float* pp = b.part;
     float* pb = b.part_bias;
     auto took = [&]() {
@@ -277,44 +279,57 @@ int mlp_backward_core(int prec, const float* packed, const SaveArgs& sv, int64_t
       pb += jobs[nj].bias_floats();
       ++nj;
     };
-    if (!grads) {  // no decoder weight gradients (the Tracker's camera-only backward)
+    const bool want_fc = fb && fb->g_fc;
+    if (!grads && !want_fc) {  // no weight gradients (the Tracker's camera-only backward)
     } else if (split) {  // f16x3 GEMMs on the fp32 saves (h / e by k_mlp_fwd16, deltas by k_mlp_bwd16)
       const float* hp = sv.hP + p0 * kHidden;
       // output layer: dWo (4x256) += g_out^T h4 ; dbo += colsum(g_out)
-      rc = launch_wgrad_out16(b.g_out + p0 * 4, hp + 3 * hstride, C, grads[9], grads[10], pp, pb, st, &jobs[nj]);
-      if (rc == 0) took();
+      if (grads) {
+        rc = launch_wgrad_out16(b.g_out + p0 * 4, hp + 3 * hstride, C, grads[9], grads[10], pp, pb, st, &jobs[nj]);
+        if (rc == 0) took();
+      }
       // hidden layers: dW_l += delta_{l+1}^T h_l  (W3: delta4.h3, W2: delta3.h2, W1: delta2.h1); delta4
-      // is not stored by k_mlp_bwd16 (rank 4: rebuilt from g_out and the h4 masks inside the GEMM)
+      // is not stored by k_mlp_bwd16 (rank 4: rebuilt from g_out and the h4 masks inside the GEMM).
+      // These GEMMs (and the fc_c ones below) are independent: prepared here, launched as one group.
       WgradSyn syn{reinterpret_cast<const float4*>(b.g_out + p0 * 4), sv.masks + 3 * (sv.ld / 32) * 64, p0 / 32,
-                   packed + packed_raw_wo_offset(), sv.xP + p0, packed + kOffFB, pp, pb};
-      if (rc == 0) {
+                   packed + packed_raw_wo_offset(), sv.xP + p0, packed + kOffFB, pp, pb, nullptr};
+      // with the feature branch k_mlp_bwd16 stores dL/dh_l only: delta_l = dL/dh_l masked in the GEMM
+      const bool fmask = fb != nullptr;
+      const int64_t mstride = (sv.ld / 32) * 64;
+      const float* dsrc = fmask ? b.gH : b.dP;
+      auto prep = [&](int kind, const float* A, const float* B, float* Cw, int64_t ldc, float* bias,
+                      const uint4* amasks) {
+        if (rc) return;
         syn.part = pp;
         syn.part_bias = pb;
-        rc = launch_wgrad16(kWgradOutDelta, nullptr, hp + 2 * hstride, C, C, grads[7], kHidden, grads[8], st, &syn,
-                            &jobs[nj]);
-        if (rc == 0) took();
+        syn.amasks = amasks;
+        rc = wgrad16_prepare(kind, A, B, C, C, Cw, ldc, bias, &syn, &gjobs[ng], &jobs[nj]);
+        syn.amasks = nullptr;
+        if (rc == 0) {
+          ++ng;
+          took();
+        }
+      };
+      if (grads) {
+        prep(kWgradOutDelta, nullptr, hp + 2 * hstride, grads[7], kHidden, grads[8], nullptr);
+        for (int l = 2; l >= 1; --l)
+          prep(kWgradHidden, dsrc + l * dstride, hp + (l - 1) * hstride, grads[1 + 2 * l], kHidden,
+               grads[2 + 2 * l], fmask ? sv.masks + l * mstride : nullptr);
+        // first layer: dW0 (256x93) += delta1^T e ; db0 -- e = sin(x@B) recomputed from the saved x
+        // (k_mlp_fwd16 saves no e)
+        prep(kWgradFirstX, dsrc, nullptr, grads[1], kFourier, grads[2], fmask ? sv.masks : nullptr);
       }
-      for (int l = 2; l >= 1 && rc == 0; --l) {
-        syn.part = pp;
-        syn.part_bias = pb;
-        rc = launch_wgrad16(kWgradHidden, b.dP + l * dstride, hp + (l - 1) * hstride, C, C, grads[1 + 2 * l],
-                            kHidden, grads[2 + 2 * l], st, &syn, &jobs[nj]);
-        if (rc == 0) took();
-      }
-      // first layer: dW0 (256x93) += delta1^T e ; db0 -- e = sin(x@B) recomputed from the saved x
-      // (k_mlp_fwd16 saves no e)
-      if (rc == 0) {
-        syn.part = pp;
-        syn.part_bias = pb;
-        rc = launch_wgrad16(kWgradFirstX, b.dP, nullptr, C, C, grads[1], kFourier, grads[2], st, &syn, &jobs[nj]);
-        if (rc == 0) took();
-      }
+      // feature branch: dWc_l (256x32) += (dL/dh_l)^T c ; dbc_l += colsum(dL/dh_l)
+      if (want_fc)
+        for (int l = 0; l < 4; ++l)
+          prep(kWgradFc, b.gH + l * dstride, fb->c + p0 * kCDim, fb->g_fc[2 * l], kCDim, fb->g_fc[2 * l + 1], nullptr);
+      if (rc == 0) rc = launch_wgrad16_group(gjobs, ng, st);
       // Fourier: dB (3x93) += x^T g_arg
-      if (rc == 0) {
+      if (rc == 0 && grads) {
         rc = launch_wgrad_fourier16(sv.xP + p0, b.gargP, C, grads[0], pp, st, &jobs[nj]);
         if (rc == 0) took();
       }
-    } else {
+    } else if (grads) {
       const float* hp = sv.hP + p0 * kHidden;
       rc = launch_wgrad(kWgradOut, b.g_out + p0 * 4, 4, hp + 3 * hstride, kHidden, C, grads[9], kHidden, grads[10],
                         b.part, b.part_bias, st);
@@ -330,17 +345,8 @@ int mlp_backward_core(int prec, const float* packed, const SaveArgs& sv, int64_t
                           grads[0], kFourier, nullptr, b.part, b.part_bias, st);
     }
     if (rc) return rc;
-    // feature branch: dWc_l (256x32) += (dL/dh_l)^T c ; dbc_l += colsum(dL/dh_l)
-    if (fb && fb->g_fc && split) {  // f16x3 GEMMs: dL/dh from k_mlp_bwd16, the fp32 features
-      WgradSyn fsyn{};
-      for (int l = 0; l < 4 && rc == 0; ++l) {
-        fsyn.part = pp;
-        fsyn.part_bias = pb;
-        rc = launch_wgrad16(kWgradFc, b.gH + l * dstride, fb->c + p0 * kCDim, C, C, fb->g_fc[2 * l], kCDim,
-                            fb->g_fc[2 * l + 1], st, &fsyn, &jobs[nj]);
-        if (rc == 0) took();
-      }
-    } else if (fb && fb->g_fc) {
+    // feature branch (fp32 mode; the split mode's fc_c GEMMs ran in the group above)
+    if (fb && fb->g_fc && !split) {
       for (int l = 0; l < 4 && rc == 0; ++l)
         rc = launch_wgrad(kWgradFc, b.gH + l * dstride, kHidden, fb->c + p0 * kCDim, kCDim, C, fb->g_fc[2 * l], kCDim,
                           fb->g_fc[2 * l + 1], b.part, b.part_bias, st);

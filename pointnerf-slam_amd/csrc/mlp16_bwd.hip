@@ -22,8 +22,9 @@ namespace pnr {
 // whatever the loss scale.  At a chain boundary the point's max over all 8 output tiles is needed
 // before tile 0 can be split, so a boundary step folds each finished tile into a running max
 // (between the MFMA groups) and converts tile 0 after its last group.
-// The deltas, dL/dh (features) and g_arg go to HBM in fp32 (point-major) for the weight-gradient
-// GEMMs of wgrad16.hip, which split them again under their own scales.
+// The deltas (or, with features, dL/dh: delta_l is dL/dh_l masked) and g_arg go to HBM in fp32
+// (point-major) for the weight-gradient GEMMs of wgrad16.hip, which split them again under their
+// own scales.
 // ---------------------------------------------------------------------------------------------
 __host__ __device__ constexpr int bwd_chain(int g) { return g == 0 ? 0 : (g <= 24 ? 1 + (g - 1) / 8 : 4); }
 __host__ __device__ constexpr int bwd_kc(int g) { return g == 0 ? 0 : (g <= 24 ? (g - 1) % 8 : g - 25); }
@@ -87,10 +88,11 @@ struct BwdGeo {
     return 0;
 #endif
     if (!bwd_conv(g)) return 0;
-    if (bnd(g)) return T == nt(g) - 1 ? (HASC ? 4 : 0) + (bwd_conv_chain(g) != 0 ? 4 : 0) : 0;
+    // conv2 stores no delta4 (chain 0: kWgradOutDelta rebuilds it) and, with the feature branch, no
+    // delta at all (the dW GEMMs mask conv1's dL/dh themselves); conv1's dL/dh (features) stays
+    const bool d = !HASC && bwd_conv_chain(g) != 0;
+    if (bnd(g)) return T == nt(g) - 1 ? (HASC ? 4 : 0) + (d ? 4 : 0) : 0;
     int n = 0;
-    // conv2 stores no delta4 (chain 0: kWgradOutDelta rebuilds it); conv1's dL/dh (features) stays
-    const bool d = bwd_conv_chain(g) != 0;
     for (int q = 0; q < 4; ++q) n += (HASC && grp1(q, 0, nt(g)) == T ? 1 : 0) + (d && grp2(q, 0, nt(g)) == T ? 1 : 0);
     return n;
   }
@@ -244,9 +246,10 @@ struct BfBwd {
       const int m = (int)(wd << (31 - bit)) >> 31;
       S.v[4 * q + i] = __int_as_float(__float_as_int(S.v[4 * q + i]) & m);
     }
-    // fp32 delta for the weight-gradient GEMMs (delta4 = chain 0's: not stored, kWgradOutDelta)
+    // fp32 delta for the weight-gradient GEMMs (delta4 = chain 0's: not stored, kWgradOutDelta;
+    // with the feature branch none: the GEMMs apply the mask words to conv1's dL/dh, wgrad16.hip MSK)
 #if !defined(PNR_EXP_NOSTORE)
-    if constexpr (CC != 0)
+    if constexpr (CC != 0 && !HASC)
 #else
     if constexpr (false)  // experiment: no delta stores (timing bound only)
 #endif

@@ -243,7 +243,43 @@ struct WgradSyn {
   // added into C / bias in a fixed order by k_part_reduce -- no float atomics, deterministic
   float* part;
   float* part_bias;
+  // kWgradHidden / kWgradFirstX with the feature branch: A is the UNMASKED dL/dh_l (the delta chain
+  // stores no delta there) and the GEMM applies the forward's ReLU mask words of that layer itself
+  const uint4* amasks;  // mask words of h_l's layer (SaveArgs::masks + (l - 1) x ld / 32 x 64) or null
 };
+// Arguments of one split weight-gradient GEMM (wgrad16.hip k_wgrad16)
+struct WxArgs {
+  const float* A;      // [K][256]
+  const float* B;      // [kb_rows][WB]
+  int nb;              // valid columns of B (columns of C)
+  int64_t K;           // multiple of 32 (rows [real K, K) of A exist and are zero)
+  int64_t kb_rows;     // rows of B that exist (reads clamp to the last one: A is zero there)
+  int64_t ks;          // points per workgroup (multiple of 32)
+  float* C;
+  int64_t ldc;
+  float* bias;
+  // SYN (dW3 = delta4^T h3): A is not read but rebuilt per element from the rank-4 product
+  // delta4 = (Wo^T g_out) * [h4 > 0] -- the forward's ReLU mask words of h4 and the tile's g_out
+  const float4* g_out;   // [K] chunk-local rows (zero past the real points)
+  const uint4* masks;    // layer-4 mask words [ld / 32][64] (k_mlp_fwd16 layout)
+  int64_t mgrp0;         // mask group of A row 0 (saved row / 32)
+  const uint4* amasks;   // MSK: mask words of A's layer (same layout as masks)
+  const float* wo;       // Wo [4][256] fp32
+  // FOUR (dW0 = delta1^T e): B = e = sin(x@B) is not read but recomputed from the saved inputs, by
+  // the forward's own arithmetic (bit-identical e)
+  const float4* xP;      // [K] saved MLP inputs (x0, x1, x2, inside), chunk rows
+  const float* fb;       // Fourier B padded [3][96]
+  float* part;           // non-null: [grid][256][NTB 32] partial tiles + part_bias [grid][256]
+  float* part_bias;      //   (plain stores; k_wgrad_reduce sums them into C / bias)
+};
+
+// a prepared GEMM of a grouped launch (wgrad16_prepare -> launch_wgrad16_group)
+struct Wgrad16Job {
+  WxArgs a;
+  int var;   // kernel variant (wgrad16.hip kVar*)
+  int nwg;   // workgroups (split-K)
+};
+constexpr int kMaxGemmJobs = 8;
 constexpr int kWgradMaxWg = 512;    // fp32 k_wgrad grid cap
 constexpr int kWgrad16MaxWg = 256;  // split k_wgrad16 grid cap
 constexpr int kSkinnyMaxWg = 1024;  // k_wgrad_skinny grid cap
@@ -281,6 +317,9 @@ int launch_wgrad(int kind, const float* A, int ma, const float* B, int nb, int64
 // defer: non-null = fill the reduction job instead of launching it (launch_part_reduce_multi later)
 int launch_wgrad16(int kind, const float* A, const float* B, int64_t K, int64_t kb_rows, float* C, int64_t ldc,
                    float* bias, hipStream_t st, const WgradSyn* syn = nullptr, ReduceJob* defer = nullptr);
+int wgrad16_prepare(int kind, const float* A, const float* B, int64_t K, int64_t kb_rows, float* C, int64_t ldc,
+                    float* bias, const WgradSyn* syn, Wgrad16Job* job, ReduceJob* red);
+int launch_wgrad16_group(const Wgrad16Job* jobs, int n, hipStream_t st);
 int launch_wgrad_out16(const float* g_out, const float* h4, int64_t K, float* C, float* bias, float* part,
                        float* part_bias, hipStream_t st, ReduceJob* defer = nullptr);
 int launch_wgrad_fourier16(const float4* xP, const float* garg, int64_t K, float* C, float* part, hipStream_t st,

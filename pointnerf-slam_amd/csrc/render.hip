@@ -98,6 +98,12 @@ __global__ void k_coarse_z(pnr_render_params prm, const float* __restrict__ ro, 
 
 // ---------------------------------------------------------------------------------------------
 // coarse weights -> sample_pdf -> z_samples (N, I) float64
+// The ray kernels below run one thread per ray; at the Mapper's batch (1,000 rays: 16 waves) every
+// one of them is latency-bound on its per-sample loads.  SS / II > 0 specialise them for the
+// config's sample counts (32 + 12): the loops unroll, so a ray's loads are all in flight at once
+// (with runtime counts they went out one sample at a time).  The arithmetic and its order are the
+// same in both forms.
+template <int SS, int II>
 __global__ __launch_bounds__(64) void k_pdf(pnr_render_params prm, const float* __restrict__ rd,
                                             const double* __restrict__ zc, const float4* __restrict__ rawc,
                                             int64_t n_rays, double* __restrict__ zi) {
@@ -106,11 +112,12 @@ __global__ __launch_bounds__(64) void k_pdf(pnr_render_params prm, const float* 
   const int tid = threadIdx.x;
   const int64_t n = (int64_t)blockIdx.x * 64 + tid;
   if (n >= n_rays) return;
-  const int S = prm.n_samples, I = prm.n_importance;
+  const int S = SS > 0 ? SS : prm.n_samples, I = II > 0 ? II : prm.n_importance;
   const double* z = zc + n * S;
   const float4* raw = rawc + n * S;
   const float nrm = ray_norm(rd + n * 3);
   double T = 1.0;
+#pragma unroll
   for (int q = 0; q < S; ++q) {
     const float dz = q < S - 1 ? (float)(z[q + 1] - z[q]) : 1e10f;
     const float delta = dz * nrm;
@@ -128,6 +135,7 @@ __global__ __launch_bounds__(64) void k_pdf(pnr_render_params prm, const float* 
     acc += (double)((wl[m + 1][tid] + 1e-5f) / sum);
     cdf[m + 1][tid] = (float)acc;
   }
+#pragma unroll 4
   for (int k = 0; k < I; ++k) {
     const float u = prm.u_vals[k];
     // searchsorted(cdf, u, right=True): first index with cdf > u (binary search over M+1 entries)
@@ -157,13 +165,17 @@ __device__ __forceinline__ bool eq_nan(double a, double b) { return (a == b) || 
 // coarse depths (near..far linspace) and the importance depths (inverse-cdf of increasing u) are
 // each non-decreasing unless far < near or a value is NaN: then a stable merge gives exactly that
 // order in O(S+I); otherwise the rank sort below does.
-__device__ void sort_ray(const double* zc, const double* zi, int S, int I, double (*zl)[64], uint8_t (*ord)[64],
-                         int tid) {
+template <int SS, int II>
+__device__ __forceinline__ void sort_ray(const double* zc, const double* zi, int S, int I, double (*zl)[64],
+                                         uint8_t (*ord)[64], int tid) {
+  if (SS > 0) S = SS;
+  if (II > 0) I = II;
   const int M = S + I;
   bool sorted = true;
   double prev = zc[0];
   zl[0][tid] = prev;
   sorted = prev == prev;
+#pragma unroll
   for (int m = 1; m < S; ++m) {
     const double v = zc[m];
     zl[m][tid] = v;
@@ -174,6 +186,7 @@ __device__ void sort_ray(const double* zc, const double* zi, int S, int I, doubl
     prev = zi[0];
     zl[S][tid] = prev;
     sorted = sorted && prev == prev;
+#pragma unroll
     for (int k = 1; k < I; ++k) {
       const double v = zi[k];
       zl[S + k][tid] = v;
@@ -203,6 +216,7 @@ __device__ void sort_ray(const double* zc, const double* zi, int S, int I, doubl
 }
 
 // final pass: depth/var (float64), rgb (float32); saves the sort order for the backward
+template <int SS, int II>
 __global__ __launch_bounds__(64) void k_fine(pnr_render_params prm, const float* __restrict__ rd,
                                              const double* __restrict__ zc, const double* __restrict__ zi,
                                              const float4* __restrict__ rawc, const float4* __restrict__ rawi,
@@ -214,11 +228,12 @@ __global__ __launch_bounds__(64) void k_fine(pnr_render_params prm, const float*
   const int tid = threadIdx.x;
   const int64_t n = (int64_t)blockIdx.x * 64 + tid;
   if (n >= n_rays) return;
-  const int S = prm.n_samples, I = prm.n_importance, M = S + I;
-  sort_ray(zc + n * S, zi + n * I, S, I, zl, ord, tid);
+  const int S = SS > 0 ? SS : prm.n_samples, I = II > 0 ? II : prm.n_importance, M = S + I;
+  sort_ray<SS, II>(zc + n * S, zi + n * I, S, I, zl, ord, tid);
   const float nrm = ray_norm(rd + n * 3);
   double T = 1.0, D = 0.0;
   float r0 = 0.f, r1 = 0.f, r2 = 0.f;
+#pragma unroll
   for (int q = 0; q < M; ++q) {
     const int s = ord[q][tid];
     const double zq = zl[s][tid];
@@ -232,6 +247,7 @@ __global__ __launch_bounds__(64) void k_fine(pnr_render_params prm, const float*
     D += (double)w * zq;
   }
   double V = 0.0;
+#pragma unroll
   for (int q = 0; q < M; ++q) {
     const double dd = zl[ord[q][tid]][tid] - D;
     V += (double)wl[q][tid] * dd * dd;
@@ -239,13 +255,22 @@ __global__ __launch_bounds__(64) void k_fine(pnr_render_params prm, const float*
   depth[n] = D;
   var[n] = V;
   rgb[n * 3 + 0] = r0; rgb[n * 3 + 1] = r1; rgb[n * 3 + 2] = r2;
-  if (ord_out)
-    for (int q = 0; q < M; ++q) ord_out[n * PNR_MAX_SAMPLES + q] = ord[q][tid];
+  if (ord_out) {  // 4 bytes per store
+    uint32_t* o = reinterpret_cast<uint32_t*>(ord_out + n * PNR_MAX_SAMPLES);
+#pragma unroll
+    for (int q = 0; q < M; q += 4) {
+      uint32_t v = 0;
+#pragma unroll
+      for (int b = 0; b < 4; ++b) v |= (q + b < M ? (uint32_t)ord[q + b][tid] : 0u) << (8 * b);
+      o[q >> 2] = v;
+    }
+  }
 }
 
 // Backward of the final compositing: writes dL/draw (float4) for every coarse and importance
 // point, sigma channel zeroed where the point was outside the bound (Renderer.py:57 assigns
 // the density, so no gradient reaches the MLP there); g_nrm[n] = dL/d|rays_d|.
+template <int SS, int II>
 __global__ __launch_bounds__(64) void k_fine_bwd(pnr_render_params prm, const float* __restrict__ rd,
                                                  const double* __restrict__ zc, const double* __restrict__ zi,
                                                  const float4* __restrict__ rawc, const float4* __restrict__ rawi,
@@ -257,7 +282,7 @@ __global__ __launch_bounds__(64) void k_fine_bwd(pnr_render_params prm, const fl
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x;
   const int64_t n = (int64_t)blockIdx.x * 64 + tid;
-  const int S = prm.n_samples, I = prm.n_importance, M = S + I;
+  const int S = SS > 0 ? SS : prm.n_samples, I = II > 0 ? II : prm.n_importance, M = S + I;
   // [M][64] per-ray columns: z (sorted), alpha and T; w = alpha * T and dz are recomputed from
   // them bit-for-bit, which keeps the LDS per block at 16 B per sample (3 blocks per CU at M = 44)
   double* zs = reinterpret_cast<double*>(smem);
@@ -265,16 +290,30 @@ __global__ __launch_bounds__(64) void k_fine_bwd(pnr_render_params prm, const fl
   float* Tl = al + M * 64;
   if (n >= n_rays) return;
   const uint8_t* ord = ord_in + n * PNR_MAX_SAMPLES;
+  // specialised: the ray's sort order in registers (16-B loads of the 64-B row), so the sample
+  // loads below depend on no other load
+  constexpr int kOw = SS > 0 ? (SS + II + 15) / 16 * 4 : 1;
+  uint32_t ow[kOw];
+  if constexpr (SS > 0) {
+#pragma unroll
+    for (int i = 0; i < kOw / 4; ++i) {
+      const uint4 v = reinterpret_cast<const uint4*>(ord)[i];
+      ow[4 * i] = v.x; ow[4 * i + 1] = v.y; ow[4 * i + 2] = v.z; ow[4 * i + 3] = v.w;
+    }
+  }
+  auto ordq = [&](int q) -> int { return SS > 0 ? (int)((ow[q >> 2] >> (8 * (q & 3))) & 0xffu) : (int)ord[q]; };
   const float* dvec = rd + n * 3;
   const float nrm = ray_norm(dvec);
   auto zsrc = [&](int s) { return s < S ? zc[n * S + s] : zi[n * I + (s - S)]; };
   auto rsrc = [&](int s) { return s < S ? rawc[n * S + s] : rawi[n * I + (s - S)]; };
   double T = 1.0, D = 0.0;
-  for (int q = 0; q < M; ++q) zs[q * 64 + tid] = zsrc(ord[q]);
+#pragma unroll
+  for (int q = 0; q < M; ++q) zs[q * 64 + tid] = zsrc(ordq(q));
+#pragma unroll
   for (int q = 0; q < M; ++q) {
     const double zq = zs[q * 64 + tid];
     const float dz = q < M - 1 ? (float)(zs[(q + 1) * 64 + tid] - zq) : 1e10f;
-    const float4 c = rsrc(ord[q]);
+    const float4 c = rsrc(ordq(q));
     const float a = 1.f - expf(-relu(c.w) * (dz * nrm));
     const float w = a * (float)T;
     Tl[q * 64 + tid] = (float)T;
@@ -288,11 +327,13 @@ __global__ __launch_bounds__(64) void k_fine_bwd(pnr_render_params prm, const fl
   const float gr1 = g_rgb ? g_rgb[n * 3 + 1] : 0.f;
   const float gr2 = g_rgb ? g_rgb[n * 3 + 2] : 0.f;
   double sdev = 0.0;
+#pragma unroll
   for (int q = 0; q < M; ++q) sdev += (double)(al[q * 64 + tid] * Tl[q * 64 + tid]) * (zs[q * 64 + tid] - D);
   const double gD = gd - 2.0 * gv * sdev;  // d var / d depth = -2 sum w (z - depth)
   float R = 0.f, gn = 0.f;
+#pragma unroll
   for (int q = M - 1; q >= 0; --q) {
-    const int s = ord[q];
+    const int s = ordq(q);
     const float4 c = rsrc(s);
     const double zq = zs[q * 64 + tid];
     const double dd = zq - D;
@@ -520,15 +561,22 @@ int launch_coarse_z(const pnr_render_params& prm, const float* ro, const float* 
 int launch_pdf(const pnr_render_params& prm, const float* rd, const double* zc, const float* rawc, int64_t n,
                double* zi, hipStream_t st) {
   if (n <= 0) return 0;
-  hipLaunchKernelGGL(k_pdf, dim3(nblk(n, 64)), dim3(64), 0, st, prm, rd, zc, (const float4*)rawc, n, zi);
+  if (prm.n_samples == 32 && prm.n_importance == 12)  // the config's counts (configs/pointNeRF_slam.yaml)
+    hipLaunchKernelGGL((k_pdf<32, 12>), dim3(nblk(n, 64)), dim3(64), 0, st, prm, rd, zc, (const float4*)rawc, n, zi);
+  else
+    hipLaunchKernelGGL((k_pdf<0, 0>), dim3(nblk(n, 64)), dim3(64), 0, st, prm, rd, zc, (const float4*)rawc, n, zi);
   return hip_status(hipGetLastError());
 }
 int launch_fine(const pnr_render_params& prm, const float* rd, const double* zc, const double* zi,
                 const float* rawc, const float* rawi, int64_t n, double* depth, double* var, float* rgb,
                 uint8_t* ord, hipStream_t st) {
   if (n <= 0) return 0;
-  hipLaunchKernelGGL(k_fine, dim3(nblk(n, 64)), dim3(64), 0, st, prm, rd, zc, zi, (const float4*)rawc,
-                     (const float4*)rawi, n, depth, var, rgb, ord);
+  if (prm.n_samples == 32 && prm.n_importance == 12)
+    hipLaunchKernelGGL((k_fine<32, 12>), dim3(nblk(n, 64)), dim3(64), 0, st, prm, rd, zc, zi, (const float4*)rawc,
+                       (const float4*)rawi, n, depth, var, rgb, ord);
+  else
+    hipLaunchKernelGGL((k_fine<0, 0>), dim3(nblk(n, 64)), dim3(64), 0, st, prm, rd, zc, zi, (const float4*)rawc,
+                       (const float4*)rawi, n, depth, var, rgb, ord);
   return hip_status(hipGetLastError());
 }
 int launch_fine_bwd(const pnr_render_params& prm, const float* rd, const double* zc, const double* zi,
@@ -538,8 +586,12 @@ int launch_fine_bwd(const pnr_render_params& prm, const float* rd, const double*
   if (n <= 0) return 0;
   const int M = prm.n_samples + prm.n_importance;
   const size_t sh = (size_t)M * 64 * (8 + 2 * 4);
-  hipLaunchKernelGGL(k_fine_bwd, dim3(nblk(n, 64)), dim3(64), sh, st, prm, rd, zc, zi, (const float4*)rawc,
-                     (const float4*)rawi, insc, insi, ord, n, gd, gv, grgb, (float4*)goc, (float4*)goi, g_nrm);
+  if (prm.n_samples == 32 && prm.n_importance == 12)
+    hipLaunchKernelGGL((k_fine_bwd<32, 12>), dim3(nblk(n, 64)), dim3(64), sh, st, prm, rd, zc, zi, (const float4*)rawc,
+                       (const float4*)rawi, insc, insi, ord, n, gd, gv, grgb, (float4*)goc, (float4*)goi, g_nrm);
+  else
+    hipLaunchKernelGGL((k_fine_bwd<0, 0>), dim3(nblk(n, 64)), dim3(64), sh, st, prm, rd, zc, zi, (const float4*)rawc,
+                       (const float4*)rawi, insc, insi, ord, n, gd, gv, grgb, (float4*)goc, (float4*)goi, g_nrm);
   return hip_status(hipGetLastError());
 }
 int launch_ray_grads_f64(const float* rd, const double* za, int sa, const double* zb, int sb, const float* gxa,

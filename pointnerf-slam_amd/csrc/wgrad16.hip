@@ -9,7 +9,9 @@
 //   dW0 = delta1^T e                                            WB = 96 (3 column tiles, 93 used)
 //   dWc_l = (dL/dh_l)^T c                                       WB = 32 (1 column tile)
 // A = deltas / dL/dh stored by k_mlp_bwd16, B = activations / Fourier features stored by
-// k_mlp_fwd16 (or the gathered point features), all fp32.
+// k_mlp_fwd16 (or the gathered point features), all fp32.  With the feature branch the delta chain
+// stores only dL/dh_l (unmasked, for dWc_l); the dW GEMMs then read it as A and apply the forward's
+// ReLU mask words themselves (MSK): delta_l = dL/dh_l * [h_l > 0], 1 KB/point less written per layer.
 //
 // Arithmetic: f16x3, the forward's split.  Each operand x = hi + lo (hi = f16(x), lo = f16(x - hi),
 // 22 significant bits); A B ~= Ah Bh + Ah Bl + Al Bh on v_mfma_f32_32x32x16_f16 with fp32
@@ -56,29 +58,7 @@ struct Wx3 {
   static constexpr int kBPer = (kB4 + kThreads - 1) / kThreads;
 };
 
-struct WxArgs {
-  const float* A;      // [K][256]
-  const float* B;      // [kb_rows][WB]
-  int nb;              // valid columns of B (columns of C)
-  int64_t K;           // multiple of 32 (rows [real K, K) of A exist and are zero)
-  int64_t kb_rows;     // rows of B that exist (reads clamp to the last one: A is zero there)
-  int64_t ks;          // points per workgroup (multiple of 32)
-  float* C;
-  int64_t ldc;
-  float* bias;
-  // SYN (dW3 = delta4^T h3): A is not read but rebuilt per element from the rank-4 product
-  // delta4 = (Wo^T g_out) * [h4 > 0] -- the forward's ReLU mask words of h4 and the tile's g_out
-  const float4* g_out;   // [K] chunk-local rows (zero past the real points)
-  const uint4* masks;    // layer-4 mask words [ld / 32][64] (k_mlp_fwd16 layout)
-  int64_t mgrp0;         // mask group of A row 0 (saved row / 32)
-  const float* wo;       // Wo [4][256] fp32
-  // FOUR (dW0 = delta1^T e): B = e = sin(x@B) is not read but recomputed from the saved inputs, by
-  // the forward's own arithmetic (bit-identical e)
-  const float4* xP;      // [K] saved MLP inputs (x0, x1, x2, inside), chunk rows
-  const float* fb;       // Fourier B padded [3][96]
-  float* part;           // non-null: [grid][256][NTB 32] partial tiles + part_bias [grid][256]
-  float* part_bias;      //   (plain stores; k_wgrad_reduce sums them into C / bias)
-};
+// WxArgs: pnr_internal.h (a grouped launch carries one per GEMM)
 
 template <int NTB, int WB>
 struct WxRegs {
@@ -87,7 +67,15 @@ struct WxRegs {
   float4 go;                                   // SYN: g_out row k0 + 32 + tid (threads < 32): the NEXT tile's
 };
 
-template <int NTB, int WB, bool SYN, bool FOUR>
+// mask-word pointer of unit u = 32 w + (lane & 31) for the 32-point group of k0: the lane's 16
+// points 8 hh + 16 s + j sit at word (8 hh + 16 s + j) * 4, bit mask_bit(u) (k_mlp_fwd16 conv1)
+__device__ __forceinline__ const uint32_t* mask_words(const uint4* masks, int64_t grp) {
+  const int u = 32 * wave_id() + (threadIdx.x & 31);
+  return reinterpret_cast<const uint32_t*>(masks + grp * 64 + 32 * ((u >> 2) & 1)) + (u >> 6);
+}
+__device__ __forceinline__ int mask_bit(int u) { return ((u >> 5) & 1) * 16 + ((u >> 3) & 3) * 4 + (u & 3); }
+
+template <int NTB, int WB, bool SYN, bool FOUR, bool MSK = false>
 __device__ __forceinline__ void wx_load(const WxArgs& a, int64_t k0, WxRegs<NTB, WB>& R) {
   using Cfg = Wx3<NTB, WB>;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -111,6 +99,17 @@ __device__ __forceinline__ void wx_load(const WxArgs& a, int64_t k0, WxRegs<NTB,
     for (int s = 0; s < 2; ++s)
 #pragma unroll
       for (int j = 0; j < 8; ++j) R.a[8 * s + j] = Ab[(16 * s + j) * 256];
+    if constexpr (MSK) {  // delta = dL/dh where the forward's ReLU passed (bit sign-extended, ANDed)
+      const uint32_t* mw = mask_words(a.amasks, a.mgrp0 + k0 / 32);
+      const int bit = mask_bit(32 * wave_id() + (lane & 31));
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int m = (int)(mw[(8 * (lane >> 5) + 16 * s + j) * 4] << (31 - bit)) >> 31;
+          R.a[8 * s + j] = __int_as_float(__float_as_int(R.a[8 * s + j]) & m);
+        }
+    }
   }
 #pragma unroll
   for (int i = 0; i < Cfg::kBPer; ++i) {
@@ -187,15 +186,17 @@ __device__ __forceinline__ f16x8 tr_frag(const char* img, int T, int s) {
   return r;
 }
 
-template <int NTB, int WB, bool SYN, bool FOUR, bool BSC>
-__global__ __launch_bounds__(512, 1) void k_wgrad16(WxArgs a) {
+// workgroup `bid` of one weight-gradient GEMM (k_wgrad16: bid = blockIdx.x; k_wgrad16_group: the
+// block's index within its job)
+template <int NTB, int WB, bool SYN, bool FOUR, bool BSC, bool MSK>
+__device__ __forceinline__ void wgrad16_body(const WxArgs& a, const int bid, char* lds) {
+  static_assert(!MSK || (!SYN && !BSC), "MSK: the hidden / first-layer GEMMs");
   static_assert(!BSC || (NTB == 1 && WB == 32 && !SYN && !FOUR), "BSC: the fc_c shape");
   static_assert(!BSC || 32 * kBscRow * 4 <= Wx3<NTB, WB>::kSlot, "BSC tile fits the slot");
   using Cfg = Wx3<NTB, WB>;
-  extern __shared__ __attribute__((aligned(16))) char lds[];
   const int lane = threadIdx.x & 63, hh = lane >> 5;
   const int w = wave_id();  // output row block of this wave
-  const int64_t kb = (int64_t)blockIdx.x * a.ks;
+  const int64_t kb = (int64_t)bid * a.ks;
   const int64_t ke = kb + a.ks < a.K ? kb + a.ks : a.K;
   const int64_t ntile = (ke - kb) / 32;
 
@@ -224,7 +225,7 @@ __global__ __launch_bounds__(512, 1) void k_wgrad16(WxArgs a) {
 #pragma unroll
       for (int e = 0; e < 4; ++e)
         fbr[i][d][e] = FOUR ? a.fb[d * kFourierPad + 4 * ((threadIdx.x + Cfg::kThreads * i) % Cfg::kC4) + e] : 0.f;
-  if (ntile > 0) wx_load<NTB, WB, SYN, FOUR>(a, kb, R);
+  if (ntile > 0) wx_load<NTB, WB, SYN, FOUR, MSK>(a, kb, R);
   if (SYN && ntile > 0) {  // the first tile's g_out rows; later tiles' are staged one tile ahead
     if (threadIdx.x < 32) reinterpret_cast<float4*>(lds + 2 * Cfg::kPlane)[threadIdx.x] = a.g_out[kb + threadIdx.x];
     __syncthreads();
@@ -276,7 +277,7 @@ __global__ __launch_bounds__(512, 1) void k_wgrad16(WxArgs a) {
       }
     {  // next tile into the (now free) registers; the last tile is re-read (keeps the loop uniform)
       const int64_t tn = t + 1 < ntile ? t + 1 : t;
-      wx_load<NTB, WB, SYN, FOUR>(a, kb + 32 * tn, R);
+      wx_load<NTB, WB, SYN, FOUR, MSK>(a, kb + 32 * tn, R);
     }
     __syncthreads();  // planes of tile t written; every wave is done with the slot of tile t - 2
     if constexpr (BSC) {
@@ -335,14 +336,46 @@ __global__ __launch_bounds__(512, 1) void k_wgrad16(WxArgs a) {
   // summation order to the scheduler.)
   // (two multiplies: 1 / (sc sb) can leave the fp32 range where each factor does not)
   const float inv = 1.f / sc, invb = BSC ? 1.f / sb : 1.f;
-  float* P = a.part + (int64_t)blockIdx.x * 256 * (NTB * 32);
+  float* P = a.part + (int64_t)bid * 256 * (NTB * 32);
 #pragma unroll
   for (int y = 0; y < NTB; ++y)
 #pragma unroll
     for (int r = 0; r < 16; ++r)
       P[(32 * w + perm(r, hh)) * (NTB * 32) + 32 * y + (lane & 31)] = BSC ? (acc[y][r] * inv) * invb : acc[y][r] * inv;
   cs += __shfl_xor(cs, 32);
-  if (a.bias && hh == 0) a.part_bias[(int64_t)blockIdx.x * 256 + 32 * w + lane] = cs;
+  if (a.bias && hh == 0) a.part_bias[(int64_t)bid * 256 + 32 * w + lane] = cs;
+}
+
+template <int NTB, int WB, bool SYN, bool FOUR, bool BSC, bool MSK>
+__global__ __launch_bounds__(512, 1) void k_wgrad16(WxArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  wgrad16_body<NTB, WB, SYN, FOUR, BSC, MSK>(a, blockIdx.x, lds);
+}
+
+// Every split weight-gradient GEMM of a backward chunk in ONE launch (they are independent): block b
+// runs workgroup b - first[q] of job q.  At the Mapper's 1,000-ray batch each GEMM fills ~170 CUs
+// for ~30 us and five of them ran back to back; grouped they share the chip, and the launch gaps go.
+// Registers and LDS are the largest variant's (all are 512-thread, one-workgroup-per-CU kernels).
+struct Wgrad16Group {
+  WxArgs a[kMaxGemmJobs];
+  int var[kMaxGemmJobs];
+  int first[kMaxGemmJobs + 1];
+  int n;
+};
+enum : int { kVarHidden = 0, kVarHiddenM, kVarSyn, kVarFirstX, kVarFirstXM, kVarFc };
+__global__ __launch_bounds__(512, 1) void k_wgrad16_group(Wgrad16Group G) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  int q = 0;
+  while (q + 1 < G.n && (int)blockIdx.x >= G.first[q + 1]) ++q;
+  const int bid = (int)blockIdx.x - G.first[q];
+  switch (G.var[q]) {
+    case kVarHidden: wgrad16_body<8, 256, false, false, false, false>(G.a[q], bid, lds); break;
+    case kVarHiddenM: wgrad16_body<8, 256, false, false, false, true>(G.a[q], bid, lds); break;
+    case kVarSyn: wgrad16_body<8, 256, true, false, false, false>(G.a[q], bid, lds); break;
+    case kVarFirstX: wgrad16_body<3, 96, false, true, false, false>(G.a[q], bid, lds); break;
+    case kVarFirstXM: wgrad16_body<3, 96, false, true, false, true>(G.a[q], bid, lds); break;
+    default: wgrad16_body<1, 32, false, false, true, false>(G.a[q], bid, lds); break;
+  }
 }
 
 // Deterministic reduction of per-workgroup partials (every weight-gradient GEMM flushes this way):
@@ -458,10 +491,10 @@ int launch_part_reduce(const float* part, const float* pbias, int nwg, int nr, i
   return hip_status(hipGetLastError());
 }
 
-template <int NTB, int WB, bool SYN = false, bool FOUR = false, bool BSC = false>
+template <int NTB, int WB, bool SYN = false, bool FOUR = false, bool BSC = false, bool MSK = false>
 static int launch_k(const WxArgs& a, hipStream_t st, ReduceJob* defer) {
   using Cfg = Wx3<NTB, WB>;
-  auto kern = k_wgrad16<NTB, WB, SYN, FOUR, BSC>;
+  auto kern = k_wgrad16<NTB, WB, SYN, FOUR, BSC, MSK>;
   static const bool attr = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                                                Cfg::kLds) == hipSuccess;
   if (!attr) return PNR_E_ARG;
@@ -477,47 +510,121 @@ static int launch_k(const WxArgs& a, hipStream_t st, ReduceJob* defer) {
 }
 
 // kind: kWgradHidden (B [K][256]), kWgradFirst (B [K][96], 93 columns) or kWgradFc (B [K][32]);
-// K is rounded up to 32 (the A rows up to it exist and carry zero deltas)
-int launch_wgrad16(int kind, const float* A, const float* B, int64_t K, int64_t kb_rows, float* C, int64_t ldc,
-                   float* bias, hipStream_t st, const WgradSyn* syn, ReduceJob* defer) {
-  if (K <= 0) return 0;
+// K is rounded up to 32 (the A rows up to it exist and carry zero deltas).  Fills the job's
+// arguments, its kernel variant and its reduction (the partials go to the backward's scratch:
+// WgradSyn part / part_bias).
+int wgrad16_prepare(int kind, const float* A, const float* B, int64_t K, int64_t kb_rows, float* C, int64_t ldc,
+                    float* bias, const WgradSyn* syn, Wgrad16Job* job, ReduceJob* red) {
   if (kb_rows <= 0) return PNR_E_ARG;
   K = (K + 31) / 32 * 32;
   // split-K over at most one workgroup per CU, >= 8 tiles per workgroup (the flush of the partial
-  // tile no longer dominates); the partials go to the backward's scratch (WgradSyn part/part_bias)
+  // tile no longer dominates)
   if (!syn || !syn->part || !syn->part_bias) return PNR_E_ARG;
   int64_t nwg = (K / 32 + 7) / 8;
   nwg = nwg < 4 ? 4 : (nwg > kWgrad16MaxWg ? kWgrad16MaxWg : nwg);
   int64_t ks = (K + nwg - 1) / nwg;
   ks = (ks + 31) / 32 * 32;
-  WxArgs a{A, B, 256, K, kb_rows, ks, C, ldc, bias, nullptr, nullptr, 0, nullptr, nullptr, nullptr, syn->part,
-           syn->part_bias};
-  TimingScope ts(kTimeWgrad, K, st);
-  if (kind == kWgradHidden) return launch_k<8, 256>(a, st, defer);
-  if (kind == kWgradOutDelta) {  // dW3 += delta4^T h3, delta4 rebuilt from g_out and the h4 masks
-    if (!syn || !syn->g_out || !syn->masks || !syn->wo) return PNR_E_ARG;
+  nwg = (K + ks - 1) / ks;
+  WxArgs a{A, B, 256, K, kb_rows, ks, C, ldc, bias, nullptr, nullptr, 0, nullptr, nullptr, nullptr, nullptr,
+           syn->part, syn->part_bias};
+  const bool msk = syn->amasks != nullptr;
+  if (msk) {
+    if (kind != kWgradHidden && kind != kWgradFirstX) return PNR_E_ARG;
+    a.amasks = syn->amasks;
+    a.mgrp0 = syn->mgrp0;
+  }
+  int var, ntb;
+  if (kind == kWgradHidden) {
+    var = msk ? kVarHiddenM : kVarHidden;
+    ntb = 8;
+  } else if (kind == kWgradOutDelta) {  // dW3 += delta4^T h3, delta4 rebuilt from g_out and the h4 masks
+    if (!syn->g_out || !syn->masks || !syn->wo) return PNR_E_ARG;
     a.g_out = syn->g_out;
     a.masks = syn->masks;
     a.mgrp0 = syn->mgrp0;
     a.wo = syn->wo;
-    return launch_k<8, 256, true>(a, st, defer);
-  }
-  if (kind == kWgradFc) {  // dWc_l (256 x 32) += gH_l^T c
+    var = kVarSyn;
+    ntb = 8;
+  } else if (kind == kWgradFc) {  // dWc_l (256 x 32) += gH_l^T c
     a.nb = kCDim;
-    return launch_k<1, 32, false, false, true>(a, st, defer);
-  }
-  if (kind == kWgradFirst) {
-    a.nb = kFourier;
-    return launch_k<3, 96>(a, st, defer);
-  }
-  if (kind == kWgradFirstX) {  // dW0 (256 x 93) += delta1^T sin(x@B): e recomputed from x
-    if (!syn || !syn->xP || !syn->fb) return PNR_E_ARG;
+    var = kVarFc;
+    ntb = 1;
+  } else if (kind == kWgradFirstX) {  // dW0 (256 x 93) += delta1^T sin(x@B): e recomputed from x
+    if (!syn->xP || !syn->fb) return PNR_E_ARG;
     a.nb = kFourier;
     a.xP = syn->xP;
     a.fb = syn->fb;
-    return launch_k<3, 96, false, true>(a, st, defer);
+    var = msk ? kVarFirstXM : kVarFirstX;
+    ntb = 3;
+  } else {
+    return PNR_E_ARG;
   }
-  return PNR_E_ARG;
+  job->a = a;
+  job->var = var;
+  job->nwg = (int)nwg;
+  *red = ReduceJob{a.part, a.part_bias, (int)nwg, 256, ntb * 32, a.nb, a.C, a.ldc, a.bias};
+  return 0;
+}
+
+int launch_wgrad16_group(const Wgrad16Job* jobs, int n, hipStream_t st) {
+  if (n <= 0) return 0;
+  if (n > kMaxGemmJobs) return PNR_E_ARG;
+  constexpr int kLds = Wx3<8, 256>::kLds;  // the largest variant
+  static_assert(Wx3<3, 96>::kLds <= kLds && Wx3<1, 32>::kLds <= kLds, "group LDS");
+  static const bool attr = hipFuncSetAttribute((const void*)k_wgrad16_group, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               kLds) == hipSuccess;
+  if (!attr) return PNR_E_ARG;
+  Wgrad16Group G{};
+  int blocks = 0;
+  int64_t units = 0;
+  for (int i = 0; i < n; ++i) {
+    G.a[i] = jobs[i].a;
+    G.var[i] = jobs[i].var;
+    G.first[i] = blocks;
+    blocks += jobs[i].nwg;
+    units += jobs[i].a.K;
+  }
+  G.first[n] = blocks;
+  G.n = n;
+  TimingScope ts(kTimeWgrad, units, st);
+  hipLaunchKernelGGL(k_wgrad16_group, dim3((unsigned)blocks), dim3(512), kLds, st, G);
+  return hip_status(hipGetLastError());
+}
+
+template <int NTB, int WB, bool SYN = false, bool FOUR = false, bool BSC = false, bool MSK = false>
+static int launch_k(const WxArgs& a, int nwg, hipStream_t st) {
+  using Cfg = Wx3<NTB, WB>;
+  auto kern = k_wgrad16<NTB, WB, SYN, FOUR, BSC, MSK>;
+  static const bool attr = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               Cfg::kLds) == hipSuccess;
+  if (!attr) return PNR_E_ARG;
+  hipLaunchKernelGGL(kern, dim3((unsigned)nwg), dim3(Cfg::kThreads), Cfg::kLds, st, a);
+  return hip_status(hipGetLastError());
+}
+
+// one GEMM on its own kernel variant; its reduction deferred into *defer or launched now
+int launch_wgrad16(int kind, const float* A, const float* B, int64_t K, int64_t kb_rows, float* C, int64_t ldc,
+                   float* bias, hipStream_t st, const WgradSyn* syn, ReduceJob* defer) {
+  if (K <= 0) return 0;
+  Wgrad16Job j;
+  ReduceJob red;
+  int rc = wgrad16_prepare(kind, A, B, K, kb_rows, C, ldc, bias, syn, &j, &red);
+  if (rc) return rc;
+  TimingScope ts(kTimeWgrad, j.a.K, st);
+  switch (j.var) {
+    case kVarHidden: rc = launch_k<8, 256>(j.a, j.nwg, st); break;
+    case kVarHiddenM: rc = launch_k<8, 256, false, false, false, true>(j.a, j.nwg, st); break;
+    case kVarSyn: rc = launch_k<8, 256, true>(j.a, j.nwg, st); break;
+    case kVarFirstX: rc = launch_k<3, 96, false, true>(j.a, j.nwg, st); break;
+    case kVarFirstXM: rc = launch_k<3, 96, false, true, false, true>(j.a, j.nwg, st); break;
+    default: rc = launch_k<1, 32, false, false, true>(j.a, j.nwg, st); break;
+  }
+  if (rc) return rc;
+  if (defer) {
+    *defer = red;
+    return 0;
+  }
+  return launch_part_reduce(red.part, red.pbias, red.nwg, red.nr, red.pw, red.nb, red.C, red.ldc, red.bias, st);
 }
 
 // Skinny weight-gradient GEMMs (fp32 FMAs), bandwidth-bound on B:
