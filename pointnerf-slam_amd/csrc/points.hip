@@ -491,9 +491,22 @@ __global__ __launch_bounds__(256) void k_gather_probe(GatherArgs a) {
     has = (a.occ[bit >> 5] >> (bit & 31u)) & 1u;
   }
   int2 gs = make_int2(0, 0);  // (group, slot in the group)
-  if (has) {
-    gs.x = (int)cell_hash(bx, by, bz, a.gmask);
-    gs.y = atomicAdd(a.gcnt + gs.x, 1);
+  if (has) gs.x = (int)cell_hash(bx, by, bz, a.gmask);
+  {
+    // one atomic per distinct group of the wave: consecutive samples of a ray share probe blocks,
+    // and same-address atomics of one instruction serialise in L2 (slots: base + rank among the peers)
+    const int lane = threadIdx.x & 63;
+    uint64_t todo = __ballot(has);
+    while (todo) {
+      const int leader = __ffsll((unsigned long long)todo) - 1;
+      const int gl = __builtin_amdgcn_readlane(gs.x, leader);
+      const uint64_t peers = __ballot(has && gs.x == gl) & todo;
+      int base = 0;
+      if (lane == leader) base = atomicAdd(a.gcnt + gl, (int)__popcll(peers));
+      base = __builtin_amdgcn_readlane(base, leader);
+      if ((peers >> lane) & 1ull) gs.y = base + (int)__popcll(peers & ((1ull << lane) - 1ull));
+      todo &= ~peers;
+    }
   }
   s_has[threadIdx.x] = has ? 1 : 0;
   __syncthreads();
@@ -555,8 +568,12 @@ struct SearchLds {
   int32_t row[64];
 };
 
+// feature-sum rows per round (k_gather_search) and the waves per SIMD its registers allow
+#ifndef PNR_FEAT_ROWS
+#define PNR_FEAT_ROWS 2
+#endif
 #ifndef PNR_SEARCH_WAVES
-#define PNR_SEARCH_WAVES 7
+#define PNR_SEARCH_WAVES (PNR_FEAT_ROWS > 1 ? 5 : 7)
 #endif
 template <int KER>
 __global__ __launch_bounds__(64, PNR_SEARCH_WAVES) void k_gather_search(GatherArgs a) {
@@ -652,8 +669,12 @@ __global__ __launch_bounds__(64, PNR_SEARCH_WAVES) void k_gather_search(GatherAr
           }
           if (__ballot(ok) == 0) continue;  // nobody keeps it: the network would be a no-op
           double kn = ok ? pack_key(dd, __float_as_int(qv.w)) : kInf;
+#if defined(PNR_EXP_NONET)  // experiment (wrong results, timing only): one stage instead of the network
+          kn = kstage(key[0], kn);
+#else
 #pragma unroll
           for (int t = 0; t < PNR_MAX_K; ++t) kn = kstage(key[t], kn);
+#endif
         }
         __syncthreads();  // the next batch overwrites the staged list
       }
@@ -709,8 +730,50 @@ __global__ __launch_bounds__(64, PNR_SEARCH_WAVES) void k_gather_search(GatherAr
     }
     __syncthreads();
     // feature sum: 8 lanes per sample, lane q owns channels 4q..4q+3
+#if PNR_FEAT_ROWS > 1
+    // PNR_FEAT_ROWS samples per round: their feature loads in flight together (the loads cannot move
+    // above the previous round's c stores on their own: the compiler must assume they alias).
+    // Measured (tools/gather_bench.py, 13.5M samples): 1 row per round 1.22 ms, 2 rows 1.13 ms.
 #pragma unroll 1
+    for (int rr = 0; rr < 8; rr += PNR_FEAT_ROWS) {
+      int rw[PNR_FEAT_ROWS];
+      float4 f[PNR_FEAT_ROWS][PNR_MAX_K];
+#pragma unroll
+      for (int u = 0; u < PNR_FEAT_ROWS; ++u) {
+        const int sl = (rr + u) * 8 + gq;
+        rw[u] = L.row[sl];
+#pragma unroll
+        for (int t = 0; t < PNR_MAX_K; ++t) {
+          const int id = L.idx[sl * PNR_MAX_K + t];
+          f[u][t] = make_float4(0.f, 0.f, 0.f, 0.f);
+          if (rw[u] >= 0 && id >= 0) f[u][t] = load_feat4(a.feats4, a.feat_half, (int64_t)id * 8 + q);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < PNR_FEAT_ROWS; ++u) {
+        if (rw[u] < 0) continue;
+        const int sl = (rr + u) * 8 + gq;
+        float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int t = 0; t < PNR_MAX_K; ++t) {
+          if (L.idx[sl * PNR_MAX_K + t] >= 0) {
+            const float wn = L.w[sl * PNR_MAX_K + t];
+            acc.x = acc.x + wn * f[u][t].x;
+            acc.y = acc.y + wn * f[u][t].y;
+            acc.z = acc.z + wn * f[u][t].z;
+            acc.w = acc.w + wn * f[u][t].w;
+          }
+        }
+        nt_store(reinterpret_cast<float4*>(a.c) + (int64_t)rw[u] * 8 + q, acc);  // 8 lanes: one 128-B row
+      }
+    }
+#else
+#pragma unroll 1
+#if defined(PNR_EXP_NOFEAT)  // experiment (wrong results, timing only): no feature sum
+    for (int rr = 0; rr < 0; ++rr) {
+#else
     for (int rr = 0; rr < 8; ++rr) {
+#endif
       const int sl = rr * 8 + gq;
       const int rw = L.row[sl];
       if (rw < 0) continue;
@@ -738,6 +801,7 @@ __global__ __launch_bounds__(64, PNR_SEARCH_WAVES) void k_gather_search(GatherAr
       }
       nt_store(reinterpret_cast<float4*>(a.c) + (int64_t)rw * 8 + q, acc);  // 8 lanes: one 128-B row
     }
+#endif
     __syncthreads();  // the next chunk rewrites the feature lists
   }
 }

@@ -140,6 +140,16 @@ def main():
         wmax = cw[:nw].view(-1, 64).max(1).values.float().mean().item() if nw else 0.0
         print(f'cells {uk.numel()} (points/cell {cnt.float().mean().item():.2f}); samples with candidates '
               f'{cw.numel()}: {cw.float().mean().item():.1f} candidates each, mean per-wave max {wmax:.1f}')
+        # probe blocks per 64-item chunk of the block-grouped list (k_gather_search's segments)
+        bk = ((b[:, 0] + off) << 42) | ((b[:, 1] + off) << 21) | (b[:, 2] + off)
+        bk = torch.sort(bk[cand > 0]).values
+        nc = bk.numel() // 64 * 64
+        if nc:
+            ch = bk[:nc].view(-1, 64)
+            segs = 1 + (ch[:, 1:] != ch[:, :-1]).sum(1)
+            _, bc = torch.unique(bk, return_counts=True)
+            print(f'search segments: {segs.float().mean().item():.1f} probe blocks per 64-item chunk '
+                  f'(max {int(segs.max().item())}); samples per block {bc.float().mean().item():.1f}')
     print(f'voxel {args.voxel} points {args.points} samples {P} ({args.rays} rays x 44) mode {args.mode} r {args.radius} k {args.k}')
     print(f'neighbours: mean {nb / P:.2f}/sample, histogram {hist}; samples with candidates {n_work} '
           f'({100 * n_work / P:.1f}%)')
