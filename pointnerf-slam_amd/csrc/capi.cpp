@@ -31,13 +31,13 @@ int launch_fine(const pnr_render_params&, const float*, const double*, const dou
                 int64_t, double*, double*, float*, uint8_t*, hipStream_t);
 int launch_fine_bwd(const pnr_render_params&, const float*, const double*, const double*, const float*,
                     const float*, const float4*, const float4*, const uint8_t*, int64_t, const double*,
-                    const double*, const float*, float*, float*, float*, hipStream_t);
+                    const double*, const float*, float*, float*, float*, float*, int, float*, int, hipStream_t);
 int launch_ray_grads_f64(const float*, const double*, int, const double*, int, const float*, const float*,
                          const float*, int64_t, float*, float*, hipStream_t);
 int launch_ray_grads_f32(const float*, const float*, int, const float*, int64_t, float*, float*, hipStream_t);
 int launch_reg_z(const pnr_render_params&, const float*, const float*, int64_t, float*, hipStream_t);
 int launch_extract_sigma(const float*, int64_t, float*, hipStream_t);
-int launch_gout_sigma(const float*, const float4*, int64_t, float*, hipStream_t);
+int launch_gout_sigma(const float*, const float4*, int64_t, int64_t, float*, hipStream_t);
 int launch_get_rays(int, int, float, float, float, float, const float*, float*, float*, hipStream_t);
 int launch_rays_from_uv(const float*, const float*, int64_t, float, float, float, float, const float*, float*,
                         float*, hipStream_t);
@@ -415,8 +415,7 @@ int pnr_mlp_pack(const float* const* params, float* packed, void* stream) {
   if (!check_params(params) || !packed) return PNR_E_ARG;
   RawParams rp;
   for (int i = 0; i < PNR_N_PARAMS; ++i) rp.p[i] = params[i];
-  const int rc = launch_pack(rp, packed, (hipStream_t)stream);
-  return rc ? rc : launch_pack_bf(rp, packed, (hipStream_t)stream);
+  return launch_pack_all(rp, packed, (hipStream_t)stream);
 }
 
 int pnr_eval_points(const float* packed, const double* p, int64_t P, const double* bound6, float* raw_out,
@@ -594,9 +593,11 @@ int pnr_render_bwd(const pnr_render_params* prm, const float* packed, const floa
   const double* zi = w.z + n * S;
   const float* rawi = w.raw + n * S * 4;
   const int64_t pc = w.pc_pad;
-  if (hipMemsetAsync(b.g_out, 0, (size_t)ld * 16, st) != hipSuccess) return (int)hipGetLastError();
+  // dL/draw of every MLP row: the samples' from the compositing backward, zeros on the padding rows
+  // [n S, pc) and [pc + n I, ld) (written by the same launch)
   int rc = launch_fine_bwd(*prm, rays_d, w.z, zi, w.raw, rawi, w.save.xP, w.save.xP + pc, w.ord, n,
-                           g_depth, g_var, g_rgb, b.g_out, b.g_out + pc * 4, b.g_nrm, st);
+                           g_depth, g_var, g_rgb, b.g_out, b.g_out + pc * 4, b.g_nrm, b.g_out + n * S * 4,
+                           (int)(pc - n * S), b.g_out + (pc + n * I) * 4, (int)(ld - pc - n * I), st);
   if (rc) return rc;
   FeatBwd fb{pts ? pts->fc_packed : nullptr, w.c, pts ? pts->g_fc : nullptr};
   rc = mlp_backward_core(prm->precision, packed, w.save, ld, b, grads, prm->need_ray_grads != 0, st,
@@ -714,8 +715,7 @@ int pnr_regulation_bwd(const pnr_render_params* prm, const float* packed, const 
   BwdWS b = carve_bwd(ld, n, bwd_ws, &bneed, pts != nullptr, save_mode(prm) != 2);
   if (ws_bytes < need || bwd_bytes < bneed) return PNR_E_WORKSPACE;
   hipStream_t st = (hipStream_t)stream;
-  if (hipMemsetAsync(b.g_out, 0, (size_t)ld * 16, st) != hipSuccess) return (int)hipGetLastError();
-  int rc = launch_gout_sigma(g_sigma, w.save.xP, P, b.g_out, st);
+  int rc = launch_gout_sigma(g_sigma, w.save.xP, P, ld, b.g_out, st);  // (zeros on the padding rows)
   if (rc) return rc;
   FeatBwd fb{pts ? pts->fc_packed : nullptr, w.c, pts ? pts->g_fc : nullptr};
   rc = mlp_backward_core(prm->precision, packed, w.save, ld, b, grads, prm->need_ray_grads != 0, st,

@@ -1,6 +1,7 @@
 // mlp16_pack.hip -- 16-bit weight images of the split-precision decoder kernels (mlp16.h) and
 // the forward dispatch on PNR_PREC_*.
 #include "mlp16.h"
+#include "pack_fp32.h"
 
 namespace pnr {
 
@@ -17,10 +18,10 @@ struct ScaleArgs {
   float* inv;
   float* scl;
 };
-__global__ __launch_bounds__(1024) void k_wscale(ScaleArgs a) {
+__device__ __forceinline__ void wscale_block(const ScaleArgs& a, const int b) {
   __shared__ float red[16];
-  const float* w = a.w[blockIdx.x];
-  const int n = a.n[blockIdx.x];
+  const float* w = a.w[b];
+  const int n = a.n[b];
   const int nt = blockDim.x, nw = nt >> 6;  // any multiple of 64 up to 1024
   float m0 = 0.f, m1 = 0.f, m2 = 0.f, m3 = 0.f;  // 4 loads in flight per thread
   int i = threadIdx.x;
@@ -45,10 +46,11 @@ __global__ __launch_bounds__(1024) void k_wscale(ScaleArgs a) {
       e = ex - 1;                     // 2^e <= 16384/max
       e = e < -20 ? -20 : (e > 20 ? 20 : e);
     }
-    a.scl[blockIdx.x] = ldexpf(1.f, e);
-    a.inv[blockIdx.x] = ldexpf(1.f, -e);
+    a.scl[b] = ldexpf(1.f, e);
+    a.inv[b] = ldexpf(1.f, -e);
   }
 }
+__global__ __launch_bounds__(1024) void k_wscale(ScaleArgs a) { wscale_block(a, blockIdx.x); }
 
 template <typename E>
 __device__ __forceinline__ uint16_t part_bits(float x, int part) {
@@ -59,9 +61,8 @@ __device__ __forceinline__ uint16_t part_bits(float x, int part) {
 
 // element (T, s, part, lane, j) of a weight fragment image for a layer with A[row][k]:
 // row = 32T + (lane&31), k = 32kc + perm(8s+j, lane>>5).  img 0: BF16X3, 1: BF16, 2: F16X3.
-__global__ void k_pack16(RawParams rp, uint16_t* __restrict__ bf2, uint16_t* __restrict__ bf1,
-                         uint16_t* __restrict__ h2, float* __restrict__ raw) {
-  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void pack16_at(const RawParams& rp, uint16_t* __restrict__ bf2, uint16_t* __restrict__ bf1,
+                                          uint16_t* __restrict__ h2, float* __restrict__ raw, const int64_t idx) {
   const int64_t n2 = bf_main_bytes(2) / 2, n1 = bf_main_bytes(1) / 2;
   if (idx < 2 * n2 + n1) {
     const int img = idx < n2 ? 0 : (idx < n2 + n1 ? 1 : 2);
@@ -125,8 +126,8 @@ __global__ void k_pack16(RawParams rp, uint16_t* __restrict__ bf2, uint16_t* __r
 
 // Transposed f16x3 images of the delta chain (element e of the backward stream), each tensor
 // scaled by the forward image's power of two (raw[kRawScl + tensor], k_wscale)
-__global__ void k_pack16_bwd(RawParams rp, uint16_t* __restrict__ out, const float* __restrict__ raw) {
-  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void pack16_bwd_at(const RawParams& rp, uint16_t* __restrict__ out,
+                                              const float* __restrict__ raw, const int64_t e) {
   if (e >= kBwdBytes / 2) return;
   const int64_t byte = 2 * e;
   int g = 0;
@@ -157,7 +158,25 @@ __global__ void k_pack16_bwd(RawParams rp, uint16_t* __restrict__ out, const flo
   out[e] = part_bits<_Float16>(v * raw[kRawScl + tensor], part);
 }
 
-int launch_pack_bf(const RawParams& rp, float* packed, hipStream_t st) {
+// The weight images of every precision in two launches (the Mapper repacks once per iteration, and
+// at its 1,000-ray batch each launch costs ~5 us of latency on the step's critical path):
+//   stage 1: blocks 0..4 the power-of-two weight scales (k_wscale), the rest the fp32 image (k_pack)
+//   stage 2: the transposed f16x3 delta-chain images, then the forward 16-bit images and the raw
+//            table (k_pack16_bwd, k_pack16) -- both read stage 1's scales
+__global__ __launch_bounds__(1024) void k_pack_stage1(ScaleArgs sa, RawParams rp, float* __restrict__ packed) {
+  if (blockIdx.x < 5) wscale_block(sa, blockIdx.x);
+  else pack_fp32_at(rp, packed, (int64_t)(blockIdx.x - 5) * 1024 + threadIdx.x);
+}
+__global__ __launch_bounds__(256) void k_pack_stage2(RawParams rp, float* __restrict__ packed, int nb_bwd) {
+  float* raw = packed + kOffRaw;
+  if ((int)blockIdx.x < nb_bwd)
+    pack16_bwd_at(rp, reinterpret_cast<uint16_t*>(packed + kOffBwd), raw, (int64_t)blockIdx.x * 256 + threadIdx.x);
+  else
+    pack16_at(rp, reinterpret_cast<uint16_t*>(packed + kOffBf2), reinterpret_cast<uint16_t*>(packed + kOffBf1),
+              reinterpret_cast<uint16_t*>(packed + kOffH2), raw, (int64_t)(blockIdx.x - nb_bwd) * 256 + threadIdx.x);
+}
+
+int launch_pack_all(const RawParams& rp, float* packed, hipStream_t st) {
   float* raw = packed + kOffRaw;
   ScaleArgs sa;
   const int nw[5] = {kHidden * kFourier, kHidden * kHidden, kHidden * kHidden, kHidden * kHidden, 4 * kHidden};
@@ -167,17 +186,12 @@ int launch_pack_bf(const RawParams& rp, float* packed, hipStream_t st) {
   }
   sa.inv = raw + kRawInv;
   sa.scl = raw + kRawScl;
-  hipLaunchKernelGGL(k_wscale, dim3(5), dim3(1024), 0, st, sa);
-  {
-    const int64_t n = kBwdBytes / 2;
-    hipLaunchKernelGGL(k_pack16_bwd, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, rp,
-                       reinterpret_cast<uint16_t*>(packed + kOffBwd), raw);
-  }
-  const int64_t n = 2 * (bf_main_bytes(2) / 2) + bf_main_bytes(1) / 2 + kRawWo + 4 * kHidden;
-  const int threads = 256;
-  hipLaunchKernelGGL(k_pack16, dim3((unsigned)((n + threads - 1) / threads)), dim3(threads), 0, st, rp,
-                     reinterpret_cast<uint16_t*>(packed + kOffBf2), reinterpret_cast<uint16_t*>(packed + kOffBf1),
-                     reinterpret_cast<uint16_t*>(packed + kOffH2), raw);
+  const int nb1 = 5 + (int)((kPackedFloats + 1023) / 1024);
+  hipLaunchKernelGGL(k_pack_stage1, dim3(nb1), dim3(1024), 0, st, sa, rp, packed);
+  const int nb_bwd = (int)((kBwdBytes / 2 + 255) / 256);
+  const int64_t n16 = 2 * (bf_main_bytes(2) / 2) + bf_main_bytes(1) / 2 + kRawWo + 4 * kHidden;
+  const int nb2 = nb_bwd + (int)((n16 + 255) / 256);
+  hipLaunchKernelGGL(k_pack_stage2, dim3(nb2), dim3(256), 0, st, rp, packed, nb_bwd);
   return hip_status(hipGetLastError());
 }
 

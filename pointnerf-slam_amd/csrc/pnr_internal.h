@@ -172,6 +172,8 @@ int launch_mlp_bwd(const float* packed, const BwdArgs& a, int64_t P, hipStream_t
 int launch_mlp_bwd_bf(const float* packed, const BwdArgs& a, int64_t P, hipStream_t st);
 
 int launch_pack(const RawParams& rp, float* packed, hipStream_t st);
+// every image (fp32, 16-bit forward, delta chain, raw table) in two launches (mlp16_pack.hip)
+int launch_pack_all(const RawParams& rp, float* packed, hipStream_t st);
 // float offset of Wo [4][256] fp32 in the packed buffer (the raw table's copy, mlp16.h kRawWo)
 int64_t packed_raw_wo_offset();
 int launch_fc_pack(const float* const* fc, float* out, hipStream_t st);
@@ -179,7 +181,7 @@ int launch_fc_pack(const float* const* fc, float* out, hipStream_t st);
 // bf16 split forward (mlp_bf.hip): images appended to the fp32 images in the same buffers
 int64_t packed_floats_all();
 int64_t fc_packed_floats_all();
-int launch_pack_bf(const RawParams& rp, float* packed, hipStream_t st);
+
 int launch_fc_pack_bf(const float* const* fc, float* out, hipStream_t st);
 // prec = PNR_PREC_BF16X3 / PNR_PREC_BF16 / PNR_PREC_F16X3
 // status: PNR_STATUS_* bits ORed in on the device (f16 range check of F16X3), or null

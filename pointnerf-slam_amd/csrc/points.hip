@@ -471,6 +471,30 @@ struct GatherArgs {
 
 // Pass 1, one thread per sample row: the occupancy bit of each sample's probe block; the hits go
 // to the work list, the block zero-fills the other rows of its 256 with coalesced stores.
+// zero rows (c, and the k index / weight slots) of a probe block: the rows without a work item, or
+// every row (all: the search rewrites the rows of its items)
+__device__ __forceinline__ void probe_fill(const GatherArgs& a, int64_t r0, int64_t nrow, int64_t p, bool has,
+                                           const uint8_t* s_has, bool all) {
+  float4* c4 = reinterpret_cast<float4*>(a.c) + r0 * 8;
+  for (int e = threadIdx.x; e < nrow * 8; e += 256)
+    if (all || !s_has[e >> 3]) nt_store(c4 + e, make_float4(0.f, 0.f, 0.f, 0.f));
+  if (a.idx && p < a.rows && (all || !has)) {  // this row's k (index, weight) slots
+    if (a.k == 8 && ((reinterpret_cast<uintptr_t>(a.idx) | reinterpret_cast<uintptr_t>(a.w)) & 15) == 0) {
+      int4* i4 = reinterpret_cast<int4*>(a.idx) + p * 2;
+      float4* w4 = reinterpret_cast<float4*>(a.w) + p * 2;
+      nt_store(i4, make_int4(-1, -1, -1, -1));
+      nt_store(i4 + 1, make_int4(-1, -1, -1, -1));
+      nt_store(w4, make_float4(0.f, 0.f, 0.f, 0.f));
+      nt_store(w4 + 1, make_float4(0.f, 0.f, 0.f, 0.f));
+    } else {
+      for (int t = 0; t < a.k; ++t) {
+        a.idx[p * a.k + t] = -1;
+        a.w[p * a.k + t] = 0.f;
+      }
+    }
+  }
+}
+
 template <int SRC>
 __global__ __launch_bounds__(256) void k_gather_probe(GatherArgs a) {
   PNR_FP_STRICT
@@ -478,6 +502,9 @@ __global__ __launch_bounds__(256) void k_gather_probe(GatherArgs a) {
   const int64_t r0 = (int64_t)blockIdx.x * 256;
   const int64_t nrow = a.rows - r0 < 256 ? a.rows - r0 : 256;
   const int64_t p = r0 + threadIdx.x;
+#if defined(PNR_EXP_FILLALL)  // experiment: every row zero-filled first, with no wait on the test
+  probe_fill(a, r0, nrow, p, false, s_has, true);
+#endif
   float x0 = 0.f, x1 = 0.f, x2 = 0.f;
   bool has = false;
   int bx = 0, by = 0, bz = 0;
@@ -509,28 +536,10 @@ __global__ __launch_bounds__(256) void k_gather_probe(GatherArgs a) {
     }
   }
   s_has[threadIdx.x] = has ? 1 : 0;
+#if !defined(PNR_EXP_FILLALL) && !defined(PNR_EXP_NOFILL)
   __syncthreads();
-  // coalesced zero fill of the rows the search pass will not write
-  {
-    float4* c4 = reinterpret_cast<float4*>(a.c) + r0 * 8;
-    for (int e = threadIdx.x; e < nrow * 8; e += 256)
-      if (!s_has[e >> 3]) nt_store(c4 + e, make_float4(0.f, 0.f, 0.f, 0.f));
-    if (a.idx && p < a.rows && !has) {  // this row's k (index, weight) slots
-      if (a.k == 8 && ((reinterpret_cast<uintptr_t>(a.idx) | reinterpret_cast<uintptr_t>(a.w)) & 15) == 0) {
-        int4* i4 = reinterpret_cast<int4*>(a.idx) + p * 2;
-        float4* w4 = reinterpret_cast<float4*>(a.w) + p * 2;
-        nt_store(i4, make_int4(-1, -1, -1, -1));
-        nt_store(i4 + 1, make_int4(-1, -1, -1, -1));
-        nt_store(w4, make_float4(0.f, 0.f, 0.f, 0.f));
-        nt_store(w4 + 1, make_float4(0.f, 0.f, 0.f, 0.f));
-      } else {
-        for (int t = 0; t < a.k; ++t) {
-          a.idx[p * a.k + t] = -1;
-          a.w[p * a.k + t] = 0.f;
-        }
-      }
-    }
-  }
+  probe_fill(a, r0, nrow, p, has, s_has, false);
+#endif
   wl_append(a.wl, has, make_float4(x0, x1, x2, __int_as_float((int)p)), gs);
 }
 

@@ -278,7 +278,8 @@ __global__ __launch_bounds__(64) void k_fine_bwd(pnr_render_params prm, const fl
                                                  const uint8_t* __restrict__ ord_in, int64_t n_rays,
                                                  const double* __restrict__ g_depth, const double* __restrict__ g_var,
                                                  const float* __restrict__ g_rgb, float4* __restrict__ goc,
-                                                 float4* __restrict__ goi, float* __restrict__ g_nrm) {
+                                                 float4* __restrict__ goi, float* __restrict__ g_nrm,
+                                                 float4* __restrict__ pad0, int np0, float4* __restrict__ pad1, int np1) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x;
   const int64_t n = (int64_t)blockIdx.x * 64 + tid;
@@ -288,6 +289,11 @@ __global__ __launch_bounds__(64) void k_fine_bwd(pnr_render_params prm, const fl
   double* zs = reinterpret_cast<double*>(smem);
   float* al = reinterpret_cast<float*>(zs + M * 64);
   float* Tl = al + M * 64;
+  {  // the padding rows of the MLP launches get dL/draw = 0 (the MLP backward reads every row)
+    const int64_t gi = (int64_t)blockIdx.x * 64 + tid, gs = (int64_t)gridDim.x * 64;
+    for (int64_t i = gi; i < np0; i += gs) pad0[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int64_t i = gi; i < np1; i += gs) pad1[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
   if (n >= n_rays) return;
   const uint8_t* ord = ord_in + n * PNR_MAX_SAMPLES;
   // specialised: the ray's sort order in registers (16-B loads of the 64-B row), so the sample
@@ -410,10 +416,12 @@ __global__ void k_extract_sigma(const float4* __restrict__ raw, int64_t P, float
   if (p < P) sigma[p] = raw[p].w;
 }
 
-__global__ void k_gout_sigma(const float* __restrict__ g_sigma, const float4* __restrict__ xP, int64_t P,
+// rows [P, ld) are the MLP launch's padding: dL/draw = 0
+__global__ void k_gout_sigma(const float* __restrict__ g_sigma, const float4* __restrict__ xP, int64_t P, int64_t ld,
                              float4* __restrict__ g_out) {
   const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (p < P) g_out[p] = make_float4(0.f, 0.f, 0.f, xP[p].w != 0.f ? g_sigma[p] : 0.f);
+  else if (p < ld) g_out[p] = make_float4(0.f, 0.f, 0.f, 0.f);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -582,16 +590,19 @@ int launch_fine(const pnr_render_params& prm, const float* rd, const double* zc,
 int launch_fine_bwd(const pnr_render_params& prm, const float* rd, const double* zc, const double* zi,
                     const float* rawc, const float* rawi, const float4* insc, const float4* insi,
                     const uint8_t* ord, int64_t n, const double* gd, const double* gv, const float* grgb,
-                    float* goc, float* goi, float* g_nrm, hipStream_t st) {
+                    float* goc, float* goi, float* g_nrm, float* pad0, int np0, float* pad1, int np1,
+                    hipStream_t st) {
   if (n <= 0) return 0;
   const int M = prm.n_samples + prm.n_importance;
   const size_t sh = (size_t)M * 64 * (8 + 2 * 4);
   if (prm.n_samples == 32 && prm.n_importance == 12)
     hipLaunchKernelGGL((k_fine_bwd<32, 12>), dim3(nblk(n, 64)), dim3(64), sh, st, prm, rd, zc, zi, (const float4*)rawc,
-                       (const float4*)rawi, insc, insi, ord, n, gd, gv, grgb, (float4*)goc, (float4*)goi, g_nrm);
+                       (const float4*)rawi, insc, insi, ord, n, gd, gv, grgb, (float4*)goc, (float4*)goi, g_nrm,
+                       (float4*)pad0, np0, (float4*)pad1, np1);
   else
     hipLaunchKernelGGL((k_fine_bwd<0, 0>), dim3(nblk(n, 64)), dim3(64), sh, st, prm, rd, zc, zi, (const float4*)rawc,
-                       (const float4*)rawi, insc, insi, ord, n, gd, gv, grgb, (float4*)goc, (float4*)goi, g_nrm);
+                       (const float4*)rawi, insc, insi, ord, n, gd, gv, grgb, (float4*)goc, (float4*)goi, g_nrm,
+                       (float4*)pad0, np0, (float4*)pad1, np1);
   return hip_status(hipGetLastError());
 }
 int launch_ray_grads_f64(const float* rd, const double* za, int sa, const double* zb, int sb, const float* gxa,
@@ -630,9 +641,9 @@ int launch_extract_sigma(const float* raw, int64_t P, float* sigma, hipStream_t 
   hipLaunchKernelGGL(k_extract_sigma, dim3(nblk(P, 256)), dim3(256), 0, st, (const float4*)raw, P, sigma);
   return hip_status(hipGetLastError());
 }
-int launch_gout_sigma(const float* g_sigma, const float4* inside, int64_t P, float* g_out, hipStream_t st) {
-  if (P <= 0) return 0;
-  hipLaunchKernelGGL(k_gout_sigma, dim3(nblk(P, 256)), dim3(256), 0, st, g_sigma, inside, P, (float4*)g_out);
+int launch_gout_sigma(const float* g_sigma, const float4* inside, int64_t P, int64_t ld, float* g_out, hipStream_t st) {
+  if (ld <= 0) return 0;
+  hipLaunchKernelGGL(k_gout_sigma, dim3(nblk(ld, 256)), dim3(256), 0, st, g_sigma, inside, P, ld, (float4*)g_out);
   return hip_status(hipGetLastError());
 }
 int launch_get_rays(int H, int W, float fx, float fy, float cx, float cy, const float* c2w, float* ro, float* rd,
