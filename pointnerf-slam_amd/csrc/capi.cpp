@@ -320,9 +320,11 @@ int mlp_backward_core(int prec, const float* packed, const SaveArgs& sv, int64_t
         prep(kWgradFirstX, dsrc, nullptr, grads[1], kFourier, grads[2], fmask ? sv.masks : nullptr);
       }
       // feature branch: dWc_l (256x32) += (dL/dh_l)^T c ; dbc_l += colsum(dL/dh_l)
+      // (dL/dh4 = Wo^T g_out is rank 4: k_mlp_bwd16 does not store it, the dWc_3 GEMM rebuilds it)
       if (want_fc)
         for (int l = 0; l < 4; ++l)
-          prep(kWgradFc, b.gH + l * dstride, fb->c + p0 * kCDim, fb->g_fc[2 * l], kCDim, fb->g_fc[2 * l + 1], nullptr);
+          prep(l == 3 ? kWgradFcOut : kWgradFc, b.gH + l * dstride, fb->c + p0 * kCDim, fb->g_fc[2 * l], kCDim,
+               fb->g_fc[2 * l + 1], nullptr);
       if (rc == 0) rc = launch_wgrad16_group(gjobs, ng, st);
       // Fourier: dB (3x93) += x^T g_arg
       if (rc == 0 && grads) {

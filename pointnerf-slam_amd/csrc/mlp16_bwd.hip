@@ -91,9 +91,11 @@ struct BwdGeo {
     // conv2 stores no delta4 (chain 0: kWgradOutDelta rebuilds it) and, with the feature branch, no
     // delta at all (the dW GEMMs mask conv1's dL/dh themselves); conv1's dL/dh (features) stays
     const bool d = !HASC && bwd_conv_chain(g) != 0;
-    if (bnd(g)) return T == nt(g) - 1 ? (HASC ? 4 : 0) + (d ? 4 : 0) : 0;
+    // dL/dh stores (features): not for chain 0's dL/dh4 = Wo^T g_out (the dWc_3 GEMM rebuilds it)
+    const bool gh = HASC && bwd_conv_chain(g) != 0;
+    if (bnd(g)) return T == nt(g) - 1 ? (gh ? 4 : 0) + (d ? 4 : 0) : 0;
     int n = 0;
-    for (int q = 0; q < 4; ++q) n += (HASC && grp1(q, 0, nt(g)) == T ? 1 : 0) + (d && grp2(q, 0, nt(g)) == T ? 1 : 0);
+    for (int q = 0; q < 4; ++q) n += (gh && grp1(q, 0, nt(g)) == T ? 1 : 0) + (d && grp2(q, 0, nt(g)) == T ? 1 : 0);
     return n;
   }
   __host__ __device__ static constexpr int stores_rng(int g, int t0, int t1) {
@@ -229,8 +231,9 @@ struct BfBwd {
     constexpr int li = 3 - CC;
 #pragma unroll
     for (int i = 0; i < 4; ++i) S.v[4 * q + i] = S.acc[CC & 1][t][4 * q + i] * S.kconv;
-    if constexpr (HASC) {  // fp32 dL/dh for dWc = gH^T c (wgrad16.hip)
-      save16(d_save(a.gH, a, S, li, t, q), make_float4(S.v[4 * q], S.v[4 * q + 1], S.v[4 * q + 2], S.v[4 * q + 3]));
+    if constexpr (HASC) {  // fp32 dL/dh for dWc = gH^T c (wgrad16.hip; dL/dh4 of chain 0 is rebuilt there)
+      if constexpr (CC != 0)
+        save16(d_save(a.gH, a, S, li, t, q), make_float4(S.v[4 * q], S.v[4 * q + 1], S.v[4 * q + 2], S.v[4 * q + 3]));
       split_scaled(S.v + 4 * q, S.sig, q, S.tmp);
     }
   }

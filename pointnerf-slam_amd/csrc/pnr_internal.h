@@ -230,7 +230,8 @@ int launch_gather_bwd(const pnr_points& pts, const PointSrc* src, int mode, cons
 enum WgradKind : int {
   kWgradHidden = 0, kWgradFirst = 1, kWgradOut = 2, kWgradFourier = 3, kWgradFc = 4,
   kWgradOutDelta = 5,  // split precisions: dW3 = delta4^T h3 with delta4 rebuilt from g_out (WgradSyn)
-  kWgradFirstX = 6     // split precisions: dW0 = delta1^T e with e = sin(x@B) recomputed (WgradSyn xP, fb)
+  kWgradFirstX = 6,    // split precisions: dW0 = delta1^T e with e = sin(x@B) recomputed (WgradSyn xP, fb)
+  kWgradFcOut = 7      // split precisions: dWc_3 = (dL/dh4)^T c with dL/dh4 = Wo^T g_out rebuilt (WgradSyn g_out, wo)
 };
 // kWgradOutDelta: delta4 = (Wo^T g_out) * [h4 > 0] is not stored by the delta chain; the GEMM
 // rebuilds it per element from the chunk's g_out rows, the forward's h4 mask words and Wo

@@ -46,12 +46,17 @@ typedef short v4i16 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
 
 constexpr int kTileB = 2112;  // bytes of one [32 points][64 B] block, +64 B pad
+// BSC (B = point features, WB = 32): the tile is staged in fp32, rows of kBscRow floats (16-B
+// aligned; a wave's 32-lane half reads 32 consecutive columns of one row: conflict-free)
+constexpr int kBscRow = 36;
 
 template <int NTB, int WB>
 struct Wx3 {
   static constexpr int kThreads = 512;                   // 8 waves, 2 per SIMD
   static constexpr int kPlane = NTB * kTileB;            // one plane (hi or lo) of a B tile
-  static constexpr int kSlot = 2 * kPlane + 512;         // + the tile's 32 g_out rows (SYN)
+  // the tile's 32 g_out rows (SYN) follow the B image: the two planes, or BSC's fp32 rows
+  static constexpr int kGo = 2 * kPlane > 32 * kBscRow * 4 ? 2 * kPlane : 32 * kBscRow * 4;
+  static constexpr int kSlot = kGo + 512;
   static constexpr int kLds = 2 * kSlot;                 // double-buffered
   static constexpr int kC4 = WB / 4;                     // float4 per B row
   static constexpr int kB4 = 32 * kC4;                   // float4 per B tile
@@ -79,7 +84,14 @@ template <int NTB, int WB, bool SYN, bool FOUR, bool MSK = false>
 __device__ __forceinline__ void wx_load(const WxArgs& a, int64_t k0, WxRegs<NTB, WB>& R) {
   using Cfg = Wx3<NTB, WB>;
   const int tid = threadIdx.x, lane = tid & 63;
-  if constexpr (SYN) {
+  // SYN with WB = 32 (dWc_3): A = dL/dh4 = Wo^T g_out unmasked, so no mask words
+  constexpr bool SYN_MASKED = SYN && WB != 32;
+  if constexpr (SYN && !SYN_MASKED) {
+    if (tid < 32) {
+      const int64_t row = k0 + 32 + tid;
+      R.go = a.g_out[row < a.K ? row : a.K - 1];
+    }
+  } else if constexpr (SYN) {
     // mask word of unit u = 32w + (lane & 31) for the lane's 16 points 8 hh + 16 s + j of the
     // 32-point group: uint4 (point + 32 ((u >> 2) & 1)), component u >> 6 (k_mlp_fwd16 conv1)
     const int u = 32 * wave_id() + (lane & 31);
@@ -123,17 +135,15 @@ __device__ __forceinline__ void wx_load(const WxArgs& a, int64_t k0, WxRegs<NTB,
   }
 }
 
-// B tile -> hi / lo f16 planes of `slot` (SYN: + the next tile's g_out rows into the other slot)
-// BSC (B = point features, WB = 32): the tile is staged in fp32, rows of kBscRow floats (16-B
-// aligned; a wave's 32-lane half reads 32 consecutive columns of one row: conflict-free)
-constexpr int kBscRow = 36;
+// B tile -> hi / lo f16 planes of `slot` (SYN: + the next tile's g_out rows into the other slot;
+// BSC: fp32 rows of kBscRow floats)
 
 template <int NTB, int WB, bool SYN, bool FOUR, bool BSC = false>
 __device__ __forceinline__ void wx_stage_b(const WxRegs<NTB, WB>& R, char* slot, char* next_slot,
                                            const float (&fbr)[Wx3<NTB, WB>::kBPer][3][4]) {
   using Cfg = Wx3<NTB, WB>;
   const int tid = threadIdx.x;
-  if (SYN && tid < 32) reinterpret_cast<float4*>(next_slot + 2 * Cfg::kPlane)[tid] = R.go;
+  if (SYN && tid < 32) reinterpret_cast<float4*>(next_slot + Cfg::kGo)[tid] = R.go;
 #pragma unroll
   for (int i = 0; i < Cfg::kBPer; ++i) {
     const int q = tid + Cfg::kThreads * i;
@@ -191,7 +201,8 @@ __device__ __forceinline__ f16x8 tr_frag(const char* img, int T, int s) {
 template <int NTB, int WB, bool SYN, bool FOUR, bool BSC, bool MSK>
 __device__ __forceinline__ void wgrad16_body(const WxArgs& a, const int bid, char* lds) {
   static_assert(!MSK || (!SYN && !BSC), "MSK: the hidden / first-layer GEMMs");
-  static_assert(!BSC || (NTB == 1 && WB == 32 && !SYN && !FOUR), "BSC: the fc_c shape");
+  static_assert(!BSC || (NTB == 1 && WB == 32 && !FOUR), "BSC: the fc_c shape");
+  static_assert(!SYN || !BSC || !MSK, "SYN + BSC: dWc_3 on A = Wo^T g_out (unmasked)");
   static_assert(!BSC || 32 * kBscRow * 4 <= Wx3<NTB, WB>::kSlot, "BSC tile fits the slot");
   using Cfg = Wx3<NTB, WB>;
   const int lane = threadIdx.x & 63, hh = lane >> 5;
@@ -227,7 +238,7 @@ __device__ __forceinline__ void wgrad16_body(const WxArgs& a, const int bid, cha
         fbr[i][d][e] = FOUR ? a.fb[d * kFourierPad + 4 * ((threadIdx.x + Cfg::kThreads * i) % Cfg::kC4) + e] : 0.f;
   if (ntile > 0) wx_load<NTB, WB, SYN, FOUR, MSK>(a, kb, R);
   if (SYN && ntile > 0) {  // the first tile's g_out rows; later tiles' are staged one tile ahead
-    if (threadIdx.x < 32) reinterpret_cast<float4*>(lds + 2 * Cfg::kPlane)[threadIdx.x] = a.g_out[kb + threadIdx.x];
+    if (threadIdx.x < 32) reinterpret_cast<float4*>(lds + Cfg::kGo)[threadIdx.x] = a.g_out[kb + threadIdx.x];
     __syncthreads();
   }
   for (int64_t t = 0; t < ntile; ++t) {
@@ -238,14 +249,14 @@ __device__ __forceinline__ void wgrad16_body(const WxArgs& a, const int bid, cha
     if constexpr (SYN) {
       // delta4 = (Wo^T g_out) masked, fp32 FMAs (the tile's g_out rows from LDS, staged before the
       // previous barrier; broadcast reads)
-      const float4* go = reinterpret_cast<const float4*>(slot + 2 * Cfg::kPlane) + 8 * hh;
+      const float4* go = reinterpret_cast<const float4*>(slot + Cfg::kGo) + 8 * hh;
 #pragma unroll
       for (int s = 0; s < 2; ++s)
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const float4 g = go[16 * s + j];
           const float d = __builtin_fmaf(wo[3], g.w, __builtin_fmaf(wo[2], g.z, __builtin_fmaf(wo[1], g.y, wo[0] * g.x)));
-          R.a[8 * s + j] = ((__float_as_uint(R.a[8 * s + j]) >> mbit) & 1u) ? d : 0.f;
+          R.a[8 * s + j] = BSC ? d : (((__float_as_uint(R.a[8 * s + j]) >> mbit) & 1u) ? d : 0.f);
         }
     }
     float m = 0.f;
@@ -362,7 +373,7 @@ struct Wgrad16Group {
   int first[kMaxGemmJobs + 1];
   int n;
 };
-enum : int { kVarHidden = 0, kVarHiddenM, kVarSyn, kVarFirstX, kVarFirstXM, kVarFc };
+enum : int { kVarHidden = 0, kVarHiddenM, kVarSyn, kVarFirstX, kVarFirstXM, kVarFc, kVarFcOut };
 __global__ __launch_bounds__(512, 1) void k_wgrad16_group(Wgrad16Group G) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   int q = 0;
@@ -374,6 +385,7 @@ __global__ __launch_bounds__(512, 1) void k_wgrad16_group(Wgrad16Group G) {
     case kVarSyn: wgrad16_body<8, 256, true, false, false, false>(G.a[q], bid, lds); break;
     case kVarFirstX: wgrad16_body<3, 96, false, true, false, false>(G.a[q], bid, lds); break;
     case kVarFirstXM: wgrad16_body<3, 96, false, true, false, true>(G.a[q], bid, lds); break;
+    case kVarFcOut: wgrad16_body<1, 32, true, false, true, false>(G.a[q], bid, lds); break;
     default: wgrad16_body<1, 32, false, false, true, false>(G.a[q], bid, lds); break;
   }
 }
@@ -549,6 +561,13 @@ int wgrad16_prepare(int kind, const float* A, const float* B, int64_t K, int64_t
     a.nb = kCDim;
     var = kVarFc;
     ntb = 1;
+  } else if (kind == kWgradFcOut) {  // dWc_3 (256 x 32) += (Wo^T g_out)^T c: dL/dh4 rebuilt, not read
+    if (!syn->g_out || !syn->wo) return PNR_E_ARG;
+    a.nb = kCDim;
+    a.g_out = syn->g_out;
+    a.wo = syn->wo;
+    var = kVarFcOut;
+    ntb = 1;
   } else if (kind == kWgradFirstX) {  // dW0 (256 x 93) += delta1^T sin(x@B): e recomputed from x
     if (!syn->xP || !syn->fb) return PNR_E_ARG;
     a.nb = kFourier;
@@ -617,6 +636,7 @@ int launch_wgrad16(int kind, const float* A, const float* B, int64_t K, int64_t 
     case kVarSyn: rc = launch_k<8, 256, true>(j.a, j.nwg, st); break;
     case kVarFirstX: rc = launch_k<3, 96, false, true>(j.a, j.nwg, st); break;
     case kVarFirstXM: rc = launch_k<3, 96, false, true, false, true>(j.a, j.nwg, st); break;
+    case kVarFcOut: rc = launch_k<1, 32, true, false, true>(j.a, j.nwg, st); break;
     default: rc = launch_k<1, 32, false, false, true>(j.a, j.nwg, st); break;
   }
   if (rc) return rc;

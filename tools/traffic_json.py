@@ -41,8 +41,8 @@ def family(name):
         return 'k_mlp_fwd_train'
     if 'k_gather_probe' in name:
         return 'k_gather_probe'
-    if 'k_gather_search' in name:
-        return 'k_gather_search'
+    if 'k_gather_search' in name or 'k_group_scatter' in name:
+        return 'k_gather_search'  # (round 3: the grouped list's scatter belongs to the gather too)
     return None
 
 
