@@ -33,8 +33,9 @@ __device__ __forceinline__ float ray_norm(const float* d) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// batch max of 1.2 gt in two launches: kGtParts blocks write partial maxima to out[1..], then one
-// block reduces them into out[0] (the workspace slot holds 64 floats).  NaN propagates (torch.max).
+// batch max of 1.2 gt in two launches (one up to 4,096 rays): kGtParts blocks write partial maxima
+// to out[1..], then one block reduces them into out[0] (the workspace slot holds 64 floats).  NaN
+// propagates (torch.max).
 constexpr int kGtParts = 63;
 __device__ __forceinline__ float max_nanf(float m, float v) { return (v > m || v != v) ? v : m; }
 __device__ __forceinline__ float block_max_256(float m, float* red) {
@@ -50,7 +51,7 @@ __global__ __launch_bounds__(256) void k_gt_max_part(const float* __restrict__ g
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
     m = max_nanf(m, gt[i] * 1.2f);
   m = block_max_256(m, red);
-  if (threadIdx.x == 0) out[1 + blockIdx.x] = m;
+  if (threadIdx.x == 0) out[gridDim.x == 1 ? 0 : 1 + blockIdx.x] = m;  // one part: the result itself
 }
 __global__ __launch_bounds__(256) void k_gt_max(int parts, float* __restrict__ out) {
   __shared__ float red[4];
@@ -557,7 +558,7 @@ static inline unsigned nblk(int64_t n, int b) { return (unsigned)((n + b - 1) / 
 int launch_gt_max(const float* gt, int64_t n, float* out, hipStream_t st) {
   const int parts = (int)std::min<int64_t>(kGtParts, std::max<int64_t>(1, (n + 4095) / 4096));
   hipLaunchKernelGGL(k_gt_max_part, dim3(parts), dim3(256), 0, st, gt, n, out);
-  hipLaunchKernelGGL(k_gt_max, dim3(1), dim3(256), 0, st, parts, out);
+  if (parts > 1) hipLaunchKernelGGL(k_gt_max, dim3(1), dim3(256), 0, st, parts, out);  // (<= 4,096 rays: one launch)
   return hip_status(hipGetLastError());
 }
 int launch_coarse_z(const pnr_render_params& prm, const float* ro, const float* rd, const float* gt,

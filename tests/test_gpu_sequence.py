@@ -156,3 +156,16 @@ def test_twenty_frame_loop_teacher_forced_modes_agree(sequence, scene, dev):
     print(f'first mapping round: map losses rel max {m0:.2e}; frame 1 first tracking loss rel {t0:.2e}')
     assert m0 < 1e-3 and t0 < 1e-3
     assert rel_w < 1e-3 and rel_m < 0.1 and rel_t < 0.25
+    # control: fp32 against itself with every decoder weight moved by 2^-22 relative (the size of one
+    # f16x3 product's rounding).  If the loop amplifies rounding, that run drifts from fp32 as well;
+    # f16x3 must not drift more than twice as far as this fp32-class perturbation (+ a small floor)
+    g = torch.Generator().manual_seed(11)
+    pert = {k: v * (1.0 + 2.0 ** -22 * (2.0 * torch.randint(0, 2, v.shape, generator=g).float() - 1.0))
+            for k, v in params.items()}
+    pc, wc, mc, tc = run_loop(pnr, scene, pert, frames, 'fp32', dev, teacher=True)
+    cw = ((wc - w32).norm() / w32.norm()).item()
+    ct = np.max(np.abs(tc - t32) / np.abs(t32))
+    cm = np.max(np.abs(np.array(mc) - np.array(m32)) / np.array(m32))
+    print(f'control (fp32, weights x (1 +- 2^-22)) vs fp32: decoder rel L2 {cw:.2e}, tracking losses rel max '
+          f'{ct:.2e}, map losses rel max {cm:.2e}')
+    assert rel_w <= 2 * cw + 1e-5 and rel_t <= 2 * ct + 1e-3 and rel_m <= 2 * cm + 1e-3, (rel_w, cw, rel_t, ct, rel_m, cm)
