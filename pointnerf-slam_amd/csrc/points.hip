@@ -519,6 +519,43 @@ __global__ __launch_bounds__(256) void k_gather_probe(GatherArgs a) {
   }
   int2 gs = make_int2(0, 0);  // (group, slot in the group)
   if (has) gs.x = (int)cell_hash(bx, by, bz, a.gmask);
+#if !defined(PNR_PROBE_SERIAL)
+  // The zero fill goes out first (stores: nothing waits on them), then the work-list atomic and the
+  // group atomics are all issued before any of their returns is read, so one wave pays one
+  // round trip instead of a chain of them in front of its fill.
+  s_has[threadIdx.x] = has ? 1 : 0;
+  __syncthreads();
+  probe_fill(a, r0, nrow, p, has, s_has, false);
+  {
+    const int lane = threadIdx.x & 63;
+    const uint64_t m = __ballot(has);
+    if (m == 0) return;
+    const int r = (int)(((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) & (kLists - 1));
+    const int wl_leader = __ffsll((unsigned long long)m) - 1;
+    uint32_t wl_base = 0;
+    if (lane == wl_leader) wl_base = atomicAdd(a.wl.cnt + r * 32, (uint32_t)__popcll(m));
+    int my_atom = 0, my_leader = 0, my_rank = 0;
+    uint64_t todo = m;
+    while (todo) {
+      const int leader = __ffsll((unsigned long long)todo) - 1;
+      const int gl = __builtin_amdgcn_readlane(gs.x, leader);
+      const uint64_t peers = __ballot(has && gs.x == gl) & todo;
+      if (lane == leader) my_atom = atomicAdd(a.gcnt + gl, (int)__popcll(peers));
+      if ((peers >> lane) & 1ull) {
+        my_leader = leader;
+        my_rank = (int)__popcll(peers & ((1ull << lane) - 1ull));
+      }
+      todo &= ~peers;
+    }
+    gs.y = __shfl(my_atom, my_leader) + my_rank;
+    wl_base = __shfl(wl_base, wl_leader);
+    if (has) {
+      const int64_t at = (int64_t)r * a.wl.cap + wl_base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+      a.wl.items[at] = make_float4(x0, x1, x2, __int_as_float((int)p));
+      a.wl.aux[at] = gs;
+    }
+  }
+#else
   {
     // one atomic per distinct group of the wave: consecutive samples of a ray share probe blocks,
     // and same-address atomics of one instruction serialise in L2 (slots: base + rank among the peers)
@@ -541,16 +578,21 @@ __global__ __launch_bounds__(256) void k_gather_probe(GatherArgs a) {
   probe_fill(a, r0, nrow, p, has, s_has, false);
 #endif
   wl_append(a.wl, has, make_float4(x0, x1, x2, __int_as_float((int)p)), gs);
+#endif
 }
 
-// work items -> the grouped list: grouped[gstart[group] + slot]
+// work items -> the grouped list: grouped[gstart[group] + slot].  kScatterStride blocks per
+// sub-list stride over its filled part (a block per 256-item chunk of the capacity launched ~52k
+// blocks for the bench scene, three quarters of them empty: 57 us)
+constexpr int kScatterStride = 16;
 __global__ __launch_bounds__(256) void k_group_scatter(GatherArgs a) {
   const int r = (int)(blockIdx.x % kLists);
-  const int64_t i = (int64_t)(blockIdx.x / kLists) * 256 + threadIdx.x;
-  if (i >= (int64_t)a.wl.cnt[r * 32]) return;
-  const int64_t at = (int64_t)r * a.wl.cap + i;
-  const int2 gs = a.wl.aux[at];
-  a.grouped[a.gstart[gs.x] + gs.y] = a.wl.items[at];
+  const int64_t n = (int64_t)a.wl.cnt[r * 32];
+  for (int64_t i = (int64_t)(blockIdx.x / kLists) * 256 + threadIdx.x; i < n; i += kScatterStride * 256) {
+    const int64_t at = (int64_t)r * a.wl.cap + i;
+    const int2 gs = a.wl.aux[at];
+    a.grouped[a.gstart[gs.x] + gs.y] = a.wl.items[at];
+  }
 }
 
 // one network stage: key <- min(key, kn), return max(key, kn); key is updated in place (a tied
@@ -570,8 +612,8 @@ __device__ __forceinline__ double kstage(double& key, double kn) {
 // memory, a candidate costs one global load per block instead of one per sample.
 constexpr int kCandBatch = 128;
 struct SearchLds {
-  float4 cand[kCandBatch];   // staged candidate points (x, y, z, index bits)
-  uint8_t tag[kCandBatch];   // probe cell n | 8 if its bucket collides
+  float4 cand[kCandBatch + 1];   // staged candidate points (x, y, z, index bits) + pair padding
+  uint8_t tag[kCandBatch + 1];   // probe cell n | 8 if its bucket collides
   int32_t idx[64 * PNR_MAX_K];
   float w[64 * PNR_MAX_K];
   int32_t row[64];
@@ -644,6 +686,29 @@ __global__ __launch_bounds__(64, PNR_SEARCH_WAVES) void k_gather_search(GatherAr
         cf[n] = __builtin_amdgcn_readlane(fl, n);
       }
       const int total = ce[7];
+      // no colliding bucket among the 8 (the common case): no tag reads, no per-point cell test
+      const bool coll_any = ((cf[0] | cf[1] | cf[2] | cf[3] | cf[4] | cf[5] | cf[6] | cf[7]) & 8) != 0;
+      auto visit = [&](const float4& qv, int tg, bool coll) {
+        const float d0 = x0 - qv.x, d1 = x1 - qv.y, d2 = x2 - qv.z;
+        const float dd = (d0 * d0 + d1 * d1) + d2 * d2;
+        bool ok;
+        if (KER == PNR_GATHER_IDW) ok = dd <= a.r2;
+        else ok = fabsf(d0) < a.h0 && fabsf(d1) < a.h1 && fabsf(d2) < a.h2;
+        ok = ok && member;
+        if (coll && (tg & 8)) {  // colliding bucket: the point must lie in this probe cell
+          ok = ok && cell_coord(qv.x, a.g.o0, a.g.inv) == lbx + (tg & 1) &&
+               cell_coord(qv.y, a.g.o1, a.g.inv) == lby + ((tg >> 1) & 1) &&
+               cell_coord(qv.z, a.g.o2, a.g.inv) == lbz + ((tg >> 2) & 1);
+        }
+        if (__ballot(ok) == 0) return;  // nobody keeps it: the network would be a no-op
+        double kn = ok ? pack_key(dd, __float_as_int(qv.w)) : kInf;
+#if defined(PNR_EXP_NONET)  // experiment (wrong results, timing only): one stage instead of the network
+        kn = kstage(key[0], kn);
+#else
+#pragma unroll
+        for (int t = 0; t < PNR_MAX_K; ++t) kn = kstage(key[t], kn);
+#endif
+      };
       for (int base = 0; base < total; base += kCandBatch) {
         const int cnt = total - base < kCandBatch ? total - base : kCandBatch;
 #pragma unroll
@@ -659,31 +724,25 @@ __global__ __launch_bounds__(64, PNR_SEARCH_WAVES) void k_gather_search(GatherAr
             }
             L.cand[j] = a.sorted[src];
             L.tag[j] = (uint8_t)tg;
+          } else if (j == cnt) {  // pair padding: a point no sample reaches (d2 = inf, never kept)
+            const float inf = __int_as_float(0x7F800000);
+            L.cand[j] = make_float4(inf, inf, inf, 0.f);
+            L.tag[j] = 0;
           }
         }
         __syncthreads();
-        for (int j = 0; j < cnt; ++j) {
-          const float4 qv = L.cand[j];
-          const float d0 = x0 - qv.x, d1 = x1 - qv.y, d2 = x2 - qv.z;
-          const float dd = (d0 * d0 + d1 * d1) + d2 * d2;
-          bool ok;
-          if (KER == PNR_GATHER_IDW) ok = dd <= a.r2;
-          else ok = fabsf(d0) < a.h0 && fabsf(d1) < a.h1 && fabsf(d2) < a.h2;
-          ok = ok && member;
-          const int tg = L.tag[j];
-          if (tg & 8) {  // colliding bucket: the point must lie in this probe cell
-            ok = ok && cell_coord(qv.x, a.g.o0, a.g.inv) == lbx + (tg & 1) &&
-                 cell_coord(qv.y, a.g.o1, a.g.inv) == lby + ((tg >> 1) & 1) &&
-                 cell_coord(qv.z, a.g.o2, a.g.inv) == lbz + ((tg >> 2) & 1);
+#if !defined(PNR_SEARCH_SERIAL)
+        if (!coll_any) {
+          // two candidates per trip: both LDS reads in flight before the first test
+          for (int j = 0; j < cnt; j += 2) {
+            const float4 q0 = L.cand[j], q1 = L.cand[j + 1];
+            visit(q0, 0, false);
+            visit(q1, 0, false);
           }
-          if (__ballot(ok) == 0) continue;  // nobody keeps it: the network would be a no-op
-          double kn = ok ? pack_key(dd, __float_as_int(qv.w)) : kInf;
-#if defined(PNR_EXP_NONET)  // experiment (wrong results, timing only): one stage instead of the network
-          kn = kstage(key[0], kn);
-#else
-#pragma unroll
-          for (int t = 0; t < PNR_MAX_K; ++t) kn = kstage(key[t], kn);
+        } else
 #endif
+        {
+          for (int j = 0; j < cnt; ++j) visit(L.cand[j], L.tag[j], true);
         }
         __syncthreads();  // the next batch overwrites the staged list
       }
@@ -1086,7 +1145,7 @@ int launch_gather(const pnr_points& pts, const PointSrc& src, int mode, int64_t 
   gather_probe(mode, dim3((unsigned)((rows + 255) / 256)), st, a);
   int rc = scan_exclusive(a.gcnt, gv.gstart, G, gv.scratch, st);
   if (rc) return rc;
-  hipLaunchKernelGGL(k_group_scatter, dim3((unsigned)(kLists * ((a.wl.cap + 255) / 256))), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(k_group_scatter, dim3((unsigned)(kLists * kScatterStride)), dim3(256), 0, st, a);
   const int64_t tasks = (P + 63) / 64;  // upper bound on the chunks (the kernel reads the real count)
   if (pts.mode == PNR_GATHER_IDW) {
     auto kern = k_gather_search<PNR_GATHER_IDW>;

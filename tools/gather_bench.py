@@ -39,8 +39,11 @@ def main():
     ap.add_argument('--k', type=int, default=8)
     ap.add_argument('--mode', default='idw')
     ap.add_argument('--reps', type=int, default=5)
+    ap.add_argument('--lib', default=None, help='load this libpnr.so build instead (experiments)')
     args = ap.parse_args()
     import pnr
+    if args.lib:
+        pnr._lib.load(os.path.abspath(args.lib))
     from pnr._lib import timing_read
     dev = torch.device('cuda:0')
     lib = pnr.library()
