@@ -240,6 +240,25 @@ def cpu_threads():
     return max(1, n)
 
 
+def host_cpus():
+    """What the CPU baseline's `cores` is drawn from: torch's pool, the CPUs this process may run on
+    (sched_getaffinity), and the machine's physical / logical counts (psutil, when importable).
+    On the GPU box the affinity set is the whole machine while the job's share is 16 CPUs
+    (OMP_NUM_THREADS), so `cores` is the pool size, not the affinity count."""
+    h = {'torch_threads': torch.get_num_threads(), 'omp_num_threads': os.environ.get('OMP_NUM_THREADS')}
+    try:
+        h['affinity_cpus'] = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        pass
+    try:
+        import psutil
+        h['physical_cores'] = psutil.cpu_count(logical=False)
+        h['logical_cpus'] = psutil.cpu_count(logical=True)
+    except ImportError:
+        pass
+    return h
+
+
 def cpu_baseline(bound, pose, params, workload, gpu_render=None, reps=5):
     """The oracle (oracle/ref_render.py, a bit-exact restatement of the reference CPU path pinned
     by tests/test_oracle_golden.py) timed on this host on a bounded sample, median of `reps` after
@@ -285,7 +304,7 @@ def cpu_baseline(bound, pose, params, workload, gpu_render=None, reps=5):
     out = {'value': round(v_all, 1), 'unit': 'rays/s', 'cores': cores, 'kind': 'port',
            'sample': f'{what} on {sizes[0]} rays ({cores} threads) and {sizes[1]} rays (1 thread), oracle (torch '
                      f'CPU restatement of src/utils/Renderer.py), median of {reps} after 1 warm-up',
-           'value_1thread': round(v_one, 1)}
+           'value_1thread': round(v_one, 1), 'host': host_cpus()}
     if gpu_render is not None:
         ro, rd, gt, col = [t.cpu() for t in synth_batch(2048, 0, pose, 'cpu', seed=7)]
         with torch.no_grad():

@@ -772,14 +772,31 @@ __global__ __launch_bounds__(64, PNR_SEARCH_WAVES) void k_gather_search(GatherAr
       W = W + w;
     }
     const float Wd = W > 0.f ? W : 1.0f;
-    L.row[lane] = row;
+#if !defined(PNR_SEARCH_NOCOMPACT)
+    // feature-sum slots: rows with neighbours first, then rows without (a zero c row, no loads),
+    // then empty lanes, so the feature rounds that wait on loads are only those of the ~half of the
+    // rows that have neighbours; the rest store zeros without a wait
+    int slot, n_live;
+    {
+      const bool hn = row >= 0 && ki[0] >= 0;
+      const uint64_t mn = __ballot(hn), mz = __ballot(row >= 0 && !hn);
+      n_live = (int)__popcll(mn | mz);
+      const uint64_t below = (1ull << lane) - 1ull;
+      if (hn) slot = (int)__popcll(mn & below);
+      else if (row >= 0) slot = (int)__popcll(mn) + (int)__popcll(mz & below);
+      else slot = (int)__popcll(mn) + (int)__popcll(mz) + (int)__popcll(~(mn | mz) & below);
+    }
+#else
+    const int slot = lane, n_live = 64;
+#endif
+    L.row[slot] = row;
     float wnv[PNR_MAX_K];
 #pragma unroll
     for (int t = 0; t < PNR_MAX_K; ++t) {
       const float wn = ki[t] >= 0 ? wv_[t] / Wd : 0.f;
       wnv[t] = wn;
-      L.idx[lane * PNR_MAX_K + t] = ki[t];
-      L.w[lane * PNR_MAX_K + t] = wn;
+      L.idx[slot * PNR_MAX_K + t] = ki[t];
+      L.w[slot * PNR_MAX_K + t] = wn;
     }
     if (row >= 0 && a.idx) {
       // k = 8: the row's 8 indices and 8 weights as 16-B stores
@@ -805,6 +822,7 @@ __global__ __launch_bounds__(64, PNR_SEARCH_WAVES) void k_gather_search(GatherAr
     // Measured (tools/gather_bench.py, 13.5M samples): 1 row per round 1.22 ms, 2 rows 1.13 ms.
 #pragma unroll 1
     for (int rr = 0; rr < 8; rr += PNR_FEAT_ROWS) {
+      if (rr * 8 >= n_live) break;  // the remaining slots are empty lanes
       int rw[PNR_FEAT_ROWS];
       float4 f[PNR_FEAT_ROWS][PNR_MAX_K];
 #pragma unroll
