@@ -178,6 +178,64 @@ def test_gather_many_tasks_per_block(pnr_mod, dev):
     close(c[sel.to(dev)], c_ref, 1e-5 * c_ref.abs().max().item(), 'c')
 
 
+def _gather_c_abi(pnr_mod, dev, pts, q, k):
+    import ctypes
+    lib = pnr_mod.library()
+    P = q.shape[0]
+    c = torch.full((P, 32), float('nan'), device=dev)
+    idx = torch.full((P, k), -7, device=dev, dtype=torch.int32)
+    w = torch.full((P, k), float('nan'), device=dev)
+    qd = q.to(dev)
+    s, _ = pts.descriptor()
+    ws = torch.empty(lib.pnr_point_gather_workspace_bytes(P), dtype=torch.uint8, device=dev)
+    assert lib.pnr_point_gather(ctypes.byref(s), qd.data_ptr(), P, c.data_ptr(), idx.data_ptr(), w.data_ptr(),
+                                ws.data_ptr(), ws.numel(), None) == 0
+    torch.cuda.synchronize()
+    return c, idx, w
+
+
+def test_gather_dense_cluster_many_candidate_batches(pnr_mod, dev):
+    """4,000 points in a 3 cm cube with a 1 cm radius: a probe block holds far more than the
+    search's 128-candidate LDS batch, so every segment runs several batches and an odd remainder
+    (the paired scan's padding entry)."""
+    gen = torch.Generator().manual_seed(21)
+    xyz = 0.5 + 0.03 * torch.rand((4000, 3), generator=gen)
+    feats = torch.randn((4000, 32), generator=gen) * 0.5
+    q = (0.5 + 0.03 * torch.rand((2048, 3), generator=gen) + 0.004 * torch.randn((2048, 3), generator=gen)).double()
+    pts = pnr_mod.NeuralPoints(xyz.to(dev), feats.to(dev), mode='idw', radius=0.01, k=8).to(dev)
+    c, idx, w = _gather_c_abi(pnr_mod, dev, pts, q, 8)
+    c_ref, idx_ref, w_ref = RP.point_gather(q, xyz, feats, 'idw', radius=0.01, k=8, return_idx=True)
+    assert (idx_ref[:, 7] >= 0).float().mean() > 0.5, 'most samples keep a full neighbourhood'
+    assert np.array_equal(idx.cpu().numpy(), idx_ref.numpy().astype(np.int32))
+    close(w, w_ref, 1e-6, 'weights')
+    close(c, c_ref, 1e-5 * c_ref.abs().max().item(), 'c')
+
+
+def test_gather_lattice_ties_break_by_index(pnr_mod, dev):
+    """Exact distance ties: dyadic lattice points (spacing 1/64) under a random index permutation,
+    queries at cube centres (8 equidistant corners) and on edge midpoints (2 equidistant), k = 3:
+    the kept neighbours are the lowest point indices among the tied ones, as the oracle's stable
+    sort on (d2, index) keeps them, whatever order the hash buckets list them in."""
+    gen = torch.Generator().manual_seed(22)
+    n = 16
+    ii = torch.stack(torch.meshgrid(torch.arange(n), torch.arange(n), torch.arange(n), indexing='ij'), -1).reshape(-1, 3)
+    perm = torch.randperm(ii.shape[0], generator=gen)
+    xyz = (ii[perm].float() / 64.0)
+    feats = torch.randn((xyz.shape[0], 32), generator=gen)
+    cc = torch.randint(1, n - 2, (1024, 3), generator=gen).double()
+    centres = (cc + 0.5) / 64.0
+    edges = (cc + torch.tensor([0.5, 0.0, 0.0], dtype=torch.float64)) / 64.0
+    q = torch.cat([centres, edges])
+    r = 0.0141  # > sqrt(3)/128 (the 8 corners of a centre), < the next shell
+    pts = pnr_mod.NeuralPoints(xyz.to(dev), feats.to(dev), mode='idw', radius=r, k=3).to(dev)
+    c, idx, w = _gather_c_abi(pnr_mod, dev, pts, q, 3)
+    c_ref, idx_ref, w_ref = RP.point_gather(q, xyz, feats, 'idw', radius=r, k=3, return_idx=True)
+    assert (idx_ref[:1024] >= 0).all(), 'every centre keeps 3 of its 8 tied corners'
+    assert np.array_equal(idx.cpu().numpy(), idx_ref.numpy().astype(np.int32))
+    close(w, w_ref, 1e-6, 'weights')
+    close(c, c_ref, 1e-5 * c_ref.abs().max().item(), 'c')
+
+
 def test_gather_backward_matches_oracle(pnr_mod, dev):
     xyz, feats, q = random_cloud(seed=5)
     pts = pnr_mod.NeuralPoints(xyz.to(dev), feats.to(dev), mode='idw', radius=0.06, k=8).to(dev)
