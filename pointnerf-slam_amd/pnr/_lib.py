@@ -12,7 +12,8 @@ import threading
 
 import torch
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'libpnr.so')
+# PNR_LIB_PATH: an experiment build (tools/xbuild.sh) to run the tests against instead
+LIB_PATH = os.environ.get('PNR_LIB_PATH') or os.path.join(os.path.dirname(os.path.abspath(__file__)), 'libpnr.so')
 MAX_SAMPLES = 64
 N_PARAMS = 11
 N_FC_PARAMS = 8
