@@ -861,6 +861,7 @@ __global__ __launch_bounds__(64, PNR_SEARCH_WAVES) void k_gather_search(GatherAr
 #else
     for (int rr = 0; rr < 8; ++rr) {
 #endif
+      if (rr * 8 >= n_live) break;  // the remaining slots are empty lanes
       const int sl = rr * 8 + gq;
       const int rw = L.row[sl];
       if (rw < 0) continue;
