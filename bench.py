@@ -88,17 +88,17 @@ def synth_batch(n, rank, pose, dev, seed=0):
 
 
 def pmc_traffic(kernel, units_per_launch):
-    """HBM bytes per launch of `kernel` from the newest committed PMC measurement
-    (profiles/r*_traffic.json, written from tools/prof_bench.sh's FETCH_SIZE/WRITE_SIZE passes):
-    measured bytes per unit x units per launch, or None."""
+    """HBM bytes per launch of `kernel` from the newest committed PMC measurement that holds it
+    (profiles/r*_traffic.json, written by tools/traffic_json.py from separate FETCH_SIZE / WRITE_SIZE
+    rocprofv3 passes): measured bytes per unit x units per launch, or None.  Files are ordered by
+    name (round, then pass letter); a newer file measuring other kernels does not hide an older
+    measurement of this one."""
     import glob
-    files = sorted(glob.glob(os.path.join(REPO, 'profiles', 'r*_traffic.json')))
-    if not files:
-        return None
-    t = json.load(open(files[-1])).get(kernel)
-    if not t:
-        return None
-    return round((t['fetch_B'] + t['write_B']) * units_per_launch)
+    for f in sorted(glob.glob(os.path.join(REPO, 'profiles', 'r*_traffic.json')), reverse=True):
+        t = json.load(open(f)).get(kernel)
+        if t:
+            return round((t['fetch_B'] + t['write_B']) * units_per_launch)
+    return None
 
 
 def neural_point_scene(dev, voxel=0.001, n_rays=W * H, seed=0):
@@ -188,33 +188,44 @@ def gather_roofline(dev, voxel=0.001, k=8, reps=5, feat_dtype='float32'):
     avg = ms / launches
     byt = gather_bytes(P, probed, nb, k, feat_bytes=64 if feat_dtype == 'float16' else 128)
     gbs = byt / (avg * 1e-3) / 1e9
-    # backward, the Mapper's form (feature gradients only: dL/df_i += w_k dL/dc, float atomics)
+    # backward, the Mapper's form (feature gradients only: dL/df_i += w_k dL/dc), deterministic: exact
+    # int64 fixed-point terms added by 64-bit integer atomics, converted once into g_feats (ABI 10)
     gf = torch.zeros_like(feats)
     gc = torch.randn_like(c)
     sb, _ = pts.descriptor(g_feats=gf)
+    bws = torch.empty(lib.pnr_point_gather_bwd_workspace_bytes(ctypes.byref(sb), P), dtype=torch.uint8, device=dev)
     rows = int((idx[:, 0] >= 0).sum().item())
     lib.pnr_timing_enable(1)
     timing_read(5)
     for _ in range(reps):
         pnr._lib.check(lib.pnr_point_gather_bwd(ctypes.byref(sb), p.data_ptr(), P, idx.data_ptr(), w.data_ptr(),
-                                                c.data_ptr(), gc.data_ptr(), None, ws.data_ptr(), ws.numel(), st),
+                                                c.data_ptr(), gc.data_ptr(), None, bws.data_ptr(), bws.numel(), st),
                        'point_gather_bwd')
     torch.cuda.synchronize()
     lib.pnr_timing_enable(0)
     bl, bms, _ = timing_read(5)
     bavg = bms / bl
-    # per sample 4 B (its first neighbour index); per row with neighbours 128 B g_c + k x 8 B idx/w;
-    # per neighbour 128 B of feature-gradient float atomics
-    b_hbm = P * 4 + rows * (128 + k * 8)
-    b_atomic = nb * 128
+    n_instr = ctypes.c_int64(0)
+    pnr._lib.check(lib.pnr_point_gather_bwd_atomics(ctypes.byref(sb), bws.data_ptr(), P, ctypes.byref(n_instr), st),
+                   'gather_bwd_atomics')
+    M = int(xyz.shape[0])
+    # HBM: per sample 4 B (its first neighbour index, the probe); per row with neighbours 128 B g_c
+    # read twice (max |g_c| pass, then the sums) + k x 8 B idx/w; the accumulators zeroed (M x 256 B),
+    # read once and the features' gradient read + written by the conversion (M x (256 + 256) B).
+    # Atomics: the 64-bit add instructions the kernel counted as it issued them (256 B each: 32 lanes x 8 B;
+    # shared neighbours are carried between a ray's rows, so far fewer go out than rows x neighbours)
+    b_hbm = P * 4 + rows * (2 * 128 + k * 8) + M * (256 + 256 + 256)
+    b_atomic = int(n_instr.value) * 256
     t_floor = (b_hbm / (HBM_PEAK_GBS * 1e9) + b_atomic / 1.3e12) * 1e3
-    bwd = {'kernel': 'k_gather_bwd_probe+k_gather_bwd (feature gradients, the Mapper case)',
-           'avg_launch_ms': round(bavg, 4), 'bytes_hbm': b_hbm, 'bytes_atomic': b_atomic, 'rows': rows,
+    bwd = {'kernel': 'k_gather_bwd_probe + k_gather_bwd_gmax + k_gather_bwd + k_gather_bwd_fin (feature gradients, '
+                     'the Mapper case; deterministic int64 fixed point)',
+           'avg_launch_ms': round(bavg, 4), 'bytes_hbm': b_hbm, 'bytes_atomic_issued': b_atomic,
+           'atomic_instructions': int(n_instr.value), 'neighbour_terms': nb, 'rows': rows,
            'achieved_gbs': round((b_hbm + b_atomic) / (bavg * 1e-3) / 1e9, 1),
            'floor_ms': round(t_floor, 4), 'frac_of_floor': round(t_floor / bavg, 4),
-           'floor_basis': 'HBM bytes at 8 TB/s + feature-gradient atomic bytes at the 1.3 TB/s chip-wide float-'
-                          'atomic rate (MI355X_MICROARCH.md); neighbours shared with the previous row are carried, '
-                          'so fewer atomics are issued than counted'}
+           'floor_basis': 'HBM bytes at 8 TB/s + the issued 64-bit atomic bytes (counted in the kernel) at the '
+                          '1.3 TB/s chip-wide atomic byte rate MI355X_MICROARCH.md measured for 32-bit float '
+                          'atomics (64-B memory-side requests; assumed the same byte rate for 64-bit integer adds)'}
     return {'bound': 'hbm', 'achieved': round(gbs, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
             'frac': round(gbs / HBM_PEAK_GBS, 4),
             # PMC bytes per sample were measured on the float32-feature gather only

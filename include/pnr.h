@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define PNR_ABI_VERSION 9
+#define PNR_ABI_VERSION 10
 #define PNR_N_PARAMS 11
 #define PNR_MAX_SAMPLES 64      /* N_samples + N_importance per ray */
 #define PNR_C_DIM 32            /* neural-point feature width (decoder.py:122-125 fc_c input) */
@@ -190,9 +190,19 @@ size_t pnr_point_gather_workspace_bytes(int64_t P);
 int pnr_point_gather(const pnr_points* pts, const double* p, int64_t P, float* c, int32_t* idx, float* w,
                      void* ws, size_t ws_bytes, void* stream);
 /* Backward of pnr_point_gather: g_c (P,32) -> pts->g_feats (+=, when non-NULL) and g_p (P,3)
- * (written, when non-NULL: dL/dp through the weights).  ws as for pnr_point_gather. */
+ * (written, when non-NULL: dL/dp through the weights).  ws: pnr_point_gather_bwd_workspace_bytes
+ * (ABI 10).  The feature gradient is DETERMINISTIC (ABI 10): every term w_k dL/dc is rounded once to
+ * an int64 multiple of 2^-s (s from max |dL/dc| of the call and the guard bits ceil(log2(P+1)), so
+ * no sum overflows), the terms are added exactly with 64-bit integer atomics, and the sum is
+ * converted once into g_feats.  Any order of the additions gives the same bits.  The absolute error
+ * of an element is at most (its term count) x 2^-(63 - guard) x max |dL/dc|: fp32-class for any
+ * element above ~2^-14 of the largest term.  A non-finite dL/dc makes every g_feats element NaN. */
+size_t pnr_point_gather_bwd_workspace_bytes(const pnr_points* pts, int64_t P);
 int pnr_point_gather_bwd(const pnr_points* pts, const double* p, int64_t P, const int32_t* idx, const float* w,
                          const float* c, const float* g_c, float* g_p, void* ws, size_t ws_bytes, void* stream);
+/* Diagnostics (ABI 10): the 64-bit atomic add instructions (32 lanes x 8 B = 256 B each) the last
+ * pnr_point_gather_bwd with workspace `ws` issued (synchronises `stream`). */
+int pnr_point_gather_bwd_atomics(const pnr_points* pts, const void* ws, int64_t P, int64_t* n_instr, void* stream);
 /* fc_c weight image of the decoder (MLP(c_dim=32)): fc_params = host array of the 8 tensors
  * fc_c.0.weight, fc_c.0.bias, ..., fc_c.3.bias (contiguous float32). */
 size_t pnr_fc_packed_floats(void);

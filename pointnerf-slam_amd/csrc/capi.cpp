@@ -156,9 +156,12 @@ SaveArgs carve_save(Carver& c, int64_t ld, int prec, bool acts = true) {
   SaveArgs s{};
   s.ld = ld;
   s.p0 = 0;
-  // mode 2: hP = eP = NULL, which tells the split forward to store masks and inputs only; e is saved
-  // by the fp32 forward only (the split dW0 GEMM recomputes it from x)
-  s.eP = acts && prec == PNR_PREC_FP32 ? c.take<float>(kFourierPad * ld) : nullptr;
+  // mode 2: hP = eP = NULL, which tells the split forward to store masks and inputs only.  e is
+  // written by the fp32 forward only (the split dW0 GEMM recomputes it from x), but its region is
+  // carved in every precision so that the layout does not depend on the precision: a forward and a
+  // backward called with different precisions still find hP / xP / masks at the same offsets
+  (void)prec;
+  s.eP = acts ? c.take<float>(kFourierPad * ld) : nullptr;
   s.hP = acts ? c.take<float>((size_t)4 * kHidden * ld) : nullptr;
   s.xP = c.take<float4>(ld);
   s.masks = c.take<uint4>((size_t)4 * (ld / 32) * 64);
@@ -206,7 +209,8 @@ struct BwdWS {
 };
 
 // wgrad: weight gradients may be asked for (the partial tiles of the weight-gradient GEMMs)
-BwdWS carve_bwd(int64_t P, int64_t n, void* ws, size_t* bytes, bool feat, bool wgrad) {
+// M: neural points of the call (the gather backward's int64 feature accumulators), 0 without
+BwdWS carve_bwd(int64_t P, int64_t n, void* ws, size_t* bytes, bool feat, bool wgrad, int64_t M = 0) {
   Carver c(ws);
   BwdWS b{};
   b.C = P < kBwdChunk ? ((P + 127) / 128) * 128 : kBwdChunk;
@@ -216,19 +220,20 @@ BwdWS carve_bwd(int64_t P, int64_t n, void* ws, size_t* bytes, bool feat, bool w
   b.g_nrm = c.take<float>(n);
   b.dP = c.take<float>((size_t)4 * kHidden * b.C);
   b.gargP = c.take<float>(kFourierPad * b.C);
-  if (wgrad) {
-    b.part = c.take<float>(kWgradPartFloats);
-    b.part_bias = c.take<float>(kWgradPartBiasFloats);
+  if (wgrad) {  // sized from the chunk: the GEMM grids of a small backward are small
+    b.part = c.take<float>(wgrad_part_floats(b.C));
+    b.part_bias = c.take<float>(wgrad_part_bias_floats(b.C));
   }
   if (feat) {
     b.gH = c.take<float>((size_t)4 * kHidden * b.C);
     b.g_c = c.take<float>((size_t)P * kCDim);
-    b.gws_bytes = gather_workspace_bytes(P);
+    b.gws_bytes = gather_bwd_workspace_bytes(P, M, true);
     b.gws = c.take<char>(b.gws_bytes);
   }
   if (bytes) *bytes = c.off;
   return b;
 }
+int64_t n_pts(const pnr_render_params* prm) { return prm->points ? prm->points->n_points : 0; }
 
 // fc_c side of the backward: image, per-row features and the 8 accumulated fc_c grads
 struct FeatBwd {
@@ -565,7 +570,7 @@ size_t pnr_render_bwd_workspace_bytes(const pnr_render_params* prm, int64_t n_ra
   if (!valid_prm(prm) || n_rays < 0) return 0;
   size_t b = 0;
   carve_bwd(pad128(n_rays * prm->n_samples) + pad128(n_rays * prm->n_importance), n_rays, nullptr, &b,
-            prm->points != nullptr, save_mode(prm) != 2);
+            prm->points != nullptr, save_mode(prm) != 2, n_pts(prm));
   return b;
 }
 
@@ -589,7 +594,7 @@ int pnr_render_bwd(const pnr_render_params* prm, const float* packed, const floa
   const int S = prm->n_samples, I = prm->n_importance;
   const int64_t ld = w.save.ld;
   const pnr_points* pts = prm->points;
-  BwdWS b = carve_bwd(ld, n, bwd_ws, &bneed, pts != nullptr, save_mode(prm) != 2);
+  BwdWS b = carve_bwd(ld, n, bwd_ws, &bneed, pts != nullptr, save_mode(prm) != 2, n_pts(prm));
   if (ws_bytes < need || bwd_bytes < bneed) return PNR_E_WORKSPACE;
   hipStream_t st = (hipStream_t)stream;
   const double* zi = w.z + n * S;
@@ -690,7 +695,8 @@ int pnr_regulation_fwd(const pnr_render_params* prm, const float* packed, const 
 size_t pnr_regulation_bwd_workspace_bytes(const pnr_render_params* prm, int64_t n_rays) {
   if (!valid_prm(prm) || n_rays < 0) return 0;
   size_t b = 0;
-  carve_bwd(pad128(n_rays * prm->n_samples), n_rays, nullptr, &b, prm->points != nullptr, save_mode(prm) != 2);
+  carve_bwd(pad128(n_rays * prm->n_samples), n_rays, nullptr, &b, prm->points != nullptr, save_mode(prm) != 2,
+            n_pts(prm));
   return b;
 }
 
@@ -714,7 +720,7 @@ int pnr_regulation_bwd(const pnr_render_params* prm, const float* packed, const 
   const int64_t P = n * prm->n_samples;
   const int64_t ld = w.save.ld;
   const pnr_points* pts = prm->points;
-  BwdWS b = carve_bwd(ld, n, bwd_ws, &bneed, pts != nullptr, save_mode(prm) != 2);
+  BwdWS b = carve_bwd(ld, n, bwd_ws, &bneed, pts != nullptr, save_mode(prm) != 2, n_pts(prm));
   if (ws_bytes < need || bwd_bytes < bneed) return PNR_E_WORKSPACE;
   hipStream_t st = (hipStream_t)stream;
   int rc = launch_gout_sigma(g_sigma, w.save.xP, P, ld, b.g_out, st);  // (zeros on the padding rows)
@@ -755,6 +761,19 @@ int pnr_point_gather(const pnr_points* pts, const double* p, int64_t P, float* c
   PointSrc s{};
   s.pts = p;
   return launch_gather(*pts, s, kPtsF64, P, P, c, idx, w, ws, ws_bytes, (hipStream_t)stream);
+}
+
+size_t pnr_point_gather_bwd_workspace_bytes(const pnr_points* pts, int64_t P) {
+  if (!pts || P < 0 || pts->n_points < 0) return 0;
+  return gather_bwd_workspace_bytes(P, pts->n_points, true);
+}
+
+int pnr_point_gather_bwd_atomics(const pnr_points* pts, const void* ws, int64_t P, int64_t* n_instr, void* stream) {
+  if (!pts || !ws || P < 0 || !n_instr) return PNR_E_ARG;
+  unsigned long long n = 0;
+  const int rc = gather_bwd_atomics(ws, P, pts->n_points, &n, (hipStream_t)stream);
+  *n_instr = (int64_t)n;
+  return rc;
 }
 
 int pnr_point_gather_bwd(const pnr_points* pts, const double* p, int64_t P, const int32_t* idx, const float* w,

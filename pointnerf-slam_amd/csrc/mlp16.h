@@ -727,6 +727,9 @@ static __device__ __forceinline__ void fwd16_tile(const BfFwdArgs& a, int mode, 
 #pragma unroll
       for (int r = 0; r < 16; ++r) cv[r] *= sc;
       S.cinv = 1.f / sc;
+      // the scaled features are split into f16 parts too: pt_scale stops at 2^-100, so a feature
+      // above ~2^114 would still overflow -- the range check covers them (PNR_STATUS_F16_RANGE)
+      S.vmax = m * sc;
     }
     split_tile<PR>(cv, S.ct);
   }

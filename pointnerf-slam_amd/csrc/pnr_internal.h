@@ -225,6 +225,10 @@ int launch_gather(const pnr_points& pts, const PointSrc& src, int mode, int64_t 
 int launch_gather_bwd(const pnr_points& pts, const PointSrc* src, int mode, const float4* xP, int64_t P,
                       const int32_t* idx, const float* w, const float* c, const float* g_c, float* g_p,
                       bool gp_accum, void* ws, size_t ws_bytes, hipStream_t st);
+// backward workspace: work list + control block + (feats) int64 feature accumulators [M][32]
+size_t gather_bwd_workspace_bytes(int64_t P, int64_t M, bool feats);
+// 64-bit atomic instructions issued by the last backward on `ws` (synchronises st)
+int gather_bwd_atomics(const void* ws, int64_t P, int64_t M, unsigned long long* n, hipStream_t st);
 
 // weight-gradient GEMM shapes (wgrad.hip): C[MA][NB] += A[K][WA]^T B[K][WB]
 enum WgradKind : int {
@@ -242,7 +246,7 @@ struct WgradSyn {
   const float* wo;      // Wo [4][256] fp32
   const float4* xP;     // kWgradFirstX: saved inputs of the chunk rows
   const float* fb;      // kWgradFirstX: Fourier B padded [3][96] (packed + kOffFB)
-  // every kind: per-workgroup partial tiles (kWgradPartFloats + kWgradPartBiasFloats of scratch),
+  // every kind: per-workgroup partial tiles (wgrad_part_floats + wgrad_part_bias_floats of scratch),
   // added into C / bias in a fixed order by k_part_reduce -- no float atomics, deterministic
   float* part;
   float* part_bias;
@@ -288,13 +292,28 @@ constexpr int kWgrad16MaxWg = 256;  // split k_wgrad16 grid cap
 constexpr int kSkinnyMaxWg = 1024;  // k_wgrad_skinny grid cap
 // split backward: every GEMM of a chunk keeps its own partial region until ONE reduce launch adds them
 // all (W3 / W2 / W1 256 x 256, W0 256 x 96, fc_c 4 x 256 x 32, Wo 4 x 256, B 3 x 93)
-constexpr int64_t kWgrad16PartFloats = (int64_t)kWgrad16MaxWg * 256 * (3 * 256 + 96 + 4 * 32) +
-                                       (int64_t)kSkinnyMaxWg * (4 * 256 + 3 * 93);
-constexpr int64_t kWgrad16PartBiasFloats = (int64_t)kWgrad16MaxWg * 256 * 8 + (int64_t)kSkinnyMaxWg * 4;
-constexpr int64_t kWgradPartFloats = kWgrad16PartFloats > (int64_t)kWgradMaxWg * 256 * 256
-                                         ? kWgrad16PartFloats : (int64_t)kWgradMaxWg * 256 * 256;
-constexpr int64_t kWgradPartBiasFloats = kWgrad16PartBiasFloats > (int64_t)kWgradMaxWg * 256
-                                             ? kWgrad16PartBiasFloats : (int64_t)kWgradMaxWg * 256;
+// Workgroup counts of one chunk of C points (upper bounds of the grids wgrad16_prepare, skinny_blocks
+// and wgrad.hip pick_ks choose for K = C), from which the partial scratch is sized
+__host__ __device__ constexpr int64_t wgrad16_nwg_max(int64_t C) {
+  return ((C + 31) / 32 + 7) / 8 < 4 ? 4 : (((C + 31) / 32 + 7) / 8 > kWgrad16MaxWg ? kWgrad16MaxWg : ((C + 31) / 32 + 7) / 8);
+}
+__host__ __device__ constexpr int64_t skinny_nwg_max(int64_t C) {
+  return (C + 255) / 256 < kSkinnyMaxWg ? (C + 255) / 256 : kSkinnyMaxWg;
+}
+__host__ __device__ constexpr int64_t wgrad32_nwg_max(int64_t C) {
+  return (C + 255) / 256 < kWgradMaxWg ? (C + 255) / 256 : kWgradMaxWg;
+}
+constexpr int64_t wgrad_part_floats(int64_t C) {
+  return wgrad16_nwg_max(C) * 256 * (3 * 256 + 96 + 4 * 32) + skinny_nwg_max(C) * (4 * 256 + 3 * 93) >
+                 wgrad32_nwg_max(C) * 256 * 256
+             ? wgrad16_nwg_max(C) * 256 * (3 * 256 + 96 + 4 * 32) + skinny_nwg_max(C) * (4 * 256 + 3 * 93)
+             : wgrad32_nwg_max(C) * 256 * 256;
+}
+constexpr int64_t wgrad_part_bias_floats(int64_t C) {
+  return wgrad16_nwg_max(C) * 256 * 8 + skinny_nwg_max(C) * 4 > wgrad32_nwg_max(C) * 256
+             ? wgrad16_nwg_max(C) * 256 * 8 + skinny_nwg_max(C) * 4
+             : wgrad32_nwg_max(C) * 256;
+}
 // C[r][c] += sum_g part[g][r pw + c] (r < nr, c < nb), bias[r] += sum_g pbias[g][r]: fixed order
 int launch_part_reduce(const float* part, const float* pbias, int nwg, int nr, int pw, int nb, float* C, int64_t ldc,
                        float* bias, hipStream_t st);

@@ -914,6 +914,13 @@ struct GatherBwdArgs {
   float* g_p;            // (P,3) or null
   int gp_accum;
   WorkList wl;           // rows with at least one neighbour
+  // Feature gradients in exact fixed point (order-independent, hence deterministic): every term
+  // w dL/dc becomes an int64 multiple of 2^-s, s from max |dL/dc| over the rows and the guard bits
+  // (a sum of <= 2^guard terms never overflows); k_gather_bwd_fin converts once into g_feats
+  long long* facc;       // [M][32] int64 accumulators (zeroed by the launcher)
+  uint32_t* gmax;        // bits of max |dL/dc| over the work list's rows (NaN / inf propagate)
+  unsigned long long* n_flush;  // int64 atomic instructions (256 B each) issued, for the roofline
+  int guard;
 };
 
 // rows with a neighbour (idx[row][0] >= 0: neighbours are stored nearest first) -> work list
@@ -923,13 +930,54 @@ __global__ __launch_bounds__(256) void k_gather_bwd_probe(GatherBwdArgs a) {
   wl_append(a.wl, has, make_float4(0.f, 0.f, 0.f, __int_as_float((int)p)));
 }
 
+// max |dL/dc| over the rows of the work list (half a wave per row; the integer max of the bits of
+// |x| is the float max, and a NaN row wins it: its bits are the largest)
+__global__ __launch_bounds__(256) void k_gather_bwd_gmax(GatherBwdArgs a) {
+  const int ch = threadIdx.x & 31, half = threadIdx.x >> 5;
+  const int64_t nchunk = (a.wl.cap + 255) / 256;
+  uint32_t m = 0u;
+  for (int64_t task = blockIdx.x; task < kLists * nchunk; task += gridDim.x) {
+    const int rl = (int)(task % kLists);
+    const int64_t j0 = task / kLists * 256;
+    const int64_t n_work = (int64_t)a.wl.cnt[rl * 32];
+    if (j0 >= n_work) continue;
+    const int64_t jn = n_work - j0 < 256 ? n_work - j0 : 256;
+#pragma unroll 4
+    for (int64_t t = half; t < jn; t += 8) {
+      const int64_t p = __float_as_int(a.wl.items[rl * a.wl.cap + j0 + t].w);
+      const uint32_t b = __float_as_uint(a.g_c[p * 32 + ch]) & 0x7FFFFFFFu;
+      m = m > b ? m : b;
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint32_t v = (uint32_t)__shfl_xor((int)m, o);
+    m = m > v ? m : v;
+  }
+  if ((threadIdx.x & 63) == 0 && m != 0u) atomicMax(a.gmax, m);
+}
+
+// 2^s of the fixed-point feature gradients: |term| <= max |dL/dc| < 2^e, so |term| 2^s < 2^(62 - guard)
+__device__ __forceinline__ int fx_shift(uint32_t gmax_bits, int guard) {
+  if (gmax_bits == 0u || gmax_bits >= 0x7F800000u) return 0;  // all zero, or non-finite (k_gather_bwd_fin)
+  int e;
+  (void)frexpf(__uint_as_float(gmax_bits), &e);
+  return 62 - guard - e;
+}
+__device__ __forceinline__ long long fx_term(float x, int s) {
+  return (long long)rintf(ldexpf(x, s));  // exact power-of-two scale, one rounding to an integer
+}
+
 // Half a wave per row: lane c owns channel c, so the feature-gradient atomics of one neighbour
-// are ONE instruction per two rows, each row a whole 128-B line (2 full 64-B atomic requests).
+// are ONE instruction per two rows, each row 256 contiguous bytes of int64 (4 full 64-B requests).
 template <int SRC, int KER>
 __global__ __launch_bounds__(256) void k_gather_bwd(GatherBwdArgs a) {
   PNR_FP_STRICT
   const int ch = threadIdx.x & 31, half = threadIdx.x >> 5;  // 8 half-waves per block
   const int64_t nchunk = (a.wl.cap + 255) / 256;
+  const int fs = a.g_feats ? fx_shift(*a.gmax, a.guard) : 0;
+  unsigned long long* facc = reinterpret_cast<unsigned long long*>(a.facc);
+  uint32_t nfl = 0;  // flushes of this half-wave (uniform over it)
   for (int64_t task = blockIdx.x; task < kLists * nchunk; task += gridDim.x) {
     const int rl = (int)(task % kLists);
     const int64_t j0 = task / kLists * 256;
@@ -938,13 +986,14 @@ __global__ __launch_bounds__(256) void k_gather_bwd(GatherBwdArgs a) {
     const int64_t jn = n_work - j0 < 256 ? n_work - j0 : 256;
     // half-wave `half` takes 32 consecutive items: rows of one ray, whose neighbour lists overlap.
     // A neighbour shared with the previous row carries its partial sum forward instead of being
-    // flushed: the atomic goes out when it leaves the list (or at the end of the run).
+    // flushed: the atomic goes out when it leaves the list (or at the end of the run).  Integer
+    // sums: the result does not depend on which rows share a run, nor on the atomics' order.
     int pid[PNR_MAX_K];
-    float pacc[PNR_MAX_K];
+    long long pacc[PNR_MAX_K];
 #pragma unroll
     for (int kk = 0; kk < PNR_MAX_K; ++kk) {
       pid[kk] = -1;
-      pacc[kk] = 0.f;
+      pacc[kk] = 0;
     }
     const int64_t te = 32 * half + 32 < jn ? 32 * half + 32 : jn;
 #pragma unroll 1
@@ -989,19 +1038,22 @@ __global__ __launch_bounds__(256) void k_gather_bwd(GatherBwdArgs a) {
         for (int kk = 0; kk < PNR_MAX_K; ++kk) dots[kk] = g * f[kk];
       }
       if (a.g_feats) {
-        float cur[PNR_MAX_K];
+        long long cur[PNR_MAX_K];
 #pragma unroll
-        for (int kk = 0; kk < PNR_MAX_K; ++kk) cur[kk] = id[kk] >= 0 ? wn[kk] * g : 0.f;
+        for (int kk = 0; kk < PNR_MAX_K; ++kk) cur[kk] = id[kk] >= 0 ? fx_term(wn[kk] * g, fs) : 0;
 #pragma unroll
         for (int j = 0; j < PNR_MAX_K; ++j) {  // ids within a row are distinct: at most one match
           bool kept = false;
 #pragma unroll
           for (int kk = 0; kk < PNR_MAX_K; ++kk) {
             const bool mt = pid[j] >= 0 && id[kk] == pid[j];
-            cur[kk] += mt ? pacc[j] : 0.f;
+            cur[kk] += mt ? pacc[j] : 0;
             kept = kept || mt;
           }
-          if (pid[j] >= 0 && !kept) unsafeAtomicAdd(a.g_feats + (int64_t)pid[j] * 32 + ch, pacc[j]);
+          if (pid[j] >= 0 && !kept) {
+            atomicAdd(facc + (int64_t)pid[j] * 32 + ch, (unsigned long long)pacc[j]);
+            ++nfl;
+          }
         }
 #pragma unroll
         for (int kk = 0; kk < PNR_MAX_K; ++kk) {
@@ -1051,8 +1103,40 @@ __global__ __launch_bounds__(256) void k_gather_bwd(GatherBwdArgs a) {
     if (a.g_feats) {
 #pragma unroll
       for (int j = 0; j < PNR_MAX_K; ++j)
-        if (pid[j] >= 0) unsafeAtomicAdd(a.g_feats + (int64_t)pid[j] * 32 + ch, pacc[j]);
+        if (pid[j] >= 0) {
+          atomicAdd(facc + (int64_t)pid[j] * 32 + ch, (unsigned long long)pacc[j]);
+          ++nfl;
+        }
     }
+  }
+  if (a.g_feats && a.n_flush) {  // one count per half-wave (lane 0 of each half), one atomic per wave
+    uint32_t n = ch == 0 ? nfl : 0u;
+    n += (uint32_t)__shfl_xor((int)n, 32);
+    if ((threadIdx.x & 63) == 0 && n) atomicAdd(a.n_flush, (unsigned long long)n);
+  }
+}
+
+// g_feats += facc 2^-s (4 values per thread); a non-finite max |dL/dc| makes every element NaN
+__global__ __launch_bounds__(256) void k_gather_bwd_fin(const long long* __restrict__ facc, float* __restrict__ g,
+                                                       int64_t n, const uint32_t* __restrict__ gmax, int guard) {
+  const int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+  if (i >= n) return;
+  const uint32_t gb = *gmax;
+  const int s = fx_shift(gb, guard);
+  const bool bad = gb >= 0x7F800000u;
+  // g may be a view at any float offset of a flat gradient buffer: 16-B accesses only when aligned
+  if (i + 4 <= n && (reinterpret_cast<uintptr_t>(g) & 15) == 0) {
+    const longlong2 v0 = *reinterpret_cast<const longlong2*>(facc + i);
+    const longlong2 v1 = *reinterpret_cast<const longlong2*>(facc + i + 2);
+    float4 o = *reinterpret_cast<float4*>(g + i);
+    o.x += bad ? __int_as_float(0x7FC00000) : (float)ldexp((double)v0.x, -s);
+    o.y += bad ? __int_as_float(0x7FC00000) : (float)ldexp((double)v0.y, -s);
+    o.z += bad ? __int_as_float(0x7FC00000) : (float)ldexp((double)v1.x, -s);
+    o.w += bad ? __int_as_float(0x7FC00000) : (float)ldexp((double)v1.y, -s);
+    *reinterpret_cast<float4*>(g + i) = o;
+  } else {
+    const int64_t e = i + 4 < n ? i + 4 : n;
+    for (int64_t j = i; j < e; ++j) g[j] += bad ? __int_as_float(0x7FC00000) : (float)ldexp((double)facc[j], -s);
   }
 }
 
@@ -1115,6 +1199,37 @@ static void gather_probe(int mode, dim3 grid, hipStream_t st, const GatherArgs& 
 size_t gather_workspace_bytes(int64_t P) {
   size_t b = 0;
   group_view(nullptr, P > 0 ? P : 0, &b);
+  return b;
+}
+
+// backward workspace: the work list of rows with a neighbour | 256-B control block (max |dL/dc| bits
+// at 0, issued atomic instructions at 8) | with feature gradients, the int64 accumulators [M][32]
+struct GatherBwdView {
+  WorkList wl;
+  char* ctl;
+  uint32_t* gmax;
+  unsigned long long* n_flush;
+  long long* facc;
+};
+static GatherBwdView gather_bwd_view(void* ws, int64_t P, int64_t M, bool feats, size_t* bytes = nullptr) {
+  GatherBwdView v{};
+  char* b = static_cast<char*>(ws);
+  size_t off = a256(wl_bytes(P > 0 ? P : 0));
+  if (b) v.wl = wl_view(b, P > 0 ? P : 0);
+  v.ctl = b ? b + off : nullptr;
+  v.gmax = reinterpret_cast<uint32_t*>(v.ctl);
+  v.n_flush = reinterpret_cast<unsigned long long*>(v.ctl ? v.ctl + 8 : nullptr);
+  off += 256;
+  if (feats) {
+    v.facc = reinterpret_cast<long long*>(b ? b + off : nullptr);
+    off += a256((size_t)(M > 0 ? M : 0) * kCDim * 8);
+  }
+  if (bytes) *bytes = off;
+  return v;
+}
+size_t gather_bwd_workspace_bytes(int64_t P, int64_t M, bool feats) {
+  size_t b = 0;
+  gather_bwd_view(nullptr, P, M, feats, &b);
   return b;
 }
 
@@ -1199,7 +1314,8 @@ int launch_gather_bwd(const pnr_points& pts, const PointSrc* src, int mode, cons
     return PNR_E_ARG;
   if (P == 0 || (!pts.g_feats && !g_p)) return PNR_OK;
   if (!idx || !w || !g_c || (g_p && !c)) return PNR_E_ARG;
-  if (!ws || ws_bytes < gather_workspace_bytes(P)) return PNR_E_WORKSPACE;
+  const bool feats = pts.g_feats != nullptr;
+  if (!ws || ws_bytes < gather_bwd_workspace_bytes(P, pts.n_points, feats)) return PNR_E_WORKSPACE;
   GatherBwdArgs a{};
   if (src) a.src = *src;
   a.xP = xP;
@@ -1219,15 +1335,39 @@ int launch_gather_bwd(const pnr_points& pts, const PointSrc* src, int mode, cons
   a.g_feats = pts.g_feats;
   a.g_p = g_p;
   a.gp_accum = gp_accum ? 1 : 0;
-  a.wl = wl_view(ws, P);
+  GatherBwdView v = gather_bwd_view(ws, P, pts.n_points, feats);
+  a.wl = v.wl;
+  a.facc = v.facc;
+  a.gmax = v.gmax;
+  a.n_flush = v.n_flush;
+  // a sum of at most P terms per element (the ids of a row are distinct): 2^guard > P
+  int guard = 1;
+  while (guard < 40 && (1ll << guard) <= P) ++guard;
+  a.guard = guard;
   if (hipMemsetAsync(a.wl.cnt, 0, kLists * 32 * 4, st) != hipSuccess) return (int)hipGetLastError();
+  if (feats) {
+    if (hipMemsetAsync(v.ctl, 0, 256, st) != hipSuccess) return (int)hipGetLastError();
+    if (hipMemsetAsync(v.facc, 0, (size_t)pts.n_points * kCDim * 8, st) != hipSuccess) return (int)hipGetLastError();
+  }
   if (g_p && !gp_accum && hipMemsetAsync(g_p, 0, (size_t)P * 12, st) != hipSuccess) return (int)hipGetLastError();
   TimingScope ts(kTimeGatherBwd, P, st);
   hipLaunchKernelGGL(k_gather_bwd_probe, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, st, a);
   const int64_t tasks = kLists * ((a.wl.cap + 255) / 256);
+  if (feats) hipLaunchKernelGGL(k_gather_bwd_gmax, dim3(resident_grid(k_gather_bwd_gmax, 256, tasks)), dim3(256), 0, st, a);
   if (pts.mode == PNR_GATHER_IDW) gather_bwd_mode<PNR_GATHER_IDW>(mode, tasks, st, a);
   else gather_bwd_mode<PNR_GATHER_TRILINEAR>(mode, tasks, st, a);
+  if (feats && pts.n_points > 0) {
+    const int64_t n = pts.n_points * kCDim;
+    hipLaunchKernelGGL(k_gather_bwd_fin, dim3((unsigned)((n / 4 + 255) / 256 + 1)), dim3(256), 0, st, v.facc, pts.g_feats,
+                       n, v.gmax, guard);
+  }
   return hip_status(hipGetLastError());
+}
+
+int gather_bwd_atomics(const void* ws, int64_t P, int64_t M, unsigned long long* n, hipStream_t st) {
+  GatherBwdView v = gather_bwd_view(const_cast<void*>(ws), P, M, true);
+  if (hipMemcpyAsync(n, v.n_flush, 8, hipMemcpyDeviceToHost, st) != hipSuccess) return (int)hipGetLastError();
+  return hip_status(hipStreamSynchronize(st));
 }
 
 }  // namespace pnr

@@ -25,7 +25,7 @@ PRECISIONS = {'fp32': 0, 'bf16x3': 1, 'bf16': 2, 'f16x3': 3}
 # f16x3: fp32-class forward AND backward (every GEMM on 22-bit split operands with fp32
 # accumulation; tests/test_gpu_parity.py runs every case under fp32 and f16x3 at the same tolerances)
 DEFAULT_PRECISION = os.environ.get('PNR_PRECISION', 'f16x3')
-ABI_VERSION = 9
+ABI_VERSION = 10
 STATUS_F16_RANGE = 1  # include/pnr.h PNR_STATUS_F16_RANGE
 
 
@@ -113,8 +113,10 @@ _SIGS = {
     'pnr_point_gather_workspace_bytes': (c_size_t, [c_int64]),
     'pnr_point_gather': (ctypes.c_int, [PPoints, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t,
                                         c_void_p]),
+    'pnr_point_gather_bwd_workspace_bytes': (c_size_t, [PPoints, c_int64]),
     'pnr_point_gather_bwd': (ctypes.c_int, [PPoints, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p,
                                             c_void_p, c_void_p, c_size_t, c_void_p]),
+    'pnr_point_gather_bwd_atomics': (ctypes.c_int, [PPoints, c_void_p, c_int64, ctypes.POINTER(c_int64), c_void_p]),
     'pnr_fc_packed_floats': (c_size_t, []),
     'pnr_fc_pack': (ctypes.c_int, [FcPtrArray, c_void_p, c_void_p]),
     'pnr_eval_points_c': (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p,

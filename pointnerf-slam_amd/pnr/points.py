@@ -198,7 +198,7 @@ class _GatherFn(torch.autograd.Function):
         g_feats = torch.zeros_like(pts.feats) if ctx.needs_input_grad[2] else None
         g_p = torch.empty((P, 3), device=dev, dtype=torch.float32) if ctx.needs_input_grad[0] else None
         s, keep = pts.descriptor(g_feats=g_feats)
-        ws = torch.empty(lib.pnr_point_gather_workspace_bytes(P), dtype=torch.uint8, device=dev)
+        ws = torch.empty(lib.pnr_point_gather_bwd_workspace_bytes(ctypes.byref(s), P), dtype=torch.uint8, device=dev)
         _lib.check(lib.pnr_point_gather_bwd(ctypes.byref(s), _lib.ptr(p), P, _lib.ptr(idx), _lib.ptr(w), _lib.ptr(c),
                                             _lib.ptr(g_c.contiguous()), _lib.ptr(g_p), _lib.ptr(ws), ws.numel(),
                                             _lib.stream_of(dev)), 'point_gather_bwd')

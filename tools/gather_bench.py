@@ -93,11 +93,12 @@ def main():
     gc = torch.randn_like(c)
     gp = torch.empty((P, 3), device=dev)
     sb, _ = pts.descriptor(g_feats=gf)
+    bws = torch.empty(lib.pnr_point_gather_bwd_workspace_bytes(ctypes.byref(sb), P), dtype=torch.uint8, device=dev)
     lib.pnr_timing_enable(1)
     timing_read(5)
     for _ in range(args.reps):
         pnr._lib.check(lib.pnr_point_gather_bwd(ctypes.byref(sb), p.data_ptr(), P, idx.data_ptr(), w.data_ptr(),
-                                                c.data_ptr(), gc.data_ptr(), gp.data_ptr(), ws.data_ptr(), ws.numel(),
+                                                c.data_ptr(), gc.data_ptr(), gp.data_ptr(), bws.data_ptr(), bws.numel(),
                                                 st), 'gather_bwd')
     torch.cuda.synchronize()
     lib.pnr_timing_enable(0)
@@ -108,11 +109,15 @@ def main():
     timing_read(5)
     for _ in range(args.reps):
         pnr._lib.check(lib.pnr_point_gather_bwd(ctypes.byref(sb), p.data_ptr(), P, idx.data_ptr(), w.data_ptr(),
-                                                c.data_ptr(), gc.data_ptr(), None, ws.data_ptr(), ws.numel(),
+                                                c.data_ptr(), gc.data_ptr(), None, bws.data_ptr(), bws.numel(),
                                                 st), 'gather_bwd')
     torch.cuda.synchronize()
     lib.pnr_timing_enable(0)
     fl, fms, _ = timing_read(5)
+    n_at = ctypes.c_int64(0)
+    pnr._lib.check(lib.pnr_point_gather_bwd_atomics(ctypes.byref(sb), bws.data_ptr(), P, ctypes.byref(n_at), st),
+                   'gather_bwd_atomics')
+    print(f'bwd int64 atomic instructions issued (256 B each): {n_at.value}')
     with torch.no_grad():  # neighbours shared with the previous row that has neighbours
         rows = idx[idx[:, 0] >= 0].long()
         prev, cur = rows[:-1], rows[1:]

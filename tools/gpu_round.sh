@@ -1,0 +1,81 @@
+#!/bin/bash
+# GPU-box driver for one round's measurements (replaces the per-call r0N_*.sh scripts).
+#   bash tools/gpu_round.sh <step> [<step> ...]      steps run in order; the first failure stops the call
+# Steps (each under its own time limit; logs under gpurun_out/<TAG>_*, TAG from $PNR_TAG, default r04):
+#   tests       the whole -m gpu suite, then __graft_entry__.smoke()    (pytest failures stop the call)
+#   test:<k>    the -m gpu tests matching -k <k>
+#   bench       the default bench line (N=1, every extra and CPU baseline)
+#   quick       the S-map line alone (no extras / CPU baseline / gather)
+#   faithful    the room0 Mapper iteration legs (graph replay) alone
+#   points      the neural-point S-map alone
+#   gather      tools/gather_bench.py (forward + backward gather timing)
+#   aux         the auxiliary benches: Tracker, render_img, Mesher grid, configs C3 / C5
+#   prof        the round profile: rocprofv3 kernel stats + FETCH/WRITE and MFMA-busy PMC passes
+#               (tools/prof_round.sh), the gather's traffic passes and kernel stats, the faithful
+#               iteration's kernel stats
+set -o pipefail
+TAG=${PNR_TAG:-r04}
+cd /tmp && export TMPDIR=/tmp
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+O=gpurun_out/${TAG}
+
+run() {  # run <seconds> <log> <cmd...>: stop the whole call on a non-zero status
+  local t=$1 log=$2; shift 2
+  timeout -k 10 "$t" "$@" > "$log" 2>&1
+  local rc=$?
+  if [ $rc -ne 0 ]; then
+    echo "FAILED rc=$rc: $*"; tail -25 "$log"; exit $rc
+  fi
+}
+
+for step in "$@"; do
+  case $step in
+    tests)
+      run 1000 ${O}_gpu_tests.log python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
+        -p no:cacheprovider
+      tail -2 ${O}_gpu_tests.log
+      run 200 ${O}_smoke.log python3 -c "import __graft_entry__ as g; g.smoke()"
+      echo "smoke ok" ;;
+    test:*)
+      run 900 ${O}_gpu_tests_${step#test:}.log python3 -u -m pytest tests -m gpu -x -v --timeout 300 \
+        --timeout-method thread -p no:cacheprovider -k "${step#test:}"
+      tail -3 ${O}_gpu_tests_${step#test:}.log ;;
+    bench)
+      run 600 ${O}_bench.log python3 bench.py
+      tail -c 300 ${O}_bench.log; echo ;;
+    quick)
+      run 300 ${O}_quick.log python3 bench.py --steps 5 --warmup 2 --no-extras --no-cpu-baseline --no-gather
+      grep -o '"value": [0-9.]*, "unit": "rays/s", "n_gpus": 1, "steps": [0-9]*, "warmup": [0-9]*, "ms_per_step": [0-9.]*' ${O}_quick.log
+      grep -o '"frac": [0-9.]*' ${O}_quick.log | head -1 ;;
+    faithful)
+      run 300 ${O}_faithful.log python3 bench.py --workload room0 --steps 100 --warmup 5 --no-cpu-baseline
+      tail -c 400 ${O}_faithful.log; echo ;;
+    points)
+      run 300 ${O}_points.log python3 bench.py --workload map-points --steps 3 --warmup 1 --no-cpu-baseline --no-gather
+      grep -o '"ms_per_step": [0-9.]*' ${O}_points.log | head -1 ;;
+    gather)
+      run 300 ${O}_gather.log python3 tools/gather_bench.py
+      tail -8 ${O}_gather.log ;;
+    aux)
+      run 200 ${O}_track.json python3 tools/track_bench.py
+      run 200 ${O}_render.json python3 tools/render_bench.py
+      run 200 ${O}_mesh.json python3 tools/mesh_eval_bench.py
+      run 400 ${O}_configs.json python3 tools/config_bench.py
+      echo "aux ok" ;;
+    prof)
+      bash tools/prof_round.sh ${TAG} || exit $?
+      for C in FETCH_SIZE WRITE_SIZE; do
+        run 200 gpurun_out/prof_${TAG}_g$C.log rocprofv3 --kernel-trace --pmc $C --output-format csv \
+          -d gpurun_out/prof_${TAG}_gtraffic -o $C -- python3 tools/gather_bench.py --reps 2
+      done
+      run 200 gpurun_out/prof_${TAG}_gb.log rocprofv3 --kernel-trace --stats --output-format csv \
+        -d gpurun_out/prof_${TAG}_gather -o gb -- python3 tools/gather_bench.py
+      run 200 gpurun_out/prof_${TAG}_f1000.log rocprofv3 --kernel-trace --stats --output-format csv \
+        -d gpurun_out/prof_${TAG}_f1000 -o f -- python3 bench.py --workload room0 --steps 50 --warmup 3 \
+        --no-cpu-baseline
+      echo "ROUND_PROF_DONE" ;;
+    *)
+      echo "unknown step $step"; exit 2 ;;
+  esac
+done
