@@ -494,13 +494,18 @@ def sfwd_extra(pnr, plib, slam, params, bound, pose, dev, ddp, lib, steps=10, cp
 MAP_FLOP_PER_RAY = 115.29e6        # (32 + 3 x 44 + 3 x 32) x 443,438 per mapping iteration
 
 
-def oracle_map_rate(bound, pose, params, n, reps=3, threads=None):
+def oracle_map_rate(bound, pose, params, n, reps=3, threads=None, rays=None):
     """The oracle's Mapper iteration (render + regulation + L1 losses + backward + Adam) on n rays on
-    this host's cores, rays/s (median of `reps` after one warm-up)."""
+    this host's cores, rays/s (median of `reps` after one warm-up).  `rays` = (ro, rd, gt, col) to
+    use instead of the synthetic S-map batch."""
     from oracle import ref_render as ref
     prev = torch.get_num_threads()
     torch.set_num_threads(threads or cpu_threads())
-    ro, rd, gt, col = [t.cpu() for t in synth_batch(n, 0, pose, 'cpu', seed=7)]
+    if rays is not None:
+        ro, rd, gt, col = [t.detach().cpu().float() for t in rays]
+        n = ro.shape[0]
+    else:
+        ro, rd, gt, col = [t.cpu() for t in synth_batch(n, 0, pose, 'cpu', seed=7)]
     p = {k: v.clone().requires_grad_(True) for k, v in params.items()}
     opt = torch.optim.Adam(list(p.values()), lr=2e-4)
 
@@ -545,6 +550,77 @@ def faithful_extra(pnr, slam, params, bound, pose, dev, ddp, lib, sizes=(1000, 5
                                            f'warm-up'}
             e['speedup_vs_cpu'] = round(rate / cr, 1)
         out[f'n{n}'] = e
+    return out
+
+
+# the room0 camera (configs/Replica/replica.yaml:22-28, inherited by configs/Replica/room0_point.yaml)
+ROOM0_CAM = {'H': 680, 'W': 1200, 'fx': 600.0, 'fy': 600.0, 'cx': 599.5, 'cy': 339.5}
+ROOM0_PIXELS, ROOM0_WINDOW = 1000, 5   # mapping.pixels (replica.yaml:21), mapping_window_size (pointNeRF_slam.yaml)
+
+
+def room0_window(pnr, params, bound, dev):
+    """The room0 Mapper's keyframe window (mapping_window_size 5: three random keyframes, the last
+    keyframe and the current frame, src/Mapper.py:362-380) as synthetic frames on the room0 camera:
+    renders of the trained decoder at the four fixture poses (tests/golden/scene.npz: gt_c2w_list
+    entries of room0) and at the current pose (pose 1000 moved 2 cm), each frame's gt depth = its
+    rendered depth (S-ref) and gt colour = its rendered colour.  The dataset frames
+    are not in the image (no network)."""
+    import types
+    s = np.load(os.path.join(REPO, 'tests', 'golden', 'scene.npz'))
+    poses = [torch.from_numpy(s['poses'][k]).float() for k in (0, 1, 3, 2)]
+    cur = poses[3].clone()
+    cur[:3, 3] += torch.tensor([0.02, -0.01, 0.01])
+    poses.append(cur)
+    slam = types.SimpleNamespace(bound=bound, **ROOM0_CAM)
+    r = pnr.Renderer(pnr.ROOM0_CFG, None, slam)
+    dec = make_decoder(pnr, pnr.ROOM0_CFG, params, dev)
+    frames = []
+    with torch.no_grad():
+        for c2w in poses:
+            d, _, c = r.render_img({}, dec, c2w.to(dev), dev, 'color')
+            frames.append((c2w.to(dev), d.float().contiguous(), c.float().clamp(0, 1).contiguous()))
+    return slam, frames
+
+
+def room0_extra(pnr, params, bound, pose, dev, ddp, lib, steps=100, warmup=5, cpu=True, graph=True):
+    """The metric's own workload: ONE room0 Mapper iteration (src/Mapper.py:507-662) at its real size,
+    1,000 rays over the 5-frame window (200 per frame) of the room0 camera, gt = the decoder's own
+    rendered depth / colour.  Timed per iteration: the window batch (torch.randint + pnr_window_rays,
+    src/Mapper.py:553-606), render (32 + 12 samples) + regulation (32) + fused L1 losses + backward +
+    Adam, all replayed from one captured HIP graph (pnr.MapGraph(batch_fn=pnr.mapping.WindowSampler))."""
+    from pnr.mapping import MapGraph, MapStep, WindowSampler
+    slam, frames = room0_window(pnr, params, bound, dev)
+    cfg = pnr.ROOM0_CFG
+    r = pnr.Renderer(cfg, None, slam)
+    dec = make_decoder(pnr, cfg, params, dev)
+    per = ROOM0_PIXELS // ROOM0_WINDOW
+    sampler = WindowSampler(frames, per, ROOM0_CAM['fx'], ROOM0_CAM['fy'], ROOM0_CAM['cx'], ROOM0_CAM['cy'],
+                            n_samples=cfg['rendering']['N_samples'])
+    mstep = MapStep(r, dec, lr=cfg['mapping']['imap_decoders_lr'], w_color_loss=cfg['mapping']['w_color_loss'])
+    if graph:
+        mg = MapGraph(mstep, batch_fn=sampler)
+        step = mg
+    else:
+        def step():
+            mstep(*sampler())
+    el, _ = timed(step, steps, warmup, ddp, lib)
+    n = per * ROOM0_WINDOW
+    rate = n * steps / el
+    tf = MAP_FLOP_PER_RAY * rate / 1e12
+    peak = ALGO_PEAK_TF['f16x3']
+    out = {'workload': 'room0 Mapper iteration: 1,000 rays = 5-frame window x 200 uniform pixels on the 680x1200 '
+                       'fx=fy=600 camera, gt = rendered depth / colour (S-ref); window sampling + render (32+12) + '
+                       'regulation (32) + L1 losses + backward + Adam in one replayed HIP graph',
+           'rays_per_iter': n, 'ms_per_iter': round(el / steps * 1e3, 4), 'rays_per_s': round(rate, 1),
+           'graph': graph, 'iters': steps, 'achieved_tflops': round(tf, 2), 'frac_of_split_peak': round(tf / peak, 4),
+           'flop_basis': '115.29 MFLOP per ray per mapping iteration (SURVEY.md 8(d)); peak 833 TF (f16 MFMA / 3)'}
+    if cpu:
+        rays = sampler()[:4]
+        cr = oracle_map_rate(bound, pose, params, n, rays=rays)
+        out['cpu_baseline'] = {'value': round(cr, 1), 'unit': 'rays/s', 'cores': cpu_threads(), 'kind': 'port',
+                               'sample': f'the oracle Mapper iteration on one drawn window batch ({n} rays), median '
+                                         f'of 3 after 1 warm-up'}
+        out['speedup_vs_cpu'] = round(rate / cr, 1)
     return out
 
 
@@ -616,7 +692,7 @@ def main():
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=5)
     ap.add_argument('--warmup', type=int, default=2)
-    ap.add_argument('--workload', choices=['map', 'fwd', 'map-points'], default='map')
+    ap.add_argument('--workload', choices=['map', 'fwd', 'map-points', 'room0'], default='map')
     ap.add_argument('--rays', type=int, default=W * H, help='rays per GPU per step (weak scaling)')
     ap.add_argument('--global-batch', type=int, default=None,
                     help='fixed global batch split over the ranks (strong scaling; SURVEY.md 8(e))')
@@ -643,6 +719,23 @@ def main():
     torch.cuda.set_device(dev)
     lib = pnr.library()
     bound, pose, params = load_scene()
+    if args.workload == 'room0':  # the metric's own iteration alone (1,000 rays per GPU and iteration)
+        ddp = pdist.DataParallel()
+        e = room0_extra(pnr, params, bound, pose, dev, ddp, lib, steps=args.steps, warmup=args.warmup,
+                        cpu=not args.no_cpu_baseline and world == 1)
+        if rank == 0:
+            out = {'metric': METRIC, 'value': round(e['rays_per_s'] * world, 1), 'unit': 'rays/s', 'n_gpus': world,
+                   'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': e['ms_per_iter'],
+                   'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': DTYPE[prec],
+                   'data': 'synthetic (renders of the trained room0 decoder fixture on the room0 camera)',
+                   'config': {'workload': e['workload'], 'rays_per_gpu': e['rays_per_iter'],
+                              'global_batch': e['rays_per_iter'] * world, 'parallelism': f'replicas{world}',
+                              'decoder_precision': prec, 'graph': True},
+                   'room0_iter': e}
+            print(json.dumps(out), flush=True)
+        if world > 1:
+            torch.distributed.destroy_process_group()
+        return
     import types
     slam = types.SimpleNamespace(bound=bound, H=H, W=W, fx=FX, fy=FY, cx=CX, cy=CY)
     cfg = pnr.ROOM0_CFG
@@ -708,6 +801,7 @@ def main():
         elif params is not None:
             extras['sfwd'] = sfwd_extra(pnr, plib, slam, params, bound, pose, dev, ddp, lib,
                                         cpu=not args.no_cpu_baseline)
+            extras['room0_iter'] = room0_extra(pnr, params, bound, pose, dev, ddp, lib, cpu=not args.no_cpu_baseline)
             extras['faithful_n1000'] = faithful_extra(pnr, slam, params, bound, pose, dev, ddp, lib,
                                                       cpu=not args.no_cpu_baseline)
             extras['map_points'] = map_points_extra(pnr, plib, slam, params, bound, pose, dev, ddp, lib,

@@ -262,6 +262,15 @@ int pnr_get_rays(int32_t H, int32_t W, float fx, float fy, float cx, float cy, c
 /* Rays for pixel coordinates i (column), j (row), float32 (n). */
 int pnr_rays_from_uv(const float* i, const float* j, int64_t n, float fx, float fy, float cx, float cy,
                      const float* c2w, float* rays_o, float* rays_d, void* stream);
+/* ABI 10: a Mapper iteration's pixel batch over its keyframe window in one launch (src/Mapper.py:560-606:
+ * per window frame get_samples(0, H, 0, W, pixs_per_image, ...), src/common.py:110-134).  Ray r uses
+ * frame f = r / n_per_frame and pixel idx[r] (int64, uniform over the H x W image, row-major: column
+ * idx % W, row idx / W; clamped into the image as select_uv clamps); c2w (F,4,4) float32, depth
+ * (F,H,W) float32, color (F,H,W,3) float32.  Writes rays_o, rays_d (n,3), gt_depth (n), gt_color (n,3):
+ * the same values as pnr_rays_from_uv + the reference's depth / colour gathers. */
+int pnr_window_rays(const int64_t* idx, int64_t n, int64_t n_per_frame, int32_t H, int32_t W, float fx, float fy,
+                    float cx, float cy, const float* c2w, const float* depth, const float* color, float* rays_o,
+                    float* rays_d, float* gt_depth, float* gt_color, void* stream);
 
 /* ---- optimizer (src/Mapper.py:498-502, 657-662: torch.optim.Adam, default betas/eps) ----- */
 /* One Adam step over `n` float32 words: p -= lr * mhat / (sqrt(vhat) + eps).  step >= 1. */

@@ -41,6 +41,8 @@ int launch_gout_sigma(const float*, const float4*, int64_t, int64_t, float*, hip
 int launch_get_rays(int, int, float, float, float, float, const float*, float*, float*, hipStream_t);
 int launch_rays_from_uv(const float*, const float*, int64_t, float, float, float, float, const float*, float*,
                         float*, hipStream_t);
+int launch_window_rays(const int64_t*, int64_t, int64_t, int, int, float, float, float, float, const float*,
+                       const float*, const float*, float*, float*, float*, float*, hipStream_t);
 int launch_adam(float*, const float*, float*, float*, int64_t, float, float, float, float, float, hipStream_t);
 int launch_adam_dev(float*, const float*, float*, float*, int64_t, float, float, float, float, const int32_t*,
                     hipStream_t);
@@ -866,6 +868,15 @@ int pnr_rays_from_uv(const float* i, const float* j, int64_t n, float fx, float 
                      const float* c2w, float* rays_o, float* rays_d, void* stream) {
   if (n < 0 || (n > 0 && (!i || !j || !c2w || !rays_o || !rays_d))) return PNR_E_ARG;
   return launch_rays_from_uv(i, j, n, fx, fy, cx, cy, c2w, rays_o, rays_d, (hipStream_t)stream);
+}
+
+int pnr_window_rays(const int64_t* idx, int64_t n, int64_t n_per_frame, int32_t H, int32_t W, float fx, float fy,
+                    float cx, float cy, const float* c2w, const float* depth, const float* color, float* rays_o,
+                    float* rays_d, float* gt_depth, float* gt_color, void* stream) {
+  if (n < 0 || H <= 0 || W <= 0 || n_per_frame <= 0) return PNR_E_ARG;
+  if (n > 0 && (!idx || !c2w || !depth || !color || !rays_o || !rays_d || !gt_depth || !gt_color)) return PNR_E_ARG;
+  return launch_window_rays(idx, n, n_per_frame, H, W, fx, fy, cx, cy, c2w, depth, color, rays_o, rays_d, gt_depth,
+                            gt_color, (hipStream_t)stream);
 }
 
 int pnr_adam_step(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1, float beta2,

@@ -9,6 +9,7 @@
 //   k_ray_grads       dL/drays_o, dL/drays_d (tracking)              Renderer.py:177-178, common.py:230
 //   k_reg_z           regulation depths (float32, jittered)          Renderer.py:280-294
 //   k_get_rays        full-frame / per-pixel rays                    common.py:74-89, 248-266
+//   k_window_rays     a mapping iteration's window pixel batch       Mapper.py:560-606, common.py:74-134
 //   k_adam            torch.optim.Adam step                          Mapper.py:498-502, 657-662
 //
 // Arithmetic follows torch's CPU semantics where it is observable: python scalars are applied
@@ -510,6 +511,30 @@ __global__ void k_rays_from_uv(const float* __restrict__ ii, const float* __rest
   make_ray(ii[k], jj[k], fx, fy, cx, cy, c2w, 4, ro + k * 3, rd + k * 3);
 }
 
+// One Mapper iteration's pixel batch over its keyframe window in one launch (src/Mapper.py:560-606
+// per frame: get_samples -> get_sample_uv / select_uv / get_rays_from_uv, src/common.py:74-134):
+// ray r belongs to frame r / per_frame, its pixel is idx[r] (uniform over the H x W image, row-major),
+// i = idx % W (column), j = idx / W (row); the ray as k_rays_from_uv, gt depth / colour gathered from
+// the frame.  c2w: (F, 4, 4); depth (F, H, W); color (F, H, W, 3).
+__global__ void k_window_rays(const int64_t* __restrict__ idx, int64_t n, int64_t per_frame, int64_t hw, int W,
+                              float fx, float fy, float cx, float cy, const float* __restrict__ c2w,
+                              const float* __restrict__ depth, const float* __restrict__ color,
+                              float* __restrict__ ro, float* __restrict__ rd, float* __restrict__ gd,
+                              float* __restrict__ gc) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const int64_t f = k / per_frame;
+  int64_t pix = idx[k];
+  pix = pix < 0 ? 0 : (pix >= hw ? hw - 1 : pix);  // select_uv's clamp (common.py:99-100) + stay in the frame
+  const float i = (float)(pix % W), j = (float)(pix / W);
+  make_ray(i, j, fx, fy, cx, cy, c2w + f * 16, 4, ro + k * 3, rd + k * 3);
+  const int64_t q = f * hw + pix;
+  gd[k] = depth[q];
+  gc[k * 3 + 0] = color[q * 3 + 0];
+  gc[k * 3 + 1] = color[q * 3 + 1];
+  gc[k * 3 + 2] = color[q * 3 + 2];
+}
+
 // torch.optim.Adam (amsgrad=False, weight_decay=0), single-tensor semantics
 __global__ void k_adam(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
                        float* __restrict__ v, int64_t n, float beta1, float beta2, float eps, float step_size,
@@ -658,6 +683,14 @@ int launch_rays_from_uv(const float* i, const float* j, int64_t n, float fx, flo
                         const float* c2w, float* ro, float* rd, hipStream_t st) {
   if (n <= 0) return 0;
   hipLaunchKernelGGL(k_rays_from_uv, dim3(nblk(n, 256)), dim3(256), 0, st, i, j, n, fx, fy, cx, cy, c2w, ro, rd);
+  return hip_status(hipGetLastError());
+}
+int launch_window_rays(const int64_t* idx, int64_t n, int64_t per_frame, int H, int W, float fx, float fy, float cx,
+                       float cy, const float* c2w, const float* depth, const float* color, float* ro, float* rd,
+                       float* gd, float* gc, hipStream_t st) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(k_window_rays, dim3(nblk(n, 256)), dim3(256), 0, st, idx, n, per_frame, (int64_t)H * W, W, fx, fy,
+                     cx, cy, c2w, depth, color, ro, rd, gd, gc);
   return hip_status(hipGetLastError());
 }
 int launch_adam_dev(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1, float beta2,

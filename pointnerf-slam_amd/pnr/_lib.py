@@ -100,6 +100,9 @@ _SIGS = {
                                     c_void_p, c_void_p]),
     'pnr_rays_from_uv': (ctypes.c_int, [c_void_p, c_void_p, c_int64, c_float, c_float, c_float, c_float, c_void_p,
                                         c_void_p, c_void_p, c_void_p]),
+    'pnr_window_rays': (ctypes.c_int, [c_void_p, c_int64, c_int64, c_int32, c_int32, c_float, c_float, c_float,
+                                       c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                       c_void_p]),
     'pnr_adam_step': (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_float, c_float, c_float,
                                      c_float, c_int64, c_void_p]),
     'pnr_adam_step_dev': (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_float, c_float,

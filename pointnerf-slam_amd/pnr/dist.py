@@ -43,10 +43,17 @@ def shard_bounds(n, rank, world):
 
 
 class DataParallel:
-    def __init__(self, group=None, shard_points=False):
+    """`force_collectives` issues the collectives even at world size 1 (a 1-GPU box has one rank per
+    GPU at most under RCCL: this is how the RCCL calls of a step, and their graph capture, run there)."""
+
+    def __init__(self, group=None, shard_points=False, force_collectives=False):
         self.group = group
         self.shard_points = bool(shard_points)
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.active = dist.is_initialized() and (self.world > 1 or force_collectives)
+        # gloo has no CUDA reduce-scatter / all-gather: those two stage through host copies (the gloo
+        # path is a CPU-test / 1-GPU rehearsal of the RCCL one)
+        self.stage = dist.is_initialized() and dist.get_backend(group) == 'gloo'
         self._bufs = {}  # padded send / receive buffers of the sharded feature update, reused per step
 
     def _buf(self, name, n, like):
@@ -67,12 +74,12 @@ class DataParallel:
             m = (g * 1.2).amax().reshape(1)
         else:
             m = torch.full((1,), float('-inf'), device=g.device)
-        if self.world > 1:
+        if self.active:
             dist.all_reduce(m, op=dist.ReduceOp.MAX, group=self.group)
         return m
 
     def allreduce_(self, flat_grad):
-        if self.world > 1:
+        if self.active:
             dist.all_reduce(flat_grad, op=dist.ReduceOp.SUM, group=self.group)
         return flat_grad
 
@@ -93,13 +100,15 @@ class DataParallel:
         as they were).  Returns (a, b)."""
         n = seg.numel()
         a, b, per = self.feature_shard(n)
-        if self.world == 1:
+        if not self.active:
             return a, b
-        buf = seg
-        if per * self.world != n:  # the padded tail stays zero: only [:n] is ever written
-            buf = self._buf('rs_in', per * self.world, seg)
-            buf[:n].copy_(seg)
-        out = self._buf('rs_out', per, seg)
+        staged = self.stage and seg.is_cuda
+        ref = seg.cpu() if staged else seg
+        buf = ref
+        if per * self.world != n or staged:  # the padded tail stays zero: only [:n] is ever written
+            buf = self._buf('rs_in', per * self.world, ref)
+            buf[:n].copy_(ref)
+        out = self._buf('rs_out', per, ref)
         dist.reduce_scatter_tensor(out, buf, op=dist.ReduceOp.SUM, group=self.group)
         seg[a:b].copy_(out[:b - a])
         return a, b
@@ -108,15 +117,16 @@ class DataParallel:
         """Every rank's owned range of `seg` (1-D) to every rank."""
         n = seg.numel()
         a, b, per = self.feature_shard(n)
-        if self.world == 1:
+        if not self.active:
             return seg
-        mine = self._buf('ag_in', per, seg)  # words past b - a stay zero (the last rank's padding)
+        ref = seg.new_empty(0, device='cpu') if (self.stage and seg.is_cuda) else seg
+        mine = self._buf('ag_in', per, ref)  # words past b - a stay zero (the last rank's padding)
         mine[:b - a].copy_(seg[a:b])
-        out = self._buf('ag_out', per * self.world, seg)
+        out = self._buf('ag_out', per * self.world, ref)
         dist.all_gather_into_tensor(out, mine, group=self.group)
         seg.copy_(out[:n])
         return seg
 
     def barrier(self):
-        if self.world > 1:
+        if self.active:
             dist.barrier(group=self.group)

@@ -16,8 +16,9 @@ global far clamp; without it the step is single-GPU.  The step is deterministic:
 gradient GEMM stores per-workgroup partial tiles that one reduction adds in a fixed order (no float
 atomics), so a replay or a rerun reproduces it bit for bit.  It is not the reference's float32
 summation order (no GPU sum is); tests/test_gpu_precision.py holds it to the correctly-rounded
-gradient.  The point-feature gradient (neural points) is scattered with float atomics and is the
-one part whose bits depend on scheduling.
+gradient.  The point-feature gradient (neural points) is summed exactly in int64 fixed point
+(include/pnr.h, ABI 10), so it does not depend on scheduling either: a neural-point step reruns and
+replays bit for bit too.
 """
 from __future__ import annotations
 
@@ -252,32 +253,46 @@ class MapGraph:
     requires work on a side stream before a capture); they are real optimisation steps.
     """
 
-    def __init__(self, mstep: MapStep, rays_o, rays_d, gt_depth, gt_color, t_rand, warmup=2):
-        if mstep.ddp is not None and mstep.ddp.world > 1:
+    def __init__(self, mstep: MapStep, rays_o=None, rays_d=None, gt_depth=None, gt_color=None, t_rand=None,
+                 warmup=2, batch_fn=None):
+        """`batch_fn` (optional): a callable producing (rays_o, rays_d, gt_depth, gt_color, t_rand) on
+        the device -- e.g. a Mapper iteration's window sampling (WindowSampler) -- captured INTO the
+        graph together with the step, so each replay draws a fresh batch (torch's CUDA RNG is
+        capture-safe); then `__call__()` takes no arguments."""
+        if mstep.ddp is not None and getattr(mstep.ddp, 'active', mstep.ddp.world > 1):
             import torch.distributed as dist
             if dist.get_backend(mstep.ddp.group) != 'nccl':
                 raise NotImplementedError('pnr.MapGraph: only RCCL (nccl) collectives can be captured in a graph')
         self.mstep = mstep
-        dev = rays_o.device
-        self.inputs = [t.detach().clone() for t in (rays_o, rays_d, gt_depth, gt_color, t_rand)]
+        self.batch_fn = batch_fn
+        if batch_fn is None:
+            dev = rays_o.device
+            self.inputs = [t.detach().clone() for t in (rays_o, rays_d, gt_depth, gt_color, t_rand)]
+            body = lambda: mstep(*self.inputs)  # noqa: E731
+        else:
+            dev = batch_fn()[0].device
+            self.inputs = None
+            body = lambda: mstep(*batch_fn())  # noqa: E731
         mstep.opt.use_device_step()
         side = torch.cuda.Stream(dev)
         side.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(side):
             for _ in range(warmup):
-                mstep(*self.inputs)
+                body()
         torch.cuda.current_stream(dev).wait_stream(side)
         mstep._invalidate()  # the captured step starts with the weight repack
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
-            self.loss = mstep(*self.inputs)
+            self.loss = body()
 
-    def __call__(self, rays_o, rays_d, gt_depth, gt_color, t_rand):
+    def __call__(self, rays_o=None, rays_d=None, gt_depth=None, gt_color=None, t_rand=None):
         """Copy the batch into the static inputs (a tensor that IS the static buffer -- the caller
-        wrote its batch into `self.inputs` directly -- is not copied), replay, return the loss."""
-        for dst, src in zip(self.inputs, (rays_o, rays_d, gt_depth, gt_color, t_rand)):
-            if src.data_ptr() != dst.data_ptr():
-                dst.copy_(src, non_blocking=True)
+        wrote its batch into `self.inputs` directly -- is not copied), replay, return the loss.  With a
+        captured `batch_fn`, just replay."""
+        if self.batch_fn is None:
+            for dst, src in zip(self.inputs, (rays_o, rays_d, gt_depth, gt_color, t_rand)):
+                if src.data_ptr() != dst.data_ptr():
+                    dst.copy_(src, non_blocking=True)
         self.graph.replay()
         return self.loss
 
@@ -293,3 +308,60 @@ def window_batch(frames, pixs_per_image, H, W, fx, fy, cx, cy, device, generator
            for c2w, d, c in frames]
     return tuple(torch.cat([o[k].float() for o in out], 0) for k in range(4))
 
+
+
+def window_rays(idx, n_per_frame, c2w, depth, color, fx, fy, cx, cy):
+    """pnr_window_rays: the window batch of `window_batch` in ONE launch, for given pixel indices.
+    c2w (F,4,4) / (F,3,4), depth (F,H,W), color (F,H,W,3) device tensors; idx (F * n_per_frame,) int64
+    pixels of the whole image (row-major), frame f's rays at [f n, (f+1) n).  Returns rays_o, rays_d
+    (N,3), gt depth (N,), gt colour (N,3) float32 -- equal to window_batch's get_samples on the same
+    pixel indices (tests/test_gpu_mapping.py)."""
+    lib = _lib.load()
+    dev = depth.device
+    F, H, W = depth.shape
+    if c2w.shape[-2] == 3:
+        c2w = torch.cat([c2w, torch.tensor([0., 0., 0., 1.], device=dev).expand(F, 1, 4)], 1)
+    c2w = c2w.to(device=dev, dtype=torch.float32).contiguous()
+    depth = depth.float().contiguous()
+    color = color.float().contiguous()
+    idx = idx.to(device=dev, dtype=torch.int64).contiguous()
+    n = idx.numel()
+    _lib.require_cuda(depth, color, idx, c2w)
+    ro = torch.empty((n, 3), device=dev)
+    rd = torch.empty((n, 3), device=dev)
+    gd = torch.empty(n, device=dev)
+    gc = torch.empty((n, 3), device=dev)
+    _lib.check(lib.pnr_window_rays(_lib.ptr(idx), n, int(n_per_frame), H, W, float(fx), float(fy), float(cx),
+                                   float(cy), _lib.ptr(c2w), _lib.ptr(depth), _lib.ptr(color), _lib.ptr(ro),
+                                   _lib.ptr(rd), _lib.ptr(gd), _lib.ptr(gc), _lib.stream_of(dev)), 'window_rays')
+    return ro, rd, gd, gc
+
+
+class WindowSampler:
+    """A Mapper iteration's batch over a fixed keyframe window (src/Mapper.py:397, 553-606):
+    `pixs_per_image` = mapping.pixels // len(window) uniform pixels per frame (torch.randint on the
+    device, one draw for the whole window) and their rays, gt depth and colour from ONE pnr_window_rays
+    launch, plus the regulation jitter t_rand (Renderer.py:293).  Two launches per batch plus the RNG,
+    so a captured iteration (MapGraph(batch_fn=sampler)) draws a fresh batch per replay.
+    frames: list of (c2w, gt depth (H,W), gt colour (H,W,3)) device tensors."""
+
+    def __init__(self, frames, pixs_per_image, fx, fy, cx, cy, n_samples=32, generator=None):
+        self.c2w = torch.stack([f[0][:3] if f[0].shape[0] == 3 else f[0] for f in frames]).float()
+        if self.c2w.shape[1] == 3:
+            self.c2w = torch.cat([self.c2w, torch.tensor([0., 0., 0., 1.], device=self.c2w.device)
+                                  .expand(len(frames), 1, 4)], 1)
+        self.c2w = self.c2w.contiguous()
+        self.depth = torch.stack([f[1].float() for f in frames]).contiguous()
+        self.color = torch.stack([f[2].float() for f in frames]).contiguous()
+        self.n = int(pixs_per_image)
+        self.cam = (fx, fy, cx, cy)
+        self.n_samples = n_samples
+        self.generator = generator
+
+    def __call__(self):
+        F, H, W = self.depth.shape
+        dev = self.depth.device
+        idx = torch.randint(H * W, (F * self.n,), device=dev, generator=self.generator)
+        ro, rd, gd, gc = window_rays(idx, self.n, self.c2w, self.depth, self.color, *self.cam)
+        t_rand = torch.rand((F * self.n, self.n_samples), device=dev, generator=self.generator)
+        return ro, rd, gd, gc, t_rand

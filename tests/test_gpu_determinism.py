@@ -1,0 +1,169 @@
+"""Determinism of the mapping step on the HIP path, with and without neural points.
+
+Every sum of the backward has a fixed result whatever the scheduling: the weight-gradient GEMMs
+store per-workgroup partial tiles that one launch adds in a fixed order, and the point-feature
+gradient (pnr_point_gather_bwd ABI 10) is an exact int64 fixed-point sum.  So:
+  * two runs of a neural-point MapStep are bitwise equal (src/Mapper.py:657-662 on the features);
+  * a neural-point MapStep captured in a HIP graph (pnr.MapGraph) replays bitwise like the eager step;
+  * the MapStep with the regulation chain on a side stream (overlap) equals the serial one bitwise;
+  * the fused Mapper loss (pnr_map_loss, src/Mapper.py:628-655) and its gradients equal the
+    autograd drop-in path (render_batch_ray + regulation + the torch loss, MapStep.loss).
+Run under both decoder precisions (fp32 MFMA and the default f16x3).
+"""
+import pytest
+import torch
+
+from conftest import golden_params, load_golden
+from oracle import ref_points as RP
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True, params=['fp32', 'f16x3'])
+def precision(request, monkeypatch):
+    from pnr import _lib
+    monkeypatch.setattr(_lib, 'DEFAULT_PRECISION', request.param)
+    return request.param
+
+
+@pytest.fixture(scope='module')
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip('no GPU')
+    return torch.device('cuda:0')
+
+
+@pytest.fixture(scope='module')
+def pnr_mod():
+    import pnr
+    pnr.library()
+    return pnr
+
+
+def _renderer(pnr, bound):
+    import types
+    slam = types.SimpleNamespace(bound=bound, H=680, W=1200, fx=600., fy=600., cx=599.5, cy=339.5)
+    return pnr.Renderer(pnr.ROOM0_CFG, None, slam)
+
+
+def _setup(pnr, dev, n=512, points=True, seed=4):
+    """Rays at the golden pose-1000 surface (gt = rendered depth), neural points scattered around
+    it, the trained decoder (+ seeded fc_c), and 4 batches (gt colour, jitter) for 4 steps."""
+    r = load_golden('render.npz')
+    ro = torch.from_numpy(r['p2_gt/rays_o'])[:n]
+    rd = torch.from_numpy(r['p2_gt/rays_d'])[:n]
+    gt = torch.from_numpy(r['p2_gt/gt_depth'])[:n]
+    gen = torch.Generator().manual_seed(seed)
+    surf = ro + rd * gt[:, None]
+    xyz = (surf.repeat(4, 1) + 0.01 * torch.randn((4 * n, 3), generator=gen)).float()
+    feats = torch.randn((xyz.shape[0], 32), generator=gen) * 0.5
+    batches = [(ro.to(dev), rd.to(dev), gt.to(dev), torch.rand((n, 3), generator=gen).to(dev),
+                torch.rand((n, 32), generator=gen).to(dev)) for _ in range(4)]
+    base = golden_params('trained')
+    params = RP.init_fc_c(base, seed=1) if points else base
+    bound = torch.from_numpy(load_golden('scene.npz')['bound'])
+
+    def make():
+        if points:
+            dec = pnr.MLP(name='color', dim=3, c_dim=32, color=True, skips=[], n_blocks=4, hidden_size=256)
+            pts = pnr.NeuralPoints(xyz.to(dev), feats.to(dev), mode='idw', radius=0.04, k=8).to(dev)
+        else:
+            dec = pnr.get_model(pnr.ROOM0_CFG, nice=False)
+            pts = None
+        dec.load_state_dict({k: v.clone() for k, v in params.items()})
+        return _renderer(pnr, bound), dec.to(dev), pts
+    return make, batches
+
+
+@pytest.mark.parametrize('points', [True, False])
+def test_map_step_reruns_bitwise(pnr_mod, dev, points):
+    """Two runs of the same 3 mapping steps give identical losses, gradients and parameters."""
+    from pnr.mapping import MapStep
+    make, batches = _setup(pnr_mod, dev, points=points)
+    runs = []
+    for _ in range(2):
+        r, dec, pts = make()
+        ms = MapStep(r, dec, points=pts, feat_lr=1e-2)
+        losses = [float(ms(*b)) for b in batches[:3]]
+        torch.cuda.synchronize()
+        runs.append((losses, ms.flat.grad.clone(), ms.flat.data.clone()))
+    assert runs[0][0] == runs[1][0]
+    assert torch.equal(runs[0][1], runs[1][1])
+    assert torch.equal(runs[0][2], runs[1][2])
+
+
+def test_points_map_graph_matches_eager(pnr_mod, dev):
+    """pnr.MapGraph over a neural-point MapStep (gather, fc_c injection, deterministic feature
+    backward, two Adam segments): the replayed iterations equal the eager ones bit for bit."""
+    from pnr.mapping import MapGraph, MapStep
+    make, batches = _setup(pnr_mod, dev, points=True)
+    runs = []
+    for graph in (False, True):
+        r, dec, pts = make()
+        ms = MapStep(r, dec, points=pts, feat_lr=1e-2)
+        ms.opt.use_device_step()
+        losses = []
+        if graph:
+            mg = MapGraph(ms, *batches[0], warmup=2)
+            for b in batches[1:]:
+                losses.append(float(mg(*b)))
+        else:
+            for _ in range(2):
+                ms(*batches[0])
+            for b in batches[1:]:
+                losses.append(float(ms(*b)))
+        torch.cuda.synchronize()
+        runs.append((losses, ms.flat.data.detach().cpu().clone(), int(ms.opt.step_dev.item())))
+    (l_e, w_e, s_e), (l_g, w_g, s_g) = runs
+    assert s_e == s_g == 5
+    assert l_g == l_e, (l_g, l_e)
+    assert torch.equal(w_g, w_e)
+
+
+@pytest.mark.parametrize('points', [True, False])
+def test_map_step_overlap_equals_serial(pnr_mod, dev, points):
+    """MapStep(overlap=True) runs the regulation chain on a side stream with its own gradient
+    buffer and adds it after the join; overlap=False accumulates both chains into one buffer on
+    the caller's stream.  Both add the same two per-chain sums once: the gradients are bitwise equal."""
+    from pnr.mapping import MapStep
+    make, batches = _setup(pnr_mod, dev, points=points)
+    out = []
+    for ov in (True, False):
+        r, dec, pts = make()
+        ms = MapStep(r, dec, points=pts, feat_lr=1e-2, overlap=ov)
+        assert ms._overlaps(batches[0][0].shape[0]) == ov
+        loss = float(ms(*batches[0]))
+        torch.cuda.synchronize()
+        out.append((loss, ms.flat.grad.clone(), ms.flat.data.clone()))
+    assert out[0][0] == out[1][0]
+    assert torch.equal(out[0][1], out[1][1])
+    assert torch.equal(out[0][2], out[1][2])
+
+
+@pytest.mark.parametrize('points', [True, False])
+def test_fused_map_loss_matches_autograd(pnr_mod, dev, points):
+    """The fused path (TrainPass + pnr_map_loss) against the drop-in autograd path
+    (Renderer.render_batch_ray / regulation + the reference's loss in torch, MapStep.loss): the loss
+    and every gradient (decoder, fc_c, point features).  The two reach the same kernels with the same
+    upstream gradients (sign terms), so the gradients agree to the order of the two chains' sums."""
+    from pnr.mapping import MapStep
+    make, batches = _setup(pnr_mod, dev, points=points)
+    ro, rd, gt, col, t_rand = batches[0]
+    r, dec, pts = make()
+    ms = MapStep(r, dec, points=pts, feat_lr=1e-2, lr=0.0)  # lr 0: Adam leaves the parameters alone
+    l_fused = float(ms(ro, rd, gt, col, t_rand))
+    g_fused = ms.flat.grad.clone()
+    r2, dec2, pts2 = make()
+    ms2 = MapStep(r2, dec2, points=pts2, feat_lr=1e-2, lr=0.0)
+    ms2.flat.grad.zero_()
+    loss = ms2.loss(ro, rd, gt, col, t_rand=t_rand)
+    loss.backward()
+    torch.cuda.synchronize()
+    # the colour term: torch sums |gt - c| in float32, pnr_map_loss in float64
+    assert abs(float(loss) - l_fused) <= 1e-6 * abs(l_fused)
+    g_auto = ms2.flat.grad.clone()  # autograd accumulated into the flat views (FlatParams)
+    scale = g_fused.abs().max()
+    diff = (g_fused - g_auto).abs()
+    print(f'fused vs autograd: max |dg| {float(diff.max()):.3e} of max |g| {float(scale):.3e}; '
+          f'bitwise equal {bool(torch.equal(g_fused, g_auto))}')
+    assert bool((diff <= 1e-6 * g_auto.abs() + 1e-9 * scale).all())

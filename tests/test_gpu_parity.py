@@ -256,6 +256,32 @@ def test_window_batch_vs_oracle(pnr_mod, dev, scene):
         assert torch.equal(gd[sl].cpu(), d.reshape(-1)[idx]) and torch.equal(gc[sl].cpu(), col.reshape(-1, 3)[idx])
 
 
+def test_window_rays_equal_window_batch(pnr_mod, dev, scene):
+    """pnr_window_rays (the whole window batch in one launch, pnr.mapping.WindowSampler) gives the
+    values of window_batch's per-frame get_samples on the same pixel indices, bit for bit; the
+    WindowSampler draws one uniform index per ray over the whole image, 5 frames x 200 pixels."""
+    from pnr.mapping import WindowSampler, window_batch, window_rays
+    H, W, fx, fy, cx, cy = 68, 120, 60., 61., 59.5, 33.5
+    g = torch.Generator().manual_seed(6)
+    frames = []
+    for k in (0, 1, 2, 3, 2):
+        c2w = torch.from_numpy(scene['poses'][k]).float()
+        frames.append((c2w.to(dev), torch.rand((H, W), generator=g).to(dev), torch.rand((H, W, 3), generator=g).to(dev)))
+    n = 200
+    ref = window_batch(frames, n, H, W, fx, fy, cx, cy, dev, generator=torch.Generator(device=dev).manual_seed(9))
+    gen = torch.Generator(device=dev).manual_seed(9)
+    idx = torch.cat([torch.randint(H * W, (n,), device=dev, generator=gen) for _ in frames])
+    c2w = torch.stack([f[0] for f in frames])
+    out = window_rays(idx, n, c2w, torch.stack([f[1] for f in frames]), torch.stack([f[2] for f in frames]),
+                      fx, fy, cx, cy)
+    for a, b, what in zip(out, ref, ('rays_o', 'rays_d', 'gt depth', 'gt colour')):
+        assert torch.equal(a, b), what
+    ws = WindowSampler(frames, n, fx, fy, cx, cy, generator=torch.Generator(device=dev).manual_seed(3))
+    ro, rd, gd, gc, tr = ws()
+    assert ro.shape == (5 * n, 3) and tr.shape == (5 * n, 32) and gd.shape == (5 * n,)
+    assert bool((tr >= 0).all() and (tr < 1).all())
+
+
 def test_adam_matches_torch(pnr_mod, dev):
     import ctypes
     lib = pnr_mod.library()
