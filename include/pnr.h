@@ -179,6 +179,27 @@ size_t pnr_mlp_bwd_workspace_bytes(int64_t P);
 int pnr_mlp_bwd(const float* packed, int64_t P, const float* g_raw, float* const* grads, float* g_p, void* ws,
                 size_t ws_bytes, void* bwd_ws, size_t bwd_bytes, int32_t precision, void* stream);
 
+/* ---- map pass (ABI 10): one Mapper iteration's two decoder passes as ONE pass --------------------
+ * src/Mapper.py:623-655 renders the window batch with gt depth (render_batch_ray: N_samples coarse +
+ * N_importance importance samples, Renderer.py:63-203) and queries the density at N_samples jittered
+ * depths per ray (regulation, Renderer.py:263-301).  pnr_map_fwd runs both with shared MLP launches:
+ * launch A over the regulation + coarse samples, launch B over the importance samples; the points and
+ * their bound tests are formed by the ray kernels in the reference's dtypes (float32 regulation,
+ * float64 render).  Outputs: depth, var (n) float64, rgb (n,3), sigma (n, N_samples) float32 -- bit for
+ * bit those of pnr_render_fwd + pnr_regulation_fwd with the same t_rand (tests/test_gpu_mapping.py).
+ * pnr_map_bwd takes dL/ddepth, dL/drgb, dL/dsigma and runs ONE delta chain / weight-gradient pass over
+ * every sample (grads accumulated, +=; neural points as in pnr_render_bwd); no ray gradients.
+ * prm: save_for_backward / need_ray_grads ignored (the pass always trains the decoder); n_importance > 0;
+ * far_mode as pnr_render_fwd; t_rand (n, N_samples) float32 in [0,1). */
+size_t pnr_map_workspace_bytes(const pnr_render_params* prm, int64_t n_rays);
+int pnr_map_fwd(const pnr_render_params* prm, const float* packed, const float* rays_o, const float* rays_d,
+                const float* gt_depth, const float* t_rand, int64_t n, double* depth, double* var, float* rgb,
+                float* sigma, void* workspace, size_t ws_bytes, void* stream);
+size_t pnr_map_bwd_workspace_bytes(const pnr_render_params* prm, int64_t n_rays);
+int pnr_map_bwd(const pnr_render_params* prm, const float* packed, const float* rays_d, int64_t n,
+                const double* g_depth, const float* g_rgb, const float* g_sigma, float* const* grads, void* workspace,
+                size_t ws_bytes, void* bwd_ws, size_t bwd_bytes, void* stream);
+
 /* ---- neural points ------------------------------------------------------------------------ */
 size_t pnr_points_index_bytes(int64_t n_points, int32_t table_bits);
 /* (Re)builds pts->index from pts->xyz (after any change of positions / cell / origin). */
@@ -283,6 +304,14 @@ int pnr_adam_step(float* p, const float* g, float* m, float* v, int64_t n, float
 int pnr_adam_step_dev(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1,
                       float beta2, float eps, const int32_t* step_count, void* stream);
 int pnr_step_advance(int32_t* step_count, void* stream);
+/* ABI 10: Adam over n_seg (1..4) learning-rate segments of one flat parameter buffer -- segment q is
+ * p[seg_offset[q] .. + seg_n[q]) with its own moments m[q], v[q] (device pointers, host array) and
+ * lr seg_lr[q] -- AND the step advance, in ONE launch: step2 (int32[2], device) = {completed steps,
+ * 0}; every element uses step = step2[0] + 1, and the launch leaves {step2[0] + 1, 0}.  Same
+ * arithmetic as pnr_adam_step_dev per segment followed by pnr_step_advance. */
+int pnr_adam_multi_dev(float* p, const float* g, int32_t n_seg, const int64_t* seg_offset, const int64_t* seg_n,
+                       float* const* m, float* const* v, const float* seg_lr, float beta1, float beta2, float eps,
+                       int32_t* step2, void* stream);
 
 /* Mapper loss terms and their gradients (src/Mapper.py:628-655, the loss of Mapper.optimize_map
  * built from render_batch_ray's depth / colour and regulation's sigma), in one pass (ABI 9):
@@ -293,8 +322,10 @@ int pnr_step_advance(int32_t* step_count, void* stream);
  *   g_sigma = w_reg sign(sigma)                       (float32, n_sigma)
  * sign(0) = 0 as torch's abs backward.  Either part may be empty (n = 0 or n_sigma = 0, its
  * pointers NULL).  The sum has a fixed order (deterministic).  workspace:
- * pnr_map_loss_workspace_bytes() bytes of device scratch.  Replaces the ~20 elementwise / reduction
- * launches the torch form of the loss and its autograd backward cost per iteration. */
+ * pnr_map_loss_workspace_bytes() bytes of device scratch, ZERO-FILLED before its first use (ABI 10: it
+ * holds a ticket word that lets the last block add the partial sums, one launch; each call leaves it
+ * zero-filled again, so a caller reuses one workspace for the calls of one stream).  Replaces the ~20
+ * elementwise / reduction launches the torch form of the loss and its autograd backward cost. */
 size_t pnr_map_loss_workspace_bytes(void);
 int pnr_map_loss(const float* gt_depth, const double* depth, const float* gt_color, const float* color, int64_t n,
                  float w_color, const float* sigma, int64_t n_sigma, float w_reg, double* loss, double* g_depth,

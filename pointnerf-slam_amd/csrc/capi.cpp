@@ -26,12 +26,18 @@ namespace pnr {
 int launch_gt_max(const float*, int64_t, float*, hipStream_t);
 int launch_coarse_z(const pnr_render_params&, const float*, const float*, const float*, const float*, int64_t,
                     double*, double*, hipStream_t);
-int launch_pdf(const pnr_render_params&, const float*, const double*, const float*, int64_t, double*, hipStream_t);
+int launch_pdf(const pnr_render_params&, const float*, const double*, const float*, int64_t, double*, hipStream_t,
+               const float* ro = nullptr, float* x4i = nullptr, int64_t x4i_pad = 0, const float* rawr = nullptr,
+               float* sigma = nullptr);
+int launch_map_pts(const pnr_render_params&, const float*, const float*, const float*, const float*, const float*,
+                   int64_t, int64_t, int64_t, double*, double*, float*, hipStream_t);
 int launch_fine(const pnr_render_params&, const float*, const double*, const double*, const float*, const float*,
                 int64_t, double*, double*, float*, uint8_t*, hipStream_t);
 int launch_fine_bwd(const pnr_render_params&, const float*, const double*, const double*, const float*,
                     const float*, const float4*, const float4*, const uint8_t*, int64_t, const double*,
-                    const double*, const float*, float*, float*, float*, float*, int, float*, int, hipStream_t);
+                    const double*, const float*, float*, float*, float*, float*, int, float*, int, hipStream_t,
+                    const float* g_sigma = nullptr, const float4* insr = nullptr, float* gor = nullptr,
+                    float* pad2 = nullptr, int np2 = 0);
 int launch_ray_grads_f64(const float*, const double*, int, const double*, int, const float*, const float*,
                          const float*, int64_t, float*, float*, hipStream_t);
 int launch_ray_grads_f32(const float*, const float*, int, const float*, int64_t, float*, float*, hipStream_t);
@@ -47,6 +53,8 @@ int launch_adam(float*, const float*, float*, float*, int64_t, float, float, flo
 int launch_adam_dev(float*, const float*, float*, float*, int64_t, float, float, float, float, const int32_t*,
                     hipStream_t);
 int launch_step_advance(int32_t*, hipStream_t);
+int launch_adam_multi(float*, const float*, int, const int64_t*, const int64_t*, float* const*, float* const*,
+                      const float*, float, float, float, int32_t*, hipStream_t);
 int launch_map_loss(const float*, const double*, const float*, const float*, int64_t, float, const float*, int64_t,
                     float, double*, double*, double*, float*, float*, hipStream_t);
 
@@ -299,7 +307,8 @@ int mlp_backward_core(int prec, const float* packed, const SaveArgs& sv, int64_t
       // is not stored by k_mlp_bwd16 (rank 4: rebuilt from g_out and the h4 masks inside the GEMM).
       // These GEMMs (and the fc_c ones below) are independent: prepared here, launched as one group.
       WgradSyn syn{reinterpret_cast<const float4*>(b.g_out + p0 * 4), sv.masks + 3 * (sv.ld / 32) * 64, p0 / 32,
-                   packed + packed_raw_wo_offset(), sv.xP + p0, packed + kOffFB, pp, pb, nullptr};
+                   packed + packed_raw_wo_offset(), sv.xP + p0, packed + kOffFB, pp, pb, nullptr,
+                   (grads ? 4 : 0) + (want_fc ? 4 : 0)};
       // with the feature branch k_mlp_bwd16 stores dL/dh_l only: delta_l = dL/dh_l masked in the GEMM
       const bool fmask = fb != nullptr;
       const int64_t mstride = (sv.ld / 32) * 64;
@@ -740,6 +749,156 @@ int pnr_regulation_bwd(const pnr_render_params* prm, const float* packed, const 
   return rc;
 }
 
+// ---- map pass: render + regulation of one Mapper iteration as ONE decoder pass --------------------
+namespace {
+// Rows of the map pass: regulation [0, pr) | coarse [pr, r1) | importance [r1, ld), each segment's
+// real rows first, then padding to a multiple of 128.  `save.xP` holds the kPtsX4 input rows.
+struct MapWS {
+  float* gmax;
+  double* z;     // [n S coarse | n I importance] float64
+  double* far;
+  float* raw;    // [ld] float4
+  uint8_t* ord;  // [n][64]
+  int64_t pr, r1, ld;
+  SaveArgs save;
+  float* c;      // neural points: [ld][32], [ld][k], [ld][k], gather work list
+  int32_t* nidx;
+  float* nw;
+  void* gws;
+  size_t gws_bytes;
+};
+MapWS carve_map(const pnr_render_params* prm, int64_t n, void* ws, size_t* bytes) {
+  Carver c(ws);
+  MapWS w{};
+  const int64_t S = prm->n_samples, I = prm->n_importance;
+  w.pr = pad128(n * S);
+  w.r1 = w.pr + pad128(n * S);
+  w.ld = w.r1 + pad128(n * I);
+  w.gmax = c.take<float>(64);
+  w.z = c.take<double>(n * (S + I));
+  w.far = c.take<double>(n);
+  w.raw = c.take<float>((size_t)w.ld * 4);
+  w.ord = c.take<uint8_t>(n * PNR_MAX_SAMPLES);
+  w.save = carve_save(c, w.ld, prm->precision);
+  if (prm->points) {
+    w.c = c.take<float>((size_t)w.ld * kCDim);
+    w.nidx = c.take<int32_t>((size_t)w.ld * prm->points->k);
+    w.nw = c.take<float>((size_t)w.ld * prm->points->k);
+    w.gws_bytes = gather_workspace_bytes(w.r1);
+    w.gws = c.take<char>(w.gws_bytes);
+  }
+  if (bytes) *bytes = c.off;
+  return w;
+}
+bool valid_map_prm(const pnr_render_params* prm) {
+  return valid_prm(prm) && prm->n_samples >= 3 && prm->n_importance > 0 && prm->precision >= PNR_PREC_FP32 &&
+         prm->precision <= PNR_PREC_F16X3;
+}
+}  // namespace
+
+size_t pnr_map_workspace_bytes(const pnr_render_params* prm, int64_t n_rays) {
+  if (!valid_map_prm(prm) || n_rays < 0) return 0;
+  size_t b = 0;
+  carve_map(prm, n_rays, nullptr, &b);
+  return b;
+}
+
+int pnr_map_fwd(const pnr_render_params* prm, const float* packed, const float* rays_o, const float* rays_d,
+                const float* gt_depth, const float* t_rand, int64_t n, double* depth, double* var, float* rgb,
+                float* sigma, void* workspace, size_t ws_bytes, void* stream) {
+  if (!valid_map_prm(prm) || !packed || n < 0) return PNR_E_ARG;
+  if (n == 0) return PNR_OK;
+  if (!rays_o || !rays_d || !gt_depth || !t_rand || !depth || !var || !rgb || !sigma || !workspace) return PNR_E_ARG;
+  if (prm->points && !prm->points->fc_packed) return PNR_E_ARG;
+  size_t need = 0;
+  MapWS w = carve_map(prm, n, workspace, &need);
+  if (ws_bytes < need) return PNR_E_WORKSPACE;
+  hipStream_t st = (hipStream_t)stream;
+  const int S = prm->n_samples, I = prm->n_importance;
+  int rc = 0;
+  if (prm->far_mode == 0) rc = launch_gt_max(gt_depth, n, w.gmax, st);
+  if (rc) return rc;
+  float* x4 = reinterpret_cast<float*>(w.save.xP);
+  rc = launch_map_pts(*prm, rays_o, rays_d, gt_depth, t_rand, prm->far_mode == 2 ? prm->far_clamp_dev : w.gmax, n, w.pr,
+                      w.r1, w.z, w.far, x4, st);
+  if (rc) return rc;
+  const pnr_points* pts = prm->points;
+  PointSrc src{};
+  src.pts = x4;
+  FeatArgs fa{pts ? pts->fc_packed : nullptr, w.c};
+  const int K = pts ? pts->k : 0;
+  uint32_t* status = reinterpret_cast<uint32_t*>(prm->status);
+  // launch A: regulation + coarse rows
+  if (pts) {
+    rc = launch_gather(*pts, src, kPtsX4, w.r1, w.r1, w.c, w.nidx, w.nw, w.gws, w.gws_bytes, st);
+    if (rc) return rc;
+  }
+  rc = mlp_fwd(prm->precision, packed, src, kPtsX4, w.r1, w.raw, &w.save, st, pts ? &fa : nullptr, status);
+  if (rc) return rc;
+  // importance depths and points from the coarse weights; the regulation densities out of launch A
+  double* zi = w.z + n * S;
+  rc = launch_pdf(*prm, rays_d, w.z, w.raw + w.pr * 4, n, zi, st, rays_o, x4 + w.r1 * 4, w.ld - w.r1 - n * I, w.raw,
+                  sigma);
+  if (rc) return rc;
+  // launch B: importance rows
+  PointSrc src2{};
+  src2.pts = x4 + w.r1 * 4;
+  SaveArgs s2 = w.save;
+  s2.p0 = w.r1;
+  if (pts) {
+    rc = launch_gather(*pts, src2, kPtsX4, n * I, w.ld - w.r1, w.c + w.r1 * kCDim, w.nidx + w.r1 * K,
+                       w.nw + w.r1 * K, w.gws, w.gws_bytes, st);
+    if (rc) return rc;
+    fa.c = w.c + w.r1 * kCDim;
+  }
+  rc = mlp_fwd(prm->precision, packed, src2, kPtsX4, n * I, w.raw + w.r1 * 4, &s2, st, pts ? &fa : nullptr, status);
+  if (rc) return rc;
+  return launch_fine(*prm, rays_d, w.z, zi, w.raw + w.pr * 4, w.raw + w.r1 * 4, n, depth, var, rgb, w.ord, st);
+}
+
+size_t pnr_map_bwd_workspace_bytes(const pnr_render_params* prm, int64_t n_rays) {
+  if (!valid_map_prm(prm) || n_rays < 0) return 0;
+  MapWS w = carve_map(prm, n_rays, nullptr, nullptr);
+  size_t b = 0;
+  carve_bwd(w.ld, n_rays, nullptr, &b, prm->points != nullptr, true, n_pts(prm));
+  return b;
+}
+
+int pnr_map_bwd(const pnr_render_params* prm, const float* packed, const float* rays_d, int64_t n,
+                const double* g_depth, const float* g_rgb, const float* g_sigma, float* const* grads, void* workspace,
+                size_t ws_bytes, void* bwd_ws, size_t bwd_bytes, void* stream) {
+  if (!valid_map_prm(prm) || !packed || n < 0) return PNR_E_ARG;
+  if (n == 0) return PNR_OK;
+  if (!workspace || !bwd_ws || !rays_d || !g_depth || !g_rgb || !g_sigma) return PNR_E_ARG;
+  if (grads)
+    for (int i = 0; i < PNR_N_PARAMS; ++i)
+      if (!grads[i]) return PNR_E_ARG;
+  size_t need = 0, bneed = 0;
+  MapWS w = carve_map(prm, n, workspace, &need);
+  const pnr_points* pts = prm->points;
+  BwdWS b = carve_bwd(w.ld, n, bwd_ws, &bneed, pts != nullptr, true, n_pts(prm));
+  if (ws_bytes < need || bwd_bytes < bneed) return PNR_E_WORKSPACE;
+  hipStream_t st = (hipStream_t)stream;
+  const int S = prm->n_samples, I = prm->n_importance;
+  const double* zi = w.z + n * S;
+  const float4* x4 = w.save.xP;
+  // dL/draw of every row: render rows from the compositing backward, regulation rows from dL/dsigma,
+  // zeros on the three segments' padding rows -- one launch
+  int rc = launch_fine_bwd(*prm, rays_d, w.z, zi, w.raw + w.pr * 4, w.raw + w.r1 * 4, x4 + w.pr, x4 + w.r1, w.ord, n,
+                           g_depth, nullptr, g_rgb, b.g_out + w.pr * 4, b.g_out + w.r1 * 4, b.g_nrm,
+                           b.g_out + (n * S) * 4, (int)(w.pr - n * S), b.g_out + (w.pr + n * S) * 4,
+                           (int)(w.r1 - w.pr - n * S), st, g_sigma, x4, b.g_out, b.g_out + (w.r1 + n * I) * 4,
+                           (int)(w.ld - w.r1 - n * I));
+  if (rc) return rc;
+  FeatBwd fb{pts ? pts->fc_packed : nullptr, w.c, pts ? pts->g_fc : nullptr};
+  rc = mlp_backward_core(prm->precision, packed, w.save, w.ld, b, grads, false, st, pts ? &fb : nullptr);
+  if (rc) return rc;
+  if (pts)
+    rc = launch_gather_bwd(*pts, nullptr, kPtsX4, x4, w.ld, w.nidx, w.nw, w.c, b.g_c, nullptr, true, b.gws, b.gws_bytes,
+                           st);
+  return rc;
+}
+
 // ---- neural points ---------------------------------------------------------------------------
 size_t pnr_points_index_bytes(int64_t n_points, int32_t table_bits) {
   if (n_points < 0 || table_bits < 10 || table_bits > 24) return 0;
@@ -895,7 +1054,7 @@ int pnr_adam_step_dev(float* p, const float* g, float* m, float* v, int64_t n, f
   return launch_adam_dev(p, g, m, v, n, lr, beta1, beta2, eps, step_count, (hipStream_t)stream);
 }
 
-size_t pnr_map_loss_workspace_bytes(void) { return 256 * sizeof(double); }
+size_t pnr_map_loss_workspace_bytes(void) { return (256 + 8) * sizeof(double); }
 
 int pnr_map_loss(const float* gt_depth, const double* depth, const float* gt_color, const float* color, int64_t n,
                  float w_color, const float* sigma, int64_t n_sigma, float w_reg, double* loss, double* g_depth,
@@ -905,6 +1064,16 @@ int pnr_map_loss(const float* gt_depth, const double* depth, const float* gt_col
   if (n_sigma > 0 && (!sigma || !g_sigma)) return PNR_E_ARG;
   return launch_map_loss(gt_depth, depth, gt_color, color, n, w_color, sigma, n_sigma, w_reg,
                          static_cast<double*>(workspace), loss, g_depth, g_color, g_sigma, (hipStream_t)stream);
+}
+
+int pnr_adam_multi_dev(float* p, const float* g, int32_t n_seg, const int64_t* seg_offset, const int64_t* seg_n,
+                       float* const* m, float* const* v, const float* seg_lr, float beta1, float beta2, float eps,
+                       int32_t* step2, void* stream) {
+  if (!p || !g || !seg_offset || !seg_n || !m || !v || !seg_lr || !step2 || n_seg < 1 || n_seg > 4) return PNR_E_ARG;
+  for (int q = 0; q < n_seg; ++q)
+    if (seg_n[q] < 0 || seg_offset[q] < 0 || (seg_n[q] > 0 && (!m[q] || !v[q]))) return PNR_E_ARG;
+  return launch_adam_multi(p, g, n_seg, seg_offset, seg_n, m, v, seg_lr, beta1, beta2, eps, step2,
+                           (hipStream_t)stream);
 }
 
 int pnr_step_advance(int32_t* step_count, void* stream) {

@@ -307,6 +307,7 @@ static void launch_fwd_mode(int mode, dim3 grid, dim3 block, hipStream_t st, con
     case kPtsF64: hipLaunchKernelGGL((k_mlp_fwd<kPtsF64, HASC>), grid, block, 0, st, a); break;
     case kPtsF32: hipLaunchKernelGGL((k_mlp_fwd<kPtsF32, HASC>), grid, block, 0, st, a); break;
     case kRaysZ64: hipLaunchKernelGGL((k_mlp_fwd<kRaysZ64, HASC>), grid, block, 0, st, a); break;
+    case kPtsX4: hipLaunchKernelGGL((k_mlp_fwd<kPtsX4, HASC>), grid, block, 0, st, a); break;
     default: hipLaunchKernelGGL((k_mlp_fwd<kRaysZ32, HASC>), grid, block, 0, st, a); break;
   }
 }
@@ -314,7 +315,7 @@ static void launch_fwd_mode(int mode, dim3 grid, dim3 block, hipStream_t st, con
 int launch_mlp_fwd(const float* packed, const PointSrc& src, int mode, int64_t P, float* raw,
                    const SaveArgs* save, hipStream_t st, const FeatArgs* feat) {
   if (P <= 0) return 0;
-  if (mode < kPtsF64 || mode > kRaysZ32) return PNR_E_ARG;
+  if (mode < kPtsF64 || mode > kPtsX4) return PNR_E_ARG;
   FwdArgs a;
   a.packed = packed;
   a.src = src;

@@ -692,6 +692,7 @@ static __device__ __forceinline__ void fwd16_tile(const BfFwdArgs& a, int mode, 
       case kPtsF64: load_point<kPtsF64>(a.src, p, x0, x1, x2, inside); break;
       case kPtsF32: load_point<kPtsF32>(a.src, p, x0, x1, x2, inside); break;
       case kRaysZ64: load_point<kRaysZ64>(a.src, p, x0, x1, x2, inside); break;
+      case kPtsX4: load_point<kPtsX4>(a.src, p, x0, x1, x2, inside); break;
       default: load_point<kRaysZ32>(a.src, p, x0, x1, x2, inside); break;
     }
   }
@@ -759,6 +760,8 @@ static __device__ __forceinline__ void fwd16_tile(const BfFwdArgs& a, int mode, 
       // no e save: the dW0 GEMM recomputes sin(x@B) from the saved x (wgrad16.hip kWgradFirstX)
       split_tile<PR>(v, S.ft[t]);
     }
+    // always issued (the step program's vmcnt counts include it); in the map pass the kPtsX4 input
+    // rows are this save, so the store rewrites the value the lane has just read
     if (SAVE && hh == 0) a.save.xP[S.col] = make_float4(x0, x1, x2, inside ? 1.f : 0.f);
   }
   PNR_TICK(1);

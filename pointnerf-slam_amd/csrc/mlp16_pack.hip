@@ -271,7 +271,7 @@ int launch_fc_pack_bf(const float* const* fcp, float* out, hipStream_t st) {
 int launch_mlp_fwd_bf(int prec, const float* packed, const PointSrc& src, int mode, int64_t P, float* raw,
                       const SaveArgs* save, hipStream_t st, const FeatArgs* feat, uint32_t* status) {
   if (P <= 0) return 0;
-  if (mode < kPtsF64 || mode > kRaysZ32) return PNR_E_ARG;
+  if (mode < kPtsF64 || mode > kPtsX4) return PNR_E_ARG;
   if (prec != PNR_PREC_BF16X3 && prec != PNR_PREC_BF16 && prec != PNR_PREC_F16X3) return PNR_E_ARG;
   BfFwdArgs a;
   a.wmain = reinterpret_cast<const char*>(packed + main_off_floats(prec));

@@ -75,6 +75,8 @@ enum PointMode : int {
   kPtsF32 = 1,      // explicit float32 points (MLP.forward on f32 / masked in f32)
   kRaysZ64 = 2,     // p = o + d * z, z float64 (render_batch_ray)
   kRaysZ32 = 3,     // p = o + d * z, z float32 (regulation)
+  kPtsX4 = 4,       // float4 (x, y, z, inside) rows written by the ray kernels of the map pass (k_map_pts,
+                    // k_pdf): the point and its bound test already evaluated in the reference's dtype
 };
 
 struct PointSrc {
@@ -112,6 +114,10 @@ __device__ __forceinline__ void load_point(const PointSrc& s, int64_t p, float& 
       inside = (q0 < s.bound[1]) && (q0 > s.bound[0]) && (q1 < s.bound[3]) && (q1 > s.bound[2]) &&
                (q2 < s.bound[5]) && (q2 > s.bound[4]);
     x0 = (float)q0; x1 = (float)q1; x2 = (float)q2;
+  } else if (MODE == kPtsX4) {
+    const float4 v = reinterpret_cast<const float4*>(s.pts)[p];
+    x0 = v.x; x1 = v.y; x2 = v.z;
+    inside = v.w != 0.f;
   } else {
     if (MODE == kPtsF32) {
       const float* pp = reinterpret_cast<const float*>(s.pts) + p * 3;
@@ -253,7 +259,11 @@ struct WgradSyn {
   // kWgradHidden / kWgradFirstX with the feature branch: A is the UNMASKED dL/dh_l (the delta chain
   // stores no delta there) and the GEMM applies the forward's ReLU mask words of that layer itself
   const uint4* amasks;  // mask words of h_l's layer (SaveArgs::masks + (l - 1) x ld / 32 x 64) or null
+  // GEMMs that will share one grouped launch (launch_wgrad16_group), 0 = a launch of its own: the
+  // split-K grid is sized so that the group fills the chip about once
+  int group_jobs;
 };
+int wgrad_wgs_per_cu();
 // Arguments of one split weight-gradient GEMM (wgrad16.hip k_wgrad16)
 struct WxArgs {
   const float* A;      // [K][256]

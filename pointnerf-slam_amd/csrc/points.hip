@@ -1192,6 +1192,7 @@ static void gather_probe(int mode, dim3 grid, hipStream_t st, const GatherArgs& 
     case kPtsF64: hipLaunchKernelGGL((k_gather_probe<kPtsF64>), grid, dim3(256), 0, st, a); break;
     case kPtsF32: hipLaunchKernelGGL((k_gather_probe<kPtsF32>), grid, dim3(256), 0, st, a); break;
     case kRaysZ64: hipLaunchKernelGGL((k_gather_probe<kRaysZ64>), grid, dim3(256), 0, st, a); break;
+    case kPtsX4: hipLaunchKernelGGL((k_gather_probe<kPtsX4>), grid, dim3(256), 0, st, a); break;
     default: hipLaunchKernelGGL((k_gather_probe<kRaysZ32>), grid, dim3(256), 0, st, a); break;
   }
 }
@@ -1235,7 +1236,7 @@ size_t gather_bwd_workspace_bytes(int64_t P, int64_t M, bool feats) {
 
 int launch_gather(const pnr_points& pts, const PointSrc& src, int mode, int64_t P, int64_t rows, float* c,
                   int32_t* idx, float* w, void* ws, size_t ws_bytes, hipStream_t st) {
-  if (!points_ok(pts) || mode < kPtsF64 || mode > kRaysZ32 || P < 0 || rows < P || P >= (1ll << 31)) return PNR_E_ARG;
+  if (!points_ok(pts) || mode < kPtsF64 || mode > kPtsX4 || P < 0 || rows < P || P >= (1ll << 31)) return PNR_E_ARG;
   if (rows == 0) return PNR_OK;
   if (!ws || ws_bytes < gather_workspace_bytes(P)) return PNR_E_WORKSPACE;
   IndexView v = index_view(pts.index, pts.n_points, pts.table_bits, nullptr);
@@ -1303,6 +1304,7 @@ static void gather_bwd_mode(int mode, int64_t tasks, hipStream_t st, const Gathe
     case kPtsF64: gather_bwd_launch<kPtsF64, KER>(tasks, st, a); break;
     case kPtsF32: gather_bwd_launch<kPtsF32, KER>(tasks, st, a); break;
     case kRaysZ64: gather_bwd_launch<kRaysZ64, KER>(tasks, st, a); break;
+    case kPtsX4: gather_bwd_launch<kPtsX4, KER>(tasks, st, a); break;
     default: gather_bwd_launch<kRaysZ32, KER>(tasks, st, a); break;
   }
 }
@@ -1310,7 +1312,7 @@ static void gather_bwd_mode(int mode, int64_t tasks, hipStream_t st, const Gathe
 int launch_gather_bwd(const pnr_points& pts, const PointSrc* src, int mode, const float4* xP, int64_t P,
                       const int32_t* idx, const float* w, const float* c, const float* g_c, float* g_p,
                       bool gp_accum, void* ws, size_t ws_bytes, hipStream_t st) {
-  if (!points_ok(pts) || P < 0 || (!src && !xP) || mode < kPtsF64 || mode > kRaysZ32 || P >= (1ll << 31))
+  if (!points_ok(pts) || P < 0 || (!src && !xP) || mode < kPtsF64 || mode > kPtsX4 || P >= (1ll << 31))
     return PNR_E_ARG;
   if (P == 0 || (!pts.g_feats && !g_p)) return PNR_OK;
   if (!idx || !w || !g_c || (g_p && !c)) return PNR_E_ARG;

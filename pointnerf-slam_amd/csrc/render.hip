@@ -98,6 +98,91 @@ __global__ void k_coarse_z(pnr_render_params prm, const float* __restrict__ ro, 
   }
 }
 
+// Cooperative staging of a 64-ray block's per-sample rows into LDS: the block's rows of a ray-major
+// array (ray n, sample m at src[n * cnt + m]) are contiguous, so the block reads them with coalesced
+// loads (64 lanes, consecutive elements) and writes them transposed, dst[m * 64 + ray], where each
+// thread later finds its own ray's samples at a stride of 64 (conflict-free).  Thread-per-ray loads
+// through a sort order were dependent global round trips: ~0.5 us each, 44 per ray.
+template <typename T>
+__device__ __forceinline__ void stage_rows(const T* __restrict__ src, int cnt, int64_t ray0, int64_t n_rays, T* dst) {
+  const int64_t nr = n_rays - ray0 < 64 ? n_rays - ray0 : 64;
+  const int64_t tot = nr * cnt;
+  const T* s = src + ray0 * cnt;
+  for (int64_t e = threadIdx.x; e < tot; e += 64) {
+    const int r = (int)(e / cnt), m = (int)(e - (int64_t)r * cnt);
+    dst[m * 64 + r] = s[e];
+  }
+}
+
+// Map pass (pnr_map_fwd): the rows of MLP launch A, one thread per row, points and bound tests in
+// the reference's dtypes (the arithmetic of k_reg_z + load_point<kRaysZ32> and of k_coarse_z +
+// load_point<kRaysZ64>, expression for expression):
+//   rows [0, n S)        regulation samples (Renderer.py:280-298): float32 z in [0, 0.85 gt] jittered,
+//                        float32 points and bound test;
+//   rows [pr, pr + n S)  the render's coarse samples (Renderer.py:90-116, 157-182): near/far with the
+//                        batch far clamp, float64 stratified z (also written to zc for k_pdf / k_fine),
+//                        float64 points and bound test;
+//   other rows < rows    padding: (0, 0, 0, outside).
+// x4 row = (x, y, z, inside ? 1 : 0) float32: the MLP input (kPtsX4) and its saved copy at once.
+__global__ void k_map_pts(pnr_render_params prm, const float* __restrict__ ro, const float* __restrict__ rd,
+                          const float* __restrict__ gt, const float* __restrict__ t_rand,
+                          const float* __restrict__ gmax, int64_t n_rays, int64_t pr, int64_t rows,
+                          double* __restrict__ zc, double* __restrict__ far_out, float4* __restrict__ x4) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= rows) return;
+  const int S = prm.n_samples;
+  float4 out = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (e < n_rays * S) {  // regulation (k_reg_z, load_point<kRaysZ32>)
+    const int64_t n = e / S;
+    const int s = (int)(e - n * S);
+    const float far = gt[n] * 0.85f;
+    auto z0 = [&](int k) { return (0.0f * (1.f - prm.t_vals[k])) + far * prm.t_vals[k]; };
+    const float zs = z0(s);
+    const float lower = s > 0 ? .5f * (zs + z0(s - 1)) : zs;
+    const float upper = s < S - 1 ? .5f * (z0(s + 1) + zs) : zs;
+    const float z = lower + (upper - lower) * t_rand[e];
+    const float x0 = ro[n * 3 + 0] + rd[n * 3 + 0] * z;
+    const float x1 = ro[n * 3 + 1] + rd[n * 3 + 1] * z;
+    const float x2 = ro[n * 3 + 2] + rd[n * 3 + 2] * z;
+    const bool inside = (x0 < (float)prm.bound[1]) && (x0 > (float)prm.bound[0]) && (x1 < (float)prm.bound[3]) &&
+                        (x1 > (float)prm.bound[2]) && (x2 < (float)prm.bound[5]) && (x2 > (float)prm.bound[4]);
+    out = make_float4(x0, x1, x2, inside ? 1.f : 0.f);
+  } else if (e >= pr && e < pr + n_rays * S) {  // render coarse (k_coarse_z, load_point<kRaysZ64>)
+    const int64_t q = e - pr;
+    const int64_t n = q / S;
+    const int s = (int)(q - n * S);
+    double fb = 0.0;
+    for (int a = 0; a < 3; ++a) {
+      const double o = (double)ro[n * 3 + a], d = (double)rd[n * 3 + a];
+      const double t0 = (prm.bound[2 * a] - o) / d;
+      const double t1 = (prm.bound[2 * a + 1] - o) / d;
+      const double mx = max_nan(t0, t1);
+      fb = a == 0 ? mx : min_nan(fb, mx);
+    }
+    fb = fb + 0.01;
+    const double hi = prm.far_mode == 1 ? prm.far_clamp : (double)(*gmax);
+    double far = fb != fb ? fb : (fb < 0.0 ? 0.0 : fb);  // clamp(min=0)
+    far = far != far ? far : (far > hi ? hi : far);
+    const float nearf = gt[n] * 0.01f;
+    if (s == 0 && far_out) far_out[n] = far;
+    const float t = prm.t_vals[s];
+    double zz;
+    if (!prm.lindisp) {
+      zz = (double)(nearf * (1.f - t)) + far * (double)t;
+    } else {
+      zz = 1.0 / ((double)((1.f / nearf) * (1.f - t)) + (1.0 / far) * (double)t);
+    }
+    zc[q] = zz;
+    const double q0 = (double)ro[n * 3 + 0] + (double)rd[n * 3 + 0] * zz;
+    const double q1 = (double)ro[n * 3 + 1] + (double)rd[n * 3 + 1] * zz;
+    const double q2 = (double)ro[n * 3 + 2] + (double)rd[n * 3 + 2] * zz;
+    const bool inside = (q0 < prm.bound[1]) && (q0 > prm.bound[0]) && (q1 < prm.bound[3]) && (q1 > prm.bound[2]) &&
+                        (q2 < prm.bound[5]) && (q2 > prm.bound[4]);
+    out = make_float4((float)q0, (float)q1, (float)q2, inside ? 1.f : 0.f);
+  }
+  x4[e] = out;
+}
+
 // ---------------------------------------------------------------------------------------------
 // coarse weights -> sample_pdf -> z_samples (N, I) float64
 // The ray kernels below run one thread per ray; at the Mapper's batch (1,000 rays: 16 waves) every
@@ -105,25 +190,62 @@ __global__ void k_coarse_z(pnr_render_params prm, const float* __restrict__ ro, 
 // config's sample counts (32 + 12): the loops unroll, so a ray's loads are all in flight at once
 // (with runtime counts they went out one sample at a time).  The arithmetic and its order are the
 // same in both forms.
-template <int SS, int II>
+// Map pass extras (MapPts, null outside pnr_map_fwd): the importance samples' kPtsX4 rows (float64
+// points and bound test, load_point<kRaysZ64>), the regulation rows' densities copied out of the MLP
+// launch (Renderer.py:299-300: sigma = raw[..., -1]), and the importance segment's padding rows zeroed.
+struct MapPts {
+  const float* ro;
+  float4* x4i;          // importance rows
+  int64_t x4i_pad;      // padding rows after the n I importance rows
+  const float4* rawr;   // regulation rows of launch A
+  float* sigma;         // (n, S) regulation densities
+};
+// STG (launches of at most a few hundred blocks: the Mapper's 1,000-ray batch): the block's coarse
+// depths and densities are first staged into LDS by coalesced loads (stage_rows); a thread per ray
+// then reads LDS only.  Large launches keep the per-thread loads and their occupancy (48 KB less LDS).
+template <int SS, int II, bool STG>
 __global__ __launch_bounds__(64) void k_pdf(pnr_render_params prm, const float* __restrict__ rd,
                                             const double* __restrict__ zc, const float4* __restrict__ rawc,
-                                            int64_t n_rays, double* __restrict__ zi) {
+                                            int64_t n_rays, double* __restrict__ zi, MapPts mp) {
   __shared__ float wl[PNR_MAX_SAMPLES][64];
   __shared__ float cdf[PNR_MAX_SAMPLES][64];
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  double (*zl)[64] = reinterpret_cast<double (*)[64]>(smem);                        // [S][64] (STG)
+  float (*sl)[64] = reinterpret_cast<float (*)[64]>(smem + PNR_MAX_SAMPLES * 64 * 8);  // [S][64] (STG)
   const int tid = threadIdx.x;
-  const int64_t n = (int64_t)blockIdx.x * 64 + tid;
-  if (n >= n_rays) return;
+  const int64_t ray0 = (int64_t)blockIdx.x * 64, n = ray0 + tid;
   const int S = SS > 0 ? SS : prm.n_samples, I = II > 0 ? II : prm.n_importance;
+  if (mp.x4i) {  // the importance launch's padding rows: outside points at x = 0
+    for (int64_t i = n; i < mp.x4i_pad; i += (int64_t)gridDim.x * 64)
+      mp.x4i[n_rays * I + i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  {
+    const int64_t nr = n_rays - ray0 < 64 ? n_rays - ray0 : 64;
+    if (mp.sigma) {  // the regulation densities of the block's rays: coalesced copy
+      for (int64_t e = tid; e < nr * S; e += 64) mp.sigma[ray0 * S + e] = mp.rawr[ray0 * S + e].w;
+    }
+    if constexpr (STG) {
+      stage_rows(zc, S, ray0, n_rays, &zl[0][0]);
+      const float4* rb = rawc + ray0 * S;
+      for (int64_t e = tid; e < nr * S; e += 64) {
+        const int r = (int)(e / S), m = (int)(e - (int64_t)r * S);
+        sl[m][r] = rb[e].w;
+      }
+      __syncthreads();
+    }
+  }
+  if (n >= n_rays) return;
   const double* z = zc + n * S;
   const float4* raw = rawc + n * S;
+  auto zq = [&](int q) -> double { if constexpr (STG) return zl[q][tid]; else return z[q]; };
+  auto sq = [&](int q) -> float { if constexpr (STG) return sl[q][tid]; else return raw[q].w; };
   const float nrm = ray_norm(rd + n * 3);
   double T = 1.0;
 #pragma unroll
   for (int q = 0; q < S; ++q) {
-    const float dz = q < S - 1 ? (float)(z[q + 1] - z[q]) : 1e10f;
+    const float dz = q < S - 1 ? (float)(zq(q + 1) - zq(q)) : 1e10f;
     const float delta = dz * nrm;
-    const float a = 1.f - expf(-relu(raw[q].w) * delta);
+    const float a = 1.f - expf(-relu(sq(q)) * delta);
     wl[q][tid] = a * (float)T;
     T *= (double)(1.f - a + 1e-10f);
   }
@@ -152,9 +274,18 @@ __global__ __launch_bounds__(64) void k_pdf(pnr_render_params prm, const float* 
     float denom = c1 - c0;
     if (denom < 1e-5f) denom = 1.f;
     const float t = (u - c0) / denom;
-    const double b0 = .5 * (z[below + 1] + z[below]);
-    const double b1 = .5 * (z[above + 1] + z[above]);
-    zi[n * I + k] = b0 + (double)t * (b1 - b0);
+    const double b0 = .5 * (zq(below + 1) + zq(below));
+    const double b1 = .5 * (zq(above + 1) + zq(above));
+    const double zz = b0 + (double)t * (b1 - b0);
+    zi[n * I + k] = zz;
+    if (mp.x4i) {  // load_point<kRaysZ64> of the importance sample
+      const double q0 = (double)mp.ro[n * 3 + 0] + (double)rd[n * 3 + 0] * zz;
+      const double q1 = (double)mp.ro[n * 3 + 1] + (double)rd[n * 3 + 1] * zz;
+      const double q2 = (double)mp.ro[n * 3 + 2] + (double)rd[n * 3 + 2] * zz;
+      const bool inside = (q0 < prm.bound[1]) && (q0 > prm.bound[0]) && (q1 < prm.bound[3]) && (q1 > prm.bound[2]) &&
+                          (q2 < prm.bound[5]) && (q2 > prm.bound[4]);
+      mp.x4i[n * I + k] = make_float4((float)q0, (float)q1, (float)q2, inside ? 1.f : 0.f);
+    }
   }
 }
 
@@ -168,30 +299,26 @@ __device__ __forceinline__ bool eq_nan(double a, double b) { return (a == b) || 
 // each non-decreasing unless far < near or a value is NaN: then a stable merge gives exactly that
 // order in O(S+I); otherwise the rank sort below does.
 template <int SS, int II>
-__device__ __forceinline__ void sort_ray(const double* zc, const double* zi, int S, int I, double (*zl)[64],
-                                         uint8_t (*ord)[64], int tid) {
+__device__ __forceinline__ void sort_ray(double (*zl)[64], int S, int I, uint8_t (*ord)[64], int tid) {
   if (SS > 0) S = SS;
   if (II > 0) I = II;
   const int M = S + I;
+  // zl[m][tid]: the ray's depths in natural order (coarse 0..S-1, importance S..M-1), staged
   bool sorted = true;
-  double prev = zc[0];
-  zl[0][tid] = prev;
+  double prev = zl[0][tid];
   sorted = prev == prev;
 #pragma unroll
   for (int m = 1; m < S; ++m) {
-    const double v = zc[m];
-    zl[m][tid] = v;
+    const double v = zl[m][tid];
     sorted = sorted && prev <= v;  // false for NaN
     prev = v;
   }
   if (I > 0) {
-    prev = zi[0];
-    zl[S][tid] = prev;
+    prev = zl[S][tid];
     sorted = sorted && prev == prev;
 #pragma unroll
     for (int k = 1; k < I; ++k) {
-      const double v = zi[k];
-      zl[S + k][tid] = v;
+      const double v = zl[S + k][tid];
       sorted = sorted && prev <= v;
       prev = v;
     }
@@ -218,7 +345,7 @@ __device__ __forceinline__ void sort_ray(const double* zc, const double* zi, int
 }
 
 // final pass: depth/var (float64), rgb (float32); saves the sort order for the backward
-template <int SS, int II>
+template <int SS, int II, bool STG>
 __global__ __launch_bounds__(64) void k_fine(pnr_render_params prm, const float* __restrict__ rd,
                                              const double* __restrict__ zc, const double* __restrict__ zi,
                                              const float4* __restrict__ rawc, const float4* __restrict__ rawi,
@@ -227,11 +354,27 @@ __global__ __launch_bounds__(64) void k_fine(pnr_render_params prm, const float*
   __shared__ double zl[PNR_MAX_SAMPLES][64];
   __shared__ uint8_t ord[PNR_MAX_SAMPLES][64];
   __shared__ float wl[PNR_MAX_SAMPLES][64];
+  // STG: the block's raw rows, natural order (coarse, importance), staged like the depths (k_pdf)
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float4 (*rl)[64] = reinterpret_cast<float4 (*)[64]>(smem);
   const int tid = threadIdx.x;
-  const int64_t n = (int64_t)blockIdx.x * 64 + tid;
-  if (n >= n_rays) return;
+  const int64_t ray0 = (int64_t)blockIdx.x * 64, n = ray0 + tid;
   const int S = SS > 0 ? SS : prm.n_samples, I = II > 0 ? II : prm.n_importance, M = S + I;
-  sort_ray<SS, II>(zc + n * S, zi + n * I, S, I, zl, ord, tid);
+  if constexpr (STG) {
+    stage_rows(zc, S, ray0, n_rays, &zl[0][0]);
+    stage_rows(zi, I, ray0, n_rays, &zl[S][0]);
+    stage_rows(rawc, S, ray0, n_rays, &rl[0][0]);
+    stage_rows(rawi, I, ray0, n_rays, &rl[S][0]);
+    __syncthreads();
+  }
+  if (n >= n_rays) return;
+  if constexpr (!STG) {  // the ray's depths, natural order
+#pragma unroll
+    for (int m = 0; m < S; ++m) zl[m][tid] = zc[n * S + m];
+#pragma unroll
+    for (int k = 0; k < I; ++k) zl[S + k][tid] = zi[n * I + k];
+  }
+  sort_ray<SS, II>(zl, S, I, ord, tid);
   const float nrm = ray_norm(rd + n * 3);
   double T = 1.0, D = 0.0;
   float r0 = 0.f, r1 = 0.f, r2 = 0.f;
@@ -240,7 +383,9 @@ __global__ __launch_bounds__(64) void k_fine(pnr_render_params prm, const float*
     const int s = ord[q][tid];
     const double zq = zl[s][tid];
     const float dz = q < M - 1 ? (float)(zl[ord[q + 1][tid]][tid] - zq) : 1e10f;
-    const float4 c = s < S ? rawc[n * S + s] : rawi[n * I + (s - S)];
+    float4 c;
+    if constexpr (STG) c = rl[s][tid];
+    else c = s < S ? rawc[n * S + s] : rawi[n * I + (s - S)];
     const float a = 1.f - expf(-relu(c.w) * (dz * nrm));
     const float w = a * (float)T;
     T *= (double)(1.f - a + 1e-10f);
@@ -269,10 +414,19 @@ __global__ __launch_bounds__(64) void k_fine(pnr_render_params prm, const float*
   }
 }
 
+// Map pass extras of k_fine_bwd (pnr_map_bwd): the regulation rows and a third padding range
+struct MapBwd {
+  const float* g_sigma;   // (n, S) dL/dsigma of the regulation samples, or null
+  const float4* insr;     // their kPtsX4 rows (inside flags)
+  float4* gor;            // their dL/draw rows
+  float4* pad2;
+  int np2;
+};
+
 // Backward of the final compositing: writes dL/draw (float4) for every coarse and importance
 // point, sigma channel zeroed where the point was outside the bound (Renderer.py:57 assigns
 // the density, so no gradient reaches the MLP there); g_nrm[n] = dL/d|rays_d|.
-template <int SS, int II>
+template <int SS, int II, bool STG>
 __global__ __launch_bounds__(64) void k_fine_bwd(pnr_render_params prm, const float* __restrict__ rd,
                                                  const double* __restrict__ zc, const double* __restrict__ zi,
                                                  const float4* __restrict__ rawc, const float4* __restrict__ rawi,
@@ -281,7 +435,8 @@ __global__ __launch_bounds__(64) void k_fine_bwd(pnr_render_params prm, const fl
                                                  const double* __restrict__ g_depth, const double* __restrict__ g_var,
                                                  const float* __restrict__ g_rgb, float4* __restrict__ goc,
                                                  float4* __restrict__ goi, float* __restrict__ g_nrm,
-                                                 float4* __restrict__ pad0, int np0, float4* __restrict__ pad1, int np1) {
+                                                 float4* __restrict__ pad0, int np0, float4* __restrict__ pad1, int np1,
+                                                 MapBwd mb) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x;
   const int64_t n = (int64_t)blockIdx.x * 64 + tid;
@@ -291,10 +446,42 @@ __global__ __launch_bounds__(64) void k_fine_bwd(pnr_render_params prm, const fl
   double* zs = reinterpret_cast<double*>(smem);
   float* al = reinterpret_cast<float*>(zs + M * 64);
   float* Tl = al + M * 64;
+  // STG (small launches): the block's rays' samples in natural order, staged by coalesced loads --
+  // depths, raw rows and inside flags -- so the sorted traversals below read LDS only
+  double* zn = reinterpret_cast<double*>(Tl + M * 64);
+  float4* rl = reinterpret_cast<float4*>(zn + M * 64);
+  float* il = reinterpret_cast<float*>(rl + M * 64);
+  const int64_t ray0 = (int64_t)blockIdx.x * 64;
   {  // the padding rows of the MLP launches get dL/draw = 0 (the MLP backward reads every row)
     const int64_t gi = (int64_t)blockIdx.x * 64 + tid, gs = (int64_t)gridDim.x * 64;
     for (int64_t i = gi; i < np0; i += gs) pad0[i] = make_float4(0.f, 0.f, 0.f, 0.f);
     for (int64_t i = gi; i < np1; i += gs) pad1[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int64_t i = gi; i < mb.np2; i += gs) mb.pad2[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  {
+    const int64_t nr = n_rays - ray0 < 64 ? n_rays - ray0 : 64;
+    if (mb.g_sigma) {  // map pass: the regulation rows' dL/draw (k_gout_sigma): sigma only, 0 outside the bound
+      const int S0 = SS > 0 ? SS : prm.n_samples;
+      for (int64_t e = tid; e < nr * S0; e += 64) {
+        const int64_t r = ray0 * S0 + e;
+        mb.gor[r] = make_float4(0.f, 0.f, 0.f, mb.insr[r].w != 0.f ? mb.g_sigma[r] : 0.f);
+      }
+    }
+    if constexpr (STG) {
+      stage_rows(zc, S, ray0, n_rays, zn);
+      stage_rows(zi, I, ray0, n_rays, zn + S * 64);
+      stage_rows(rawc, S, ray0, n_rays, rl);
+      stage_rows(rawi, I, ray0, n_rays, rl + S * 64);
+      for (int64_t e = tid; e < nr * S; e += 64) {
+        const int r = (int)(e / S), m = (int)(e - (int64_t)r * S);
+        il[m * 64 + r] = insc[ray0 * S + e].w;
+      }
+      for (int64_t e = tid; e < nr * I; e += 64) {
+        const int r = (int)(e / I), m = (int)(e - (int64_t)r * I);
+        il[(S + m) * 64 + r] = insi[ray0 * I + e].w;
+      }
+      __syncthreads();
+    }
   }
   if (n >= n_rays) return;
   const uint8_t* ord = ord_in + n * PNR_MAX_SAMPLES;
@@ -312,8 +499,14 @@ __global__ __launch_bounds__(64) void k_fine_bwd(pnr_render_params prm, const fl
   auto ordq = [&](int q) -> int { return SS > 0 ? (int)((ow[q >> 2] >> (8 * (q & 3))) & 0xffu) : (int)ord[q]; };
   const float* dvec = rd + n * 3;
   const float nrm = ray_norm(dvec);
-  auto zsrc = [&](int s) { return s < S ? zc[n * S + s] : zi[n * I + (s - S)]; };
-  auto rsrc = [&](int s) { return s < S ? rawc[n * S + s] : rawi[n * I + (s - S)]; };
+  auto zsrc = [&](int s) -> double {
+    if constexpr (STG) return zn[s * 64 + tid];
+    else return s < S ? zc[n * S + s] : zi[n * I + (s - S)];
+  };
+  auto rsrc = [&](int s) -> float4 {
+    if constexpr (STG) return rl[s * 64 + tid];
+    else return s < S ? rawc[n * S + s] : rawi[n * I + (s - S)];
+  };
   double T = 1.0, D = 0.0;
 #pragma unroll
   for (int q = 0; q < M; ++q) zs[q * 64 + tid] = zsrc(ordq(q));
@@ -355,7 +548,9 @@ __global__ __launch_bounds__(64) void k_fine_bwd(pnr_render_params prm, const fl
     const float sr = relu(c.w);
     const float ex = expf(-sr * delta);
     float gs = c.w > 0.f ? ga * ex * delta : 0.f;
-    const bool inside = s < S ? insc[n * S + s].w != 0.f : insi[n * I + (s - S)].w != 0.f;
+    bool inside;
+    if constexpr (STG) inside = il[s * 64 + tid] != 0.f;
+    else inside = s < S ? insc[n * S + s].w != 0.f : insi[n * I + (s - S)].w != 0.f;
     if (!inside) gs = 0.f;
     gn += (ga * ex * sr) * dz;
     const float4 go = make_float4(gr0 * w, gr1 * w, gr2 * w, gs);
@@ -441,7 +636,8 @@ __global__ __launch_bounds__(256) void k_map_loss(const float* __restrict__ gt, 
                                                   int64_t n, float w_color, const float* __restrict__ sigma,
                                                   int64_t ns, float w_reg, double* __restrict__ part,
                                                   double* __restrict__ g_depth, float* __restrict__ g_color,
-                                                  float* __restrict__ g_sigma) {
+                                                  float* __restrict__ g_sigma, uint32_t* __restrict__ ticket,
+                                                  double* __restrict__ out) {
   __shared__ double red[4];
   double acc = 0.0;
   const int64_t stride = (int64_t)gridDim.x * 256;
@@ -469,17 +665,35 @@ __global__ __launch_bounds__(256) void k_map_loss(const float* __restrict__ gt, 
   for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
   __syncthreads();
-  if (threadIdx.x == 0) part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
-}
-__global__ __launch_bounds__(256) void k_map_loss_sum(const double* __restrict__ part, int parts,
-                                                      double* __restrict__ out) {
-  __shared__ double red[4];
-  double v = (int)threadIdx.x < parts ? part[threadIdx.x] : 0.0;
+  // the block's partial, then a ticket: the block that takes the last one adds every partial in a
+  // fixed order (one launch; the sum is the same whichever block finishes last).  Hand-off per
+  // MI355X_MICROARCH.md (Valid forms): store, vmcnt(0), agent release, vmcnt(0), ticket atomic;
+  // the last block: agent acquire, vmcnt(0), barrier, plain loads.
+  __shared__ uint32_t last;
+  if (threadIdx.x == 0) {
+    part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t t = atomicAdd(ticket, 1u);
+    last = t == gridDim.x - 1 ? 1u : 0u;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  __syncthreads();
+  if (!last) return;
+  double v = (int)threadIdx.x < (int)gridDim.x ? part[threadIdx.x] : 0.0;
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  __syncthreads();
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
   __syncthreads();
-  if (threadIdx.x == 0) out[0] = (red[0] + red[1]) + (red[2] + red[3]);
+  if (threadIdx.x == 0) {
+    out[0] = (red[0] + red[1]) + (red[2] + red[3]);
+    *ticket = 0u;  // zero again for the next call on this workspace
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -571,6 +785,50 @@ __global__ void k_adam_dev(float* __restrict__ p, const float* __restrict__ g, f
   const float denom = sqrtf(vi) / bc2_sqrt + eps;
   p[i] = p[i] + (-step_size) * (mi / denom);
 }
+// Adam over up to kAdamSegs learning-rate segments of one flat buffer in ONE launch (block ranges per
+// segment), the step read on the device (step2[0] + 1) and advanced by the block that takes the last
+// ticket (step2[1], zero between launches): every block has read the step before its ticket.
+constexpr int kAdamSegs = 4;
+struct AdamSegs {
+  int64_t off[kAdamSegs], n[kAdamSegs];
+  float* m[kAdamSegs];
+  float* v[kAdamSegs];
+  float lr[kAdamSegs];
+  int first[kAdamSegs + 1];  // first block of each segment
+  int nseg;
+};
+__global__ __launch_bounds__(256) void k_adam_multi(float* __restrict__ p, const float* __restrict__ g, AdamSegs S,
+                                                    float beta1, float beta2, float eps, int32_t* __restrict__ step2) {
+  int q = 0;
+  while (q + 1 < S.nseg && (int)blockIdx.x >= S.first[q + 1]) ++q;
+  const int64_t i0 = (int64_t)((int)blockIdx.x - S.first[q]) * 256 + threadIdx.x;
+  const int64_t stride = (int64_t)(S.first[q + 1] - S.first[q]) * 256;
+  const int32_t step = step2[0];
+  const double t = (double)(step + 1);
+  const double bc1 = 1.0 - pow((double)beta1, t), bc2 = 1.0 - pow((double)beta2, t);
+  const float step_size = (float)((double)S.lr[q] / bc1);
+  const float bc2_sqrt = (float)sqrt(bc2);
+  for (int64_t i = i0; i < S.n[q]; i += stride) {
+    const int64_t k = S.off[q] + i;
+    const float gi = g[k];
+    float mi = S.m[q][i];
+    mi = mi + (1.f - beta1) * (gi - mi);
+    float vi = S.v[q][i] * beta2 + (1.f - beta2) * gi * gi;
+    S.m[q][i] = mi;
+    S.v[q][i] = vi;
+    const float denom = sqrtf(vi) / bc2_sqrt + eps;
+    p[k] = p[k] + (-step_size) * (mi / denom);
+  }
+  __syncthreads();  // the block's step reads come before its ticket
+  if (threadIdx.x == 0) {
+    const uint32_t t = atomicAdd(reinterpret_cast<uint32_t*>(step2 + 1), 1u);
+    if (t == gridDim.x - 1) {
+      step2[0] = step + 1;
+      step2[1] = 0;
+    }
+  }
+}
+
 __global__ void k_step_advance(int32_t* step_count) {
   if (threadIdx.x == 0) atomicAdd(step_count, 1);
 }
@@ -579,6 +837,9 @@ __global__ void k_step_advance(int32_t* step_count) {
 // launchers
 // ---------------------------------------------------------------------------------------------
 static inline unsigned nblk(int64_t n, int b) { return (unsigned)((n + b - 1) / b); }
+// ray launches of at most this many rays (a block per CU or fewer) stage their rows through LDS
+// (k_pdf / k_fine / k_fine_bwd STG): they are latency-bound, not occupancy-bound
+constexpr int64_t kStageRays = 16384;
 
 int launch_gt_max(const float* gt, int64_t n, float* out, hipStream_t st) {
   const int parts = (int)std::min<int64_t>(kGtParts, std::max<int64_t>(1, (n + 4095) / 4096));
@@ -593,42 +854,71 @@ int launch_coarse_z(const pnr_render_params& prm, const float* ro, const float* 
   return hip_status(hipGetLastError());
 }
 int launch_pdf(const pnr_render_params& prm, const float* rd, const double* zc, const float* rawc, int64_t n,
-               double* zi, hipStream_t st) {
+               double* zi, hipStream_t st, const float* ro = nullptr, float* x4i = nullptr, int64_t x4i_pad = 0,
+               const float* rawr = nullptr, float* sigma = nullptr) {
   if (n <= 0) return 0;
-  if (prm.n_samples == 32 && prm.n_importance == 12)  // the config's counts (configs/pointNeRF_slam.yaml)
-    hipLaunchKernelGGL((k_pdf<32, 12>), dim3(nblk(n, 64)), dim3(64), 0, st, prm, rd, zc, (const float4*)rawc, n, zi);
-  else
-    hipLaunchKernelGGL((k_pdf<0, 0>), dim3(nblk(n, 64)), dim3(64), 0, st, prm, rd, zc, (const float4*)rawc, n, zi);
+  const MapPts mp{ro, reinterpret_cast<float4*>(x4i), x4i_pad, reinterpret_cast<const float4*>(rawr), sigma};
+  const bool stg = n <= kStageRays;
+  const size_t sh = stg ? (size_t)PNR_MAX_SAMPLES * 64 * (8 + 4) : 0;
+  const bool cfg = prm.n_samples == 32 && prm.n_importance == 12;  // the config's counts (pointNeRF_slam.yaml)
+  const dim3 g(nblk(n, 64)), b(64);
+  if (cfg && stg) hipLaunchKernelGGL((k_pdf<32, 12, true>), g, b, sh, st, prm, rd, zc, (const float4*)rawc, n, zi, mp);
+  else if (cfg) hipLaunchKernelGGL((k_pdf<32, 12, false>), g, b, 0, st, prm, rd, zc, (const float4*)rawc, n, zi, mp);
+  else if (stg) hipLaunchKernelGGL((k_pdf<0, 0, true>), g, b, sh, st, prm, rd, zc, (const float4*)rawc, n, zi, mp);
+  else hipLaunchKernelGGL((k_pdf<0, 0, false>), g, b, 0, st, prm, rd, zc, (const float4*)rawc, n, zi, mp);
+  return hip_status(hipGetLastError());
+}
+int launch_map_pts(const pnr_render_params& prm, const float* ro, const float* rd, const float* gt, const float* t_rand,
+                   const float* gmax, int64_t n, int64_t pr, int64_t rows, double* zc, double* far_out, float* x4,
+                   hipStream_t st) {
+  if (rows <= 0) return 0;
+  hipLaunchKernelGGL(k_map_pts, dim3(nblk(rows, 256)), dim3(256), 0, st, prm, ro, rd, gt, t_rand, gmax, n, pr, rows, zc,
+                     far_out, (float4*)x4);
   return hip_status(hipGetLastError());
 }
 int launch_fine(const pnr_render_params& prm, const float* rd, const double* zc, const double* zi,
                 const float* rawc, const float* rawi, int64_t n, double* depth, double* var, float* rgb,
                 uint8_t* ord, hipStream_t st) {
   if (n <= 0) return 0;
-  if (prm.n_samples == 32 && prm.n_importance == 12)
-    hipLaunchKernelGGL((k_fine<32, 12>), dim3(nblk(n, 64)), dim3(64), 0, st, prm, rd, zc, zi, (const float4*)rawc,
-                       (const float4*)rawi, n, depth, var, rgb, ord);
-  else
-    hipLaunchKernelGGL((k_fine<0, 0>), dim3(nblk(n, 64)), dim3(64), 0, st, prm, rd, zc, zi, (const float4*)rawc,
-                       (const float4*)rawi, n, depth, var, rgb, ord);
+  const bool stg = n <= kStageRays;
+  const size_t sh = stg ? (size_t)(prm.n_samples + prm.n_importance) * 64 * 16 : 0;
+  const bool cfg = prm.n_samples == 32 && prm.n_importance == 12;
+  const dim3 g(nblk(n, 64)), b(64);
+  const float4 *rc = (const float4*)rawc, *ri = (const float4*)rawi;
+  if (cfg && stg) hipLaunchKernelGGL((k_fine<32, 12, true>), g, b, sh, st, prm, rd, zc, zi, rc, ri, n, depth, var, rgb, ord);
+  else if (cfg) hipLaunchKernelGGL((k_fine<32, 12, false>), g, b, 0, st, prm, rd, zc, zi, rc, ri, n, depth, var, rgb, ord);
+  else if (stg) hipLaunchKernelGGL((k_fine<0, 0, true>), g, b, sh, st, prm, rd, zc, zi, rc, ri, n, depth, var, rgb, ord);
+  else hipLaunchKernelGGL((k_fine<0, 0, false>), g, b, 0, st, prm, rd, zc, zi, rc, ri, n, depth, var, rgb, ord);
   return hip_status(hipGetLastError());
 }
 int launch_fine_bwd(const pnr_render_params& prm, const float* rd, const double* zc, const double* zi,
                     const float* rawc, const float* rawi, const float4* insc, const float4* insi,
                     const uint8_t* ord, int64_t n, const double* gd, const double* gv, const float* grgb,
                     float* goc, float* goi, float* g_nrm, float* pad0, int np0, float* pad1, int np1,
-                    hipStream_t st) {
+                    hipStream_t st, const float* g_sigma = nullptr, const float4* insr = nullptr,
+                    float* gor = nullptr, float* pad2 = nullptr, int np2 = 0) {
   if (n <= 0) return 0;
   const int M = prm.n_samples + prm.n_importance;
-  const size_t sh = (size_t)M * 64 * (8 + 2 * 4);
-  if (prm.n_samples == 32 && prm.n_importance == 12)
-    hipLaunchKernelGGL((k_fine_bwd<32, 12>), dim3(nblk(n, 64)), dim3(64), sh, st, prm, rd, zc, zi, (const float4*)rawc,
-                       (const float4*)rawi, insc, insi, ord, n, gd, gv, grgb, (float4*)goc, (float4*)goi, g_nrm,
-                       (float4*)pad0, np0, (float4*)pad1, np1);
+  const bool stg = n <= kStageRays;
+  // z sorted (8), alpha and T (4 + 4); staged: z (8), raw (16), inside flags (4) in natural order
+  const size_t sh = (size_t)M * 64 * (8 + 2 * 4 + (stg ? 8 + 16 + 4 : 0));
+  const MapBwd mb{g_sigma, insr, reinterpret_cast<float4*>(gor), reinterpret_cast<float4*>(pad2), np2};
+  const bool cfg = prm.n_samples == 32 && prm.n_importance == 12;
+  const dim3 g(nblk(n, 64)), b(64);
+  const float4 *rc = (const float4*)rawc, *ri = (const float4*)rawi;
+  float4 *oc = (float4*)goc, *oi = (float4*)goi, *p0 = (float4*)pad0, *p1 = (float4*)pad1;
+  if (cfg && stg)
+    hipLaunchKernelGGL((k_fine_bwd<32, 12, true>), g, b, sh, st, prm, rd, zc, zi, rc, ri, insc, insi, ord, n, gd, gv, grgb,
+                       oc, oi, g_nrm, p0, np0, p1, np1, mb);
+  else if (cfg)
+    hipLaunchKernelGGL((k_fine_bwd<32, 12, false>), g, b, sh, st, prm, rd, zc, zi, rc, ri, insc, insi, ord, n, gd, gv,
+                       grgb, oc, oi, g_nrm, p0, np0, p1, np1, mb);
+  else if (stg)
+    hipLaunchKernelGGL((k_fine_bwd<0, 0, true>), g, b, sh, st, prm, rd, zc, zi, rc, ri, insc, insi, ord, n, gd, gv, grgb,
+                       oc, oi, g_nrm, p0, np0, p1, np1, mb);
   else
-    hipLaunchKernelGGL((k_fine_bwd<0, 0>), dim3(nblk(n, 64)), dim3(64), sh, st, prm, rd, zc, zi, (const float4*)rawc,
-                       (const float4*)rawi, insc, insi, ord, n, gd, gv, grgb, (float4*)goc, (float4*)goi, g_nrm,
-                       (float4*)pad0, np0, (float4*)pad1, np1);
+    hipLaunchKernelGGL((k_fine_bwd<0, 0, false>), g, b, sh, st, prm, rd, zc, zi, rc, ri, insc, insi, ord, n, gd, gv,
+                       grgb, oc, oi, g_nrm, p0, np0, p1, np1, mb);
   return hip_status(hipGetLastError());
 }
 int launch_ray_grads_f64(const float* rd, const double* za, int sa, const double* zb, int sb, const float* gxa,
@@ -657,9 +947,10 @@ int launch_map_loss(const float* gt, const double* depth, const float* gtc, cons
   const int64_t m = n > ns ? n : ns;
   int parts = (int)((m + 1023) / 1024);
   parts = parts < 1 ? 1 : (parts > kLossParts ? kLossParts : parts);
+  // ticket word after the kLossParts partials (the workspace holds kLossParts + 8 doubles, zeroed
+  // by the caller before its first use; the kernel leaves it zero)
   hipLaunchKernelGGL(k_map_loss, dim3(parts), dim3(256), 0, st, gt, depth, gtc, col, n, w_color, sigma, ns, w_reg,
-                     part, g_depth, g_color, g_sigma);
-  hipLaunchKernelGGL(k_map_loss_sum, dim3(1), dim3(256), 0, st, part, parts, loss);
+                     part, g_depth, g_color, g_sigma, reinterpret_cast<uint32_t*>(part + kLossParts), loss);
   return hip_status(hipGetLastError());
 }
 int launch_extract_sigma(const float* raw, int64_t P, float* sigma, hipStream_t st) {
@@ -698,6 +989,29 @@ int launch_adam_dev(float* p, const float* g, float* m, float* v, int64_t n, flo
   if (n <= 0) return 0;
   hipLaunchKernelGGL(k_adam_dev, dim3(nblk(n, 256)), dim3(256), 0, st, p, g, m, v, n, lr, beta1, beta2, eps,
                      step_count);
+  return hip_status(hipGetLastError());
+}
+int launch_adam_multi(float* p, const float* g, int nseg, const int64_t* off, const int64_t* n, float* const* m,
+                      float* const* v, const float* lr, float beta1, float beta2, float eps, int32_t* step2,
+                      hipStream_t st) {
+  if (nseg < 1 || nseg > kAdamSegs) return PNR_E_ARG;
+  AdamSegs S{};
+  int blocks = 0;
+  for (int q = 0; q < nseg; ++q) {
+    S.off[q] = off[q];
+    S.n[q] = n[q];
+    S.m[q] = m[q];
+    S.v[q] = v[q];
+    S.lr[q] = lr[q];
+    S.first[q] = blocks;
+    // grid-stride over at most 64 blocks per segment: every block takes one ticket, and a ticket per
+    // 256 elements (870 for the decoder) queued on one address for ~10 us
+    const int64_t nb = nblk(n[q] > 0 ? n[q] : 1, 256);
+    blocks += (int)(nb < 64 ? nb : 64);
+  }
+  S.first[nseg] = blocks;
+  S.nseg = nseg;
+  hipLaunchKernelGGL(k_adam_multi, dim3((unsigned)blocks), dim3(256), 0, st, p, g, S, beta1, beta2, eps, step2);
   return hip_status(hipGetLastError());
 }
 int launch_step_advance(int32_t* step_count, hipStream_t st) {

@@ -37,6 +37,7 @@
 //  - One register set: tile t+1 is loaded while tile t runs its MFMAs; the LDS planes are double
 //    buffered, so one barrier per tile orders both.
 #include <cmath>
+#include <cstdlib>
 
 #include "mlp16.h"
 
@@ -532,7 +533,18 @@ int wgrad16_prepare(int kind, const float* A, const float* B, int64_t K, int64_t
   // split-K over at most one workgroup per CU, >= 8 tiles per workgroup (the flush of the partial
   // tile no longer dominates)
   if (!syn || !syn->part || !syn->part_bias) return PNR_E_ARG;
-  int64_t nwg = (K / 32 + 7) / 8;
+  // Tiles (32 points) per workgroup: >= 8, and in a grouped launch enough that the group's GEMMs fill
+  // the chip about once (one 512-thread workgroup per CU): every workgroup flushes a whole 256 x 256
+  // partial tile that k_part_reduce_multi re-reads, so at a small K (the Mapper's 1,000-ray batch:
+  // ~2,400 tiles) many short workgroups spent more on flushes and their reduction than on the GEMM.
+  const int64_t tiles = K / 32;
+  int64_t per = 8;
+  if (syn->group_jobs > 0) {
+    const int64_t slots = (int64_t)device_cu_count() * wgrad_wgs_per_cu();
+    const int64_t p2 = (tiles * syn->group_jobs + slots - 1) / slots;
+    per = p2 > per ? p2 : per;
+  }
+  int64_t nwg = (tiles + per - 1) / per;
   nwg = nwg < 4 ? 4 : (nwg > kWgrad16MaxWg ? kWgrad16MaxWg : nwg);
   int64_t ks = (K + nwg - 1) / nwg;
   ks = (ks + 31) / 32 * 32;
@@ -583,6 +595,16 @@ int wgrad16_prepare(int kind, const float* A, const float* B, int64_t K, int64_t
   job->nwg = (int)nwg;
   *red = ReduceJob{a.part, a.part_bias, (int)nwg, 256, ntb * 32, a.nb, a.C, a.ldc, a.bias};
   return 0;
+}
+
+// workgroups per CU a grouped weight-gradient launch aims at (PNR_WGRAD_WGS_PER_CU, default 1)
+int wgrad_wgs_per_cu() {
+  static const int v = [] {
+    const char* e = getenv("PNR_WGRAD_WGS_PER_CU");
+    const int x = e ? atoi(e) : 1;
+    return x >= 1 && x <= 64 ? x : 1;
+  }();
+  return v;
 }
 
 int launch_wgrad16_group(const Wgrad16Job* jobs, int n, hipStream_t st) {

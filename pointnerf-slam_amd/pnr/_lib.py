@@ -96,6 +96,12 @@ _SIGS = {
     'pnr_regulation_bwd': (ctypes.c_int, [ctypes.POINTER(RenderParams), c_void_p, c_void_p, c_void_p, c_void_p,
                                           c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t,
                                           c_void_p, c_size_t, c_void_p]),
+    'pnr_map_workspace_bytes': (c_size_t, [ctypes.POINTER(RenderParams), c_int64]),
+    'pnr_map_fwd': (ctypes.c_int, [ctypes.POINTER(RenderParams), c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                   c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
+    'pnr_map_bwd_workspace_bytes': (c_size_t, [ctypes.POINTER(RenderParams), c_int64]),
+    'pnr_map_bwd': (ctypes.c_int, [ctypes.POINTER(RenderParams), c_void_p, c_void_p, c_int64, c_void_p, c_void_p,
+                                   c_void_p, c_void_p, c_void_p, c_size_t, c_void_p, c_size_t, c_void_p]),
     'pnr_get_rays': (ctypes.c_int, [c_int32, c_int32, c_float, c_float, c_float, c_float, c_void_p, c_void_p,
                                     c_void_p, c_void_p]),
     'pnr_rays_from_uv': (ctypes.c_int, [c_void_p, c_void_p, c_int64, c_float, c_float, c_float, c_float, c_void_p,
@@ -108,6 +114,8 @@ _SIGS = {
     'pnr_adam_step_dev': (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_float, c_float,
                                          c_float, c_float, c_void_p, c_void_p]),
     'pnr_step_advance': (ctypes.c_int, [c_void_p, c_void_p]),
+    'pnr_adam_multi_dev': (ctypes.c_int, [c_void_p, c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                          c_float, c_float, c_float, c_void_p, c_void_p]),
     'pnr_map_loss_workspace_bytes': (c_size_t, []),
     'pnr_map_loss': (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_float, c_void_p, c_int64,
                                     c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),

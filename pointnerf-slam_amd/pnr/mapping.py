@@ -52,8 +52,9 @@ class FlatParams:
 class Adam:
     """torch.optim.Adam(lr, betas=(0.9, 0.999), eps=1e-8) over a FlatParams buffer, one launch per
     learning-rate segment.  `segments` = [(first word, words, lr)], default the whole buffer.
-    `use_device_step()` switches the step number to a device counter (pnr_adam_step_dev +
-    pnr_step_advance), so a step captured in a graph replays with the right bias corrections."""
+    `use_device_step()` switches the step number to a device counter (pnr_adam_multi_dev: every
+    segment and the step advance in one launch), so a step captured in a graph replays with the right
+    bias corrections."""
 
     def __init__(self, flat: FlatParams, lr: float, betas=(0.9, 0.999), eps=1e-8, on_update=None, segments=None):
         self.flat = flat
@@ -69,45 +70,53 @@ class Adam:
         self.step_dev = None  # int32 device counter of completed steps (graph mode)
 
     def use_device_step(self):
+        """step_dev = int32 {completed steps, ticket 0} on the device (pnr_adam_multi_dev): every
+        segment and the step advance in ONE launch per step."""
         if self.step_dev is None:
-            self.step_dev = torch.tensor([self.step_count], dtype=torch.int32, device=self.flat.data.device)
+            import ctypes
+            self.step_dev = torch.tensor([self.step_count, 0], dtype=torch.int32, device=self.flat.data.device)
+            k = len(self.segments)
+            self._seg_args = ((ctypes.c_int64 * k)(*[a for a, _, _ in self.segments]),
+                              (ctypes.c_int64 * k)(*[n for _, n, _ in self.segments]),
+                              (ctypes.c_void_p * k)(*[m.data_ptr() for m, _ in self.mv]),
+                              (ctypes.c_void_p * k)(*[v.data_ptr() for _, v in self.mv]),
+                              (ctypes.c_float * k)(*[lr for _, _, lr in self.segments]))
 
     def step(self):
         self.step_count += 1
         lib = _lib.load()
         f = self.flat
         st = _lib.stream_of(f.data.device)
-        for (a, n, lr), (m, v) in zip(self.segments, self.mv):
-            if self.step_dev is not None:
-                _lib.check(lib.pnr_adam_step_dev(_lib.ptr(f.data[a:]), _lib.ptr(f.grad[a:]), _lib.ptr(m),
-                                                 _lib.ptr(v), n, lr, self.b1, self.b2, self.eps,
-                                                 _lib.ptr(self.step_dev), st), 'adam_step_dev')
-            else:
+        if self.step_dev is not None:
+            off, n, m, v, lr = self._seg_args
+            _lib.check(lib.pnr_adam_multi_dev(_lib.ptr(f.data), _lib.ptr(f.grad), len(self.segments), off, n, m, v, lr,
+                                              self.b1, self.b2, self.eps, _lib.ptr(self.step_dev), st),
+                       'adam_multi_dev')
+        else:
+            for (a, n, lr), (m, v) in zip(self.segments, self.mv):
                 _lib.check(lib.pnr_adam_step(_lib.ptr(f.data[a:]), _lib.ptr(f.grad[a:]), _lib.ptr(m),
                                              _lib.ptr(v), n, lr, self.b1, self.b2, self.eps, self.step_count,
                                              st), 'adam_step')
-        if self.step_dev is not None:
-            _lib.check(lib.pnr_step_advance(_lib.ptr(self.step_dev), st), 'step_advance')
         if self.on_update is not None:  # weights changed behind autograd: drop the packed image
             self.on_update()
 
 
 class MapStep:
-    """One Mapper iteration.  The render and the regulation run as two independent chains: the
-    regulation's forward, loss term and backward on a side stream (its own gradient buffer), the
-    render's on the caller's stream; the chains join before the gradients are summed (render +
-    regulation, a fixed order) and Adam runs.  At the faithful batch (1,000 rays) every phase is
-    latency-bound and leaves CUs idle, so the two chains overlap.  Neither chain goes through
-    autograd: pnr.renderer.TrainPass calls the C ABI directly and pnr_map_loss forms the loss and its
-    gradient in one pass.  `overlap=False` runs both chains on the caller's stream; the default
-    'auto' overlaps them up to OVERLAP_MAX_RAYS rays.  Beyond that each chain fills the chip on its
-    own (the persistent MLP kernels hold every CU's LDS, so the two chains' launches only take turns)
-    and running them in order keeps each kernel's launch interval its own (bench.py times them)."""
+    """One Mapper iteration.  Default (`fused=True`): the render and the regulation are ONE decoder
+    pass (pnr.renderer.MapPass -> pnr_map_fwd / pnr_map_bwd): the regulation and coarse samples share
+    one MLP launch, the importance samples take a second, pnr_map_loss forms both loss terms and their
+    gradients in one launch, and one delta-chain / weight-gradient pass covers every sample.  (The MLP
+    kernels hold every CU's registers and LDS, so two chains on two streams could only take turns,
+    and the small ray kernels of one chain waited behind the other's MLP launches.)
+    `fused=False` keeps the two-chain form: the regulation's forward, loss term and backward on a side
+    stream with its own gradient buffer (`overlap` True / 'auto' up to OVERLAP_MAX_RAYS rays) or on the
+    caller's stream (`overlap=False`), joined before the gradients are summed (render + regulation, a
+    fixed order).  No path goes through autograd (MapStep.loss is the autograd drop-in form)."""
 
     OVERLAP_MAX_RAYS = 32768
 
     def __init__(self, renderer, decoder, lr=2e-4, w_color_loss=0.05, w_reg=0.0005, ddp=None, points=None,
-                 feat_lr=None, overlap='auto'):
+                 feat_lr=None, overlap='auto', fused=True):
         self.renderer = renderer
         self.decoder = decoder
         self.points = points
@@ -137,9 +146,18 @@ class MapStep:
         if overlap not in (True, False, 'auto'):
             raise ValueError(f'overlap must be True, False or "auto", not {overlap!r}')
         self.overlap = overlap
+        self.fused = bool(fused)
         self.side = None   # the side stream and the regulation chain's gradient buffer (same layout
         self.grad2 = None  # as flat.grad) with its views: made on the first overlapped step
         self._views = {'main': self._split(self.flat.grad)}
+
+    def _loss_ws(self, chain):
+        """The pnr_map_loss workspace of a chain's stream (zero-filled once; each call leaves it zero)."""
+        ws = self.__dict__.setdefault('_lws', {})
+        if chain not in ws:
+            from .renderer import map_loss_workspace
+            ws[chain] = map_loss_workspace(self.flat.data.device)
+        return ws[chain]
 
     def _overlaps(self, n_rays):
         if self.overlap != 'auto':
@@ -166,7 +184,7 @@ class MapStep:
         from .renderer import TrainPass, map_loss
         reg = TrainPass(self.renderer, self.c, self.decoder, 'regulation')
         (sigma,) = reg.forward(rays_o, rays_d, gt_depth, t_rand=t_rand)
-        loss, _, _, g_s = map_loss(None, None, None, None, 0.0, sigma=sigma, w_reg=self.w_reg)
+        loss, _, _, g_s = map_loss(None, None, None, None, 0.0, sigma=sigma, w_reg=self.w_reg, ws=self._loss_ws('side'))
         reg.backward(views[0], g_fc=views[1], g_feats=views[2], g_sigma=g_s)
         return loss
 
@@ -191,6 +209,15 @@ class MapStep:
             ren.feat.fc_owner.image(ren.feat.fc)
             self.points.index()
             self.points._feats_for_gather()
+        if self.fused:  # render + regulation as ONE decoder pass (pnr_map_fwd / pnr_map_bwd)
+            from .renderer import MapPass
+            mp = MapPass(r, self.c, self.decoder)
+            d, _, c, sigma = mp.forward(rays_o, rays_d, gt_depth, t_rand, far_clamp=far_clamp)
+            loss, g_d, g_c, g_s = map_loss(gt_depth, d, gt_color, c, self.w_color, sigma=sigma, w_reg=self.w_reg,
+                                           ws=self._loss_ws('main'))
+            views = self._views['main']
+            mp.backward(views[0], g_fc=views[1], g_feats=views[2], g_depth=g_d, g_rgb=g_c, g_sigma=g_s)
+            return self._finish(loss)
         main = torch.cuda.current_stream(dev)
         overlap = self._overlaps(rays_o.shape[0])
         if overlap and self.side is None:
@@ -203,7 +230,7 @@ class MapStep:
                 self.grad2.zero_()
                 l_reg = self._regulation_chain(self._views['side'], rays_o, rays_d, gt_depth, t_rand)
         d, _, c = ren.forward(rays_o, rays_d, gt_depth, far_clamp=far_clamp)
-        l_ren, g_d, g_c, _ = map_loss(gt_depth, d, gt_color, c, self.w_color)
+        l_ren, g_d, g_c, _ = map_loss(gt_depth, d, gt_color, c, self.w_color, ws=self._loss_ws('main'))
         views = self._views['main']
         ren.backward(views[0], g_fc=views[1], g_feats=views[2], g_depth=g_d, g_rgb=g_c)
         if overlap:
@@ -211,7 +238,10 @@ class MapStep:
             self.flat.grad.add_(self.grad2)  # render + regulation gradients, a fixed order
         else:
             l_reg = self._regulation_chain(views, rays_o, rays_d, gt_depth, t_rand)
-        loss = l_ren + l_reg
+        return self._finish(l_ren + l_reg)
+
+    def _finish(self, loss):
+        """The gradient exchange (data parallel) and the Adam step."""
         if self.ddp is not None and self.shard:
             self.ddp.allreduce_(self.flat.grad[:self.n_dec])
             self.ddp.reduce_scatter_(self.flat.grad[self.n_dec:])

@@ -304,16 +304,84 @@ class TrainPass:
         self.ws = self.packed = None  # release the saved activations
 
 
-def map_loss(gt_depth, depth, gt_color, color, w_color, sigma=None, w_reg=0.0):
+class MapPass:
+    """One Mapper iteration's render_batch_ray (with gt depth) AND regulation as ONE decoder pass
+    (pnr_map_fwd / pnr_map_bwd, ABI 10): the regulation and coarse samples share one MLP launch, the
+    importance samples take a second, and the backward is one delta-chain / weight-gradient pass over
+    every sample (src/Mapper.py:623-655).  Same outputs as TrainPass('render') + TrainPass('regulation')
+    bit for bit; the gradient sums differ from that pair's only in association."""
+
+    def __init__(self, renderer, c, decoders):
+        self.r = renderer
+        self.params = _decoder_params(decoders)
+        self.pts, fc_owner, extra = _feature_inputs(c, decoders)
+        self.feat = _Feat(self.pts, fc_owner, [*self.params, *extra])
+        self.packer = _packer(decoders)
+
+    def forward(self, rays_o, rays_d, gt_depth, t_rand, far_clamp=None):
+        lib = _lib.load()
+        r = self.r
+        dev = rays_o.device
+        n = rays_o.shape[0]
+        prm = r.params()
+        prm.status = r.status_word(dev).data_ptr()
+        prm.save_for_backward = 1
+        prm.need_ray_grads = 0
+        packed = self.packer.image(self.feat.params)
+        self.feat.attach(prm)
+        if isinstance(far_clamp, torch.Tensor):
+            far_clamp = far_clamp.reshape(-1)[:1].float().contiguous()
+            prm.far_mode = 2
+            prm.far_clamp_dev = far_clamp.data_ptr()
+        elif far_clamp is not None:
+            prm.far_mode = 1
+            prm.far_clamp = float(far_clamp)
+        ws = torch.empty(lib.pnr_map_workspace_bytes(ctypes_ref(prm), n), dtype=torch.uint8, device=dev)
+        depth = torch.empty(n, dtype=torch.float64, device=dev)
+        var = torch.empty(n, dtype=torch.float64, device=dev)
+        rgb = torch.empty((n, 3), dtype=torch.float32, device=dev)
+        sigma = torch.empty(n * prm.n_samples, dtype=torch.float32, device=dev)
+        _lib.check(lib.pnr_map_fwd(ctypes_ref(prm), _lib.ptr(packed), _lib.ptr(rays_o), _lib.ptr(rays_d),
+                                   _lib.ptr(gt_depth), _lib.ptr(t_rand), n, _lib.ptr(depth), _lib.ptr(var),
+                                   _lib.ptr(rgb), _lib.ptr(sigma), _lib.ptr(ws), ws.numel(), _lib.stream_of(dev)),
+                   'map_fwd')
+        prm.points = None
+        self.prm, self.ws, self.packed, self.rays = prm, ws, packed, (rays_o, rays_d, far_clamp)
+        return depth, var, rgb, sigma
+
+    def backward(self, grads, g_fc=None, g_feats=None, g_depth=None, g_rgb=None, g_sigma=None):
+        lib = _lib.load()
+        prm, ws, packed = self.prm, self.ws, self.packed
+        rays_o, rays_d, _ = self.rays
+        dev = rays_o.device
+        n = rays_o.shape[0]
+        arr = _lib.PtrArray(*[g.data_ptr() for g in grads])
+        self.feat.attach(prm, g_feats, g_fc)
+        bws = torch.empty(lib.pnr_map_bwd_workspace_bytes(ctypes_ref(prm), n), dtype=torch.uint8, device=dev)
+        _lib.check(lib.pnr_map_bwd(ctypes_ref(prm), _lib.ptr(packed), _lib.ptr(rays_d), n, _lib.ptr(g_depth),
+                                   _lib.ptr(g_rgb), _lib.ptr(g_sigma), arr, _lib.ptr(ws), ws.numel(), _lib.ptr(bws),
+                                   bws.numel(), _lib.stream_of(dev)), 'map_bwd')
+        self.ws = self.packed = None
+
+
+def map_loss_workspace(device):
+    """A zero-filled pnr_map_loss workspace (each call leaves it zero-filled: reuse it for the calls of
+    one stream; two streams need two)."""
+    return torch.zeros(_lib.load().pnr_map_loss_workspace_bytes(), dtype=torch.uint8, device=device)
+
+
+def map_loss(gt_depth, depth, gt_color, color, w_color, sigma=None, w_reg=0.0, ws=None):
     """pnr_map_loss: the Mapper loss terms (src/Mapper.py:628-655) and their gradients in one pass.
-    Returns (loss float64 0-dim, g_depth, g_color, g_sigma); either part may be None."""
+    Returns (loss float64 0-dim, g_depth, g_color, g_sigma); either part may be None.  `ws`: a
+    map_loss_workspace of the calling stream (default: a fresh zero-filled one)."""
     lib = _lib.load()
     ref = depth if depth is not None else sigma
     dev = ref.device
     n = 0 if depth is None else depth.shape[0]
     ns = 0 if sigma is None else sigma.numel()
     loss = torch.empty((), dtype=torch.float64, device=dev)
-    ws = torch.empty(lib.pnr_map_loss_workspace_bytes(), dtype=torch.uint8, device=dev)
+    if ws is None:
+        ws = map_loss_workspace(dev)
     g_d = torch.empty(n, dtype=torch.float64, device=dev) if n else None
     g_c = torch.empty((n, 3), dtype=torch.float32, device=dev) if n else None
     g_s = torch.empty(ns, dtype=torch.float32, device=dev) if ns else None

@@ -84,7 +84,7 @@ def grad_elementwise(g, cr, f32, rel_f32, what):
 
 def test_library_info(pnr_mod):
     lib = pnr_mod.library()
-    assert lib.pnr_abi_version() == 9
+    assert lib.pnr_abi_version() == 10
     assert lib.pnr_mlp_packed_floats() > 0
 
 
@@ -460,7 +460,7 @@ def test_map_graph_matches_eager(pnr_mod, dev, scene):
             for b in batches[1:]:
                 losses.append(float(ms(*b)))
         torch.cuda.synchronize()
-        runs.append((losses, ms.flat.data.detach().cpu().clone(), int(ms.opt.step_dev.item())))
+        runs.append((losses, ms.flat.data.detach().cpu().clone(), int(ms.opt.step_dev[0].item())))
     (l_e, w_e, s_e), (l_g, w_g, s_g) = runs
     assert s_e == s_g == 5
     # every weight-gradient GEMM flushes per-workgroup partials that k_part_reduce sums in a fixed

@@ -21,7 +21,9 @@ Checked on rank 0 after the first step, before Adam can amplify anything:
     step of its shard, and the 2-rank sum adds the two shard gradients once);
   * against the 1-process gradient of the whole batch it agrees elementwise to
     |g_dp - g_1| <= 1e-6 |g_1| + 1e-5 max|g_1|: the two are float32 sums of the same terms in
-    different associations (rtol 1e-6, plus an association floor for elements whose terms cancel);
+    different associations (rtol 1e-6, plus an association floor for elements whose terms cancel; the
+    f16x3 fc_c gradients, whose per-wave split scales follow the batch split, take the neural-point
+    floor 5e-4 max|g| of tests/test_gpu_points.py);
 and after all steps: every rank holds bit-identical parameters, a second 1-process run reproduces
 the first bit for bit, and the per-step losses agree.  Launched by torchrun before any GPU call; on
 a 1-GPU box both ranks share cuda:0 over gloo (RCCL needs one GPU per rank), on a node the same
@@ -198,7 +200,6 @@ def main():
         # the rounding of the partial sums, ~2^-24 x the element's sum of |terms| per level, which a
         # cancelling element does not show in |g|: a floor of 1e-5 max|g| stands for it (measured:
         # ~1e-7 max|g| on the plain decoder, ~1.3e-6 with the fc_c branch, whose dL/dh sums cancel more)
-        viol = float((dg / (1e-6 * gref + 1e-5 * gref.max() + 1e-30)).max())
         strict = float((dg > 1e-6 * gref).float().mean())
         names = ['decoder'] + (['fc_c', 'features'] if shard else [])
         cuts = [slice(0, 222747), slice(222747, n_dec)] if shard else [slice(0, n_dec)]
@@ -206,6 +207,12 @@ def main():
             cuts.append(slice(*own_f))
         per_part = {nm: float((g_first[c] - g_1[c]).abs().max() / g_1[c].abs().max().clamp_min(1e-30))
                     for nm, c in zip(names, cuts)}
+        # the fc_c weight gradients of the f16x3 split GEMMs take per-wave power-of-two scales of the
+        # point features, which depend on the points a wave sees (the batch split): the repository's
+        # neural-point gradient floor (tests/test_gpu_points.py FLIP_CAP, 5e-4 max|g|) applies there
+        floors = {'decoder': 1e-5, 'fc_c': 1e-5 if pnr._lib.DEFAULT_PRECISION == 'fp32' else 5e-4, 'features': 1e-5}
+        viol = max(float(((g_first[c] - g_1[c]).abs() / (1e-6 * g_1[c].abs() + floors[nm] * g_1[c].abs().max()
+                                                          + 1e-30)).max()) for nm, c in zip(names, cuts))
         loss_rel = [abs(x - y) / abs(y) for x, y in zip(lt.tolist(), full)]
         dw = (w_dp - w1).abs()
         res = {'case': args.case, 'world': world, 'backend': torch.distributed.get_backend(), 'global_batch': n,
@@ -216,7 +223,8 @@ def main():
                    'max_abs_diff_vs_1proc': float(dg.max()), 'max_abs_grad': float(gref.max()),
                    'frac_elements_not_equal': float((dg > 0).float().mean()),
                    'worst_ratio_to_bound': viol, 'frac_beyond_rtol_1e-6_alone': strict,
-                   'bound': '|g_dp - g_1| <= 1e-6 |g_1| + 1e-5 max|g_1| (association floor)',
+                   'bound': '|g_dp - g_1| <= 1e-6 |g_1| + floor max|g_1| per part (association floor 1e-5; '
+                            'f16x3 fc_c 5e-4, the neural-point floor)',
                    'max_abs_diff_over_max_abs_grad_per_part': per_part,
                    'checked': 'decoder' + (' + fc_c, and rank 0 owned feature range' if shard else '')},
                'weights_max_abs_diff_after_steps': float(dw.max()),
