@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Benchmark: rendered rays/s per mapping iteration (BASELINE.json metric) on MI355X.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload map|fwd|map-points] [--rays R]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload map|fwd|map-points|room0] [--rays R]
                   [--global-batch B] [--precision P] [--graph] [--no-extras] [--no-cpu-baseline]
 
 Workload `map` (default; SURVEY.md 8(d) "S-map"): one full Mapper iteration of
@@ -12,6 +12,9 @@ Adam lr 2e-4) over R rays per GPU (default 307,200 = one 640x480 pixel batch).  
 arithmetic: f16x3 by default -- fp32-class end to end (every forward and backward GEMM on 22-bit
 split operands with fp32 accumulation, include/pnr.h); `--precision fp32` runs fp32 MFMA.
 Workload `fwd` ("S-fwd"): render_batch_ray forward, 640x480 rays x 64 stratified samples.
+Workload `room0`: the room0 Mapper iteration as the reference runs it (1,000 rays over the 5-frame
+keyframe window, window sampling on the device included), replayed from one captured HIP graph;
+`value` = rays/s, plus ms per iteration.
 
 Extra keys of the N=1 line (measured after the timed region, never part of `value`):
   sfwd            the north-star S-fwd batch (640x480 x 64 samples, forward) with its own roofline
@@ -23,6 +26,7 @@ Extra keys of the N=1 line (measured after the timed region, never part of `valu
                   the oracle's CPU rate
   fp32            the same S-map step with fp32-MFMA decoder arithmetic
   gather_roofline the neural-point gather (A15) on its HBM roofline
+  room0_iter      the `room0` workload above (ms per Mapper iteration)
 N>1 lines add `fixed_global_batch`: the 307,200-ray batch split over the N ranks.
 
 Data: synthetic.  Decoder = the trained room0 weights committed as a golden fixture
@@ -585,8 +589,8 @@ def room0_window(pnr, params, bound, dev):
 def room0_extra(pnr, params, bound, pose, dev, ddp, lib, steps=100, warmup=5, cpu=True, graph=True):
     """The metric's own workload: ONE room0 Mapper iteration (src/Mapper.py:507-662) at its real size,
     1,000 rays over the 5-frame window (200 per frame) of the room0 camera, gt = the decoder's own
-    rendered depth / colour.  Timed per iteration: the window batch (torch.randint + pnr_window_rays,
-    src/Mapper.py:553-606), render (32 + 12 samples) + regulation (32) + fused L1 losses + backward +
+    rendered depth / colour.  Timed per iteration: the window batch (pnr_window_sample: pixels, jitter
+    and far clamp drawn on the device in one launch, src/Mapper.py:553-606), render (32 + 12 samples) + regulation (32) + fused L1 losses + backward +
     Adam, all replayed from one captured HIP graph (pnr.MapGraph(batch_fn=pnr.mapping.WindowSampler))."""
     from pnr.mapping import MapGraph, MapStep, WindowSampler
     slam, frames = room0_window(pnr, params, bound, dev)
@@ -772,7 +776,7 @@ def main():
 
     if args.workload in ('map', 'map-points'):
         step = map_step_fn(pnr, renderer, dec, cfg, ro, rd, gt, col, dev, ddp=ddp if world > 1 else None,
-                           points=points, graph=args.graph and points is None)
+                           points=points, graph=args.graph)
     else:
         def step():
             with torch.no_grad():

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define PNR_ABI_VERSION 10
+#define PNR_ABI_VERSION 11
 #define PNR_N_PARAMS 11
 #define PNR_MAX_SAMPLES 64      /* N_samples + N_importance per ray */
 #define PNR_C_DIM 32            /* neural-point feature width (decoder.py:122-125 fc_c input) */
@@ -292,6 +292,21 @@ int pnr_rays_from_uv(const float* i, const float* j, int64_t n, float fx, float 
 int pnr_window_rays(const int64_t* idx, int64_t n, int64_t n_per_frame, int32_t H, int32_t W, float fx, float fy,
                     float cx, float cy, const float* c2w, const float* depth, const float* color, float* rays_o,
                     float* rays_d, float* gt_depth, float* gt_color, void* stream);
+
+/* ABI 11: the same batch with its draws made on the device, plus the regulation jitter and the far
+ * clamp, in ONE launch (a captured Mapper iteration replays it without torch's RNG launches):
+ * pixel r ~ uniform over [0, H*W) (get_samples' torch.randint), t_rand (n, n_samples) ~ uniform
+ * [0,1) with 24-bit resolution (Renderer.py:293's torch.rand), far_clamp[0] = max(1.2 * gt_depth)
+ * (Renderer.py:112; pass it as far_clamp_dev, far_mode 2).  The draws are a counter-based hash of
+ * (seed, batch, draw index) -- the reference's distribution, not torch's Philox sequence.  `state`
+ * (pnr_window_sample_state_bytes(), zero-filled before the first call, not shared by concurrent
+ * calls) holds the batch counter, advanced by each call on the device.  idx (n, int64) receives the
+ * drawn pixels and may be NULL; far_clamp may be NULL.  Rays and gt equal pnr_window_rays on idx. */
+size_t pnr_window_sample_state_bytes(void);
+int pnr_window_sample(uint64_t seed, void* state, int64_t n, int64_t n_per_frame, int32_t H, int32_t W, float fx,
+                      float fy, float cx, float cy, const float* c2w, const float* depth, const float* color,
+                      int32_t n_samples, float* rays_o, float* rays_d, float* gt_depth, float* gt_color,
+                      float* t_rand, int64_t* idx, float* far_clamp, void* stream);
 
 /* ---- optimizer (src/Mapper.py:498-502, 657-662: torch.optim.Adam, default betas/eps) ----- */
 /* One Adam step over `n` float32 words: p -= lr * mhat / (sqrt(vhat) + eps).  step >= 1. */

@@ -47,6 +47,10 @@ int launch_gout_sigma(const float*, const float4*, int64_t, int64_t, float*, hip
 int launch_get_rays(int, int, float, float, float, float, const float*, float*, float*, hipStream_t);
 int launch_rays_from_uv(const float*, const float*, int64_t, float, float, float, float, const float*, float*,
                         float*, hipStream_t);
+int64_t window_sample_state_bytes();
+int launch_window_sample(uint64_t, void*, int64_t, int64_t, int, int, float, float, float, float, const float*,
+                         const float*, const float*, int, float*, float*, float*, float*, float*, int64_t*, float*,
+                         hipStream_t);
 int launch_window_rays(const int64_t*, int64_t, int64_t, int, int, float, float, float, float, const float*,
                        const float*, const float*, float*, float*, float*, float*, hipStream_t);
 int launch_adam(float*, const float*, float*, float*, int64_t, float, float, float, float, float, hipStream_t);
@@ -1036,6 +1040,21 @@ int pnr_window_rays(const int64_t* idx, int64_t n, int64_t n_per_frame, int32_t 
   if (n > 0 && (!idx || !c2w || !depth || !color || !rays_o || !rays_d || !gt_depth || !gt_color)) return PNR_E_ARG;
   return launch_window_rays(idx, n, n_per_frame, H, W, fx, fy, cx, cy, c2w, depth, color, rays_o, rays_d, gt_depth,
                             gt_color, (hipStream_t)stream);
+}
+
+size_t pnr_window_sample_state_bytes(void) { return (size_t)window_sample_state_bytes(); }
+
+int pnr_window_sample(uint64_t seed, void* state, int64_t n, int64_t n_per_frame, int32_t H, int32_t W, float fx,
+                      float fy, float cx, float cy, const float* c2w, const float* depth, const float* color,
+                      int32_t n_samples, float* rays_o, float* rays_d, float* gt_depth, float* gt_color,
+                      float* t_rand, int64_t* idx, float* far_clamp, void* stream) {
+  if (n < 0 || H <= 0 || W <= 0 || n_per_frame <= 0 || n_samples < 0) return PNR_E_ARG;
+  if ((int64_t)H * W >= (1LL << 32)) return PNR_E_ARG;
+  if (n > 0 && (!state || !c2w || !depth || !color || !rays_o || !rays_d || !gt_depth || !gt_color ||
+                (n_samples > 0 && !t_rand)))
+    return PNR_E_ARG;
+  return launch_window_sample(seed, state, n, n_per_frame, H, W, fx, fy, cx, cy, c2w, depth, color, n_samples, rays_o,
+                              rays_d, gt_depth, gt_color, t_rand, idx, far_clamp, (hipStream_t)stream);
 }
 
 int pnr_adam_step(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1, float beta2,

@@ -1,5 +1,7 @@
 // mlp16_pack.hip -- 16-bit weight images of the split-precision decoder kernels (mlp16.h) and
 // the forward dispatch on PNR_PREC_*.
+#include <algorithm>
+
 #include "mlp16.h"
 #include "pack_fp32.h"
 
@@ -20,19 +22,27 @@ struct ScaleArgs {
 };
 __device__ __forceinline__ void wscale_block(const ScaleArgs& a, const int b) {
   __shared__ float red[16];
-  const float* w = a.w[b];
-  const int n = a.n[b];
-  const int nt = blockDim.x, nw = nt >> 6;  // any multiple of 64 up to 1024
-  float m0 = 0.f, m1 = 0.f, m2 = 0.f, m3 = 0.f;  // 4 loads in flight per thread
-  int i = threadIdx.x;
-  for (; i + 3 * nt < n; i += 4 * nt) {
-    m0 = fmaxf(m0, fabsf(w[i]));
-    m1 = fmaxf(m1, fabsf(w[i + nt]));
-    m2 = fmaxf(m2, fabsf(w[i + 2 * nt]));
-    m3 = fmaxf(m3, fabsf(w[i + 3 * nt]));
+  const float* w = a.w[0];  // a.w[b], a.n[b] without a private copy of the arrays (b is uniform)
+  int n = a.n[0];
+#pragma unroll
+  for (int k = 1; k < 5; ++k) {
+    w = b == k ? a.w[k] : w;
+    n = b == k ? a.n[k] : n;
   }
-  for (; i < n; i += nt) m0 = fmaxf(m0, fabsf(w[i]));
-  float m = fmaxf(fmaxf(m0, m1), fmaxf(m2, m3));
+  const int nt = blockDim.x, nw = nt >> 6;  // any multiple of 64 up to 1024
+  // 32 loads in flight per thread (one pass covers a 256 x 256 tensor at 1024 threads x 2): the
+  // reduction is one block per tensor, so its time is the number of dependent load rounds
+  float m = 0.f;
+  for (int i0 = 0; i0 < n; i0 += 32 * nt) {
+    float v[32];
+#pragma unroll
+    for (int k = 0; k < 32; ++k) {  // clamped, unconditional loads (a repeated element leaves the max
+      const int i = i0 + k * nt + (int)threadIdx.x;  // alone): a predicated load waits on its own
+      v[k] = fabsf(w[i < n ? i : n - 1]);
+    }
+#pragma unroll
+    for (int k = 0; k < 32; ++k) m = fmaxf(m, v[k]);
+  }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
@@ -62,41 +72,43 @@ __device__ __forceinline__ uint16_t part_bits(float x, int part) {
 // element (T, s, part, lane, j) of a weight fragment image for a layer with A[row][k]:
 // row = 32T + (lane&31), k = 32kc + perm(8s+j, lane>>5).  img 0: BF16X3, 1: BF16, 2: F16X3.
 __device__ __forceinline__ void pack16_at(const RawParams& rp, uint16_t* __restrict__ bf2, uint16_t* __restrict__ bf1,
-                                          uint16_t* __restrict__ h2, float* __restrict__ raw, const int64_t idx) {
-  const int64_t n2 = bf_main_bytes(2) / 2, n1 = bf_main_bytes(1) / 2;
-  if (idx < 2 * n2 + n1) {
+                                          uint16_t* __restrict__ h2, float* __restrict__ raw, const int64_t idx64) {
+  constexpr int n2 = (int)(bf_main_bytes(2) / 2), n1 = (int)(bf_main_bytes(1) / 2);
+  static_assert(2LL * n2 + n1 < (1LL << 30), "32-bit pack indices");
+  if (idx64 < 2 * n2 + n1) {
+    const int idx = (int)idx64;  // 32-bit index arithmetic (64-bit divisions dominated the pack)
     const int img = idx < n2 ? 0 : (idx < n2 + n1 ? 1 : 2);
     const int np = img == 1 ? 1 : 2;
-    const int64_t e0 = img == 0 ? idx : (img == 1 ? idx - n2 : idx - n2 - n1);
-    int64_t e = e0;
-    const int64_t hstep = (int64_t)np * 8192;  // 16-bit elements per hidden step
+    const int e0 = img == 0 ? idx : (img == 1 ? idx - n2 : idx - n2 - n1);
+    int e = e0;
+    const int hstep = np * 8192;  // 16-bit elements per hidden step
     float v = 0.f;
     int part = 0, tensor = 4;
     if (e < 27 * hstep) {
-      const int g = (int)(e / hstep);
-      int64_t r = e % hstep;
-      const int j = (int)(r % 8); r /= 8;
-      const int lane = (int)(r % 64); r /= 64;
-      part = (int)(r % np); r /= np;
-      const int s = (int)(r % 2);
-      const int T = (int)(r / 2);
+      const int g = e / hstep;
+      int r = e - g * hstep;
+      const int j = r & 7; r >>= 3;
+      const int lane = r & 63; r >>= 6;
+      part = r % np; r /= np;
+      const int s = r & 1;
+      const int T = r >> 1;
       const int layer = g < 3 ? 0 : 1 + (g - 3) / 8;
       const int kc = g < 3 ? g : (g - 3) % 8;
       const int row = 32 * T + (lane & 31);
       const int k = 32 * kc + perm(8 * s + j, lane >> 5);
-      const float* W = rp.p[1 + 2 * layer];
+      const float* W = rp.at(1 + 2 * layer);
       tensor = layer;
       if (layer == 0) v = k < kFourier ? W[row * kFourier + k] : 0.f;
       else v = W[row * kHidden + k];
     } else {
       e -= 27 * hstep;
-      const int kc = (int)(e / 2048);
-      int64_t r = e % 2048;  // 4 KiB piece = 2048 elements
-      if (r < (int64_t)np * 1024) {
-        const int j = (int)(r % 8); r /= 8;
-        const int lane = (int)(r % 64); r /= 64;
-        part = (int)(r % np);
-        const int s = (int)(r / np);
+      const int kc = e >> 11;
+      int r = e & 2047;  // 4 KiB piece = 2048 elements
+      if (r < np * 1024) {
+        const int j = r & 7; r >>= 3;
+        const int lane = r & 63; r >>= 6;
+        part = r % np;
+        const int s = r / np;
         const int row = lane & 31;
         const int k = 32 * kc + perm(8 * s + j, lane >> 5);
         v = row < 4 ? rp.p[9][row * kHidden + k] : 0.f;
@@ -106,6 +118,7 @@ __device__ __forceinline__ void pack16_at(const RawParams& rp, uint16_t* __restr
     else (img == 0 ? bf2 : bf1)[e0] = part_bits<__bf16>(v, part);
     return;
   }
+  const int64_t idx = idx64;
   const int64_t ri = idx - 2 * n2 - n1;
   if (ri >= kRawWo && ri < kRawWo + 4 * kHidden) {  // Wo fp32 (the VALU output layer)
     raw[ri] = rp.p[9][ri - kRawWo];
@@ -114,7 +127,7 @@ __device__ __forceinline__ void pack16_at(const RawParams& rp, uint16_t* __restr
   if (ri < kRawInv) {
     float v = 0.f;
     const int i = (int)ri;
-    if (i < kRawBo) v = rp.p[2 + 2 * (i / 256)][i % 256];
+    if (i < kRawBo) v = rp.at(2 + 2 * (i / 256))[i % 256];
     else if (i < kRawFB) v = (i - kRawBo) < 4 ? rp.p[10][i - kRawBo] : 0.f;
     else {
       const int c = (i - kRawFB) / kFourierPad, k = (i - kRawFB) % kFourierPad;
@@ -129,26 +142,29 @@ __device__ __forceinline__ void pack16_at(const RawParams& rp, uint16_t* __restr
 __device__ __forceinline__ void pack16_bwd_at(const RawParams& rp, uint16_t* __restrict__ out,
                                               const float* __restrict__ raw, const int64_t e) {
   if (e >= kBwdBytes / 2) return;
-  const int64_t byte = 2 * e;
-  int g = 0;
-  while (g + 1 < kBwdSteps && bwd_main_off(g + 1) <= byte) ++g;
-  int64_t r = (byte - bwd_main_off(g)) / 2;
-  const int j = (int)(r % 8); r /= 8;
-  const int lane = (int)(r % 64); r /= 64;
-  const int part = (int)(r % 2); r /= 2;
+  static_assert(kBwdBytes < (1LL << 31), "32-bit pack indices");
+  const int byte = 2 * (int)e;
+  static_assert(bwd_main_off(1) == 16384 && bwd_main_off(25) == 16384 + 24 * 32768 && kBwdSteps == 33, "bwd steps");
+  // step g of byte (bwd_main_off): 16 KiB for Wo^T, 24 x 32 KiB for W3..W1, 8 x 12 KiB for W0^T
+  const int g = byte < 16384 ? 0 : (byte < 16384 + 24 * 32768 ? 1 + ((byte - 16384) >> 15)
+                                                                : 25 + (byte - 16384 - 24 * 32768) / 12288);
+  int r = (byte - (int)bwd_main_off(g)) >> 1;
+  const int j = r & 7; r >>= 3;
+  const int lane = r & 63; r >>= 6;
+  const int part = r & 1; r >>= 1;
   float v = 0.f;
   int tensor = 4;
   if (g == 0) {  // Wo^T: A[row = unit 32T + i][k = o = perm(j, hh)], k < 4
-    const int T = (int)r, row = 32 * T + (lane & 31), k = perm(j, lane >> 5);
+    const int T = r, row = 32 * T + (lane & 31), k = perm(j, lane >> 5);
     v = k < 4 ? rp.p[9][k * kHidden + row] : 0.f;
   } else {
-    const int s = (int)(r % 2), T = (int)(r / 2);
+    const int s = r & 1, T = r >> 1;
     const int row = 32 * T + (lane & 31);
     const int kc = g <= 24 ? (g - 1) % 8 : g - 25;
     const int k = 32 * kc + perm(8 * s + j, lane >> 5);
     if (g <= 24) {
       const int l = 3 - (g - 1) / 8;  // W3, W2, W1
-      v = rp.p[1 + 2 * l][k * kHidden + row];
+      v = rp.at(1 + 2 * l)[k * kHidden + row];
       tensor = l;
     } else {
       v = row < kFourier ? rp.p[1][k * kFourier + row] : 0.f;
@@ -163,9 +179,17 @@ __device__ __forceinline__ void pack16_bwd_at(const RawParams& rp, uint16_t* __r
 //   stage 1: blocks 0..4 the power-of-two weight scales (k_wscale), the rest the fp32 image (k_pack)
 //   stage 2: the transposed f16x3 delta-chain images, then the forward 16-bit images and the raw
 //            table (k_pack16_bwd, k_pack16) -- both read stage 1's scales
+// (the fp32 image is grid-strided over at most kPack1Blocks blocks: the scale blocks' registers allow
+// one 1,024-thread block per CU, so a block per 1,024 elements took two rounds)
+constexpr int kPack1Blocks = 248;
 __global__ __launch_bounds__(1024) void k_pack_stage1(ScaleArgs sa, RawParams rp, float* __restrict__ packed) {
-  if (blockIdx.x < 5) wscale_block(sa, blockIdx.x);
-  else pack_fp32_at(rp, packed, (int64_t)(blockIdx.x - 5) * 1024 + threadIdx.x);
+  if (blockIdx.x < 5) {
+    wscale_block(sa, blockIdx.x);
+    return;
+  }
+  const int64_t stride = (int64_t)(gridDim.x - 5) * 1024;
+  for (int64_t i = (int64_t)(blockIdx.x - 5) * 1024 + threadIdx.x; i < kPackedFloats; i += stride)
+    pack_fp32_at(rp, packed, i);
 }
 __global__ __launch_bounds__(256) void k_pack_stage2(RawParams rp, float* __restrict__ packed, int nb_bwd) {
   float* raw = packed + kOffRaw;
@@ -186,7 +210,7 @@ int launch_pack_all(const RawParams& rp, float* packed, hipStream_t st) {
   }
   sa.inv = raw + kRawInv;
   sa.scl = raw + kRawScl;
-  const int nb1 = 5 + (int)((kPackedFloats + 1023) / 1024);
+  const int nb1 = 5 + (int)std::min<int64_t>(kPack1Blocks, (kPackedFloats + 1023) / 1024);
   hipLaunchKernelGGL(k_pack_stage1, dim3(nb1), dim3(1024), 0, st, sa, rp, packed);
   const int nb_bwd = (int)((kBwdBytes / 2 + 255) / 256);
   const int64_t n16 = 2 * (bf_main_bytes(2) / 2) + bf_main_bytes(1) / 2 + kRawWo + 4 * kHidden;
@@ -197,6 +221,12 @@ int launch_pack_all(const RawParams& rp, float* packed, hipStream_t st) {
 
 struct FcRaw16 {
   const float* p[PNR_N_FC_PARAMS];
+  __device__ __forceinline__ const float* at(int i) const {  // see RawParams::at
+    const float* r = p[0];
+#pragma unroll
+    for (int k = 1; k < PNR_N_FC_PARAMS; ++k) r = i == k ? p[k] : r;
+    return r;
+  }
 };
 
 // fc entry e = 8L + t: A[row = unit 32t + (lane&31)][k = channel perm(8s+j, lane>>5)] of Wc_L
@@ -220,14 +250,14 @@ __global__ void k_fc_pack16(FcRaw16 fc, uint16_t* __restrict__ bf2, uint16_t* __
       const int s = (int)(r / np);
       const int unit = 32 * t + (lane & 31);
       const int ch = perm(8 * s + j, lane >> 5);
-      v = fc.p[2 * L][unit * kCDim + ch];
+      v = fc.at(2 * L)[unit * kCDim + ch];
     }
     if (img == 2) h2[e] = part_bits<_Float16>(v * raw[kFcRawScl + L], part);
     else (img == 0 ? bf2 : bf1)[e] = part_bits<__bf16>(v, part);
     return;
   }
   const int64_t ri = idx - 3 * n;
-  if (ri < kFcRawInv) raw[ri] = fc.p[2 * (int)(ri / 256) + 1][ri % 256];
+  if (ri < kFcRawInv) raw[ri] = fc.at(2 * (int)(ri / 256) + 1)[ri % 256];
 }
 
 // fc backward entry e = 8(3 - l) + t: A[row = channel (lane&31)][k = unit 32t + perm(8s+j, lane>>5)]
@@ -243,7 +273,7 @@ __global__ void k_fc_pack16_bwd(FcRaw16 fc, uint16_t* __restrict__ out, const fl
   const int s = (int)(r / 2);
   const int l = 3 - ent / 8, t = ent % 8;
   const int unit = 32 * t + perm(8 * s + j, lane >> 5);
-  out[e] = part_bits<_Float16>(fc.p[2 * l][unit * kCDim + (lane & 31)] * raw[kFcRawScl + l], part);
+  out[e] = part_bits<_Float16>(fc.at(2 * l)[unit * kCDim + (lane & 31)] * raw[kFcRawScl + l], part);
 }
 
 int launch_fc_pack_bf(const float* const* fcp, float* out, hipStream_t st) {

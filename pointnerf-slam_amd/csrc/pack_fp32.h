@@ -5,45 +5,47 @@
 
 namespace pnr {
 
-__device__ __forceinline__ void pack_fp32_at(const RawParams& rp, float* __restrict__ out, const int64_t idx) {
-  if (idx >= kPackedFloats) return;
+// (32-bit index arithmetic: the image is ~0.5 M floats, and 64-bit divisions dominated the pack)
+__device__ __forceinline__ void pack_fp32_at(const RawParams& rp, float* __restrict__ out, const int64_t idx64) {
+  if (idx64 >= kPackedFloats) return;
+  static_assert(kPackedFloats < (1LL << 31), "32-bit pack indices");
+  const int idx = (int)idx64;
   float v = 0.f;
-  auto frag = [](int64_t i, int& kc, int& t, int& r, int& lane, int tiles) {
+  auto frag = [](int i, int& kc, int& t, int& r, int& lane, int tiles) {
     // [kc][t][rq][lane][4]
-    const int64_t per_chunk = (int64_t)tiles * 1024;
-    kc = (int)(i / per_chunk);
-    int64_t rem = i % per_chunk;
-    t = (int)(rem / 1024);
-    rem %= 1024;
-    const int rq = (int)(rem / 256);
-    lane = (int)((rem % 256) / 4);
-    r = rq * 4 + (int)(rem % 4);
+    const int per_chunk = tiles * 1024;
+    kc = i / per_chunk;
+    int rem = i % per_chunk;
+    t = rem >> 10;
+    rem &= 1023;
+    const int rq = rem >> 8;
+    lane = (rem & 255) >> 2;
+    r = rq * 4 + (rem & 3);
   };
   int kc, t, r, lane;
   if (idx < kOffOF) {  // forward hidden images
-    int layer;
-    int64_t i;
-    if (idx < kOffL1F) { layer = 0; i = idx - kOffL0F; }
-    else if (idx < kOffL2F) { layer = 1; i = idx - kOffL1F; }
-    else if (idx < kOffL3F) { layer = 2; i = idx - kOffL2F; }
-    else { layer = 3; i = idx - kOffL3F; }
+    int layer, i;
+    if (idx < kOffL1F) { layer = 0; i = idx - (int)kOffL0F; }
+    else if (idx < kOffL2F) { layer = 1; i = idx - (int)kOffL1F; }
+    else if (idx < kOffL3F) { layer = 2; i = idx - (int)kOffL2F; }
+    else { layer = 3; i = idx - (int)kOffL3F; }
     frag(i, kc, t, r, lane, 8);
     const int row = 32 * t + (lane & 31);
     const int col = 32 * kc + perm(r, lane >> 5);
-    const float* W = rp.p[1 + 2 * layer];
+    const float* W = rp.at(1 + 2 * layer);
     if (layer == 0) v = col < kFourier ? W[row * kFourier + col] : 0.f;
     else v = W[row * kHidden + col];
   } else if (idx < kOffB0) {  // output layer forward image [kc][rq][lane][4]
-    frag(idx - kOffOF, kc, t, r, lane, 1);
+    frag(idx - (int)kOffOF, kc, t, r, lane, 1);
     const int row = lane & 31;
     const int col = 32 * kc + perm(r, lane >> 5);
     v = row < 4 ? rp.p[9][row * kHidden + col] : 0.f;
   } else if (idx < kOffBO) {  // bias images [t][rq][lane][4]
-    const int layer = (int)((idx - kOffB0) / kBiasFloats);
-    frag((idx - kOffB0) % kBiasFloats, kc, t, r, lane, 8);
-    v = rp.p[2 + 2 * layer][32 * t + perm(r, lane >> 5)];
+    const int layer = (idx - (int)kOffB0) / (int)kBiasFloats;
+    frag((idx - (int)kOffB0) % (int)kBiasFloats, kc, t, r, lane, 8);
+    v = rp.at(2 + 2 * layer)[32 * t + perm(r, lane >> 5)];
   } else if (idx < kOffFB) {  // output bias [rq][lane][4]
-    frag(idx - kOffBO, kc, t, r, lane, 1);
+    frag(idx - (int)kOffBO, kc, t, r, lane, 1);
     const int u = perm(r, lane >> 5);
     v = u < 4 ? rp.p[10][u] : 0.f;
   } else if (idx < kOffOT) {  // Fourier B padded [3][96]
@@ -58,14 +60,14 @@ __device__ __forceinline__ void pack_fp32_at(const RawParams& rp, float* __restr
     const int o = perm(r, lane >> 5);
     v = o < 4 ? rp.p[9][o * kHidden + 32 * t + (lane & 31)] : 0.f;
   } else if (idx < kOffL0T) {  // W_l^T, l = 3,2,1
-    const int which = (int)((idx - kOffL3T) / (8 * kChunkFloats));  // 0:W3 1:W2 2:W1
-    frag((idx - kOffL3T) % (8 * kChunkFloats), kc, t, r, lane, 8);
-    const float* W = rp.p[7 - 2 * which];
+    const int which = (idx - (int)kOffL3T) / (int)(8 * kChunkFloats);  // 0:W3 1:W2 2:W1
+    frag((idx - (int)kOffL3T) % (int)(8 * kChunkFloats), kc, t, r, lane, 8);
+    const float* W = rp.at(7 - 2 * which);
     const int row = 32 * t + (lane & 31);         // input unit of W
     const int col = 32 * kc + perm(r, lane >> 5);  // output unit of W (the K index here)
     v = W[col * kHidden + row];
   } else {  // W0^T, 3 out tiles
-    frag(idx - kOffL0T, kc, t, r, lane, 3);
+    frag(idx - (int)kOffL0T, kc, t, r, lane, 3);
     const int row = 32 * t + (lane & 31);
     const int col = 32 * kc + perm(r, lane >> 5);
     v = row < kFourier ? rp.p[1][col * kFourier + row] : 0.f;

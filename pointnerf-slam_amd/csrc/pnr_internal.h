@@ -67,6 +67,13 @@ __host__ __device__ inline int perm(int r, int hh) { return (r & 3) + 8 * (r >> 
 // Device views of the 11 reference tensors (src/conv_onet/models/decoder.py state_dict order).
 struct RawParams {
   const float* p[PNR_N_PARAMS];
+  // p[i] for a per-thread i without the private-memory copy of the array a dynamic index makes
+  __host__ __device__ __forceinline__ const float* at(int i) const {
+    const float* r = p[0];
+#pragma unroll
+    for (int k = 1; k < PNR_N_PARAMS; ++k) r = i == k ? p[k] : r;
+    return r;
+  }
 };
 
 // Where the MLP reads its points from.
@@ -259,11 +266,10 @@ struct WgradSyn {
   // kWgradHidden / kWgradFirstX with the feature branch: A is the UNMASKED dL/dh_l (the delta chain
   // stores no delta there) and the GEMM applies the forward's ReLU mask words of that layer itself
   const uint4* amasks;  // mask words of h_l's layer (SaveArgs::masks + (l - 1) x ld / 32 x 64) or null
-  // GEMMs that will share one grouped launch (launch_wgrad16_group), 0 = a launch of its own: the
-  // split-K grid is sized so that the group fills the chip about once
+  // GEMMs that will share one grouped launch (launch_wgrad16_group), 0 = a launch of its own (see
+  // wgrad16_prepare's grid rule)
   int group_jobs;
 };
-int wgrad_wgs_per_cu();
 // Arguments of one split weight-gradient GEMM (wgrad16.hip k_wgrad16)
 struct WxArgs {
   const float* A;      // [K][256]

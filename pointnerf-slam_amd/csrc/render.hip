@@ -10,6 +10,7 @@
 //   k_reg_z           regulation depths (float32, jittered)          Renderer.py:280-294
 //   k_get_rays        full-frame / per-pixel rays                    common.py:74-89, 248-266
 //   k_window_rays     a mapping iteration's window pixel batch       Mapper.py:560-606, common.py:74-134
+//   k_window_sample   the same batch drawn on the device + t_rand + the far clamp (one launch)
 //   k_adam            torch.optim.Adam step                          Mapper.py:498-502, 657-662
 //
 // Arithmetic follows torch's CPU semantics where it is observable: python scalars are applied
@@ -95,22 +96,6 @@ __global__ void k_coarse_z(pnr_render_params prm, const float* __restrict__ ro, 
       zz = 1.0 / ((double)(inv_near * (1.f - t)) + (1.0 / far) * (double)t);
     }
     z[n * S + s] = zz;
-  }
-}
-
-// Cooperative staging of a 64-ray block's per-sample rows into LDS: the block's rows of a ray-major
-// array (ray n, sample m at src[n * cnt + m]) are contiguous, so the block reads them with coalesced
-// loads (64 lanes, consecutive elements) and writes them transposed, dst[m * 64 + ray], where each
-// thread later finds its own ray's samples at a stride of 64 (conflict-free).  Thread-per-ray loads
-// through a sort order were dependent global round trips: ~0.5 us each, 44 per ray.
-template <typename T>
-__device__ __forceinline__ void stage_rows(const T* __restrict__ src, int cnt, int64_t ray0, int64_t n_rays, T* dst) {
-  const int64_t nr = n_rays - ray0 < 64 ? n_rays - ray0 : 64;
-  const int64_t tot = nr * cnt;
-  const T* s = src + ray0 * cnt;
-  for (int64_t e = threadIdx.x; e < tot; e += 64) {
-    const int r = (int)(e / cnt), m = (int)(e - (int64_t)r * cnt);
-    dst[m * 64 + r] = s[e];
   }
 }
 
@@ -200,18 +185,12 @@ struct MapPts {
   const float4* rawr;   // regulation rows of launch A
   float* sigma;         // (n, S) regulation densities
 };
-// STG (launches of at most a few hundred blocks: the Mapper's 1,000-ray batch): the block's coarse
-// depths and densities are first staged into LDS by coalesced loads (stage_rows); a thread per ray
-// then reads LDS only.  Large launches keep the per-thread loads and their occupancy (48 KB less LDS).
-template <int SS, int II, bool STG>
+template <int SS, int II>
 __global__ __launch_bounds__(64) void k_pdf(pnr_render_params prm, const float* __restrict__ rd,
                                             const double* __restrict__ zc, const float4* __restrict__ rawc,
                                             int64_t n_rays, double* __restrict__ zi, MapPts mp) {
   __shared__ float wl[PNR_MAX_SAMPLES][64];
   __shared__ float cdf[PNR_MAX_SAMPLES][64];
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  double (*zl)[64] = reinterpret_cast<double (*)[64]>(smem);                        // [S][64] (STG)
-  float (*sl)[64] = reinterpret_cast<float (*)[64]>(smem + PNR_MAX_SAMPLES * 64 * 8);  // [S][64] (STG)
   const int tid = threadIdx.x;
   const int64_t ray0 = (int64_t)blockIdx.x * 64, n = ray0 + tid;
   const int S = SS > 0 ? SS : prm.n_samples, I = II > 0 ? II : prm.n_importance;
@@ -219,26 +198,15 @@ __global__ __launch_bounds__(64) void k_pdf(pnr_render_params prm, const float* 
     for (int64_t i = n; i < mp.x4i_pad; i += (int64_t)gridDim.x * 64)
       mp.x4i[n_rays * I + i] = make_float4(0.f, 0.f, 0.f, 0.f);
   }
-  {
-    const int64_t nr = n_rays - ray0 < 64 ? n_rays - ray0 : 64;
-    if (mp.sigma) {  // the regulation densities of the block's rays: coalesced copy
-      for (int64_t e = tid; e < nr * S; e += 64) mp.sigma[ray0 * S + e] = mp.rawr[ray0 * S + e].w;
-    }
-    if constexpr (STG) {
-      stage_rows(zc, S, ray0, n_rays, &zl[0][0]);
-      const float4* rb = rawc + ray0 * S;
-      for (int64_t e = tid; e < nr * S; e += 64) {
-        const int r = (int)(e / S), m = (int)(e - (int64_t)r * S);
-        sl[m][r] = rb[e].w;
-      }
-      __syncthreads();
-    }
+  if (mp.sigma) {  // the regulation densities of the block's rays: coalesced copy
+    const int nr = (int)(n_rays - ray0 < 64 ? n_rays - ray0 : 64);
+    for (int e = tid; e < nr * S; e += 64) mp.sigma[ray0 * S + e] = mp.rawr[ray0 * S + e].w;
   }
   if (n >= n_rays) return;
   const double* z = zc + n * S;
   const float4* raw = rawc + n * S;
-  auto zq = [&](int q) -> double { if constexpr (STG) return zl[q][tid]; else return z[q]; };
-  auto sq = [&](int q) -> float { if constexpr (STG) return sl[q][tid]; else return raw[q].w; };
+  auto zq = [&](int q) -> double { return z[q]; };
+  auto sq = [&](int q) -> float { return raw[q].w; };
   const float nrm = ray_norm(rd + n * 3);
   double T = 1.0;
 #pragma unroll
@@ -345,7 +313,7 @@ __device__ __forceinline__ void sort_ray(double (*zl)[64], int S, int I, uint8_t
 }
 
 // final pass: depth/var (float64), rgb (float32); saves the sort order for the backward
-template <int SS, int II, bool STG>
+template <int SS, int II>
 __global__ __launch_bounds__(64) void k_fine(pnr_render_params prm, const float* __restrict__ rd,
                                              const double* __restrict__ zc, const double* __restrict__ zi,
                                              const float4* __restrict__ rawc, const float4* __restrict__ rawi,
@@ -354,26 +322,15 @@ __global__ __launch_bounds__(64) void k_fine(pnr_render_params prm, const float*
   __shared__ double zl[PNR_MAX_SAMPLES][64];
   __shared__ uint8_t ord[PNR_MAX_SAMPLES][64];
   __shared__ float wl[PNR_MAX_SAMPLES][64];
-  // STG: the block's raw rows, natural order (coarse, importance), staged like the depths (k_pdf)
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  float4 (*rl)[64] = reinterpret_cast<float4 (*)[64]>(smem);
   const int tid = threadIdx.x;
-  const int64_t ray0 = (int64_t)blockIdx.x * 64, n = ray0 + tid;
+  const int64_t n = (int64_t)blockIdx.x * 64 + tid;
   const int S = SS > 0 ? SS : prm.n_samples, I = II > 0 ? II : prm.n_importance, M = S + I;
-  if constexpr (STG) {
-    stage_rows(zc, S, ray0, n_rays, &zl[0][0]);
-    stage_rows(zi, I, ray0, n_rays, &zl[S][0]);
-    stage_rows(rawc, S, ray0, n_rays, &rl[0][0]);
-    stage_rows(rawi, I, ray0, n_rays, &rl[S][0]);
-    __syncthreads();
-  }
   if (n >= n_rays) return;
-  if constexpr (!STG) {  // the ray's depths, natural order
+  // the ray's depths, natural order
 #pragma unroll
-    for (int m = 0; m < S; ++m) zl[m][tid] = zc[n * S + m];
+  for (int m = 0; m < S; ++m) zl[m][tid] = zc[n * S + m];
 #pragma unroll
-    for (int k = 0; k < I; ++k) zl[S + k][tid] = zi[n * I + k];
-  }
+  for (int k = 0; k < I; ++k) zl[S + k][tid] = zi[n * I + k];
   sort_ray<SS, II>(zl, S, I, ord, tid);
   const float nrm = ray_norm(rd + n * 3);
   double T = 1.0, D = 0.0;
@@ -383,9 +340,7 @@ __global__ __launch_bounds__(64) void k_fine(pnr_render_params prm, const float*
     const int s = ord[q][tid];
     const double zq = zl[s][tid];
     const float dz = q < M - 1 ? (float)(zl[ord[q + 1][tid]][tid] - zq) : 1e10f;
-    float4 c;
-    if constexpr (STG) c = rl[s][tid];
-    else c = s < S ? rawc[n * S + s] : rawi[n * I + (s - S)];
+    const float4 c = s < S ? rawc[n * S + s] : rawi[n * I + (s - S)];
     const float a = 1.f - expf(-relu(c.w) * (dz * nrm));
     const float w = a * (float)T;
     T *= (double)(1.f - a + 1e-10f);
@@ -426,7 +381,7 @@ struct MapBwd {
 // Backward of the final compositing: writes dL/draw (float4) for every coarse and importance
 // point, sigma channel zeroed where the point was outside the bound (Renderer.py:57 assigns
 // the density, so no gradient reaches the MLP there); g_nrm[n] = dL/d|rays_d|.
-template <int SS, int II, bool STG>
+template <int SS, int II>
 __global__ __launch_bounds__(64) void k_fine_bwd(pnr_render_params prm, const float* __restrict__ rd,
                                                  const double* __restrict__ zc, const double* __restrict__ zi,
                                                  const float4* __restrict__ rawc, const float4* __restrict__ rawi,
@@ -446,11 +401,6 @@ __global__ __launch_bounds__(64) void k_fine_bwd(pnr_render_params prm, const fl
   double* zs = reinterpret_cast<double*>(smem);
   float* al = reinterpret_cast<float*>(zs + M * 64);
   float* Tl = al + M * 64;
-  // STG (small launches): the block's rays' samples in natural order, staged by coalesced loads --
-  // depths, raw rows and inside flags -- so the sorted traversals below read LDS only
-  double* zn = reinterpret_cast<double*>(Tl + M * 64);
-  float4* rl = reinterpret_cast<float4*>(zn + M * 64);
-  float* il = reinterpret_cast<float*>(rl + M * 64);
   const int64_t ray0 = (int64_t)blockIdx.x * 64;
   {  // the padding rows of the MLP launches get dL/draw = 0 (the MLP backward reads every row)
     const int64_t gi = (int64_t)blockIdx.x * 64 + tid, gs = (int64_t)gridDim.x * 64;
@@ -458,29 +408,12 @@ __global__ __launch_bounds__(64) void k_fine_bwd(pnr_render_params prm, const fl
     for (int64_t i = gi; i < np1; i += gs) pad1[i] = make_float4(0.f, 0.f, 0.f, 0.f);
     for (int64_t i = gi; i < mb.np2; i += gs) mb.pad2[i] = make_float4(0.f, 0.f, 0.f, 0.f);
   }
-  {
-    const int64_t nr = n_rays - ray0 < 64 ? n_rays - ray0 : 64;
-    if (mb.g_sigma) {  // map pass: the regulation rows' dL/draw (k_gout_sigma): sigma only, 0 outside the bound
-      const int S0 = SS > 0 ? SS : prm.n_samples;
-      for (int64_t e = tid; e < nr * S0; e += 64) {
-        const int64_t r = ray0 * S0 + e;
-        mb.gor[r] = make_float4(0.f, 0.f, 0.f, mb.insr[r].w != 0.f ? mb.g_sigma[r] : 0.f);
-      }
-    }
-    if constexpr (STG) {
-      stage_rows(zc, S, ray0, n_rays, zn);
-      stage_rows(zi, I, ray0, n_rays, zn + S * 64);
-      stage_rows(rawc, S, ray0, n_rays, rl);
-      stage_rows(rawi, I, ray0, n_rays, rl + S * 64);
-      for (int64_t e = tid; e < nr * S; e += 64) {
-        const int r = (int)(e / S), m = (int)(e - (int64_t)r * S);
-        il[m * 64 + r] = insc[ray0 * S + e].w;
-      }
-      for (int64_t e = tid; e < nr * I; e += 64) {
-        const int r = (int)(e / I), m = (int)(e - (int64_t)r * I);
-        il[(S + m) * 64 + r] = insi[ray0 * I + e].w;
-      }
-      __syncthreads();
+  if (mb.g_sigma) {  // map pass: the regulation rows' dL/draw (k_gout_sigma): sigma only, 0 outside the bound
+    const int S0 = SS > 0 ? SS : prm.n_samples;
+    const int nr = (int)(n_rays - ray0 < 64 ? n_rays - ray0 : 64);
+    for (int e = tid; e < nr * S0; e += 64) {  // the block's rows, coalesced
+      const int64_t r = ray0 * S0 + e;
+      mb.gor[r] = make_float4(0.f, 0.f, 0.f, mb.insr[r].w != 0.f ? mb.g_sigma[r] : 0.f);
     }
   }
   if (n >= n_rays) return;
@@ -499,14 +432,8 @@ __global__ __launch_bounds__(64) void k_fine_bwd(pnr_render_params prm, const fl
   auto ordq = [&](int q) -> int { return SS > 0 ? (int)((ow[q >> 2] >> (8 * (q & 3))) & 0xffu) : (int)ord[q]; };
   const float* dvec = rd + n * 3;
   const float nrm = ray_norm(dvec);
-  auto zsrc = [&](int s) -> double {
-    if constexpr (STG) return zn[s * 64 + tid];
-    else return s < S ? zc[n * S + s] : zi[n * I + (s - S)];
-  };
-  auto rsrc = [&](int s) -> float4 {
-    if constexpr (STG) return rl[s * 64 + tid];
-    else return s < S ? rawc[n * S + s] : rawi[n * I + (s - S)];
-  };
+  auto zsrc = [&](int s) { return s < S ? zc[n * S + s] : zi[n * I + (s - S)]; };
+  auto rsrc = [&](int s) { return s < S ? rawc[n * S + s] : rawi[n * I + (s - S)]; };
   double T = 1.0, D = 0.0;
 #pragma unroll
   for (int q = 0; q < M; ++q) zs[q * 64 + tid] = zsrc(ordq(q));
@@ -548,15 +475,240 @@ __global__ __launch_bounds__(64) void k_fine_bwd(pnr_render_params prm, const fl
     const float sr = relu(c.w);
     const float ex = expf(-sr * delta);
     float gs = c.w > 0.f ? ga * ex * delta : 0.f;
-    bool inside;
-    if constexpr (STG) inside = il[s * 64 + tid] != 0.f;
-    else inside = s < S ? insc[n * S + s].w != 0.f : insi[n * I + (s - S)].w != 0.f;
+    const bool inside = s < S ? insc[n * S + s].w != 0.f : insi[n * I + (s - S)].w != 0.f;
     if (!inside) gs = 0.f;
     gn += (ga * ex * sr) * dz;
     const float4 go = make_float4(gr0 * w, gr1 * w, gr2 * w, gs);
     if (s < S) goc[n * S + s] = go; else goi[n * I + (s - S)] = go;
   }
   if (g_nrm) g_nrm[n] = gn;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Wave-per-ray forms of k_pdf / k_fine / k_fine_bwd for small batches (the Mapper's 1,000 rays: 16
+// waves of the thread-per-ray kernels on 1,024 SIMDs, each a ~13 k-instruction serial chain).  Lane
+// l of a 64-lane workgroup holds sample l: the per-sample work (loads, expf, alpha, the gradient
+// terms, the stores) runs across the lanes, and only the accumulations the reference performs in
+// order -- cumprod T (float64), the float / float64 sums, the backward recurrence R -- run as
+// serial chains over v_readlane in the same order with the same roundings, so the results are the
+// thread-per-ray kernels' bit for bit (tests/test_gpu_render_small.py).
+__device__ __forceinline__ float rlf(float v, int l) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
+}
+__device__ __forceinline__ double rld(double v, int l) {
+  const uint64_t b = __builtin_bit_cast(uint64_t, v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, l);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), l);
+  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+// exclusive float64 cumprod of f over lanes 0..M-1 (T_0 = 1; torch.cumprod order): lane l gets T_l
+__device__ __forceinline__ double excl_cumprod(double f, int M, int l) {
+  double T = 1.0, Tl = 1.0;
+  for (int q = 0; q < M; ++q) {
+    Tl = l == q ? T : Tl;
+    T *= rld(f, q);
+  }
+  return Tl;
+}
+
+template <int SS, int II>
+__global__ __launch_bounds__(64) void k_pdf_w(pnr_render_params prm, const float* __restrict__ rd,
+                                              const double* __restrict__ zc, const float4* __restrict__ rawc,
+                                              int64_t n_rays, double* __restrict__ zi, MapPts mp) {
+  __shared__ float cdf[PNR_MAX_SAMPLES];
+  __shared__ double zs[PNR_MAX_SAMPLES + 1];
+  const int l = threadIdx.x;
+  const int64_t n = blockIdx.x;
+  const int S = SS > 0 ? SS : prm.n_samples, I = II > 0 ? II : prm.n_importance;
+  if (mp.x4i) {
+    for (int64_t i = n * 64 + l; i < mp.x4i_pad; i += (int64_t)gridDim.x * 64)
+      mp.x4i[n_rays * I + i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  if (mp.sigma && l < S) mp.sigma[n * S + l] = mp.rawr[n * S + l].w;
+  const int lq = l < S ? l : S - 1;  // clamped, unconditional loads (lanes >= S are never read)
+  const double z = zc[n * S + lq];
+  const float sg = rawc[n * S + lq].w;
+  zs[l] = z;
+  __syncthreads();
+  const float nrm = ray_norm(rd + n * 3);
+  const float dz = l < S - 1 ? (float)(zs[l + 1] - z) : 1e10f;
+  const float delta = dz * nrm;
+  const float a = 1.f - expf(-relu(sg) * delta);
+  const double Tl = excl_cumprod((double)(1.f - a + 1e-10f), S, l);
+  const float w = a * (float)Tl;  // weights[q] (k_pdf's wl)
+  // sample_pdf(bins = mid(z) (S-1), weights[1:-1] (S-2)): the float sum, then the float64 cdf
+  const int M = S - 2;
+  const float wt = w + 1e-5f;
+  float sum = 0.f;
+  for (int m = 0; m < M; ++m) sum += rlf(wt, m + 1);
+  const float term = wt / sum;  // lane m + 1: term m
+  double acc = 0.0;
+  float c = 0.f;
+  for (int m = 0; m < M; ++m) {
+    acc += (double)rlf(term, m + 1);
+    c = l == m + 1 ? (float)acc : c;
+  }
+  if (l <= M) cdf[l] = c;  // cdf[0] = 0
+  float u = 0.f;  // u_vals[l] (uniform loads; no per-lane index into the kernel arguments)
+  for (int k = 0; k < I; ++k) u = l == k ? prm.u_vals[k] : u;
+  __syncthreads();
+  if (l >= I) return;
+  int lo = 0, hi = M + 1;  // searchsorted(cdf, u, right=True), as k_pdf
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (cdf[mid] <= u) lo = mid + 1; else hi = mid;
+  }
+  const int below = lo - 1 > 0 ? lo - 1 : 0;
+  const int above = lo < M ? lo : M;
+  const float c0 = cdf[below], c1 = cdf[above];
+  float denom = c1 - c0;
+  if (denom < 1e-5f) denom = 1.f;
+  const float t = (u - c0) / denom;
+  const double b0 = .5 * (zs[below + 1] + zs[below]);
+  const double b1 = .5 * (zs[above + 1] + zs[above]);
+  const double zz = b0 + (double)t * (b1 - b0);
+  zi[n * I + l] = zz;
+  if (mp.x4i) {
+    const double q0 = (double)mp.ro[n * 3 + 0] + (double)rd[n * 3 + 0] * zz;
+    const double q1 = (double)mp.ro[n * 3 + 1] + (double)rd[n * 3 + 1] * zz;
+    const double q2 = (double)mp.ro[n * 3 + 2] + (double)rd[n * 3 + 2] * zz;
+    const bool inside = (q0 < prm.bound[1]) && (q0 > prm.bound[0]) && (q1 < prm.bound[3]) && (q1 > prm.bound[2]) &&
+                        (q2 < prm.bound[5]) && (q2 > prm.bound[4]);
+    mp.x4i[n * I + l] = make_float4((float)q0, (float)q1, (float)q2, inside ? 1.f : 0.f);
+  }
+}
+
+template <int SS, int II>
+__global__ __launch_bounds__(64) void k_fine_w(pnr_render_params prm, const float* __restrict__ rd,
+                                               const double* __restrict__ zc, const double* __restrict__ zi,
+                                               const float4* __restrict__ rawc, const float4* __restrict__ rawi,
+                                               int64_t n_rays, double* __restrict__ depth, double* __restrict__ var,
+                                               float* __restrict__ rgb, uint8_t* __restrict__ ord_out) {
+  __shared__ double zn[PNR_MAX_SAMPLES];
+  __shared__ uint8_t os[PNR_MAX_SAMPLES + 4];
+  const int l = threadIdx.x;
+  const int64_t n = blockIdx.x;
+  const int S = SS > 0 ? SS : prm.n_samples, I = II > 0 ? II : prm.n_importance, M = S + I;
+  const int lq = l < M ? l : M - 1;  // clamped, unconditional loads (lanes >= M are never ranked)
+  const double zl = *(lq < S ? zc + n * S + lq : zi + n * I + (lq - S));
+  zn[l] = zl;
+  os[l] = 0;
+  if (l < 4) os[64 + l] = 0;
+  __syncthreads();
+  if (l < M) {  // stable rank (torch.sort, NaN last): sort_ray's order for any input
+    int r = 0;
+    for (int m = 0; m < M; ++m) {
+      const double v = zn[m];
+      r += (lt_nan(v, zl) || (eq_nan(v, zl) && m < l)) ? 1 : 0;
+    }
+    os[r] = (uint8_t)l;
+  }
+  __syncthreads();
+  const int s = os[l];
+  const double zq = zn[s];
+  const double znx = l + 1 < M ? zn[os[l + 1]] : 0.0;
+  const float4 c = *(s < S ? rawc + n * S + s : rawi + n * I + (s - S));  // lanes >= M: s = 0, never read
+  const float nrm = ray_norm(rd + n * 3);
+  const float dz = l < M - 1 ? (float)(znx - zq) : 1e10f;
+  const float a = 1.f - expf(-relu(c.w) * (dz * nrm));
+  const double Tl = excl_cumprod((double)(1.f - a + 1e-10f), M, l);
+  const float w = a * (float)Tl;
+  const float p0 = w * c.x, p1 = w * c.y, p2 = w * c.z;
+  const double pD = (double)w * zq;
+  float r0 = 0.f, r1 = 0.f, r2 = 0.f;
+  double D = 0.0;
+  for (int q = 0; q < M; ++q) {
+    r0 += rlf(p0, q); r1 += rlf(p1, q); r2 += rlf(p2, q);
+    D += rld(pD, q);
+  }
+  const double dd = zq - D;
+  const double pV = (double)w * dd * dd;
+  double V = 0.0;
+  for (int q = 0; q < M; ++q) V += rld(pV, q);
+  if (l == 0) {
+    depth[n] = D;
+    var[n] = V;
+    rgb[n * 3 + 0] = r0; rgb[n * 3 + 1] = r1; rgb[n * 3 + 2] = r2;
+  }
+  if (ord_out && (l & 3) == 0 && l < M) {  // 4 bytes per store, zero past M (as k_fine)
+    uint32_t v = 0;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) v |= (l + b < M ? (uint32_t)os[l + b] : 0u) << (8 * b);
+    reinterpret_cast<uint32_t*>(ord_out + n * PNR_MAX_SAMPLES)[l >> 2] = v;
+  }
+}
+
+template <int SS, int II>
+__global__ __launch_bounds__(64) void k_fine_bwd_w(pnr_render_params prm, const float* __restrict__ rd,
+                                                   const double* __restrict__ zc, const double* __restrict__ zi,
+                                                   const float4* __restrict__ rawc, const float4* __restrict__ rawi,
+                                                   const float4* __restrict__ insc, const float4* __restrict__ insi,
+                                                   const uint8_t* __restrict__ ord_in, int64_t n_rays,
+                                                   const double* __restrict__ g_depth, const double* __restrict__ g_var,
+                                                   const float* __restrict__ g_rgb, float4* __restrict__ goc,
+                                                   float4* __restrict__ goi, float* __restrict__ g_nrm,
+                                                   float4* __restrict__ pad0, int np0, float4* __restrict__ pad1,
+                                                   int np1, MapBwd mb) {
+  const int l = threadIdx.x;
+  const int64_t n = blockIdx.x;
+  const int S = SS > 0 ? SS : prm.n_samples, I = II > 0 ? II : prm.n_importance, M = S + I;
+  {
+    const int64_t gi = n * 64 + l, gs = (int64_t)gridDim.x * 64;
+    for (int64_t i = gi; i < np0; i += gs) pad0[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int64_t i = gi; i < np1; i += gs) pad1[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int64_t i = gi; i < mb.np2; i += gs) mb.pad2[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  if (mb.g_sigma && l < S) {
+    const int64_t r = n * S + l;
+    mb.gor[r] = make_float4(0.f, 0.f, 0.f, mb.insr[r].w != 0.f ? mb.g_sigma[r] : 0.f);
+  }
+  const bool act = l < M;
+  // clamped, unconditional loads (a predicated load waits on its own); lanes >= M are never read
+  const int s = ord_in[n * PNR_MAX_SAMPLES + (act ? l : M - 1)];
+  const double zq = *(s < S ? zc + n * S + s : zi + n * I + (s - S));
+  const float4 c = *(s < S ? rawc + n * S + s : rawi + n * I + (s - S));
+  const bool inside = act && (s < S ? insc + n * S + s : insi + n * I + (s - S))->w != 0.f;
+  const double gd = g_depth ? g_depth[n] : 0.0;
+  const double gv = g_var ? g_var[n] : 0.0;
+  const float gr0 = g_rgb ? g_rgb[n * 3 + 0] : 0.f;
+  const float gr1 = g_rgb ? g_rgb[n * 3 + 1] : 0.f;
+  const float gr2 = g_rgb ? g_rgb[n * 3 + 2] : 0.f;
+  const double znx = __shfl_down(zq, 1);
+  const float nrm = ray_norm(rd + n * 3);
+  const float dz = l < M - 1 ? (float)(znx - zq) : 1e10f;
+  const float delta = dz * nrm;
+  const float sr = relu(c.w);
+  const float ex = expf(-sr * delta);
+  const float a = 1.f - ex;
+  const float Tf = (float)excl_cumprod((double)(1.f - a + 1e-10f), M, l);
+  const float w = a * Tf;
+  const double pD = (double)w * zq;
+  double D = 0.0;
+  for (int q = 0; q < M; ++q) D += rld(pD, q);
+  const double pS = (double)(a * Tf) * (zq - D);
+  double sdev = 0.0;
+  for (int q = 0; q < M; ++q) sdev += rld(pS, q);
+  const double gD = gd - 2.0 * gv * sdev;  // d var / d depth = -2 sum w (z - depth)
+  const double dd = zq - D;
+  const float gw = (gr0 * c.x + gr1 * c.y + gr2 * c.z) + (float)(gD * zq) + (float)(gv * dd * dd);
+  // R before sample q (samples q+1..M-1 folded in, k_fine_bwd's reverse loop)
+  const float pa = gw * a, g1 = 1.f - a + 1e-10f;
+  float R = 0.f, Rl = 0.f;
+  for (int q = M - 1; q >= 0; --q) {
+    Rl = l == q ? R : Rl;
+    R = rlf(pa, q) + rlf(g1, q) * R;
+  }
+  const float ga = Tf * (gw - Rl);
+  float gs = c.w > 0.f ? ga * ex * delta : 0.f;
+  if (!inside) gs = 0.f;
+  const float pg = (ga * ex * sr) * dz;
+  float gn = 0.f;
+  for (int q = M - 1; q >= 0; --q) gn += rlf(pg, q);
+  if (act) {
+    const float4 go = make_float4(gr0 * w, gr1 * w, gr2 * w, gs);
+    if (s < S) goc[n * S + s] = go; else goi[n * I + (s - S)] = go;
+  }
+  if (g_nrm && l == 0) g_nrm[n] = gn;
 }
 
 // dL/drays_o = sum_s dL/dx_s ; dL/drays_d = sum_s dL/dx_s * z_s + g_nrm * d/|d|
@@ -749,6 +901,84 @@ __global__ void k_window_rays(const int64_t* __restrict__ idx, int64_t n, int64_
   gc[k * 3 + 2] = color[q * 3 + 2];
 }
 
+// A mapping iteration's whole window batch in ONE launch, drawn on the device: the uniform pixels
+// (torch.randint(H*W) per ray in Mapper.py:560-606's get_samples), the regulation jitter t_rand
+// (torch.rand, Renderer.py:293), the rays and gt of k_window_rays, and the batch far clamp
+// max(1.2 gt) (k_gt_max, Renderer.py:112) -- in place of randint + rand (+ the two seed / offset
+// fills torch's RNG records in a captured graph) + the gt max.  The draws are a counter-based hash
+// (splitmix64 finaliser of seed, batch and draw index), not torch's Philox stream: the same
+// distribution, a different sequence.  The state holds the batch counter (advanced by the block
+// that takes the last ticket, so a captured graph draws a fresh batch per replay), the ticket and
+// the per-block maxima.
+constexpr int kSampleParts = 64;
+struct SampleState {
+  int64_t batch;
+  uint32_t ticket;
+  uint32_t pad;
+  float part[kSampleParts];
+};
+static_assert(sizeof(SampleState) == 16 + 4 * kSampleParts, "sampler state layout");
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+__global__ __launch_bounds__(256) void k_window_sample(uint64_t seed, SampleState* __restrict__ stt, int64_t n,
+                                                       int64_t per_frame, int64_t hw, int W, float fx, float fy,
+                                                       float cx, float cy, const float* __restrict__ c2w,
+                                                       const float* __restrict__ depth,
+                                                       const float* __restrict__ color, int S, float* __restrict__ ro,
+                                                       float* __restrict__ rd, float* __restrict__ gd,
+                                                       float* __restrict__ gc, float* __restrict__ t_rand,
+                                                       int64_t* __restrict__ idx_out, float* __restrict__ far_out) {
+  __shared__ float red[4];
+  __shared__ uint32_t last;
+  const int64_t batch = stt->batch;
+  const uint64_t base = mix64(seed + (uint64_t)batch * 0x9E3779B97F4A7C15ull);
+  float m = -INFINITY;
+  for (int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x; k < n; k += (int64_t)gridDim.x * 256) {
+    const int64_t f = k / per_frame;
+    const uint64_t r = mix64(base + (uint64_t)k * 0xD1B54A32D192ED03ull);
+    const int64_t pix = (int64_t)(((r >> 32) * (uint64_t)hw) >> 32);  // uniform in [0, hw) (hw < 2^32)
+    if (idx_out) idx_out[k] = pix;
+    make_ray((float)(pix % W), (float)(pix / W), fx, fy, cx, cy, c2w + f * 16, 4, ro + k * 3, rd + k * 3);
+    const int64_t q = f * hw + pix;
+    const float d = depth[q];
+    gd[k] = d;
+    gc[k * 3 + 0] = color[q * 3 + 0];
+    gc[k * 3 + 1] = color[q * 3 + 1];
+    gc[k * 3 + 2] = color[q * 3 + 2];
+    m = max_nanf(m, d * 1.2f);
+    for (int s = 0; s < S; ++s) {  // 24-bit uniforms in [0, 1), like torch.rand's float32
+      const uint64_t u = mix64(base + (uint64_t)(n + k * S + s) * 0xD1B54A32D192ED03ull);
+      t_rand[k * S + s] = (float)(uint32_t)(u >> 40) * 0x1p-24f;
+    }
+  }
+  m = block_max_256(m, red);
+  // ticket hand-off as k_map_loss; the last block reduces the maxima and advances the batch
+  if (threadIdx.x == 0) {
+    stt->part[blockIdx.x] = m;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t t = atomicAdd(&stt->ticket, 1u);
+    last = t == gridDim.x - 1 ? 1u : 0u;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  __syncthreads();
+  if (!last) return;
+  __shared__ float red2[4];
+  const float v = block_max_256((int)threadIdx.x < (int)gridDim.x ? stt->part[threadIdx.x] : -INFINITY, red2);
+  if (threadIdx.x == 0) {
+    if (far_out) far_out[0] = v;
+    stt->batch = batch + 1;
+    stt->ticket = 0u;
+  }
+}
+
 // torch.optim.Adam (amsgrad=False, weight_decay=0), single-tensor semantics
 __global__ void k_adam(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
                        float* __restrict__ v, int64_t n, float beta1, float beta2, float eps, float step_size,
@@ -808,16 +1038,33 @@ __global__ __launch_bounds__(256) void k_adam_multi(float* __restrict__ p, const
   const double bc1 = 1.0 - pow((double)beta1, t), bc2 = 1.0 - pow((double)beta2, t);
   const float step_size = (float)((double)S.lr[q] / bc1);
   const float bc2_sqrt = (float)sqrt(bc2);
-  for (int64_t i = i0; i < S.n[q]; i += stride) {
-    const int64_t k = S.off[q] + i;
-    const float gi = g[k];
-    float mi = S.m[q][i];
-    mi = mi + (1.f - beta1) * (gi - mi);
-    float vi = S.v[q][i] * beta2 + (1.f - beta2) * gi * gi;
-    S.m[q][i] = mi;
-    S.v[q][i] = vi;
-    const float denom = sqrtf(vi) / bc2_sqrt + eps;
-    p[k] = p[k] + (-step_size) * (mi / denom);
+  // four elements in flight per thread (loads first), so the grid stays small without a serial
+  // chain of dependent loads per thread
+  const int64_t nq = S.n[q], off = S.off[q];
+  float* __restrict__ mq = S.m[q];
+  float* __restrict__ vq = S.v[q];
+  for (int64_t b = i0; b < nq; b += 4 * stride) {
+    float gi[4], mi[4], vi[4], pi[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {  // clamped, unconditional loads (a predicated load waits on its own)
+      const int64_t i = b + u * stride < nq ? b + u * stride : nq - 1;
+      gi[u] = g[off + i];
+      mi[u] = mq[i];
+      vi[u] = vq[i];
+      pi[u] = p[off + i];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t i = b + u * stride;
+      if (i < nq) {
+        const float mn = mi[u] + (1.f - beta1) * (gi[u] - mi[u]);
+        const float vn = vi[u] * beta2 + (1.f - beta2) * gi[u] * gi[u];
+        mq[i] = mn;
+        vq[i] = vn;
+        const float denom = sqrtf(vn) / bc2_sqrt + eps;
+        p[off + i] = pi[u] + (-step_size) * (mn / denom);
+      }
+    }
   }
   __syncthreads();  // the block's step reads come before its ticket
   if (threadIdx.x == 0) {
@@ -837,9 +1084,6 @@ __global__ void k_step_advance(int32_t* step_count) {
 // launchers
 // ---------------------------------------------------------------------------------------------
 static inline unsigned nblk(int64_t n, int b) { return (unsigned)((n + b - 1) / b); }
-// ray launches of at most this many rays (a block per CU or fewer) stage their rows through LDS
-// (k_pdf / k_fine / k_fine_bwd STG): they are latency-bound, not occupancy-bound
-constexpr int64_t kStageRays = 16384;
 
 int launch_gt_max(const float* gt, int64_t n, float* out, hipStream_t st) {
   const int parts = (int)std::min<int64_t>(kGtParts, std::max<int64_t>(1, (n + 4095) / 4096));
@@ -853,19 +1097,27 @@ int launch_coarse_z(const pnr_render_params& prm, const float* ro, const float* 
   hipLaunchKernelGGL(k_coarse_z, dim3(nblk(n, 128)), dim3(128), 0, st, prm, ro, rd, gt, gmax, n, z, far_out);
   return hip_status(hipGetLastError());
 }
+// batches up to this many rays run the wave-per-ray compositing kernels (k_pdf_w / k_fine_w /
+// k_fine_bwd_w): below it the thread-per-ray kernels leave most SIMDs idle
+constexpr int64_t kWaveRays = 32768;
 int launch_pdf(const pnr_render_params& prm, const float* rd, const double* zc, const float* rawc, int64_t n,
                double* zi, hipStream_t st, const float* ro = nullptr, float* x4i = nullptr, int64_t x4i_pad = 0,
                const float* rawr = nullptr, float* sigma = nullptr) {
   if (n <= 0) return 0;
   const MapPts mp{ro, reinterpret_cast<float4*>(x4i), x4i_pad, reinterpret_cast<const float4*>(rawr), sigma};
-  const bool stg = n <= kStageRays;
-  const size_t sh = stg ? (size_t)PNR_MAX_SAMPLES * 64 * (8 + 4) : 0;
-  const bool cfg = prm.n_samples == 32 && prm.n_importance == 12;  // the config's counts (pointNeRF_slam.yaml)
-  const dim3 g(nblk(n, 64)), b(64);
-  if (cfg && stg) hipLaunchKernelGGL((k_pdf<32, 12, true>), g, b, sh, st, prm, rd, zc, (const float4*)rawc, n, zi, mp);
-  else if (cfg) hipLaunchKernelGGL((k_pdf<32, 12, false>), g, b, 0, st, prm, rd, zc, (const float4*)rawc, n, zi, mp);
-  else if (stg) hipLaunchKernelGGL((k_pdf<0, 0, true>), g, b, sh, st, prm, rd, zc, (const float4*)rawc, n, zi, mp);
-  else hipLaunchKernelGGL((k_pdf<0, 0, false>), g, b, 0, st, prm, rd, zc, (const float4*)rawc, n, zi, mp);
+  if (n <= kWaveRays) {
+    if (prm.n_samples == 32 && prm.n_importance == 12)
+      hipLaunchKernelGGL((k_pdf_w<32, 12>), dim3((unsigned)n), dim3(64), 0, st, prm, rd, zc, (const float4*)rawc, n, zi,
+                         mp);
+    else
+      hipLaunchKernelGGL((k_pdf_w<0, 0>), dim3((unsigned)n), dim3(64), 0, st, prm, rd, zc, (const float4*)rawc, n, zi,
+                         mp);
+    return hip_status(hipGetLastError());
+  }
+  if (prm.n_samples == 32 && prm.n_importance == 12)  // the config's counts (configs/pointNeRF_slam.yaml)
+    hipLaunchKernelGGL((k_pdf<32, 12>), dim3(nblk(n, 64)), dim3(64), 0, st, prm, rd, zc, (const float4*)rawc, n, zi, mp);
+  else
+    hipLaunchKernelGGL((k_pdf<0, 0>), dim3(nblk(n, 64)), dim3(64), 0, st, prm, rd, zc, (const float4*)rawc, n, zi, mp);
   return hip_status(hipGetLastError());
 }
 int launch_map_pts(const pnr_render_params& prm, const float* ro, const float* rd, const float* gt, const float* t_rand,
@@ -880,15 +1132,21 @@ int launch_fine(const pnr_render_params& prm, const float* rd, const double* zc,
                 const float* rawc, const float* rawi, int64_t n, double* depth, double* var, float* rgb,
                 uint8_t* ord, hipStream_t st) {
   if (n <= 0) return 0;
-  const bool stg = n <= kStageRays;
-  const size_t sh = stg ? (size_t)(prm.n_samples + prm.n_importance) * 64 * 16 : 0;
-  const bool cfg = prm.n_samples == 32 && prm.n_importance == 12;
-  const dim3 g(nblk(n, 64)), b(64);
-  const float4 *rc = (const float4*)rawc, *ri = (const float4*)rawi;
-  if (cfg && stg) hipLaunchKernelGGL((k_fine<32, 12, true>), g, b, sh, st, prm, rd, zc, zi, rc, ri, n, depth, var, rgb, ord);
-  else if (cfg) hipLaunchKernelGGL((k_fine<32, 12, false>), g, b, 0, st, prm, rd, zc, zi, rc, ri, n, depth, var, rgb, ord);
-  else if (stg) hipLaunchKernelGGL((k_fine<0, 0, true>), g, b, sh, st, prm, rd, zc, zi, rc, ri, n, depth, var, rgb, ord);
-  else hipLaunchKernelGGL((k_fine<0, 0, false>), g, b, 0, st, prm, rd, zc, zi, rc, ri, n, depth, var, rgb, ord);
+  if (n <= kWaveRays) {
+    if (prm.n_samples == 32 && prm.n_importance == 12)
+      hipLaunchKernelGGL((k_fine_w<32, 12>), dim3((unsigned)n), dim3(64), 0, st, prm, rd, zc, zi, (const float4*)rawc,
+                         (const float4*)rawi, n, depth, var, rgb, ord);
+    else
+      hipLaunchKernelGGL((k_fine_w<0, 0>), dim3((unsigned)n), dim3(64), 0, st, prm, rd, zc, zi, (const float4*)rawc,
+                         (const float4*)rawi, n, depth, var, rgb, ord);
+    return hip_status(hipGetLastError());
+  }
+  if (prm.n_samples == 32 && prm.n_importance == 12)
+    hipLaunchKernelGGL((k_fine<32, 12>), dim3(nblk(n, 64)), dim3(64), 0, st, prm, rd, zc, zi, (const float4*)rawc,
+                       (const float4*)rawi, n, depth, var, rgb, ord);
+  else
+    hipLaunchKernelGGL((k_fine<0, 0>), dim3(nblk(n, 64)), dim3(64), 0, st, prm, rd, zc, zi, (const float4*)rawc,
+                       (const float4*)rawi, n, depth, var, rgb, ord);
   return hip_status(hipGetLastError());
 }
 int launch_fine_bwd(const pnr_render_params& prm, const float* rd, const double* zc, const double* zi,
@@ -899,26 +1157,27 @@ int launch_fine_bwd(const pnr_render_params& prm, const float* rd, const double*
                     float* gor = nullptr, float* pad2 = nullptr, int np2 = 0) {
   if (n <= 0) return 0;
   const int M = prm.n_samples + prm.n_importance;
-  const bool stg = n <= kStageRays;
-  // z sorted (8), alpha and T (4 + 4); staged: z (8), raw (16), inside flags (4) in natural order
-  const size_t sh = (size_t)M * 64 * (8 + 2 * 4 + (stg ? 8 + 16 + 4 : 0));
+  const size_t sh = (size_t)M * 64 * (8 + 2 * 4);
   const MapBwd mb{g_sigma, insr, reinterpret_cast<float4*>(gor), reinterpret_cast<float4*>(pad2), np2};
-  const bool cfg = prm.n_samples == 32 && prm.n_importance == 12;
-  const dim3 g(nblk(n, 64)), b(64);
-  const float4 *rc = (const float4*)rawc, *ri = (const float4*)rawi;
-  float4 *oc = (float4*)goc, *oi = (float4*)goi, *p0 = (float4*)pad0, *p1 = (float4*)pad1;
-  if (cfg && stg)
-    hipLaunchKernelGGL((k_fine_bwd<32, 12, true>), g, b, sh, st, prm, rd, zc, zi, rc, ri, insc, insi, ord, n, gd, gv, grgb,
-                       oc, oi, g_nrm, p0, np0, p1, np1, mb);
-  else if (cfg)
-    hipLaunchKernelGGL((k_fine_bwd<32, 12, false>), g, b, sh, st, prm, rd, zc, zi, rc, ri, insc, insi, ord, n, gd, gv,
-                       grgb, oc, oi, g_nrm, p0, np0, p1, np1, mb);
-  else if (stg)
-    hipLaunchKernelGGL((k_fine_bwd<0, 0, true>), g, b, sh, st, prm, rd, zc, zi, rc, ri, insc, insi, ord, n, gd, gv, grgb,
-                       oc, oi, g_nrm, p0, np0, p1, np1, mb);
+  if (n <= kWaveRays) {
+    if (prm.n_samples == 32 && prm.n_importance == 12)
+      hipLaunchKernelGGL((k_fine_bwd_w<32, 12>), dim3((unsigned)n), dim3(64), 0, st, prm, rd, zc, zi,
+                         (const float4*)rawc, (const float4*)rawi, insc, insi, ord, n, gd, gv, grgb, (float4*)goc,
+                         (float4*)goi, g_nrm, (float4*)pad0, np0, (float4*)pad1, np1, mb);
+    else
+      hipLaunchKernelGGL((k_fine_bwd_w<0, 0>), dim3((unsigned)n), dim3(64), 0, st, prm, rd, zc, zi,
+                         (const float4*)rawc, (const float4*)rawi, insc, insi, ord, n, gd, gv, grgb, (float4*)goc,
+                         (float4*)goi, g_nrm, (float4*)pad0, np0, (float4*)pad1, np1, mb);
+    return hip_status(hipGetLastError());
+  }
+  if (prm.n_samples == 32 && prm.n_importance == 12)
+    hipLaunchKernelGGL((k_fine_bwd<32, 12>), dim3(nblk(n, 64)), dim3(64), sh, st, prm, rd, zc, zi, (const float4*)rawc,
+                       (const float4*)rawi, insc, insi, ord, n, gd, gv, grgb, (float4*)goc, (float4*)goi, g_nrm,
+                       (float4*)pad0, np0, (float4*)pad1, np1, mb);
   else
-    hipLaunchKernelGGL((k_fine_bwd<0, 0, false>), g, b, sh, st, prm, rd, zc, zi, rc, ri, insc, insi, ord, n, gd, gv,
-                       grgb, oc, oi, g_nrm, p0, np0, p1, np1, mb);
+    hipLaunchKernelGGL((k_fine_bwd<0, 0>), dim3(nblk(n, 64)), dim3(64), sh, st, prm, rd, zc, zi, (const float4*)rawc,
+                       (const float4*)rawi, insc, insi, ord, n, gd, gv, grgb, (float4*)goc, (float4*)goi, g_nrm,
+                       (float4*)pad0, np0, (float4*)pad1, np1, mb);
   return hip_status(hipGetLastError());
 }
 int launch_ray_grads_f64(const float* rd, const double* za, int sa, const double* zb, int sb, const float* gxa,
@@ -984,6 +1243,17 @@ int launch_window_rays(const int64_t* idx, int64_t n, int64_t per_frame, int H, 
                      cx, cy, c2w, depth, color, ro, rd, gd, gc);
   return hip_status(hipGetLastError());
 }
+int64_t window_sample_state_bytes() { return (int64_t)sizeof(SampleState); }
+int launch_window_sample(uint64_t seed, void* state, int64_t n, int64_t per_frame, int H, int W, float fx, float fy,
+                         float cx, float cy, const float* c2w, const float* depth, const float* color, int S,
+                         float* ro, float* rd, float* gd, float* gc, float* t_rand, int64_t* idx, float* far_out,
+                         hipStream_t st) {
+  if (n <= 0) return 0;
+  const int64_t nb = std::min<int64_t>(kSampleParts, nblk(n, 256));
+  hipLaunchKernelGGL(k_window_sample, dim3((unsigned)nb), dim3(256), 0, st, seed, (SampleState*)state, n, per_frame,
+                     (int64_t)H * W, W, fx, fy, cx, cy, c2w, depth, color, S, ro, rd, gd, gc, t_rand, idx, far_out);
+  return hip_status(hipGetLastError());
+}
 int launch_adam_dev(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1, float beta2,
                     float eps, const int32_t* step_count, hipStream_t st) {
   if (n <= 0) return 0;
@@ -1004,10 +1274,10 @@ int launch_adam_multi(float* p, const float* g, int nseg, const int64_t* off, co
     S.v[q] = v[q];
     S.lr[q] = lr[q];
     S.first[q] = blocks;
-    // grid-stride over at most 64 blocks per segment: every block takes one ticket, and a ticket per
+    // grid-stride over at most 128 blocks per segment: every block takes one ticket, and a ticket per
     // 256 elements (870 for the decoder) queued on one address for ~10 us
-    const int64_t nb = nblk(n[q] > 0 ? n[q] : 1, 256);
-    blocks += (int)(nb < 64 ? nb : 64);
+    const int64_t nb = nblk(n[q] > 0 ? n[q] : 1, 1024);
+    blocks += (int)(nb < 128 ? nb : 128);
   }
   S.first[nseg] = blocks;
   S.nseg = nseg;

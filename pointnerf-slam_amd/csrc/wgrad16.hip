@@ -533,16 +533,18 @@ int wgrad16_prepare(int kind, const float* A, const float* B, int64_t K, int64_t
   // split-K over at most one workgroup per CU, >= 8 tiles per workgroup (the flush of the partial
   // tile no longer dominates)
   if (!syn || !syn->part || !syn->part_bias) return PNR_E_ARG;
-  // Tiles (32 points) per workgroup: >= 8, and in a grouped launch enough that the group's GEMMs fill
-  // the chip about once (one 512-thread workgroup per CU): every workgroup flushes a whole 256 x 256
-  // partial tile that k_part_reduce_multi re-reads, so at a small K (the Mapper's 1,000-ray batch:
-  // ~2,400 tiles) many short workgroups spent more on flushes and their reduction than on the GEMM.
+  // Tiles (32 points) per workgroup: >= 8, up to 256 workgroups per GEMM.  Every workgroup flushes a
+  // whole 256 x 256 partial tile that k_part_reduce_multi re-reads, so a grouped launch whose GEMMs
+  // are small (the Mapper's 1,000-ray batch: 2,400 tiles x 4 GEMMs) is sized to fill the chip about
+  // once instead (one workgroup per CU: 133 + 18 us of GEMM + reduction there against 166 + 46 us at
+  // 8 tiles per workgroup); large GEMMs (S-map) keep the wide grid, which hides latency better
+  // (109 ms against 117 ms for the S-map step with one workgroup per CU).
   const int64_t tiles = K / 32;
   int64_t per = 8;
   if (syn->group_jobs > 0) {
-    const int64_t slots = (int64_t)device_cu_count() * wgrad_wgs_per_cu();
-    const int64_t p2 = (tiles * syn->group_jobs + slots - 1) / slots;
-    per = p2 > per ? p2 : per;
+    const int64_t cus = device_cu_count();
+    const int64_t fill = (tiles * syn->group_jobs + cus - 1) / cus;
+    if (fill <= 256) per = fill > per ? fill : per;
   }
   int64_t nwg = (tiles + per - 1) / per;
   nwg = nwg < 4 ? 4 : (nwg > kWgrad16MaxWg ? kWgrad16MaxWg : nwg);
@@ -595,16 +597,6 @@ int wgrad16_prepare(int kind, const float* A, const float* B, int64_t K, int64_t
   job->nwg = (int)nwg;
   *red = ReduceJob{a.part, a.part_bias, (int)nwg, 256, ntb * 32, a.nb, a.C, a.ldc, a.bias};
   return 0;
-}
-
-// workgroups per CU a grouped weight-gradient launch aims at (PNR_WGRAD_WGS_PER_CU, default 1)
-int wgrad_wgs_per_cu() {
-  static const int v = [] {
-    const char* e = getenv("PNR_WGRAD_WGS_PER_CU");
-    const int x = e ? atoi(e) : 1;
-    return x >= 1 && x <= 64 ? x : 1;
-  }();
-  return v;
 }
 
 int launch_wgrad16_group(const Wgrad16Job* jobs, int n, hipStream_t st) {
@@ -697,7 +689,7 @@ __global__ __launch_bounds__(256) void k_wgrad_skinny(const float4* __restrict__
     for (int j = 0; j < 8; ++j) acc[m][j] = 0.f;
   float bs[4] = {0.f, 0.f, 0.f, 0.f};
   if (act) {
-    constexpr int U = 4;  // rows in flight per thread (HBM latency: bytes in flight per CU)
+    constexpr int U = 8;  // rows in flight per thread (HBM latency: bytes in flight per CU)
     for (int64_t k = kb + r; k < ke; k += U * RPI) {
       float4 av[U], b0[U], b1[U];
 #pragma unroll

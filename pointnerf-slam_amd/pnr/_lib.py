@@ -25,7 +25,7 @@ PRECISIONS = {'fp32': 0, 'bf16x3': 1, 'bf16': 2, 'f16x3': 3}
 # f16x3: fp32-class forward AND backward (every GEMM on 22-bit split operands with fp32
 # accumulation; tests/test_gpu_parity.py runs every case under fp32 and f16x3 at the same tolerances)
 DEFAULT_PRECISION = os.environ.get('PNR_PRECISION', 'f16x3')
-ABI_VERSION = 10
+ABI_VERSION = 11
 STATUS_F16_RANGE = 1  # include/pnr.h PNR_STATUS_F16_RANGE
 
 
@@ -109,6 +109,10 @@ _SIGS = {
     'pnr_window_rays': (ctypes.c_int, [c_void_p, c_int64, c_int64, c_int32, c_int32, c_float, c_float, c_float,
                                        c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                        c_void_p]),
+    'pnr_window_sample_state_bytes': (c_size_t, []),
+    'pnr_window_sample': (ctypes.c_int, [ctypes.c_uint64, c_void_p, c_int64, c_int64, c_int32, c_int32, c_float,
+                                         c_float, c_float, c_float, c_void_p, c_void_p, c_void_p, c_int32, c_void_p,
+                                         c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     'pnr_adam_step': (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_float, c_float, c_float,
                                      c_float, c_int64, c_void_p]),
     'pnr_adam_step_dev': (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_float, c_float,

@@ -65,15 +65,18 @@ class DataParallel:
             self._bufs[key] = b
         return b
 
-    def global_far_clamp(self, gt_depth_local):
+    def global_far_clamp(self, gt_depth_local, local_far=None):
         """max(1.2 * gt) over every rank's rays (Renderer.py:112), as a one-element float32 device
         tensor: the renderer reads it on the device (far_mode 2), so the step has no host sync and
-        can be captured in a graph."""
-        g = gt_depth_local.reshape(-1).float()
-        if g.numel():
-            m = (g * 1.2).amax().reshape(1)
+        can be captured in a graph.  local_far: this rank's value if already on the device."""
+        if local_far is not None:
+            m = local_far.reshape(-1)[:1].float().clone()
         else:
-            m = torch.full((1,), float('-inf'), device=g.device)
+            g = gt_depth_local.reshape(-1).float()
+            if g.numel():
+                m = (g * 1.2).amax().reshape(1)
+            else:
+                m = torch.full((1,), float('-inf'), device=g.device)
         if self.active:
             dist.all_reduce(m, op=dist.ReduceOp.MAX, group=self.group)
         return m

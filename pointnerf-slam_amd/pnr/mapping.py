@@ -188,7 +188,9 @@ class MapStep:
         reg.backward(views[0], g_fc=views[1], g_feats=views[2], g_sigma=g_s)
         return loss
 
-    def __call__(self, rays_o, rays_d, gt_depth, gt_color, t_rand=None):
+    def __call__(self, rays_o, rays_d, gt_depth, gt_color, t_rand=None, far_clamp=None):
+        """One Mapper iteration.  far_clamp (optional): the batch's max(1.2 gt) as a device scalar
+        (e.g. from WindowSampler), else computed by the render pass (or all-reduced, data parallel)."""
         from .renderer import TrainPass, map_loss
         r = self.renderer
         dev = rays_o.device
@@ -200,7 +202,8 @@ class MapStep:
             t_rand = torch.rand((rays_o.shape[0], r.N_samples), device=dev)
         t_rand = t_rand.float().contiguous()
         self.flat.zero_grad()
-        far_clamp = self.ddp.global_far_clamp(gt_depth) if self.ddp is not None else None
+        if self.ddp is not None:
+            far_clamp = self.ddp.global_far_clamp(gt_depth, far_clamp)
         ren = TrainPass(r, self.c, self.decoder, 'render')
         # the weight images, the point index and the f16 feature copy: built on this stream before the
         # chains fork (both read them)
@@ -369,13 +372,19 @@ def window_rays(idx, n_per_frame, c2w, depth, color, fx, fy, cx, cy):
 
 class WindowSampler:
     """A Mapper iteration's batch over a fixed keyframe window (src/Mapper.py:397, 553-606):
-    `pixs_per_image` = mapping.pixels // len(window) uniform pixels per frame (torch.randint on the
-    device, one draw for the whole window) and their rays, gt depth and colour from ONE pnr_window_rays
-    launch, plus the regulation jitter t_rand (Renderer.py:293).  Two launches per batch plus the RNG,
-    so a captured iteration (MapGraph(batch_fn=sampler)) draws a fresh batch per replay.
-    frames: list of (c2w, gt depth (H,W), gt colour (H,W,3)) device tensors."""
+    `pixs_per_image` = mapping.pixels // len(window) uniform pixels per frame, their rays, gt depth
+    and colour, and the regulation jitter t_rand (Renderer.py:293).
+    frames: list of (c2w, gt depth (H,W), gt colour (H,W,3)) device tensors.
 
-    def __init__(self, frames, pixs_per_image, fx, fy, cx, cy, n_samples=32, generator=None):
+    device_rng=True (default): ONE pnr_window_sample launch draws the pixels and the jitter on the
+    device (counter-based hash of `seed` and a device batch counter) and also returns the batch far
+    clamp max(1.2 gt) as a device scalar -- a captured iteration (MapGraph(batch_fn=sampler)) then
+    spends one launch on its batch.  device_rng=False: torch.randint / torch.rand (torch's Philox
+    stream, `generator`) + one pnr_window_rays launch; far clamp None (computed by the render pass).
+    __call__ returns (rays_o, rays_d, gt_depth, gt_color, t_rand, far_clamp)."""
+
+    def __init__(self, frames, pixs_per_image, fx, fy, cx, cy, n_samples=32, generator=None, device_rng=True,
+                 seed=0):
         self.c2w = torch.stack([f[0][:3] if f[0].shape[0] == 3 else f[0] for f in frames]).float()
         if self.c2w.shape[1] == 3:
             self.c2w = torch.cat([self.c2w, torch.tensor([0., 0., 0., 1.], device=self.c2w.device)
@@ -387,11 +396,35 @@ class WindowSampler:
         self.cam = (fx, fy, cx, cy)
         self.n_samples = n_samples
         self.generator = generator
+        self.device_rng = device_rng
+        self.seed = int(seed) & ((1 << 64) - 1)
+        self.idx = None  # the last batch's pixel indices (device_rng)
+        if device_rng:
+            lib = _lib.load()
+            dev = self.depth.device
+            self.state = torch.zeros(lib.pnr_window_sample_state_bytes(), dtype=torch.uint8, device=dev)
 
     def __call__(self):
         F, H, W = self.depth.shape
         dev = self.depth.device
-        idx = torch.randint(H * W, (F * self.n,), device=dev, generator=self.generator)
-        ro, rd, gd, gc = window_rays(idx, self.n, self.c2w, self.depth, self.color, *self.cam)
-        t_rand = torch.rand((F * self.n, self.n_samples), device=dev, generator=self.generator)
-        return ro, rd, gd, gc, t_rand
+        N = F * self.n
+        if not self.device_rng:
+            idx = torch.randint(H * W, (N,), device=dev, generator=self.generator)
+            ro, rd, gd, gc = window_rays(idx, self.n, self.c2w, self.depth, self.color, *self.cam)
+            t_rand = torch.rand((N, self.n_samples), device=dev, generator=self.generator)
+            return ro, rd, gd, gc, t_rand, None
+        lib = _lib.load()
+        _lib.require_cuda(self.depth, self.color, self.c2w)
+        ro = torch.empty((N, 3), device=dev)
+        rd = torch.empty((N, 3), device=dev)
+        gd = torch.empty(N, device=dev)
+        gc = torch.empty((N, 3), device=dev)
+        t_rand = torch.empty((N, self.n_samples), device=dev)
+        self.idx = torch.empty(N, dtype=torch.int64, device=dev)
+        far = torch.empty(1, device=dev)
+        _lib.check(lib.pnr_window_sample(self.seed, _lib.ptr(self.state), N, self.n, H, W,
+                                         *[float(v) for v in self.cam], _lib.ptr(self.c2w), _lib.ptr(self.depth),
+                                         _lib.ptr(self.color), self.n_samples, _lib.ptr(ro), _lib.ptr(rd),
+                                         _lib.ptr(gd), _lib.ptr(gc), _lib.ptr(t_rand), _lib.ptr(self.idx),
+                                         _lib.ptr(far), _lib.stream_of(dev)), 'window_sample')
+        return ro, rd, gd, gc, t_rand, far

@@ -84,7 +84,7 @@ def grad_elementwise(g, cr, f32, rel_f32, what):
 
 def test_library_info(pnr_mod):
     lib = pnr_mod.library()
-    assert lib.pnr_abi_version() == 10
+    assert lib.pnr_abi_version() == 11
     assert lib.pnr_mlp_packed_floats() > 0
 
 
@@ -276,10 +276,60 @@ def test_window_rays_equal_window_batch(pnr_mod, dev, scene):
                       fx, fy, cx, cy)
     for a, b, what in zip(out, ref, ('rays_o', 'rays_d', 'gt depth', 'gt colour')):
         assert torch.equal(a, b), what
-    ws = WindowSampler(frames, n, fx, fy, cx, cy, generator=torch.Generator(device=dev).manual_seed(3))
-    ro, rd, gd, gc, tr = ws()
-    assert ro.shape == (5 * n, 3) and tr.shape == (5 * n, 32) and gd.shape == (5 * n,)
+    ws = WindowSampler(frames, n, fx, fy, cx, cy, generator=torch.Generator(device=dev).manual_seed(3),
+                       device_rng=False)
+    ro, rd, gd, gc, tr, far = ws()
+    assert ro.shape == (5 * n, 3) and tr.shape == (5 * n, 32) and gd.shape == (5 * n,) and far is None
     assert bool((tr >= 0).all() and (tr < 1).all())
+
+
+def test_window_sample_device_draws(pnr_mod, dev, scene):
+    """pnr_window_sample (the batch drawn on the device in one launch): its rays and gt are
+    pnr_window_rays' on the pixels it drew, bit for bit; far clamp = max(1.2 gt) exactly (the value
+    Renderer.py:112 computes); every call draws a new batch (device counter), a fresh state with
+    the same seed repeats the sequence, another seed does not; draws are uniform: pixel rows /
+    columns and jitter means within 5 sigma of uniform over 100 batches (parity of the distribution,
+    not of torch's Philox sequence -- documented in include/pnr.h)."""
+    from pnr.mapping import WindowSampler, window_rays
+    H, W, fx, fy, cx, cy = 68, 120, 60., 61., 59.5, 33.5
+    g = torch.Generator().manual_seed(7)
+    frames = []
+    for k in (0, 1, 2, 3, 2):
+        c2w = torch.from_numpy(scene['poses'][k]).float()
+        frames.append((c2w.to(dev), torch.rand((H, W), generator=g).to(dev), torch.rand((H, W, 3), generator=g).to(dev)))
+    n = 200
+    ws = WindowSampler(frames, n, fx, fy, cx, cy, seed=11)
+    c2w = torch.stack([f[0] for f in frames])
+    dep, col = torch.stack([f[1] for f in frames]), torch.stack([f[2] for f in frames])
+    idxs, trs = [], []
+    for it in range(100):
+        ro, rd, gd, gc, tr, far = ws()
+        idx = ws.idx.clone()
+        if it < 3:
+            ref = window_rays(idx, n, c2w, dep, col, fx, fy, cx, cy)
+            for a, b, what in zip((ro, rd, gd, gc), ref, ('rays_o', 'rays_d', 'gt depth', 'gt colour')):
+                assert torch.equal(a, b), what
+            assert torch.equal(far, (gd * 1.2).max().reshape(1)), 'far clamp'
+        idxs.append(idx)
+        trs.append(tr.clone())
+    idx = torch.stack(idxs)
+    assert bool(((idx >= 0) & (idx < H * W)).all())
+    assert not torch.equal(idxs[0], idxs[1])
+    ws2 = WindowSampler(frames, n, fx, fy, cx, cy, seed=11)
+    ws2()
+    assert torch.equal(ws2.idx, idxs[0])
+    ws3 = WindowSampler(frames, n, fx, fy, cx, cy, seed=12)
+    ws3()
+    assert not torch.equal(ws3.idx, idxs[0])
+    tr = torch.stack(trs).double()
+    assert bool((tr >= 0).all() and (tr < 1).all())
+    N = tr.numel()
+    assert abs(tr.mean().item() - 0.5) < 5 * (1 / 12) ** 0.5 / N ** 0.5
+    for cnt, k in ((torch.bincount((idx // W).reshape(-1), minlength=H), H),
+                   (torch.bincount((idx % W).reshape(-1), minlength=W), W)):
+        e = idx.numel() / k
+        chi2 = (((cnt.double() - e) ** 2) / e).sum().item()
+        assert abs(chi2 - (k - 1)) < 5 * (2 * (k - 1)) ** 0.5, chi2
 
 
 def test_adam_matches_torch(pnr_mod, dev):

@@ -52,9 +52,13 @@ def pnr_mod():
 # rounding of the threshold), where two float32 orders take different branches.  A flipped sample
 # changes one rank-1 term of a weight gradient (its delta times its activations), so it can move ANY
 # fraction of the elements, each by about one sample's share: ~max|g| / n for n samples (~2.7e4 here).
-# FLIP_CAP = 5e-4 max|g| admits about a dozen such terms; the share of elements beyond the strict bound
-# is printed (it was 0-2% over the runs; it is not what a flip bounds, so it is not asserted).
+# FLIP_CAP = 5e-4 max|g| admits about a dozen such terms, and only on a bounded share of the elements:
+# at most FLIP_FRAC of a tensor's elements (at least one) may use the allowance, i.e. lie beyond the
+# strict bound.  Measured maxima (round 4): 0.75% of fc_c.1.weight and 0.34% of fc_c.0.weight (the
+# trilinear render), 0.26% of dL/drays_o (IDW tracking), 0.15% of pts_linears.0.weight, one of C3's
+# 256 pts_linears.2.bias.
 FLIP_CAP = 5e-4
+FLIP_FRAC = 1e-2
 # summation-magnitude floor, in ulps (u = 2^-24) of M = sum_p |t_p|: a gradient element is a sum over
 # samples of terms that each carry a few ulps from the forward / delta chain, and the sum itself
 # rounds in a blocked order; 64 u M bounds both (an element without cancellation has M ~ |g|, where
@@ -62,12 +66,13 @@ FLIP_CAP = 5e-4
 MAG_ULPS = 64.0
 
 
-def grad_elementwise(g, cr, f32, what, rel_f32=None, rtol=1e-3, atol=1e-6, flips=False, mag=None):
+def grad_elementwise(g, cr, f32, what, rel_f32=None, rtol=1e-3, atol=1e-6, flips=False, mag=None,
+                     flip_frac=FLIP_FRAC):
     """|g - g_cr| <= rtol |g_cr| + (atol + d32) max|g_cr| + MAG_ULPS u M and |g - g_f32| <= the same
     with g_f32 elementwise, d32 = rel_f32 or max |g_f32 - g_cr| / max |g_cr|, M = the element's
     summation magnitude sum_p |t_p| (oracle.ref_points.magnitudes; 0 when not given): the float32
-    rounding floor of a sum that cancels.  flips: elements may exceed that by up to FLIP_CAP max|g|
-    (decision-edge samples, see above)."""
+    rounding floor of a sum that cancels.  flips: up to a share flip_frac of the elements may exceed
+    that by up to FLIP_CAP max|g| (decision-edge samples, see above)."""
     g = g.detach().cpu().numpy() if isinstance(g, torch.Tensor) else np.asarray(g)
     cr, f32 = (t.detach().cpu().numpy() if isinstance(t, torch.Tensor) else np.asarray(t) for t in (cr, f32))
     mfloor = 0.0 if mag is None else MAG_ULPS * 2.0 ** -24 * np.asarray(mag)
@@ -83,6 +88,8 @@ def grad_elementwise(g, cr, f32, what, rel_f32=None, rtol=1e-3, atol=1e-6, flips
         if flips:
             np.testing.assert_array_less(np.abs(g - ref), rtol * np.abs(ref) + np.maximum(a, FLIP_CAP * m) + 1e-45,
                                          err_msg=f'{what} vs {tag}')
+            assert int(np.sum(viol > 1)) <= max(1.0, flip_frac * g.size), \
+                f'{what} vs {tag}: {out:.2e} of the elements use the flip allowance'
         else:
             np.testing.assert_array_less(np.abs(g - ref), rtol * np.abs(ref) + a + 1e-45, err_msg=f'{what} vs {tag}')
 
@@ -248,7 +255,39 @@ def test_gather_backward_matches_oracle(pnr_mod, dev):
     qr = q.clone().requires_grad_(True)
     (RP.point_gather(qr, xyz, fr, 'idw', radius=0.06, k=8) * gc).sum().backward()
     close(pts.feats.grad, fr.grad, 2e-5 * fr.grad.abs().max().item(), 'dL/dfeats')
-    close(qd.grad, qr.grad, 2e-3 * qr.grad.abs().max().item(), 'dL/dp')
+    # dL/dp elementwise at rtol 1e-3 against the correctly-rounded gradient (float64 weights, sums and
+    # backward over the same neighbour sets, the inputs rounded to float32 as the kernels read them),
+    # with the float32 summation floor 64 u M, M = sum_j |dw_j/dp| (|g_j| + sum_k wn_k |g_k|) / W
+    _, idx, _ = _gather_c_abi(pnr_mod, dev, pts, q, 8)
+    _, idx_ref, _ = RP.point_gather(q, xyz, feats, 'idw', radius=0.06, k=8, return_idx=True)
+    assert np.array_equal(idx.cpu().numpy(), idx_ref.numpy().astype(np.int32))
+    gcr, mag = idw_grad_p_cr(q.float().double(), xyz.double(), feats.double(), idx_ref, gc.double())
+    grad_elementwise(qd.grad, gcr, qr.grad, 'dL/dp', mag=mag)
+
+
+def idw_grad_p_cr(p, xyz, feats, idx, gc, eps=1e-6):
+    """d(sum c(p) . gc)/dp of the IDW gather (oracle.ref_points.neighbour_weights / point_gather) in
+    float64 on a fixed neighbour set, and each element's summation magnitude M."""
+    p = p.clone().requires_grad_(True)
+    valid = idx >= 0
+    ic = idx.clamp(min=0)
+    dl = p[:, None, :] - xyz[ic]
+    d2 = (dl * dl).sum(-1)
+    d = torch.sqrt(torch.clamp(d2, min=eps * eps * 0.25))
+    w = torch.where(valid, 1.0 / torch.clamp(d, min=eps), torch.zeros_like(d))
+    W = w.sum(1)
+    W = torch.where(W > 0, W, torch.ones_like(W))
+    wn = w / W[:, None]
+    fk = feats[ic]
+    c = (wn[:, :, None] * fk).sum(1)
+    (c * gc).sum().backward()
+    with torch.no_grad():
+        gabs = torch.where(valid, (fk.abs() * gc.abs()[:, None, :]).sum(-1), torch.zeros_like(d))  # |g_j|
+        dw = torch.where(valid, 1.0 / torch.clamp(d, min=eps) ** 2, torch.zeros_like(d))[..., None] * \
+            (dl.abs() / torch.clamp(d, min=eps)[..., None])                                      # |dw_j/dp|
+        a = (gabs + (wn * gabs).sum(1, keepdim=True)) / W[:, None]
+        mag = (dw * a[..., None]).sum(1)
+    return p.grad.detach(), mag.numpy()
 
 
 def test_decoder_c32_matches_reference(pnr_mod, dev):

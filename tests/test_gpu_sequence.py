@@ -150,12 +150,13 @@ def test_twenty_frame_loop_teacher_forced_modes_agree(sequence, scene, dev):
     # the first mapping round (10 iterations on frame 0, before any tracking) and the first tracking
     # iteration of frame 1 (after it) follow fp32 closely; later rounds amplify rounding through Adam's
     # per-element normalisation and the Tracker's 1/sqrt(var) weights (var is a cancellation-heavy
-    # float64 second moment), so the loop as a whole is held to a looser bound
+    # float64 second moment), so the loop as a whole is held to what the loop does to an fp32-class
+    # perturbation of fp32 itself (the control below), not to a fixed bound
     m0 = np.max(np.abs(np.array(m16[:MAP_ITERS]) - np.array(m32[:MAP_ITERS])) / np.array(m32[:MAP_ITERS]))
     t0 = abs(t16[0, 0] - t32[0, 0]) / abs(t32[0, 0])
     print(f'first mapping round: map losses rel max {m0:.2e}; frame 1 first tracking loss rel {t0:.2e}')
     assert m0 < 1e-3 and t0 < 1e-3
-    assert rel_w < 1e-3 and rel_m < 0.1 and rel_t < 0.25
+    assert rel_w < 1e-3
     # control: fp32 against itself with every decoder weight moved by 2^-22 relative (the size of one
     # f16x3 product's rounding).  If the loop amplifies rounding, that run drifts from fp32 as well;
     # f16x3 must not drift more than twice as far as this fp32-class perturbation (+ a small floor)

@@ -2,10 +2,10 @@
 tests/test_gpu_configs.py, which holds their parity against the oracle).
 
   C3  office3 scaled bound, 200k neural points (IDW r = 1 cm, k = 8), Replica 680x1200 camera, bf16 and
-      f16x3 decoders: the Mapper iteration at mapping.pixels = 1,000 (HIP-graph-free eager MapStep)
-      and at a 307,200-ray batch
+      f16x3 decoders: the Mapper iteration at mapping.pixels = 1,000 (eager MapStep and replayed from a
+      captured HIP graph, pnr.mapping.MapGraph) and at a 307,200-ray batch
   C5  Apartment scaled bound, 1M points with float16 features, 720x1280 camera: the Mapper
-      iteration at mapping.pixels = 5,000 and at 307,200 rays
+      iteration at mapping.pixels = 5,000 (eager and graph-replayed) and at 307,200 rays
 
   python tools/config_bench.py [--iters N] > profiles/<tag>_configs.json"""
 import argparse
@@ -23,7 +23,7 @@ from oracle import ref_render as RR  # noqa: E402  (scene construction only, nev
 import test_gpu_configs as TC  # noqa: E402
 
 
-def map_rate(pnr, slam, dec, pts, bound, cam, n, precision, iters, seed):
+def map_rate(pnr, slam, dec, pts, bound, cam, n, precision, iters, seed, graph=False):
     from pnr.mapping import MapStep
     H, W, fx, fy, cx, cy = cam
     dev = torch.device('cuda:0')
@@ -48,8 +48,23 @@ def map_rate(pnr, slam, dec, pts, bound, cam, n, precision, iters, seed):
     torch.cuda.synchronize()
     el = (time.perf_counter() - t0) / iters
     assert r.status(dev) == 0
-    return {'rays': n, 'ms_per_iter': round(el * 1e3, 3), 'rays_per_s': round(n / el, 1), 'precision': precision,
-            'iters': iters}
+    out = {'rays': n, 'ms_per_iter': round(el * 1e3, 3), 'rays_per_s': round(n / el, 1), 'precision': precision,
+           'iters': iters}
+    if graph:  # the same step captured once (gather, fc_c injection, deterministic feature backward, Adam)
+        from pnr.mapping import MapGraph
+        mg = MapGraph(ms, ro, rd, gt, col, tr)
+        gi = max(iters, 20)
+        for _ in range(3):
+            mg()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(gi):
+            mg()
+        torch.cuda.synchronize()
+        eg = (time.perf_counter() - t0) / gi
+        assert r.status(dev) == 0
+        out['graph'] = {'ms_per_iter': round(eg * 1e3, 3), 'rays_per_s': round(n / eg, 1), 'iters': gi}
+    return out
 
 
 def main():
@@ -61,14 +76,16 @@ def main():
     dev = torch.device('cuda:0')
     out = {'what': 'MapStep (render + regulation + L1 losses + backward + decoder and point-feature Adam) with '
                    'the neural-point decoder (c_dim 32, fc_c injection), synthetic room scenes of '
-                   'tests/test_gpu_configs.py; eager launches, mean of --iters after 2 warm-ups'}
+                   'tests/test_gpu_configs.py; eager launches, mean of --iters after 2 warm-ups; `graph`: the '
+                   'same step replayed from a captured HIP graph (MapGraph), mean of max(--iters, 20)'}
     cam3 = (680, 1200, 600., 600., 599.5, 339.5)
     bound, xyz, feats, params, _, _, slam, pts = TC.scene_case(pnr, dev, TC.OFFICE3, *cam3, 200_000, 8, 0.01, seed=31)
     out['C3'] = {'points': int(pts.xyz.shape[0]), 'bound': bound.tolist(), 'runs': []}
     for prec in ('bf16', 'f16x3'):
         dec = TC.make_decoder(pnr, params, dev, prec)
         for n in (1000, 307200):
-            out['C3']['runs'].append(map_rate(pnr, slam, dec, pts, bound, cam3, n, prec, args.iters, 3))
+            out['C3']['runs'].append(map_rate(pnr, slam, dec, pts, bound, cam3, n, prec, args.iters, 3,
+                                              graph=n <= 5000))
             print(json.dumps(out['C3']['runs'][-1]), file=sys.stderr, flush=True)
     del pts
     cam5 = (720, 1280, 607.4694, 607.4535, 636.9967, 369.2690)
@@ -77,7 +94,8 @@ def main():
     out['C5'] = {'points': int(pts.xyz.shape[0]), 'point_features': 'float16', 'bound': bound.tolist(), 'runs': []}
     dec = TC.make_decoder(pnr, params, dev, 'f16x3')
     for n in (5000, 307200):
-        out['C5']['runs'].append(map_rate(pnr, slam, dec, pts, bound, cam5, n, 'f16x3', args.iters, 5))
+        out['C5']['runs'].append(map_rate(pnr, slam, dec, pts, bound, cam5, n, 'f16x3', args.iters, 5,
+                                          graph=n <= 5000))
         print(json.dumps(out['C5']['runs'][-1]), file=sys.stderr, flush=True)
     print(json.dumps(out))
 
