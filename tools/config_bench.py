@@ -55,11 +55,11 @@ def map_rate(pnr, slam, dec, pts, bound, cam, n, precision, iters, seed, graph=F
         mg = MapGraph(ms, ro, rd, gt, col, tr)
         gi = max(iters, 20)
         for _ in range(3):
-            mg()
+            mg(*mg.inputs)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(gi):
-            mg()
+            mg(*mg.inputs)
         torch.cuda.synchronize()
         eg = (time.perf_counter() - t0) / gi
         assert r.status(dev) == 0

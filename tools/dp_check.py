@@ -56,7 +56,7 @@ class FixedClamp:
     def __init__(self, clamp):
         self.clamp = clamp
 
-    def global_far_clamp(self, g):
+    def global_far_clamp(self, g, local_far=None):
         return self.clamp
 
     def allreduce_(self, x):
