@@ -144,6 +144,10 @@ typedef struct pnr_render_params {
   int32_t need_ray_grads;          /* backward also produces dL/drays_o, dL/drays_d (tracking) */
   const pnr_points* points;        /* neural-point features, NULL = the reference decoder (c_dim=0) */
   int32_t precision;               /* PNR_PREC_* of the decoder matmuls                           */
+  int32_t grads_overwrite;         /* ABI 11, backward: 0 = add the decoder / fc_c weight gradients
+                                      into `grads` / `g_fc` (autograd's accumulation), 1 = store them
+                                      (the caller need not zero them first; point-feature gradients
+                                      always accumulate)                                          */
   int32_t* status;                 /* ABI 7: device int32 receiving PNR_STATUS_* bits (ORed), or NULL */
   const float* far_clamp_dev;      /* ABI 7: device float32 far clamp of far_mode 2                */
 } pnr_render_params;

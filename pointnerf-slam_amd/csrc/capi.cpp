@@ -263,8 +263,18 @@ __global__ void k_fill(float* p, int64_t n, float v) {
 
 // Shared backward core over P points with saved activations `sv` and dL/draw in b.g_out.
 int mlp_backward_core(int prec, const float* packed, const SaveArgs& sv, int64_t P, BwdWS& b, float* const* grads,
-                      bool want_gx, hipStream_t st, const FeatBwd* fb = nullptr) {
+                      bool want_gx, hipStream_t st, const FeatBwd* fb = nullptr, bool overwrite = false) {
   const bool split = prec != PNR_PREC_FP32;  // f16x3 delta chain + f16x3 weight-gradient GEMMs
+  if (overwrite && !split) {  // the fp32 GEMMs add into C: store = add into zeroed gradients
+    static const int64_t dec_n[PNR_N_PARAMS] = {3 * kFourier, kHidden * kFourier, kHidden, kHidden * kHidden, kHidden,
+                                                kHidden * kHidden, kHidden, kHidden * kHidden, kHidden, 4 * kHidden, 4};
+    for (int i = 0; grads && i < PNR_N_PARAMS; ++i)
+      if (int rc = hip_status(hipMemsetAsync(grads[i], 0, dec_n[i] * sizeof(float), st))) return rc;
+    for (int i = 0; fb && fb->g_fc && i < PNR_N_FC_PARAMS; ++i)
+      if (int rc = hip_status(hipMemsetAsync(fb->g_fc[i], 0, (i % 2 ? kHidden : kHidden * kCDim) * sizeof(float), st)))
+        return rc;
+    overwrite = false;
+  }
   for (int64_t p0 = 0; p0 < P; p0 += b.C) {
     const int64_t C = (P - p0) < b.C ? (P - p0) : b.C;
     BwdArgs a;
@@ -280,9 +290,6 @@ int mlp_backward_core(int prec, const float* packed, const SaveArgs& sv, int64_t
     a.fcw = fb ? fb->fcw : nullptr;
     a.gH = b.gH;
     a.g_c = fb ? b.g_c + p0 * kCDim : nullptr;
-    // the delta chain: exact fp32 MFMA for PNR_PREC_FP32, f16x3 split MFMA otherwise
-    int rc = prec == PNR_PREC_FP32 ? launch_mlp_bwd(packed, a, C, st) : launch_mlp_bwd_bf(packed, a, C, st);
-    if (rc) return rc;
     const int64_t hstride = sv.ld * kHidden;  // h_l rows of this chunk: h + l_idx * ld * 256 + p0 * 256
     const int64_t dstride = b.C * kHidden;
     // split precisions: every GEMM of the chunk writes its own partial region, and ONE reduce launch
@@ -299,14 +306,22 @@ int mlp_backward_core(int prec, const float* packed, const SaveArgs& sv, int64_t
       ++nj;
     };
     const bool want_fc = fb && fb->g_fc;
+    int rc = 0;
+    // output layer (split precisions): dWo (4x256) += g_out^T h4 ; dbo += colsum(g_out).  It needs only
+    // g_out and the forward's h4, so it streams its 1 KB/point BEFORE the delta chain, not behind the
+    // chain's 3 KB/point of stores (measured at the 1,000-ray Mapper batch: 32 us after the chain)
+    if (split && grads) {
+      rc = launch_wgrad_out16(b.g_out + p0 * 4, sv.hP + p0 * kHidden + 3 * hstride, C, grads[9], grads[10], pp, pb,
+                              st, &jobs[nj]);
+      if (rc) return rc;
+      took();
+    }
+    // the delta chain: exact fp32 MFMA for PNR_PREC_FP32, f16x3 split MFMA otherwise
+    rc = prec == PNR_PREC_FP32 ? launch_mlp_bwd(packed, a, C, st) : launch_mlp_bwd_bf(packed, a, C, st);
+    if (rc) return rc;
     if (!grads && !want_fc) {  // no weight gradients (the Tracker's camera-only backward)
     } else if (split) {  // f16x3 GEMMs on the fp32 saves (h / e by k_mlp_fwd16, deltas by k_mlp_bwd16)
       const float* hp = sv.hP + p0 * kHidden;
-      // output layer: dWo (4x256) += g_out^T h4 ; dbo += colsum(g_out)
-      if (grads) {
-        rc = launch_wgrad_out16(b.g_out + p0 * 4, hp + 3 * hstride, C, grads[9], grads[10], pp, pb, st, &jobs[nj]);
-        if (rc == 0) took();
-      }
       // hidden layers: dW_l += delta_{l+1}^T h_l  (W3: delta4.h3, W2: delta3.h2, W1: delta2.h1); delta4
       // is not stored by k_mlp_bwd16 (rank 4: rebuilt from g_out and the h4 masks inside the GEMM).
       // These GEMMs (and the fc_c ones below) are independent: prepared here, launched as one group.
@@ -373,6 +388,8 @@ int mlp_backward_core(int prec, const float* packed, const SaveArgs& sv, int64_t
         rc = launch_wgrad(kWgradFc, b.gH + l * dstride, kHidden, fb->c + p0 * kCDim, kCDim, C, fb->g_fc[2 * l], kCDim,
                           fb->g_fc[2 * l + 1], b.part, b.part_bias, st);
     }
+    if (overwrite && p0 == 0)  // the first chunk stores its sums; the later chunks add to them
+      for (int i = 0; i < nj; ++i) jobs[i].overwrite = 1;
     if (rc == 0) rc = launch_part_reduce_multi(jobs, nj, st);
     if (rc) return rc;
   }
@@ -392,8 +409,9 @@ extern "C" {
 
 // the ctypes mirror (pnr/_lib.py) and tests/test_capi.py assume these offsets
 static_assert(offsetof(pnr_points, feat_half) == 104 && sizeof(pnr_points) == 112, "pnr_points layout (ABI 6)");
-static_assert(offsetof(pnr_render_params, status) == 608 && sizeof(pnr_render_params) == 624,
-              "pnr_render_params layout (ABI 7)");
+static_assert(offsetof(pnr_render_params, status) == 608 && sizeof(pnr_render_params) == 624 &&
+                  offsetof(pnr_render_params, grads_overwrite) == 604,
+              "pnr_render_params layout (ABI 7; ABI 11 grads_overwrite in the padding after precision)");
 int pnr_abi_version(void) { return PNR_ABI_VERSION; }
 
 int pnr_timing_enable(int on) {
@@ -623,7 +641,7 @@ int pnr_render_bwd(const pnr_render_params* prm, const float* packed, const floa
   if (rc) return rc;
   FeatBwd fb{pts ? pts->fc_packed : nullptr, w.c, pts ? pts->g_fc : nullptr};
   rc = mlp_backward_core(prm->precision, packed, w.save, ld, b, grads, prm->need_ray_grads != 0, st,
-                         pts ? &fb : nullptr);
+                         pts ? &fb : nullptr, prm->grads_overwrite != 0);
   if (rc) return rc;
   if (pts) {  // neural-point features and dL/dp through the gather weights
     rc = launch_gather_bwd(*pts, nullptr, kRaysZ64, w.save.xP, ld, w.nidx, w.nw, w.c, b.g_c,
@@ -742,7 +760,7 @@ int pnr_regulation_bwd(const pnr_render_params* prm, const float* packed, const 
   if (rc) return rc;
   FeatBwd fb{pts ? pts->fc_packed : nullptr, w.c, pts ? pts->g_fc : nullptr};
   rc = mlp_backward_core(prm->precision, packed, w.save, ld, b, grads, prm->need_ray_grads != 0, st,
-                         pts ? &fb : nullptr);
+                         pts ? &fb : nullptr, prm->grads_overwrite != 0);
   if (rc) return rc;
   if (pts) {
     rc = launch_gather_bwd(*pts, nullptr, kRaysZ32, w.save.xP, ld, w.nidx, w.nw, w.c, b.g_c,
@@ -895,7 +913,8 @@ int pnr_map_bwd(const pnr_render_params* prm, const float* packed, const float* 
                            (int)(w.ld - w.r1 - n * I));
   if (rc) return rc;
   FeatBwd fb{pts ? pts->fc_packed : nullptr, w.c, pts ? pts->g_fc : nullptr};
-  rc = mlp_backward_core(prm->precision, packed, w.save, w.ld, b, grads, false, st, pts ? &fb : nullptr);
+  rc = mlp_backward_core(prm->precision, packed, w.save, w.ld, b, grads, false, st, pts ? &fb : nullptr,
+                         prm->grads_overwrite != 0);
   if (rc) return rc;
   if (pts)
     rc = launch_gather_bwd(*pts, nullptr, kPtsX4, x4, w.ld, w.nidx, w.nw, w.c, b.g_c, nullptr, true, b.gws, b.gws_bytes,

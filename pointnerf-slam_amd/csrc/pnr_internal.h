@@ -341,6 +341,7 @@ struct ReduceJob {
   float* C;
   int64_t ldc;
   float* bias;
+  int overwrite = 0;  // 1: C / bias = the sum (+ 0, as into zeroed gradients) instead of += the sum
   int64_t part_floats() const { return (int64_t)nwg * nr * pw; }
   int64_t bias_floats() const { return (int64_t)nwg * nr; }
 };

@@ -472,8 +472,8 @@ __global__ __launch_bounds__(64 * kRedWaves) void k_part_reduce_multi(ReduceJobs
     float s = red[0][lane];
 #pragma unroll
     for (int i = 1; i < kRedWaves; ++i) s += red[i][lane];
-    if (is_bias) jb.bias[e] += s;
-    else jb.C[(e / jb.pw) * jb.ldc + e % jb.pw] += s;
+    float* dst = is_bias ? jb.bias + e : jb.C + (e / jb.pw) * jb.ldc + e % jb.pw;
+    *dst = (jb.overwrite ? 0.f : *dst) + s;
   }
 }
 

@@ -59,7 +59,7 @@ class RenderParams(ctypes.Structure):
         ('bound', ctypes.c_double * 6), ('far_clamp', ctypes.c_double),
         ('t_vals', c_float * MAX_SAMPLES), ('u_vals', c_float * MAX_SAMPLES),
         ('save_for_backward', c_int32), ('need_ray_grads', c_int32),
-        ('points', ctypes.POINTER(Points)), ('precision', c_int32),
+        ('points', ctypes.POINTER(Points)), ('precision', c_int32), ('grads_overwrite', c_int32),
         ('status', c_void_p), ('far_clamp_dev', c_void_p),
     ]
 

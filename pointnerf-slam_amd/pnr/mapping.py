@@ -201,7 +201,11 @@ class MapStep:
         if t_rand is None:
             t_rand = torch.rand((rays_o.shape[0], r.N_samples), device=dev)
         t_rand = t_rand.float().contiguous()
-        self.flat.zero_grad()
+        if self.fused:  # the map pass stores the decoder / fc_c gradients (grads_overwrite): zero the rest
+            if self.points is not None:
+                self._views['main'][2].zero_()
+        else:
+            self.flat.zero_grad()
         if self.ddp is not None:
             far_clamp = self.ddp.global_far_clamp(gt_depth, far_clamp)
         ren = TrainPass(r, self.c, self.decoder, 'render')
@@ -219,7 +223,8 @@ class MapStep:
             loss, g_d, g_c, g_s = map_loss(gt_depth, d, gt_color, c, self.w_color, sigma=sigma, w_reg=self.w_reg,
                                            ws=self._loss_ws('main'))
             views = self._views['main']
-            mp.backward(views[0], g_fc=views[1], g_feats=views[2], g_depth=g_d, g_rgb=g_c, g_sigma=g_s)
+            mp.backward(views[0], g_fc=views[1], g_feats=views[2], g_depth=g_d, g_rgb=g_c, g_sigma=g_s,
+                        overwrite=True)
             return self._finish(loss)
         main = torch.cuda.current_stream(dev)
         overlap = self._overlaps(rays_o.shape[0])

@@ -349,9 +349,12 @@ class MapPass:
         self.prm, self.ws, self.packed, self.rays = prm, ws, packed, (rays_o, rays_d, far_clamp)
         return depth, var, rgb, sigma
 
-    def backward(self, grads, g_fc=None, g_feats=None, g_depth=None, g_rgb=None, g_sigma=None):
+    def backward(self, grads, g_fc=None, g_feats=None, g_depth=None, g_rgb=None, g_sigma=None, overwrite=False):
+        """Adds the decoder / fc_c gradients into grads / g_fc, or stores them (overwrite: no zero fill
+        needed, pnr_render_params.grads_overwrite); the point-feature gradients always add."""
         lib = _lib.load()
         prm, ws, packed = self.prm, self.ws, self.packed
+        prm.grads_overwrite = 1 if overwrite else 0
         rays_o, rays_d, _ = self.rays
         dev = rays_o.device
         n = rays_o.shape[0]
