@@ -546,7 +546,12 @@ def faithful_extra(pnr, slam, params, bound, pose, dev, ddp, lib, sizes=(1000, 5
         peak = ALGO_PEAK_TF['f16x3']
         e = {'ms_per_iter': round(el / steps * 1e3, 4), 'rays_per_s': round(rate, 1), 'graph': True, 'iters': steps,
              'achieved_tflops': round(tf, 2), 'frac_of_split_peak': round(tf / peak, 4),
-             'flop_basis': '115.29 MFLOP per ray per mapping iteration (SURVEY.md 8(d)); peak 833 TF (f16 MFMA / 3)'}
+             'flop_basis': '115.29 MFLOP per ray per mapping iteration (SURVEY.md 8(d)); peak 833 TF (f16 MFMA / 3)',
+           'eager_ms_per_iter': round(el_e / 20 * 1e3, 4),
+           'roofline': kernel_roofline(kt, 'f16x3', el_e, traffic_units=True),
+           'kernel_rooflines': kernel_table(kt, 'f16x3', el_e, 20),
+           'kernel_profile': 'profiles/r04_room0_timeline.txt, profiles/r04_room0_kernel_stats.csv (rocprofv3 of '
+                             'the graph replay)'}
         if cpu:
             cr = oracle_map_rate(bound, pose, params, n)
             e['cpu_baseline'] = {'value': round(cr, 1), 'unit': 'rays/s', 'cores': cpu_threads(), 'kind': 'port',
@@ -610,6 +615,9 @@ def room0_extra(pnr, params, bound, pose, dev, ddp, lib, steps=100, warmup=5, cp
     el, _ = timed(step, steps, warmup, ddp, lib)
     n = per * ROOM0_WINDOW
     rate = n * steps / el
+    # the same iteration launched eagerly, for the live per-kernel times (hipEvents around each launch;
+    # a graph replay has no per-launch host hook): the MLP kernels' rooflines at this batch size
+    el_e, kt = timed(lambda: mstep(*sampler()), 20, 3, ddp, lib)
     tf = MAP_FLOP_PER_RAY * rate / 1e12
     peak = ALGO_PEAK_TF['f16x3']
     out = {'workload': 'room0 Mapper iteration: 1,000 rays = 5-frame window x 200 uniform pixels on the 680x1200 '
@@ -735,6 +743,7 @@ def main():
                    'config': {'workload': e['workload'], 'rays_per_gpu': e['rays_per_iter'],
                               'global_batch': e['rays_per_iter'] * world, 'parallelism': f'replicas{world}',
                               'decoder_precision': prec, 'graph': True},
+                   'roofline': e.get('roofline'), 'cpu_baseline': e.get('cpu_baseline'),
                    'room0_iter': e}
             print(json.dumps(out), flush=True)
         if world > 1:

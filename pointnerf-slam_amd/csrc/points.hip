@@ -30,6 +30,8 @@
 //   k_gather_bwd    dL/df_i += w_k dL/dc (float atomics) and dL/dp through the weights.
 #include <mutex>
 
+#include <type_traits>
+
 #include "pnr_internal.h"
 
 namespace pnr {
@@ -627,7 +629,9 @@ struct SearchLds {
 #ifndef PNR_SEARCH_WAVES
 #define PNR_SEARCH_WAVES (PNR_FEAT_ROWS > 1 ? 5 : 7)
 #endif
-template <int KER>
+// HALF: float16 features (pnr_points.feat_half), its own instantiation (a run-time dtype branch in the
+// feature rounds added register pressure that spilled)
+template <int KER, bool HALF>
 __global__ __launch_bounds__(64, PNR_SEARCH_WAVES) void k_gather_search(GatherArgs a) {
   PNR_FP_STRICT
   __shared__ SearchLds L;
@@ -714,16 +718,19 @@ __global__ __launch_bounds__(64, PNR_SEARCH_WAVES) void k_gather_search(GatherAr
         const int cnt = total - base < kCandBatch ? total - base : kCandBatch;
 #pragma unroll
         for (int j = lane; j < kCandBatch; j += 64) {
-          if (j < cnt) {
-            const int g = base + j;
-            int src = 0, tg = 0;
+          // both of a lane's candidates loaded unconditionally (past the batch: sorted point 0 -- the
+          // search runs only when the cloud has points -- not stored), so their round trips overlap
+          const int g = base + j;
+          int src = 0, tg = 0;
 #pragma unroll
-            for (int n = 0; n < 8; ++n) {
-              const bool in = g >= cs[n] && g < ce[n];
-              src = in ? cb[n] + (g - cs[n]) : src;
-              tg = in ? cf[n] : tg;
-            }
-            L.cand[j] = a.sorted[src];
+          for (int n = 0; n < 8; ++n) {
+            const bool in = g >= cs[n] && g < ce[n];
+            src = in ? cb[n] + (g - cs[n]) : src;
+            tg = in ? cf[n] : tg;
+          }
+          const float4 v = a.sorted[src];
+          if (j < cnt) {
+            L.cand[j] = v;
             L.tag[j] = (uint8_t)tg;
           } else if (j == cnt) {  // pair padding: a point no sample reaches (d2 = inf, never kept)
             const float inf = __int_as_float(0x7F800000);
@@ -820,38 +827,89 @@ __global__ __launch_bounds__(64, PNR_SEARCH_WAVES) void k_gather_search(GatherAr
     // PNR_FEAT_ROWS samples per round: their feature loads in flight together (the loads cannot move
     // above the previous round's c stores on their own: the compiler must assume they alias).
     // Measured (tools/gather_bench.py, 13.5M samples): 1 row per round 1.22 ms, 2 rows 1.13 ms.
+    // f16 features: every load of a round is issued before any of them is used (the indices read
+    // from LDS first, each row loaded raw, converted afterwards).  An f16 load whose conversion sits
+    // in its own branch compiled to a vmcnt(0) wait inside it, serialising the round's 16 loads
+    // (measured, tools/gather_bench.py --feat-dtype float16: 1.158-1.174 -> 1.084-1.099 ms).  The
+    // fp32 form keeps its direct loads (the raw form split them into 8-B halves: 1.08 -> 1.13 ms).
+    if constexpr (HALF) {
 #pragma unroll 1
-    for (int rr = 0; rr < 8; rr += PNR_FEAT_ROWS) {
-      if (rr * 8 >= n_live) break;  // the remaining slots are empty lanes
-      int rw[PNR_FEAT_ROWS];
-      float4 f[PNR_FEAT_ROWS][PNR_MAX_K];
+      for (int rr = 0; rr < 8; rr += PNR_FEAT_ROWS) {
+        if (rr * 8 >= n_live) break;  // the remaining slots are empty lanes
+        int rw[PNR_FEAT_ROWS];
+        uint2 raw[PNR_FEAT_ROWS][PNR_MAX_K];
 #pragma unroll
-      for (int u = 0; u < PNR_FEAT_ROWS; ++u) {
-        const int sl = (rr + u) * 8 + gq;
-        rw[u] = L.row[sl];
+        for (int u = 0; u < PNR_FEAT_ROWS; ++u) {
+          const int sl = (rr + u) * 8 + gq;
+          rw[u] = L.row[sl];
 #pragma unroll
-        for (int t = 0; t < PNR_MAX_K; ++t) {
-          const int id = L.idx[sl * PNR_MAX_K + t];
-          f[u][t] = make_float4(0.f, 0.f, 0.f, 0.f);
-          if (rw[u] >= 0 && id >= 0) f[u][t] = load_feat4(a.feats4, a.feat_half, (int64_t)id * 8 + q);
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < PNR_FEAT_ROWS; ++u) {
-        if (rw[u] < 0) continue;
-        const int sl = (rr + u) * 8 + gq;
-        float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-        for (int t = 0; t < PNR_MAX_K; ++t) {
-          if (L.idx[sl * PNR_MAX_K + t] >= 0) {
-            const float wn = L.w[sl * PNR_MAX_K + t];
-            acc.x = acc.x + wn * f[u][t].x;
-            acc.y = acc.y + wn * f[u][t].y;
-            acc.z = acc.z + wn * f[u][t].z;
-            acc.w = acc.w + wn * f[u][t].w;
+          for (int t = 0; t < PNR_MAX_K; ++t) {  // missing neighbour / empty slot: point 0, skipped below
+            const int id = L.idx[sl * PNR_MAX_K + t];
+            const uint32_t off = (uint32_t)(rw[u] >= 0 && id >= 0 ? id : 0) * 8u + (uint32_t)q;  // < 2^32
+            raw[u][t] = reinterpret_cast<const uint2*>(a.feats4)[off];
           }
         }
-        nt_store(reinterpret_cast<float4*>(a.c) + (int64_t)rw[u] * 8 + q, acc);  // 8 lanes: one 128-B row
+#pragma unroll
+        for (int u = 0; u < PNR_FEAT_ROWS; ++u) {
+          if (rw[u] < 0) continue;
+          const int sl = (rr + u) * 8 + gq;
+          float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+          for (int t = 0; t < PNR_MAX_K; ++t) {
+            if (L.idx[sl * PNR_MAX_K + t] >= 0) {
+              const uint2 r = raw[u][t];
+              const float f0 = (float)__builtin_bit_cast(_Float16, (uint16_t)(r.x & 0xffffu));
+              const float f1 = (float)__builtin_bit_cast(_Float16, (uint16_t)(r.x >> 16));
+              const float f2 = (float)__builtin_bit_cast(_Float16, (uint16_t)(r.y & 0xffffu));
+              const float f3 = (float)__builtin_bit_cast(_Float16, (uint16_t)(r.y >> 16));
+              const float wn = L.w[sl * PNR_MAX_K + t];
+              acc.x = acc.x + wn * f0;
+              acc.y = acc.y + wn * f1;
+              acc.z = acc.z + wn * f2;
+              acc.w = acc.w + wn * f3;
+            }
+          }
+          nt_store(reinterpret_cast<float4*>(a.c) + (int64_t)rw[u] * 8 + q, acc);  // 8 lanes: one 128-B row
+        }
+      }
+    } else {
+#pragma unroll 1
+      for (int rr = 0; rr < 8; rr += PNR_FEAT_ROWS) {
+        if (rr * 8 >= n_live) break;  // the remaining slots are empty lanes
+        int rw[PNR_FEAT_ROWS];
+        float4 f[PNR_FEAT_ROWS][PNR_MAX_K];
+#pragma unroll
+        for (int u = 0; u < PNR_FEAT_ROWS; ++u) {
+          const int sl = (rr + u) * 8 + gq;
+          rw[u] = L.row[sl];
+#pragma unroll
+          for (int t = 0; t < PNR_MAX_K; ++t) {
+            const int id = L.idx[sl * PNR_MAX_K + t];
+#if defined(PNR_EXP_F32UNCOND)  // experiment: clamped, unconditional loads (point 0 for a missing one)
+            f[u][t] = a.feats4[(uint32_t)(rw[u] >= 0 && id >= 0 ? id : 0) * 8u + (uint32_t)q];
+#else
+            f[u][t] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (rw[u] >= 0 && id >= 0) f[u][t] = load_feat4(a.feats4, a.feat_half, (int64_t)id * 8 + q);
+#endif
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < PNR_FEAT_ROWS; ++u) {
+          if (rw[u] < 0) continue;
+          const int sl = (rr + u) * 8 + gq;
+          float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+          for (int t = 0; t < PNR_MAX_K; ++t) {
+            if (L.idx[sl * PNR_MAX_K + t] >= 0) {
+              const float wn = L.w[sl * PNR_MAX_K + t];
+              acc.x = acc.x + wn * f[u][t].x;
+              acc.y = acc.y + wn * f[u][t].y;
+              acc.z = acc.z + wn * f[u][t].z;
+              acc.w = acc.w + wn * f[u][t].w;
+            }
+          }
+          nt_store(reinterpret_cast<float4*>(a.c) + (int64_t)rw[u] * 8 + q, acc);  // 8 lanes: one 128-B row
+        }
       }
     }
 #else
@@ -871,10 +929,9 @@ __global__ __launch_bounds__(64, PNR_SEARCH_WAVES) void k_gather_search(GatherAr
         int id[4];
         float4 f[4];
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
+        for (int t = 0; t < 4; ++t) {  // unconditional loads (see the PNR_FEAT_ROWS > 1 form)
           id[t] = L.idx[sl * PNR_MAX_K + t0 + t];
-          f[t] = make_float4(0.f, 0.f, 0.f, 0.f);
-          if (id[t] >= 0) f[t] = load_feat4(a.feats4, a.feat_half, (int64_t)id[t] * 8 + q);
+          f[t] = load_feat4(a.feats4, a.feat_half, (int64_t)(id[t] >= 0 ? id[t] : 0) * 8 + q);
         }
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
@@ -1283,13 +1340,11 @@ int launch_gather(const pnr_points& pts, const PointSrc& src, int mode, int64_t 
   if (rc) return rc;
   hipLaunchKernelGGL(k_group_scatter, dim3((unsigned)(kLists * ((a.wl.cap + 255) / 256))), dim3(256), 0, st, a);
   const int64_t tasks = (P + 63) / 64;  // upper bound on the chunks (the kernel reads the real count)
-  if (pts.mode == PNR_GATHER_IDW) {
-    auto kern = k_gather_search<PNR_GATHER_IDW>;
-    hipLaunchKernelGGL(kern, dim3(resident_grid(kern, 64, tasks)), dim3(64), 0, st, a);
-  } else {
-    auto kern = k_gather_search<PNR_GATHER_TRILINEAR>;
-    hipLaunchKernelGGL(kern, dim3(resident_grid(kern, 64, tasks)), dim3(64), 0, st, a);
-  }
+  auto kern = pts.mode == PNR_GATHER_IDW
+                  ? (a.feat_half ? k_gather_search<PNR_GATHER_IDW, true> : k_gather_search<PNR_GATHER_IDW, false>)
+                  : (a.feat_half ? k_gather_search<PNR_GATHER_TRILINEAR, true>
+                                 : k_gather_search<PNR_GATHER_TRILINEAR, false>);
+  hipLaunchKernelGGL(kern, dim3(resident_grid(kern, 64, tasks)), dim3(64), 0, st, a);
   return hip_status(hipGetLastError());
 }
 

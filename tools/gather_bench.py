@@ -40,6 +40,7 @@ def main():
     ap.add_argument('--mode', default='idw')
     ap.add_argument('--reps', type=int, default=5)
     ap.add_argument('--lib', default=None, help='load this libpnr.so build instead (experiments)')
+    ap.add_argument('--feat-dtype', default='float32', choices=['float32', 'float16'])
     args = ap.parse_args()
     import pnr
     if args.lib:
@@ -52,7 +53,7 @@ def main():
     if args.radius is None:
         args.radius = 2 * args.voxel
     pts = pnr.NeuralPoints(xyz, feats, mode=args.mode, radius=args.radius, k=args.k,
-                           spacing=[args.radius] * 3).to(dev)
+                           spacing=[args.radius] * 3, feat_dtype=args.feat_dtype).to(dev)
     P = p.shape[0]
     c = torch.empty((P, 32), device=dev)
     idx = torch.empty((P, args.k), device=dev, dtype=torch.int32)
