@@ -546,12 +546,7 @@ def faithful_extra(pnr, slam, params, bound, pose, dev, ddp, lib, sizes=(1000, 5
         peak = ALGO_PEAK_TF['f16x3']
         e = {'ms_per_iter': round(el / steps * 1e3, 4), 'rays_per_s': round(rate, 1), 'graph': True, 'iters': steps,
              'achieved_tflops': round(tf, 2), 'frac_of_split_peak': round(tf / peak, 4),
-             'flop_basis': '115.29 MFLOP per ray per mapping iteration (SURVEY.md 8(d)); peak 833 TF (f16 MFMA / 3)',
-           'eager_ms_per_iter': round(el_e / 20 * 1e3, 4),
-           'roofline': kernel_roofline(kt, 'f16x3', el_e, traffic_units=True),
-           'kernel_rooflines': kernel_table(kt, 'f16x3', el_e, 20),
-           'kernel_profile': 'profiles/r04_room0_timeline.txt, profiles/r04_room0_kernel_stats.csv (rocprofv3 of '
-                             'the graph replay)'}
+             'flop_basis': '115.29 MFLOP per ray per mapping iteration (SURVEY.md 8(d)); peak 833 TF (f16 MFMA / 3)'}
         if cpu:
             cr = oracle_map_rate(bound, pose, params, n)
             e['cpu_baseline'] = {'value': round(cr, 1), 'unit': 'rays/s', 'cores': cpu_threads(), 'kind': 'port',
@@ -625,7 +620,12 @@ def room0_extra(pnr, params, bound, pose, dev, ddp, lib, steps=100, warmup=5, cp
                        'regulation (32) + L1 losses + backward + Adam in one replayed HIP graph',
            'rays_per_iter': n, 'ms_per_iter': round(el / steps * 1e3, 4), 'rays_per_s': round(rate, 1),
            'graph': graph, 'iters': steps, 'achieved_tflops': round(tf, 2), 'frac_of_split_peak': round(tf / peak, 4),
-           'flop_basis': '115.29 MFLOP per ray per mapping iteration (SURVEY.md 8(d)); peak 833 TF (f16 MFMA / 3)'}
+           'flop_basis': '115.29 MFLOP per ray per mapping iteration (SURVEY.md 8(d)); peak 833 TF (f16 MFMA / 3)',
+           'eager_ms_per_iter': round(el_e / 20 * 1e3, 4),
+           'roofline': kernel_roofline(kt, 'f16x3', el_e, traffic_units=True),
+           'kernel_rooflines': kernel_table(kt, 'f16x3', el_e, 20),
+           'kernel_profile': 'profiles/r04_room0_timeline.txt, profiles/r04_room0_kernel_stats.csv (rocprofv3 of '
+                             'the graph replay)'}
     if cpu:
         rays = sampler()[:4]
         cr = oracle_map_rate(bound, pose, params, n, rays=rays)
