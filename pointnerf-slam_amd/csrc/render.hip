@@ -935,29 +935,37 @@ __global__ __launch_bounds__(256) void k_window_sample(uint64_t seed, SampleStat
   __shared__ uint32_t last;
   const int64_t batch = stt->batch;
   const uint64_t base = mix64(seed + (uint64_t)batch * 0x9E3779B97F4A7C15ull);
+  // blocks [0, nbr) draw the rays (and their gt maxima, part[0..nbr)); the others draw the jitter,
+  // one value per thread (a thread per ray drawing its 32 values serially was the launch's latency)
+  const int nbr = (int)(n < (int64_t)kSampleParts * 256 ? (n + 255) / 256 : kSampleParts);
   float m = -INFINITY;
-  for (int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x; k < n; k += (int64_t)gridDim.x * 256) {
-    const int64_t f = k / per_frame;
-    const uint64_t r = mix64(base + (uint64_t)k * 0xD1B54A32D192ED03ull);
-    const int64_t pix = (int64_t)(((r >> 32) * (uint64_t)hw) >> 32);  // uniform in [0, hw) (hw < 2^32)
-    if (idx_out) idx_out[k] = pix;
-    make_ray((float)(pix % W), (float)(pix / W), fx, fy, cx, cy, c2w + f * 16, 4, ro + k * 3, rd + k * 3);
-    const int64_t q = f * hw + pix;
-    const float d = depth[q];
-    gd[k] = d;
-    gc[k * 3 + 0] = color[q * 3 + 0];
-    gc[k * 3 + 1] = color[q * 3 + 1];
-    gc[k * 3 + 2] = color[q * 3 + 2];
-    m = max_nanf(m, d * 1.2f);
-    for (int s = 0; s < S; ++s) {  // 24-bit uniforms in [0, 1), like torch.rand's float32
-      const uint64_t u = mix64(base + (uint64_t)(n + k * S + s) * 0xD1B54A32D192ED03ull);
-      t_rand[k * S + s] = (float)(uint32_t)(u >> 40) * 0x1p-24f;
+  if ((int)blockIdx.x < nbr) {
+    for (int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x; k < n; k += (int64_t)nbr * 256) {
+      const int64_t f = k / per_frame;
+      const uint64_t r = mix64(base + (uint64_t)k * 0xD1B54A32D192ED03ull);
+      const int64_t pix = (int64_t)(((r >> 32) * (uint64_t)hw) >> 32);  // uniform in [0, hw) (hw < 2^32)
+      if (idx_out) idx_out[k] = pix;
+      make_ray((float)(pix % W), (float)(pix / W), fx, fy, cx, cy, c2w + f * 16, 4, ro + k * 3, rd + k * 3);
+      const int64_t q = f * hw + pix;
+      const float d = depth[q];
+      gd[k] = d;
+      gc[k * 3 + 0] = color[q * 3 + 0];
+      gc[k * 3 + 1] = color[q * 3 + 1];
+      gc[k * 3 + 2] = color[q * 3 + 2];
+      m = max_nanf(m, d * 1.2f);
+    }
+  } else {
+    const int64_t ns = n * S, stride = (int64_t)(gridDim.x - nbr) * 256;
+    for (int64_t e = (int64_t)(blockIdx.x - nbr) * 256 + threadIdx.x; e < ns; e += stride) {
+      // 24-bit uniforms in [0, 1), like torch.rand's float32: value (k, s) is draw n + k S + s
+      const uint64_t u = mix64(base + (uint64_t)(n + e) * 0xD1B54A32D192ED03ull);
+      t_rand[e] = (float)(uint32_t)(u >> 40) * 0x1p-24f;
     }
   }
   m = block_max_256(m, red);
   // ticket hand-off as k_map_loss; the last block reduces the maxima and advances the batch
   if (threadIdx.x == 0) {
-    stt->part[blockIdx.x] = m;
+    if ((int)blockIdx.x < nbr) stt->part[blockIdx.x] = m;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -971,7 +979,7 @@ __global__ __launch_bounds__(256) void k_window_sample(uint64_t seed, SampleStat
   __syncthreads();
   if (!last) return;
   __shared__ float red2[4];
-  const float v = block_max_256((int)threadIdx.x < (int)gridDim.x ? stt->part[threadIdx.x] : -INFINITY, red2);
+  const float v = block_max_256((int)threadIdx.x < nbr ? stt->part[threadIdx.x] : -INFINITY, red2);
   if (threadIdx.x == 0) {
     if (far_out) far_out[0] = v;
     stt->batch = batch + 1;
@@ -1249,7 +1257,9 @@ int launch_window_sample(uint64_t seed, void* state, int64_t n, int64_t per_fram
                          float* ro, float* rd, float* gd, float* gc, float* t_rand, int64_t* idx, float* far_out,
                          hipStream_t st) {
   if (n <= 0) return 0;
-  const int64_t nb = std::min<int64_t>(kSampleParts, nblk(n, 256));
+  const int64_t nbr = std::min<int64_t>(kSampleParts, nblk(n, 256));                  // ray blocks
+  const int64_t nbj = std::min<int64_t>(192, nblk(n * (S > 0 ? S : 0), 1024));      // jitter blocks (4 per thread)
+  const int64_t nb = nbr + nbj;
   hipLaunchKernelGGL(k_window_sample, dim3((unsigned)nb), dim3(256), 0, st, seed, (SampleState*)state, n, per_frame,
                      (int64_t)H * W, W, fx, fy, cx, cy, c2w, depth, color, S, ro, rd, gd, gc, t_rand, idx, far_out);
   return hip_status(hipGetLastError());
