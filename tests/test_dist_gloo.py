@@ -54,6 +54,11 @@ def _worker(rank, world, port, q):
     tr = torch.from_numpy(G['map_t_rand'][:n][a:b].copy())
     ddp = pdist.DataParallel()
     fc = float(ddp.global_far_clamp(gt))  # a device tensor (far_mode 2); the oracle takes a float
+    # the device window sampler hands its batch's clamp over instead (pnr_window_sample): the same
+    # all-reduced value, and the rank's own tensor is left untouched
+    local = (gt * 1.2).max().reshape(1)
+    fc_l = ddp.global_far_clamp(gt, local)
+    assert float(fc_l) == fc and float(local) == float((gt * 1.2).max())
     params = {k: v.clone().requires_grad_(True) for k, v in golden_params('trained').items()}
     d, v, c = ref.render_batch_ray(params, rd, ro, bound, gt_depth=gt, far_clamp=fc)
     sig = ref.regulation(params, rd, ro, gt, bound, t_rand=tr)
