@@ -41,6 +41,7 @@ def main():
     ap.add_argument('--reps', type=int, default=5)
     ap.add_argument('--lib', default=None, help='load this libpnr.so build instead (experiments)')
     ap.add_argument('--feat-dtype', default='float32', choices=['float32', 'float16'])
+    ap.add_argument('--dump', default=None, help='save the first launch\'s c / idx / w here (A/B bitwise checks)')
     args = ap.parse_args()
     import pnr
     if args.lib:
@@ -66,8 +67,13 @@ def main():
         pnr._lib.check(lib.pnr_point_gather(ctypes.byref(s), p.data_ptr(), P, c.data_ptr(), idx.data_ptr(),
                                             w.data_ptr(), ws.data_ptr(), ws.numel(), st), 'gather')
 
+    c.fill_(float('nan'))  # every row must be written (zero-filled or gathered)
+    idx.fill_(-7)
+    w.fill_(float('nan'))
     run()
     torch.cuda.synchronize()
+    if args.dump:
+        torch.save({'c': c.cpu(), 'idx': idx.cpu(), 'w': w.cpu()}, args.dump)
     nb = int((idx >= 0).sum().item())
     n_work = int(ws[:64 * 32 * 4].view(torch.int32)[::32].sum().item())
     hist = torch.bincount((idx >= 0).sum(1), minlength=args.k + 1).tolist()
