@@ -10,6 +10,8 @@ units of that launch (tools/traffic.py documents the counter units and the gfx95
   k_mlp_bwd16        split-precision delta chain, per point (128 points / block)
   k_mlp_fwd_train    fp32 forward with saves, per point (grid = points)
   k_gather           probe + search of one gather, per sample (probe grid = sample rows)
+  k_wgrad16_group    the grouped split weight-gradient GEMMs, per point (--mlp-points)
+  k_wgrad_skinny     dWo + dB (fp32 FMA skinny GEMMs), per point (--mlp-points)
 """
 import collections
 import csv
@@ -41,6 +43,10 @@ def family(name):
         return 'k_mlp_fwd_train'
     if 'k_gather_probe' in name:
         return 'k_gather_probe'
+    if 'k_wgrad16_group' in name:
+        return 'k_wgrad16_group'
+    if 'k_wgrad_skinny' in name:
+        return 'k_wgrad_skinny'
     if 'k_gather_search' in name or 'k_group_scatter' in name:
         return 'k_gather_search'  # (round 3: the grouped list's scatter belongs to the gather too)
     return None
@@ -72,7 +78,7 @@ def main():
     # --mlp-points=N (the run's training points, the same for the forward and the delta chain)
     # replaces the grid-derived unit count of both families
     if mlp_pts:
-        for fam in ('k_mlp_fwd16_train', 'k_mlp_bwd16'):
+        for fam in ('k_mlp_fwd16_train', 'k_mlp_bwd16', 'k_wgrad16_group', 'k_wgrad_skinny'):
             if fam in acc:
                 acc[fam][2] = mlp_pts[0]
     res = {'source': note}
