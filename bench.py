@@ -1,43 +1,45 @@
 #!/usr/bin/env python3
 """Benchmark: rendered rays/s per mapping iteration (BASELINE.json metric) on MI355X.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload map|fwd|map-points|room0] [--rays R]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload room0|map|fwd|map-points] [--rays R]
                   [--global-batch B] [--precision P] [--graph] [--no-extras] [--no-cpu-baseline]
 
-Workload `map` (default; SURVEY.md 8(d) "S-map"): one full Mapper iteration of
-src/Mapper.py:507-662 for the effective room0 config (configs/pointNeRF_slam.yaml +
-configs/Replica/room0_point.yaml: 32 stratified + 12 importance samples, gt-depth near/far,
-regulation with 32 jittered samples, L1 depth + 0.05 L1 colour + 0.0005 |sigma|, backward,
-Adam lr 2e-4) over R rays per GPU (default 307,200 = one 640x480 pixel batch).  Decoder
-arithmetic: f16x3 by default -- fp32-class end to end (every forward and backward GEMM on 22-bit
-split operands with fp32 accumulation, include/pnr.h); `--precision fp32` runs fp32 MFMA.
-Workload `fwd` ("S-fwd"): render_batch_ray forward, 640x480 rays x 64 stratified samples.
-Workload `room0`: the room0 Mapper iteration as the reference runs it (1,000 rays over the 5-frame
-keyframe window, window sampling on the device included), replayed from one captured HIP graph;
-`value` = rays/s, plus ms per iteration.
+Workload `room0` (default; the metric's own iteration, configs/Replica/replica.yaml:21-22 +
+configs/pointNeRF_slam.yaml): ONE room0 Mapper iteration of src/Mapper.py:507-662 at its real size --
+1,000 rays over the 5-frame keyframe window of the 680x1200 room0 camera, window sampling on the
+device, render (32 stratified + 12 importance samples, gt-depth near/far) + regulation (32 jittered
+samples) + L1 depth + 0.05 L1 colour + 0.0005 |sigma| + backward + Adam lr 2e-4 -- replayed from one
+captured HIP graph; `value` = rays/s over all ranks, `ms_per_step` = ms per iteration.
+Workload `map` ("S-map"): the same iteration over R rays per GPU (default 307,200 = one
+640x480 pixel batch).  Workload `fwd` ("S-fwd"): render_batch_ray forward, 640x480 rays x 64 stratified
+samples.  Decoder arithmetic: f16x3 by default -- fp32-class end to end (every forward and backward GEMM
+on 22-bit split operands with fp32 accumulation, include/pnr.h); `--precision fp32` runs fp32 MFMA.
 
-Extra keys of the N=1 line (measured after the timed region, never part of `value`):
+Extra keys of the default line (measured after the timed region, never part of `value`):
+  smap            S-map at 307,200 rays per GPU with its MLP rooflines and the oracle's CPU rate
+                  (`smap_value` repeats its rays/s at the top level)
   sfwd            the north-star S-fwd batch (640x480 x 64 samples, forward) with its own roofline
                   and the oracle's CPU rate at 64 samples
-  faithful_n1000  the room0 Mapper iteration at its real size (N = 1,000 rays), replayed from a
-                  captured HIP graph (pnr.mapping.MapGraph), and N = 5,000 (C4/C5), each with its
-                  fraction of the split peak and the oracle's CPU rate on the same rays
+  faithful_n1000  the Mapper iteration on synthetic rays at N = 1,000 and 5,000 (C4/C5), graph replay
   map_points      the neural-point Mapper iteration (A15) at 307,200 rays with its MLP roofline and
                   the oracle's CPU rate
-  fp32            the same S-map step with fp32-MFMA decoder arithmetic
+  fp32            the S-map step with fp32-MFMA decoder arithmetic
   gather_roofline the neural-point gather (A15) on its HBM roofline
-  room0_iter      the `room0` workload above (ms per Mapper iteration)
-N>1 lines add `fixed_global_batch`: the 307,200-ray batch split over the N ranks.
+N>1 lines (one rank per GPU, RCCL) carry `smap` (weak: 307,200 rays per GPU) and `fixed_global_batch`
+(ONE 307,200-ray batch split over the ranks: strong scaling) and `distributed` (the
+backend and world size the ranks saw).
 
 Data: synthetic.  Decoder = the trained room0 weights committed as a golden fixture
-(tests/golden/weights.npz, from the reference's own checkpoint) -- random init if absent; rays
-from room0 pose gt_c2w_list[1000] through ScanNet-style 640x480 intrinsics; gt depth U[0.05,0.6]
-with 10% zeros; gt colour U[0,1]; seed 0 + rank.
+(tests/golden/weights.npz, from the reference's own checkpoint) -- random init if absent.  room0: renders
+of that decoder at four room0 poses + a moved current pose as the window frames (gt = rendered depth /
+colour).  S-map: rays from room0 pose gt_c2w_list[1000] through ScanNet-style 640x480 intrinsics; gt
+depth U[0.05,0.6] with 10% zeros; gt colour U[0,1]; seed 0 + rank.
 
-Multi-GPU (torchrun, one process per GPU, RCCL): every rank maps its own R rays (weak scaling;
-`--global-batch B` splits B rays over the ranks instead: strong scaling); per step one scalar
-all_reduce(MAX) (global far clamp, read on the device) and one 891 KB gradient all_reduce(SUM).
-Rank 0 prints ONE JSON line.
+Multi-GPU: `python bench.py --gpus N` starts N ranks itself (torch.distributed.run as a child
+process, before any GPU call) unless it already runs under a launcher (WORLD_SIZE set, which must equal
+N); fewer than N GPUs is an error.  Every rank maps its own batch (weak scaling); per iteration one scalar
+all_reduce(MAX) (global far clamp, read on the device) and one 891 KB gradient all_reduce(SUM), captured
+in the graph.  Rank 0 prints ONE JSON line.
 """
 import argparse
 import json
@@ -586,7 +588,7 @@ def room0_window(pnr, params, bound, dev):
     return slam, frames
 
 
-def room0_extra(pnr, params, bound, pose, dev, ddp, lib, steps=100, warmup=5, cpu=True, graph=True):
+def room0_extra(pnr, params, bound, pose, dev, ddp, lib, steps=100, warmup=5, cpu=True, graph=True, rank=0):
     """The metric's own workload: ONE room0 Mapper iteration (src/Mapper.py:507-662) at its real size,
     1,000 rays over the 5-frame window (200 per frame) of the room0 camera, gt = the decoder's own
     rendered depth / colour.  Timed per iteration: the window batch (pnr_window_sample: pixels, jitter
@@ -598,9 +600,13 @@ def room0_extra(pnr, params, bound, pose, dev, ddp, lib, steps=100, warmup=5, cp
     r = pnr.Renderer(cfg, None, slam)
     dec = make_decoder(pnr, cfg, params, dev)
     per = ROOM0_PIXELS // ROOM0_WINDOW
+    # data parallel: every rank draws its own 1,000-ray window batch (seed = rank), the
+    # batch far clamp is all-reduced (MAX) on the device and the 891 KB gradient all-reduced (SUM) once
+    # per iteration, both captured in the graph with the step (RCCL)
     sampler = WindowSampler(frames, per, ROOM0_CAM['fx'], ROOM0_CAM['fy'], ROOM0_CAM['cx'], ROOM0_CAM['cy'],
-                            n_samples=cfg['rendering']['N_samples'])
-    mstep = MapStep(r, dec, lr=cfg['mapping']['imap_decoders_lr'], w_color_loss=cfg['mapping']['w_color_loss'])
+                            n_samples=cfg['rendering']['N_samples'], seed=rank)
+    mstep = MapStep(r, dec, lr=cfg['mapping']['imap_decoders_lr'], w_color_loss=cfg['mapping']['w_color_loss'],
+                    ddp=ddp if ddp.world > 1 else None)
     if graph:
         mg = MapGraph(mstep, batch_fn=sampler)
         step = mg
@@ -624,7 +630,7 @@ def room0_extra(pnr, params, bound, pose, dev, ddp, lib, steps=100, warmup=5, cp
            'eager_ms_per_iter': round(el_e / 20 * 1e3, 4),
            'roofline': kernel_roofline(kt, 'f16x3', el_e, traffic_units=True),
            'kernel_rooflines': kernel_table(kt, 'f16x3', el_e, 20),
-           'kernel_profile': 'profiles/r04_room0_timeline.txt, profiles/r04_room0_kernel_stats.csv (rocprofv3 of '
+           'kernel_profile': 'profiles/r05_room0_timeline.txt, profiles/r05_room0_kernel_stats.csv (rocprofv3 of '
                              'the graph replay)'}
     if cpu:
         rays = sampler()[:4]
@@ -699,24 +705,56 @@ def map_points_extra(pnr, plib, slam, params, bound, pose, dev, ddp, lib, n=W * 
     return out
 
 
+def launch_ranks(args):
+    """`--gpus N` (N > 1) outside torchrun: start N ranks, one per GPU, as ONE child process
+    (python -m torch.distributed.run --nproc-per-node N, rendezvous on 127.0.0.1) and return its exit
+    code.  Nothing here touches the GPU (torch.cuda.device_count does not initialise it on this image),
+    so the launcher never replaces a process that holds a GPU context."""
+    import socket
+    import subprocess
+    n_dev = torch.cuda.device_count()
+    if n_dev < args.gpus:
+        print(f'bench.py: --gpus {args.gpus} needs {args.gpus} GPUs, this node has {n_dev}', file=sys.stderr,
+              flush=True)
+        return 2
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(('127.0.0.1', 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', f'--nproc-per-node={args.gpus}',
+           '--master-addr', '127.0.0.1', '--master-port', str(port), os.path.abspath(__file__), *sys.argv[1:]]
+    env = dict(os.environ)
+    env.setdefault('PNR_DIST_BACKEND', 'nccl')   # RCCL over xGMI
+    return subprocess.run(cmd, env=env).returncode
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
-    ap.add_argument('--steps', type=int, default=5)
-    ap.add_argument('--warmup', type=int, default=2)
-    ap.add_argument('--workload', choices=['map', 'fwd', 'map-points', 'room0'], default='map')
-    ap.add_argument('--rays', type=int, default=W * H, help='rays per GPU per step (weak scaling)')
+    ap.add_argument('--steps', type=int, default=None, help='timed steps (default: 100 room0 / 5 other workloads)')
+    ap.add_argument('--warmup', type=int, default=None, help='untimed steps (default: 5 room0 / 2 others)')
+    ap.add_argument('--workload', choices=['room0', 'map', 'fwd', 'map-points'], default='room0',
+                    help='room0 (default, the metric\'s own iteration) | map (S-map, 307,200 rays) | fwd (S-fwd) | '
+                         'map-points (neural-point S-map)')
+    ap.add_argument('--rays', type=int, default=W * H, help='rays per GPU per step of the S-map workloads (weak scaling)')
     ap.add_argument('--global-batch', type=int, default=None,
                     help='fixed global batch split over the ranks (strong scaling; SURVEY.md 8(e))')
     ap.add_argument('--graph', action='store_true',
-                    help='replay the mapping iteration from a captured HIP graph (pnr.mapping.MapGraph)')
+                    help='replay the S-map iteration from a captured HIP graph (pnr.mapping.MapGraph)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-gather', action='store_true', help='skip the point-gather roofline line')
-    ap.add_argument('--no-extras', action='store_true', help='skip sfwd / faithful_n1000 / fp32 extras')
+    ap.add_argument('--no-extras', action='store_true', help='skip the extra workloads (smap, sfwd, faithful, ...)')
     ap.add_argument('--precision', default=None, help="decoder matmuls: f16x3 (default) | fp32 | bf16x3 | bf16")
     ap.add_argument('--feat-dtype', default='float32', choices=['float32', 'float16'],
                     help='neural-point feature storage (map-points workload and the gather line; C5: float16)')
     args = ap.parse_args()
+    if args.steps is None:
+        args.steps = 100 if args.workload == 'room0' else 5
+    if args.warmup is None:
+        args.warmup = 5 if args.workload == 'room0' else 2
+    if args.gpus < 1:
+        ap.error('--gpus must be >= 1')
+    if args.gpus > 1 and 'WORLD_SIZE' not in os.environ:
+        sys.exit(launch_ranks(args))
 
     import pnr
     from pnr import _lib as plib
@@ -726,38 +764,73 @@ def main():
         plib.DEFAULT_PRECISION = args.precision
     prec = plib.DEFAULT_PRECISION
 
+    env_world = pdist.env_rank_world()[1]
+    if env_world != args.gpus:
+        print(f'bench.py: --gpus {args.gpus} but the launcher started {env_world} rank(s)', file=sys.stderr, flush=True)
+        sys.exit(2)
+    if torch.cuda.device_count() < env_world:
+        print(f'bench.py: {env_world} ranks need {env_world} GPUs, this node has {torch.cuda.device_count()}',
+              file=sys.stderr, flush=True)
+        sys.exit(2)
     rank, world, local = pdist.init()
     dev = torch.device('cuda', local % torch.cuda.device_count())
     torch.cuda.set_device(dev)
+    dist_info = None
+    if world > 1:
+        import torch.distributed as tdist
+        dist_info = {'backend': tdist.get_backend(), 'world_size': tdist.get_world_size(),
+                     'collective': 'RCCL over xGMI' if tdist.get_backend() == 'nccl' else tdist.get_backend()}
+        if rank == 0:
+            print(f'bench.py: {dist_info["backend"]} process group, world size {dist_info["world_size"]}',
+                  file=sys.stderr, flush=True)
     lib = pnr.library()
     bound, pose, params = load_scene()
-    if args.workload == 'room0':  # the metric's own iteration alone (1,000 rays per GPU and iteration)
-        ddp = pdist.DataParallel()
-        e = room0_extra(pnr, params, bound, pose, dev, ddp, lib, steps=args.steps, warmup=args.warmup,
-                        cpu=not args.no_cpu_baseline and world == 1)
+    import types
+    slam = types.SimpleNamespace(bound=bound, H=H, W=W, fx=FX, fy=FY, cx=CX, cy=CY)
+    ddp = pdist.DataParallel()
+    cpu_ok = not args.no_cpu_baseline and world == 1 and params is not None
+
+    if args.workload == 'room0':  # the metric's own iteration (1,000 rays per GPU and iteration)
+        e = room0_extra(pnr, params, bound, pose, dev, ddp, lib, steps=args.steps, warmup=args.warmup, cpu=cpu_ok,
+                        rank=rank)
+        extras = {}
+        if not args.no_extras:
+            extras['smap'] = smap_run(pnr, plib, slam, params, bound, pose, dev, ddp, lib, rank, world, prec,
+                                      steps=5, warmup=2, cpu=cpu_ok)
+            if world > 1:
+                extras['fixed_global_batch'] = fixed_global_run(pnr, slam, params, pose, dev, ddp, lib, rank, world,
+                                                                steps=5, warmup=2)
+            elif params is not None:
+                extras.update(n1_extras(pnr, plib, slam, params, bound, pose, dev, ddp, lib, prec, args, cpu_ok))
         if rank == 0:
             out = {'metric': METRIC, 'value': round(e['rays_per_s'] * world, 1), 'unit': 'rays/s', 'n_gpus': world,
                    'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': e['ms_per_iter'],
                    'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': DTYPE[prec],
                    'data': 'synthetic (renders of the trained room0 decoder fixture on the room0 camera)',
                    'config': {'workload': e['workload'], 'rays_per_gpu': e['rays_per_iter'],
-                              'global_batch': e['rays_per_iter'] * world, 'parallelism': f'replicas{world}',
+                              'global_batch': e['rays_per_iter'] * world,
+                              'parallelism': f'dp{world}' if world > 1 else 'dp1',
                               'decoder_precision': prec, 'graph': True},
                    'roofline': e.get('roofline'), 'cpu_baseline': e.get('cpu_baseline'),
                    'room0_iter': e}
+            if dist_info:
+                out['distributed'] = dist_info
+            if 'smap' in extras:  # the S-map rays/s next to the headline (SURVEY.md 8(d) throughput batch)
+                out['smap_value'] = extras['smap']['value']
+            out.update(extras)
+            if world == 1 and not args.no_gather and not args.no_extras and params is not None:
+                out['gather_roofline'] = gather_roofline(dev, feat_dtype=args.feat_dtype)
             print(json.dumps(out), flush=True)
         if world > 1:
             torch.distributed.destroy_process_group()
         return
-    import types
-    slam = types.SimpleNamespace(bound=bound, H=H, W=W, fx=FX, fy=FY, cx=CX, cy=CY)
+
     cfg = pnr.ROOM0_CFG
     if args.workload == 'fwd':
         import copy
         cfg = copy.deepcopy(cfg)
         cfg['rendering']['N_samples'], cfg['rendering']['N_importance'] = 64, 0
     renderer = pnr.Renderer(cfg, None, slam)
-    ddp = pdist.DataParallel()
     strong = args.global_batch is not None
     if strong:  # this rank's contiguous share of one global batch
         a, b = pdist.shard_bounds(args.global_batch, rank, world)
@@ -800,51 +873,16 @@ def main():
         raise FloatingPointError('bench: the f16x3 forward met a value outside the f16 range (PNR_STATUS_F16_RANGE)')
 
     extras = {}
-    if not args.no_extras and args.workload == 'map' and not strong:
-        if world > 1:
-            # the fixed-global-batch (strong-scaling) form of the same step: 307,200 rays over the ranks
-            ga, gb = pdist.shard_bounds(W * H, rank, world)
-            sro, srd, sgt, scol = [t[ga:gb].contiguous() for t in synth_batch(W * H, 0, pose, dev)]
-            sdec = make_decoder(pnr, cfg, params, dev)
-            sstep = map_step_fn(pnr, pnr.Renderer(cfg, None, slam), sdec, cfg, sro, srd, sgt, scol, dev, ddp=ddp)
-            sel, _ = timed(sstep, args.steps, args.warmup, ddp, lib)
-            extras['fixed_global_batch'] = {'global_batch': W * H, 'rays_per_gpu': gb - ga, 'scaling': 'strong',
-                                            'ms_per_step': round(sel / args.steps * 1e3, 3),
-                                            'value': round(W * H * args.steps / sel, 1), 'unit': 'rays/s'}
-        elif params is not None:
-            extras['sfwd'] = sfwd_extra(pnr, plib, slam, params, bound, pose, dev, ddp, lib,
-                                        cpu=not args.no_cpu_baseline)
-            extras['room0_iter'] = room0_extra(pnr, params, bound, pose, dev, ddp, lib, cpu=not args.no_cpu_baseline)
-            extras['faithful_n1000'] = faithful_extra(pnr, slam, params, bound, pose, dev, ddp, lib,
-                                                      cpu=not args.no_cpu_baseline)
-            extras['map_points'] = map_points_extra(pnr, plib, slam, params, bound, pose, dev, ddp, lib,
-                                                    cpu=not args.no_cpu_baseline)
-            if prec != 'fp32':
-                saved = plib.DEFAULT_PRECISION
-                plib.DEFAULT_PRECISION = 'fp32'
-                fdec = make_decoder(pnr, cfg, params, dev)
-                fstep = map_step_fn(pnr, pnr.Renderer(cfg, None, slam), fdec, cfg, ro, rd, gt, col, dev)
-                fel, fkt = timed(fstep, 3, 1, ddp, lib)
-                plib.DEFAULT_PRECISION = saved
-                extras['fp32'] = {'value': round(n * 3 / fel, 1), 'unit': 'rays/s',
-                                  'ms_per_step': round(fel / 3 * 1e3, 3), 'steps': 3, 'dtype': DTYPE['fp32'],
-                                  'roofline': kernel_roofline(fkt, 'fp32', fel, traffic_units=False)}
+    if not args.no_extras and args.workload == 'map' and not strong and world > 1:
+        extras['fixed_global_batch'] = fixed_global_run(pnr, slam, params, pose, dev, ddp, lib, rank, world,
+                                                        steps=args.steps, warmup=args.warmup)
 
     if rank == 0:
         cpu = None
-        if world == 1 and not args.no_cpu_baseline and params is not None and args.workload != 'map-points':
-            def gpu_render(ro_c, rd_c, gt_c):
-                d0 = make_decoder(pnr, cfg, params, dev)
-                with torch.no_grad():
-                    d, _, c = renderer.render_batch_ray({}, d0, rd_c.to(dev), ro_c.to(dev), dev, 'color',
-                                                        gt_depth=None if gt_c is None else gt_c.to(dev))
-                return d.cpu(), c.cpu()
-            cpu = cpu_baseline(bound, pose, params, args.workload, gpu_render=gpu_render)
+        if cpu_ok and args.workload != 'map-points':
+            cpu = cpu_baseline(bound, pose, params, args.workload, gpu_render=gpu_render_fn(pnr, renderer, cfg, params,
+                                                                                            dev))
         samples = '64' if args.workload == 'fwd' else '32+12 (+32 regulation)'
-        wl_name = {'map': 'S-map: full mapping iteration (render+regulation+L1 losses+backward+Adam)',
-                   'fwd': 'S-fwd: render_batch_ray forward',
-                   'map-points': 'S-map with neural points (A15): c_dim=32 decoder, IDW k=8 r=2 mm gather, '
-                                 'fc_c injection, feature + decoder Adam'}[args.workload]
         out = {
             'metric': METRIC, 'value': round(value, 1), 'unit': 'rays/s', 'n_gpus': world, 'steps': args.steps,
             'warmup': args.warmup, 'ms_per_step': round(ms_per_step, 3), 'higher_is_better': True,
@@ -852,7 +890,7 @@ def main():
             'dtype': DTYPE[prec],
             'data': 'synthetic (640x480 ScanNet-intrinsics rays at room0 pose 1000, U[0.05,0.6] gt depth, trained '
                     'room0 decoder fixture)',
-            'config': {'workload': wl_name,
+            'config': {'workload': WL_NAME[args.workload],
                        'rays_per_gpu': n, 'global_batch': total, 'samples_per_ray': samples,
                        'parallelism': f'dp{world}', 'decoder_precision': prec,
                        'graph': bool(args.graph and args.workload == 'map'),
@@ -861,6 +899,8 @@ def main():
             'kernel_rooflines': kernel_table(kt, prec, el, args.steps) if args.workload != 'fwd' else None,
             'kernels': {k: {'launches': v[0], 'ms': round(v[1], 3), 'units': v[2]} for k, v in kt.items()},
         }
+        if dist_info:
+            out['distributed'] = dist_info
         if cpu is not None:
             out['speedup_vs_cpu'] = round(value / cpu['value'], 1)
         out.update(extras)
@@ -870,6 +910,86 @@ def main():
         print(json.dumps(out), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()
+
+
+WL_NAME = {'map': 'S-map: full mapping iteration (render+regulation+L1 losses+backward+Adam)',
+           'fwd': 'S-fwd: render_batch_ray forward',
+           'map-points': 'S-map with neural points (A15): c_dim=32 decoder, IDW k=8 r=2 mm gather, fc_c injection, '
+                         'feature + decoder Adam'}
+
+
+def gpu_render_fn(pnr, renderer, cfg, params, dev):
+    """The HIP render of the CPU baseline's rays with the initial weights (the parity line)."""
+    def gpu_render(ro_c, rd_c, gt_c):
+        d0 = make_decoder(pnr, cfg, params, dev)
+        with torch.no_grad():
+            d, _, c = renderer.render_batch_ray({}, d0, rd_c.to(dev), ro_c.to(dev), dev, 'color',
+                                                gt_depth=None if gt_c is None else gt_c.to(dev))
+        return d.cpu(), c.cpu()
+    return gpu_render
+
+
+def smap_run(pnr, plib, slam, params, bound, pose, dev, ddp, lib, rank, world, prec, steps=5, warmup=2, cpu=True):
+    """S-map: one full Mapper iteration over 307,200 rays per GPU (weak scaling), with
+    the roofline of its dominant MLP kernel, every MLP kernel family's roofline and the oracle's CPU rate."""
+    cfg = pnr.ROOM0_CFG
+    renderer = pnr.Renderer(cfg, None, slam)
+    dec = make_decoder(pnr, cfg, params, dev)
+    n = W * H
+    ro, rd, gt, col = synth_batch(n, rank, pose, dev)
+    step = map_step_fn(pnr, renderer, dec, cfg, ro, rd, gt, col, dev, ddp=ddp if world > 1 else None)
+    el, kt = timed(step, steps, warmup, ddp, lib)
+    if renderer.status(dev):
+        raise FloatingPointError('bench: the f16x3 forward met a value outside the f16 range (PNR_STATUS_F16_RANGE)')
+    value = n * world * steps / el
+    out = {'workload': WL_NAME['map'] + ', 307,200 rays per GPU (640x480 ScanNet-intrinsics rays at room0 pose '
+                                        '1000, U[0.05,0.6] gt depth)',
+           'value': round(value, 1), 'unit': 'rays/s', 'n_gpus': world, 'scaling': 'weak', 'steps': steps,
+           'ms_per_step': round(el / steps * 1e3, 3),
+           'roofline': kernel_roofline(kt, prec, el, traffic_units=True),
+           'kernel_rooflines': kernel_table(kt, prec, el, steps),
+           'kernels': {k: {'launches': v[0], 'ms': round(v[1], 3), 'units': v[2]} for k, v in kt.items()}}
+    if cpu and rank == 0:
+        out['cpu_baseline'] = cpu_baseline(bound, pose, params, 'map',
+                                           gpu_render=gpu_render_fn(pnr, renderer, cfg, params, dev))
+        out['speedup_vs_cpu'] = round(value / out['cpu_baseline']['value'], 1)
+    return out
+
+
+def fixed_global_run(pnr, slam, params, pose, dev, ddp, lib, rank, world, steps=5, warmup=2):
+    """The fixed-global-batch (strong-scaling) form of S-map: ONE 307,200-ray batch split over the
+    ranks, the global far clamp all-reduced, one gradient all-reduce per step."""
+    cfg = pnr.ROOM0_CFG
+    from pnr import dist as pdist
+    ga, gb = pdist.shard_bounds(W * H, rank, world)
+    sro, srd, sgt, scol = [t[ga:gb].contiguous() for t in synth_batch(W * H, 0, pose, dev)]
+    sdec = make_decoder(pnr, cfg, params, dev)
+    sstep = map_step_fn(pnr, pnr.Renderer(cfg, None, slam), sdec, cfg, sro, srd, sgt, scol, dev,
+                        ddp=ddp if world > 1 else None)
+    sel, _ = timed(sstep, steps, warmup, ddp, lib)
+    return {'global_batch': W * H, 'rays_per_gpu': gb - ga, 'scaling': 'strong', 'n_gpus': world,
+            'ms_per_step': round(sel / steps * 1e3, 3), 'value': round(W * H * steps / sel, 1), 'unit': 'rays/s'}
+
+
+def n1_extras(pnr, plib, slam, params, bound, pose, dev, ddp, lib, prec, args, cpu_ok):
+    """The 1-GPU extras of the default line, measured after the headline's timed region."""
+    extras = {'sfwd': sfwd_extra(pnr, plib, slam, params, bound, pose, dev, ddp, lib, cpu=cpu_ok),
+              'faithful_n1000': faithful_extra(pnr, slam, params, bound, pose, dev, ddp, lib, cpu=cpu_ok),
+              'map_points': map_points_extra(pnr, plib, slam, params, bound, pose, dev, ddp, lib, cpu=cpu_ok)}
+    if prec != 'fp32':
+        cfg = pnr.ROOM0_CFG
+        n = W * H
+        ro, rd, gt, col = synth_batch(n, 0, pose, dev)
+        saved = plib.DEFAULT_PRECISION
+        plib.DEFAULT_PRECISION = 'fp32'
+        fdec = make_decoder(pnr, cfg, params, dev)
+        fstep = map_step_fn(pnr, pnr.Renderer(cfg, None, slam), fdec, cfg, ro, rd, gt, col, dev)
+        fel, fkt = timed(fstep, 3, 1, ddp, lib)
+        plib.DEFAULT_PRECISION = saved
+        extras['fp32'] = {'value': round(n * 3 / fel, 1), 'unit': 'rays/s',
+                          'ms_per_step': round(fel / 3 * 1e3, 3), 'steps': 3, 'dtype': DTYPE['fp32'],
+                          'roofline': kernel_roofline(fkt, 'fp32', fel, traffic_units=False)}
+    return extras
 
 
 if __name__ == '__main__':

@@ -247,7 +247,11 @@ BwdWS carve_bwd(int64_t P, int64_t n, void* ws, size_t* bytes, bool feat, bool w
   if (bytes) *bytes = c.off;
   return b;
 }
-int64_t n_pts(const pnr_render_params* prm) { return prm->points ? prm->points->n_points : 0; }
+// neural points whose feature gradients the backward accumulates (the gather backward's int64
+// accumulators are sized from it): none when no g_feats is asked for (e.g. a camera-only backward)
+int64_t n_pts(const pnr_render_params* prm) {
+  return prm->points && prm->points->g_feats ? prm->points->n_points : 0;
+}
 
 // fc_c side of the backward: image, per-row features and the 8 accumulated fc_c grads
 struct FeatBwd {
@@ -261,18 +265,25 @@ __global__ void k_fill(float* p, int64_t n, float v) {
   if (i < n) p[i] = v;
 }
 
+// Store semantics (grads_overwrite) with nothing to store: the weight gradients of an empty batch
+// are zero, exactly as autograd's would be (an early return would leave the previous step's values).
+int zero_weight_grads(float* const* grads, float* const* g_fc, hipStream_t st) {
+  static const int64_t dec_n[PNR_N_PARAMS] = {3 * kFourier, kHidden * kFourier, kHidden, kHidden * kHidden, kHidden,
+                                              kHidden * kHidden, kHidden, kHidden * kHidden, kHidden, 4 * kHidden, 4};
+  for (int i = 0; grads && i < PNR_N_PARAMS; ++i)
+    if (int rc = hip_status(hipMemsetAsync(grads[i], 0, dec_n[i] * sizeof(float), st))) return rc;
+  for (int i = 0; g_fc && i < PNR_N_FC_PARAMS; ++i)
+    if (int rc = hip_status(hipMemsetAsync(g_fc[i], 0, (i % 2 ? kHidden : kHidden * kCDim) * sizeof(float), st)))
+      return rc;
+  return PNR_OK;
+}
+
 // Shared backward core over P points with saved activations `sv` and dL/draw in b.g_out.
 int mlp_backward_core(int prec, const float* packed, const SaveArgs& sv, int64_t P, BwdWS& b, float* const* grads,
                       bool want_gx, hipStream_t st, const FeatBwd* fb = nullptr, bool overwrite = false) {
   const bool split = prec != PNR_PREC_FP32;  // f16x3 delta chain + f16x3 weight-gradient GEMMs
-  if (overwrite && !split) {  // the fp32 GEMMs add into C: store = add into zeroed gradients
-    static const int64_t dec_n[PNR_N_PARAMS] = {3 * kFourier, kHidden * kFourier, kHidden, kHidden * kHidden, kHidden,
-                                                kHidden * kHidden, kHidden, kHidden * kHidden, kHidden, 4 * kHidden, 4};
-    for (int i = 0; grads && i < PNR_N_PARAMS; ++i)
-      if (int rc = hip_status(hipMemsetAsync(grads[i], 0, dec_n[i] * sizeof(float), st))) return rc;
-    for (int i = 0; fb && fb->g_fc && i < PNR_N_FC_PARAMS; ++i)
-      if (int rc = hip_status(hipMemsetAsync(fb->g_fc[i], 0, (i % 2 ? kHidden : kHidden * kCDim) * sizeof(float), st)))
-        return rc;
+  if (overwrite && (!split || P == 0)) {  // the fp32 GEMMs add into C: store = add into zeroed gradients
+    if (int rc = zero_weight_grads(grads, fb ? fb->g_fc : nullptr, st)) return rc;
     overwrite = false;
   }
   for (int64_t p0 = 0; p0 < P; p0 += b.C) {
@@ -614,7 +625,13 @@ int pnr_render_bwd(const pnr_render_params* prm, const float* packed, const floa
   (void)params;
   (void)rays_o;
   if (!valid_prm(prm) || !packed || n < 0 || !prm->save_for_backward) return PNR_E_ARG;
-  if (n == 0) return PNR_OK;
+  if (n == 0) {  // store semantics: an empty batch's weight gradients are zero
+    if (!prm->grads_overwrite) return PNR_OK;
+    if (grads)
+      for (int i = 0; i < PNR_N_PARAMS; ++i)
+        if (!grads[i]) return PNR_E_ARG;
+    return zero_weight_grads(grads, prm->points ? prm->points->g_fc : nullptr, (hipStream_t)stream);
+  }
   if (!workspace || !bwd_ws || !rays_d) return PNR_E_ARG;
   if (grads)  // NULL: no decoder weight gradients
     for (int i = 0; i < PNR_N_PARAMS; ++i)
@@ -740,7 +757,13 @@ int pnr_regulation_bwd(const pnr_render_params* prm, const float* packed, const 
   (void)params;
   (void)rays_o;
   if (!valid_prm(prm) || !packed || n < 0 || !prm->save_for_backward) return PNR_E_ARG;
-  if (n == 0) return PNR_OK;
+  if (n == 0) {  // store semantics: an empty batch's weight gradients are zero
+    if (!prm->grads_overwrite) return PNR_OK;
+    if (grads)
+      for (int i = 0; i < PNR_N_PARAMS; ++i)
+        if (!grads[i]) return PNR_E_ARG;
+    return zero_weight_grads(grads, prm->points ? prm->points->g_fc : nullptr, (hipStream_t)stream);
+  }
   if (!workspace || !bwd_ws || !g_sigma) return PNR_E_ARG;
   if (grads)  // NULL: no decoder weight gradients
     for (int i = 0; i < PNR_N_PARAMS; ++i)
@@ -806,7 +829,9 @@ MapWS carve_map(const pnr_render_params* prm, int64_t n, void* ws, size_t* bytes
     w.c = c.take<float>((size_t)w.ld * kCDim);
     w.nidx = c.take<int32_t>((size_t)w.ld * prm->points->k);
     w.nw = c.take<float>((size_t)w.ld * prm->points->k);
-    w.gws_bytes = gather_workspace_bytes(w.r1);
+    // launch A gathers the r1 regulation + coarse rows, launch B the ld - r1 importance rows (more
+    // than r1 when n_importance > 2 n_samples): one workspace serves both
+    w.gws_bytes = gather_workspace_bytes(w.r1 > w.ld - w.r1 ? w.r1 : w.ld - w.r1);
     w.gws = c.take<char>(w.gws_bytes);
   }
   if (bytes) *bytes = c.off;
@@ -890,7 +915,13 @@ int pnr_map_bwd(const pnr_render_params* prm, const float* packed, const float* 
                 const double* g_depth, const float* g_rgb, const float* g_sigma, float* const* grads, void* workspace,
                 size_t ws_bytes, void* bwd_ws, size_t bwd_bytes, void* stream) {
   if (!valid_map_prm(prm) || !packed || n < 0) return PNR_E_ARG;
-  if (n == 0) return PNR_OK;
+  if (n == 0) {  // store semantics: an empty batch's weight gradients are zero
+    if (!prm->grads_overwrite) return PNR_OK;
+    if (grads)
+      for (int i = 0; i < PNR_N_PARAMS; ++i)
+        if (!grads[i]) return PNR_E_ARG;
+    return zero_weight_grads(grads, prm->points ? prm->points->g_fc : nullptr, (hipStream_t)stream);
+  }
   if (!workspace || !bwd_ws || !rays_d || !g_depth || !g_rgb || !g_sigma) return PNR_E_ARG;
   if (grads)
     for (int i = 0; i < PNR_N_PARAMS; ++i)

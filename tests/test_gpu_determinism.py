@@ -209,3 +209,78 @@ def test_map_pass_equals_two_chains(pnr_mod, dev, points, precision):
     print(f'map pass vs two chains: max |dg| {float(diff.max()):.3e} of max |g| {float(g2.abs().max()):.3e}')
     floor = 1e-6 if precision == 'fp32' else 1e-5  # f16x3: per-wave split scales (see above)
     assert bool((diff <= 1e-6 * g2.abs() + floor * g2.abs().max()).all())
+
+
+@pytest.mark.parametrize('points', [True, False])
+def test_map_step_stores_over_dirty_grads(pnr_mod, dev, points, precision):
+    """The fused MapStep stores the decoder / fc_c gradients (grads_overwrite) instead of zeroing the
+    buffer first: a buffer full of garbage from an earlier step must give exactly the gradients of a
+    clean one (a regression to accumulation would add the garbage in)."""
+    from pnr.mapping import MapStep
+    make, batches = _setup(pnr_mod, dev, points=points)
+    ro, rd, gt, col, t_rand = batches[0]
+    out = []
+    for dirty in (False, True):
+        r, dec, pts = make()
+        ms = MapStep(r, dec, points=pts, feat_lr=1e-2, lr=0.0)
+        if dirty:
+            ms.flat.grad.copy_(torch.randn_like(ms.flat.grad) * 1e3)
+        ms(ro, rd, gt, col, t_rand)
+        torch.cuda.synchronize()
+        out.append(ms.flat.grad.clone())
+    assert torch.equal(out[0], out[1])
+
+
+@pytest.mark.parametrize('points', [True, False])
+def test_map_bwd_empty_batch_zeroes_stored_grads(pnr_mod, dev, points, precision):
+    """pnr_map_bwd with n = 0 and grads_overwrite: the stored decoder / fc_c gradients of an empty
+    batch are zero (autograd's), not the previous step's values left in the buffer."""
+    from pnr.mapping import MapStep
+    from pnr.renderer import MapPass
+    make, _ = _setup(pnr_mod, dev, points=points)
+    r, dec, pts = make()
+    c = {} if pts is None else {'points_color': pts}
+    ms = MapStep(r, dec, points=pts, lr=0.0)
+    views, g_fc, g_feats = ms._views['main']
+    ms.flat.grad.fill_(7.0)
+    e3 = torch.empty((0, 3), device=dev)
+    e1 = torch.empty(0, device=dev)
+    mp = MapPass(r, c, dec)
+    mp.forward(e3, e3, e1, torch.empty((0, 32), device=dev))
+    mp.backward(views, g_fc=g_fc, g_feats=g_feats, g_depth=torch.empty(0, dtype=torch.float64, device=dev),
+                g_rgb=e3, g_sigma=e1, overwrite=True)
+    torch.cuda.synchronize()
+    n_dec = ms.n_dec
+    assert bool((ms.flat.grad[:n_dec] == 0).all())
+    if points:  # point-feature gradients always accumulate: left as they were
+        assert bool((ms.flat.grad[n_dec:] == 7.0).all())
+
+
+def test_map_step_multi_chunk_store(pnr_mod, dev, precision):
+    """More rows than one backward chunk (kBwdChunk = 4M rows: 56,000 rays x 76 rows): the first chunk
+    stores, later chunks add.  Over a dirty buffer the fused step must equal the two-chain step (zero
+    fill + accumulate) to float32 association, like test_map_pass_equals_two_chains."""
+    from pnr.mapping import MapStep
+    make, _ = _setup(pnr_mod, dev, points=False)
+    r0 = load_golden('render.npz')
+    n = 56000
+    ro = torch.from_numpy(r0['p2_gt/rays_o'])
+    rd = torch.from_numpy(r0['p2_gt/rays_d'])
+    gt = torch.from_numpy(r0['p2_gt/gt_depth'])
+    reps = -(-n // ro.shape[0])
+    gen = torch.Generator().manual_seed(11)
+    ro, rd, gt = [t.repeat(reps, *([1] * (t.dim() - 1)))[:n].to(dev) for t in (ro, rd, gt)]
+    col = torch.rand((n, 3), generator=gen).to(dev)
+    t_rand = torch.rand((n, 32), generator=gen).to(dev)
+    out = []
+    for fused in (True, False):
+        r, dec, _ = make()
+        ms = MapStep(r, dec, lr=0.0, fused=fused, overlap=False)
+        ms.flat.grad.copy_(torch.randn_like(ms.flat.grad) * 1e3)
+        ms(ro, rd, gt, col, t_rand)
+        torch.cuda.synchronize()
+        out.append(ms.flat.grad.clone())
+    g1, g2 = out
+    diff = (g1 - g2).abs()
+    floor = 1e-6 if precision == 'fp32' else 1e-5
+    assert bool((diff <= 1e-6 * g2.abs() + floor * g2.abs().max()).all()), float(diff.max())

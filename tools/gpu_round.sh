@@ -14,7 +14,7 @@
 #               (tools/prof_round.sh), the gather's traffic passes and kernel stats, the faithful
 #               iteration's kernel stats
 set -o pipefail
-TAG=${PNR_TAG:-r04}
+TAG=${PNR_TAG:-r05}
 cd /tmp && export TMPDIR=/tmp
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
@@ -38,18 +38,19 @@ for step in "$@"; do
       run 200 ${O}_smoke.log python3 -c "import __graft_entry__ as g; g.smoke()"
       echo "smoke ok" ;;
     test:*)
-      run 900 ${O}_gpu_tests_${step#test:}.log python3 -u -m pytest tests -m gpu -x -v --timeout 300 \
-        --timeout-method thread -p no:cacheprovider -k "${step#test:}"
-      tail -3 ${O}_gpu_tests_${step#test:}.log ;;
+      K="${step#test:}"; L="${O}_gpu_tests_${K//[^A-Za-z0-9_]/_}.log"
+      run 900 "$L" python3 -u -m pytest tests -m gpu -x -v --timeout 300 \
+        --timeout-method thread -p no:cacheprovider -k "$K"
+      tail -3 "$L" ;;
     bench)
       run 600 ${O}_bench.log python3 bench.py
       tail -c 300 ${O}_bench.log; echo ;;
     quick)
-      run 300 ${O}_quick.log python3 bench.py --steps 5 --warmup 2 --no-extras --no-cpu-baseline --no-gather
+      run 300 ${O}_quick.log python3 bench.py --workload map --steps 5 --warmup 2 --no-extras --no-cpu-baseline --no-gather
       grep -o '"value": [0-9.]*, "unit": "rays/s", "n_gpus": 1, "steps": [0-9]*, "warmup": [0-9]*, "ms_per_step": [0-9.]*' ${O}_quick.log
       grep -o '"frac": [0-9.]*' ${O}_quick.log | head -1 ;;
     faithful)
-      run 300 ${O}_faithful.log python3 bench.py --workload room0 --steps 100 --warmup 5 --no-cpu-baseline
+      run 300 ${O}_faithful.log python3 bench.py --workload room0 --steps 100 --warmup 5 --no-cpu-baseline --no-extras
       tail -c 400 ${O}_faithful.log; echo ;;
     points)
       run 300 ${O}_points.log python3 bench.py --workload map-points --steps 3 --warmup 1 --no-cpu-baseline --no-gather
@@ -72,7 +73,7 @@ for step in "$@"; do
       run 200 gpurun_out/prof_${TAG}_gb.log rocprofv3 --kernel-trace --stats --output-format csv \
         -d gpurun_out/prof_${TAG}_gather -o gb -- python3 tools/gather_bench.py
       run 200 gpurun_out/prof_${TAG}_f1000.log rocprofv3 --kernel-trace --stats --output-format csv \
-        -d gpurun_out/prof_${TAG}_f1000 -o f -- python3 bench.py --workload room0 --steps 50 --warmup 3 \
+        -d gpurun_out/prof_${TAG}_f1000 -o f -- python3 bench.py --workload room0 --steps 50 --warmup 3 --no-extras \
         --no-cpu-baseline
       echo "ROUND_PROF_DONE" ;;
     *)

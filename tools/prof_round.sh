@@ -7,7 +7,7 @@
 TAG=${1:-r02}
 cd /tmp && export TMPDIR=/tmp; cd $GRAFT_REPO_ROOT
 set -e
-MAP="python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-extras --no-gather"
+MAP="python3 bench.py --workload map --steps 3 --warmup 1 --no-cpu-baseline --no-extras --no-gather"
 FWD="python3 bench.py --workload fwd --steps 5 --warmup 1 --no-cpu-baseline --no-extras"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$TAG -o map -- \
   $MAP > gpurun_out/prof_${TAG}_map.log 2>&1
@@ -15,7 +15,7 @@ echo map-trace
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_${TAG}_fwd -o fwd -- \
   $FWD > gpurun_out/prof_${TAG}_fwd.log 2>&1
 echo fwd-trace
-ONE="python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-extras --no-gather"
+ONE="python3 bench.py --workload map --steps 1 --warmup 0 --no-cpu-baseline --no-extras --no-gather"
 for C in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 300 rocprofv3 --kernel-trace --pmc $C --output-format csv -d gpurun_out/prof_${TAG}_traffic -o $C -- \
     $ONE > gpurun_out/prof_${TAG}_$C.log 2>&1
