@@ -33,6 +33,46 @@ __device__ __forceinline__ void glds16s(const void* sbase, uint32_t voff, uint32
                : "=&s"(keep) : "v"(voff), "s"(sbase), "s"(lds_byte) : "memory");
 }
 
+// f16 hi / lo split of two fp32 values as packed pairs (element 0 in bits 15:0): hi = f16(x) (RNE),
+// lo = f16(x - hi) (RNE; x - hi is exact in fp32).  Three VALU per pair -- v_cvt_pk_f16_f32 and one
+// v_fma_mixlo / mixhi_f16 per value, which forms fma(hi, -1, x) from the f16 half in fp32 and rounds
+// it to f16 in place -- where the scalar form took six conversions and two subtractions (and the
+// packing).  Bit-identical to it (tools/micro/split_check.hip).
+// lo is formed in x0's register (tied), so a split whose inputs die there costs one new register.
+__device__ __forceinline__ void split2(float x0, float x1, uint32_t& hi, uint32_t& lo) {
+  uint32_t t = __float_as_uint(x0);
+  asm("v_cvt_pk_f16_f32 %0, %1, %2\n\t"
+      "v_fma_mixlo_f16 %1, %0, -1.0, %1 op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mixhi_f16 %1, %0, -1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
+      : "=&v"(hi), "+v"(t)
+      : "v"(x1));
+  lo = t;
+}
+
+// Eight LDS-DMA pieces of 1 KB per wave, 4 KB apart in the source and in LDS (one weight step of the
+// MLP kernels), in ONE statement: M0 is saved and restored once and stepped by s_add between the
+// pieces, and each source base serves two pieces (lane offsets voff and voff + 4096; the 13-bit
+// instruction offset cannot be used: it moves the LDS destination too, and stops at 4095): 18 SALU per
+// step where eight glds16s took 40.
+__device__ __forceinline__ void glds16s_x8(const char* src, uint32_t voff, uint32_t lds_byte) {
+  unsigned keep;
+  const uint32_t voff2 = voff + 4096;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %7\n\ts_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, %3\n\ts_add_u32 m0, m0, 0x1000\n\ts_nop 0\n\t"
+      "global_load_lds_dwordx4 %2, %3\n\ts_add_u32 m0, m0, 0x1000\n\ts_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, %4\n\ts_add_u32 m0, m0, 0x1000\n\ts_nop 0\n\t"
+      "global_load_lds_dwordx4 %2, %4\n\ts_add_u32 m0, m0, 0x1000\n\ts_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, %5\n\ts_add_u32 m0, m0, 0x1000\n\ts_nop 0\n\t"
+      "global_load_lds_dwordx4 %2, %5\n\ts_add_u32 m0, m0, 0x1000\n\ts_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, %6\n\ts_add_u32 m0, m0, 0x1000\n\ts_nop 0\n\t"
+      "global_load_lds_dwordx4 %2, %6\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "v"(voff2), "s"(src), "s"(src + 8192), "s"(src + 16384), "s"(src + 24576), "s"(lds_byte)
+      : "memory");
+}
+
 // 16-B store of a training save (activations, deltas), read back only by a later kernel.
 // PNR_SAVE_SC1: write-through (sc1) -- the line is dropped from the XCD's L2 instead of kept
 // (MI355X_MICROARCH.md "stores of each flavour"), so the save stream does not evict the weight
@@ -66,6 +106,8 @@ template <int N>
 __device__ __forceinline__ void sync_chunk() {
 #if defined(PNR_EXP_NOWAIT)  // experiment: barrier without the DMA wait (races on LDS: timing only)
   asm volatile("s_barrier" ::: "memory");
+#elif defined(PNR_EXP_NOBAR)  // experiment: the DMA wait without the barrier (races on LDS: timing only)
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 #else
   asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
 #endif

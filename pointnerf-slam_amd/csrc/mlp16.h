@@ -204,10 +204,39 @@ struct BfState {
   bool valid, inside;
 };
 
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// 8 values times s split into f16 hi / lo operands (packed pairs, dev_common.h split2)
+__device__ __forceinline__ void split8(const float* x, float s, f16x8& hi, f16x8& lo) {
+  uint32_t h[4], l[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) split2(x[2 * j] * s, x[2 * j + 1] * s, h[j], l[j]);
+  hi = __builtin_bit_cast(f16x8, u32x4{h[0], h[1], h[2], h[3]});
+  lo = __builtin_bit_cast(f16x8, u32x4{l[0], l[1], l[2], l[3]});
+}
+
 // values 4q..4q+3 of a tile = k-step q>>1, elements 4(q&1)..4(q&1)+3
-template <int PR, typename T>
+// PK: the packed f16 split (the feature-branch kernels, at their register limit, keep the scalar form:
+// the packed one's extra live registers spill there)
+template <int PR, typename T, bool PK = true>
 __device__ __forceinline__ void split_quad(const float* v4, int q, T (&t)[Prec<PR>::NP][2]) {
   using E = typename Prec<PR>::E;
+  if constexpr (Prec<PR>::F16 && PK) {
+    // f16x3: packed pairs (dev_common.h split2: 6 VALU per quad where the scalar form took ~16),
+    // dwords 2(q&1), 2(q&1)+1 of the k-step's operand
+    uint32_t h0, l0, h1, l1;
+    split2(v4[0], v4[1], h0, l0);
+    split2(v4[2], v4[3], h1, l1);
+    u32x4 hv = __builtin_bit_cast(u32x4, t[0][q >> 1]);
+    u32x4 lv = __builtin_bit_cast(u32x4, t[1][q >> 1]);
+    hv[2 * (q & 1)] = h0;
+    hv[2 * (q & 1) + 1] = h1;
+    lv[2 * (q & 1)] = l0;
+    lv[2 * (q & 1) + 1] = l1;
+    t[0][q >> 1] = __builtin_bit_cast(T, hv);
+    t[1][q >> 1] = __builtin_bit_cast(T, lv);
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const float x = v4[i];
@@ -217,10 +246,10 @@ __device__ __forceinline__ void split_quad(const float* v4, int q, T (&t)[Prec<P
   }
 }
 
-template <int PR, typename T>
+template <int PR, typename T, bool PK = true>
 __device__ __forceinline__ void split_tile(const float (&v)[16], T (&t)[Prec<PR>::NP][2]) {
 #pragma unroll
-  for (int q = 0; q < 4; ++q) split_quad<PR>(v + 4 * q, q, t);
+  for (int q = 0; q < 4; ++q) split_quad<PR, T, PK>(v + 4 * q, q, t);
 }
 
 
@@ -314,8 +343,12 @@ struct BfFwd {
           lds_addr(reinterpret_cast<const float*>(lds + ((g + sb) % G::kNbuf) * G::kSlot)) + w * 1024;
       const uint32_t voff = lane * 16;
       const char* src = a.wmain + G::main_off(st) + w * 1024;  // wave-uniform (SGPRs)
+      if constexpr (G::main_n(st) == 8 && !HASC) {  // (the feature-branch kernels: no SGPRs to spare)
+        glds16s_x8(src, voff, slot);
+      } else {
 #pragma unroll
-      for (int i = 0; i < G::main_n(st); ++i) glds16s(src + i * 4096, voff, slot + i * 4096);
+        for (int i = 0; i < G::main_n(st); ++i) glds16s(src + i * 4096, voff, slot + i * 4096);
+      }
       if constexpr (G::fc_n(st) > 0) glds16s(a.wfc + (int64_t)(st - 2) * 4096 + w * 1024, voff, slot + G::kMainH);
     }
   }
@@ -395,7 +428,7 @@ struct BfFwd {
       save16(h_save(a, S, L, t, q), make_float4(S.v[4 * q], S.v[4 * q + 1], S.v[4 * q + 2], S.v[4 * q + 3]));
     S.vmax = fmaxf(S.vmax, fmaxf(fmaxf(fabsf(S.v[4 * q]), fabsf(S.v[4 * q + 1])),
                                  fmaxf(fabsf(S.v[4 * q + 2]), fabsf(S.v[4 * q + 3]))));
-    split_quad<PR>(S.v + 4 * q, q, S.nxt);
+    split_quad<PR, V8, !HASC>(S.v + 4 * q, q, S.nxt);
   }
 
   // epilogue pieces scheduled after MFMA group T of a step with NT groups
@@ -732,7 +765,7 @@ static __device__ __forceinline__ void fwd16_tile(const BfFwdArgs& a, int mode, 
       // above ~2^114 would still overflow -- the range check covers them (PNR_STATUS_F16_RANGE)
       S.vmax = m * sc;
     }
-    split_tile<PR>(cv, S.ct);
+    split_tile<PR, typename K::V8, false>(cv, S.ct);
   }
   // no accumulator zero fill: the first input tile of every layer starts its tiles from 0 (ZERO in
   // mfma_frag), and nothing reads a tile before that (256 v_accvgpr_mov saved per workgroup)
@@ -758,7 +791,7 @@ static __device__ __forceinline__ void fwd16_tile(const BfFwdArgs& a, int mode, 
         v[r] = k < kFourier ? fourier_sc<false>(arg) : 0.f;
       }
       // no e save: the dW0 GEMM recomputes sin(x@B) from the saved x (wgrad16.hip kWgradFirstX)
-      split_tile<PR>(v, S.ft[t]);
+      split_tile<PR, typename K::V8, !HASC>(v, S.ft[t]);
     }
     // always issued (the step program's vmcnt counts include it); in the map pass the kPtsX4 input
     // rows are this save, so the store rewrites the value the lane has just read

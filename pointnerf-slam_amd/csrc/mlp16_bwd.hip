@@ -202,8 +202,12 @@ struct BfBwd {
       // addresses are loop-invariant, get hoisted out of the persistent tile loop and spill
       const uint32_t voff = lane * 16;
       const char* src = wmain + bwd_main_off(st) + w * 1024;
+      if constexpr (G::main_n(st) == 8 && !HASC) {  // (the feature-branch kernels: no SGPRs to spare)
+        glds16s_x8(src, voff, slot);
+      } else {
 #pragma unroll
-      for (int i = 0; i < G::main_n(st); ++i) glds16s(src + i * 4096, voff, slot + i * 4096);
+        for (int i = 0; i < G::main_n(st); ++i) glds16s(src + i * 4096, voff, slot + i * 4096);
+      }
       if constexpr (G::fc_n(st) > 0) glds16s(wfc + (int64_t)st * 4096 + w * 1024, voff, slot + 32768);
     }
   }
@@ -212,7 +216,7 @@ struct BfBwd {
   template <typename T>
   static __device__ __forceinline__ void split_scaled(const float* v4, float s, int q, T (&t)[2][2]) {
     const float u[4] = {v4[0] * s, v4[1] * s, v4[2] * s, v4[3] * s};
-    split_quad<PR>(u, q, t);
+    split_quad<PR, f16x8, !HASC>(u, q, t);
   }
 
   // fp32 save address of this lane's unit quad (t, q) of layer li: point-major row S.dcol
@@ -459,7 +463,7 @@ static __device__ __forceinline__ void bwd16_tile(const float* __restrict__ W, c
     if (hh == 0) {
       gv[0] = go.x * s0; gv[1] = go.y * s0; gv[2] = go.z * s0; gv[3] = go.w * s0;
     }
-    split_tile<PNR_PREC_F16X3>(gv, S.cur);
+    split_tile<PNR_PREC_F16X3, f16x8, !HASC>(gv, S.cur);
     S.kacc = inv[4] / s0;
   }
   if (HASC) {

@@ -469,6 +469,7 @@ struct GatherArgs {
   const int32_t* gstart; // [G + 1] group start offsets in `grouped`; gstart[G] = all items
   float4* grouped;       // the work items in group order
   uint32_t gmask;        // G - 1
+  int chunk;             // work items per search chunk (one wave): 64, or fewer for small launches
 };
 
 // Pass 1, one thread per sample row: the occupancy bit of each sample's probe block; the hits go
@@ -638,10 +639,11 @@ __global__ __launch_bounds__(64, PNR_SEARCH_WAVES) void k_gather_search(GatherAr
   const int lane = threadIdx.x, gq = lane >> 3, q = lane & 7;
   const double kInf = __longlong_as_double(0x7FF0000000000000ll);
   const int64_t n_items = a.gstart[(int64_t)a.gmask + 1];
-  const int64_t nchunk = (n_items + 63) / 64;
+  const int cs = a.chunk;  // items per chunk (lanes >= cs idle in the scan, still stage and sum)
+  const int64_t nchunk = (n_items + cs - 1) / cs;
   for (int64_t chunk = blockIdx.x; chunk < nchunk; chunk += gridDim.x) {
-    const int64_t it = chunk * 64 + lane;
-    const bool has = it < n_items;
+    const int64_t it = chunk * cs + lane;
+    const bool has = lane < cs && it < n_items;
     float x0 = 0.f, x1 = 0.f, x2 = 0.f;
     int row = -1, bx = 0, by = 0, bz = 0;
     if (has) {
@@ -978,6 +980,7 @@ struct GatherBwdArgs {
   uint32_t* gmax;        // bits of max |dL/dc| over the work list's rows (NaN / inf propagate)
   unsigned long long* n_flush;  // int64 atomic instructions (256 B each) issued, for the roofline
   int guard;
+  int run;               // work items per half-wave run (32, fewer for small launches)
 };
 
 // rows with a neighbour (idx[row][0] >= 0: neighbours are stored nearest first) -> work list
@@ -1031,17 +1034,18 @@ template <int SRC, int KER>
 __global__ __launch_bounds__(256) void k_gather_bwd(GatherBwdArgs a) {
   PNR_FP_STRICT
   const int ch = threadIdx.x & 31, half = threadIdx.x >> 5;  // 8 half-waves per block
-  const int64_t nchunk = (a.wl.cap + 255) / 256;
+  const int R = a.run, per = 8 * R;  // items per half-wave run / per block task
+  const int64_t nchunk = (a.wl.cap + per - 1) / per;
   const int fs = a.g_feats ? fx_shift(*a.gmax, a.guard) : 0;
   unsigned long long* facc = reinterpret_cast<unsigned long long*>(a.facc);
   uint32_t nfl = 0;  // flushes of this half-wave (uniform over it)
   for (int64_t task = blockIdx.x; task < kLists * nchunk; task += gridDim.x) {
     const int rl = (int)(task % kLists);
-    const int64_t j0 = task / kLists * 256;
+    const int64_t j0 = task / kLists * per;
     const int64_t n_work = (int64_t)a.wl.cnt[rl * 32];
     if (j0 >= n_work) continue;  // uniform over the block
-    const int64_t jn = n_work - j0 < 256 ? n_work - j0 : 256;
-    // half-wave `half` takes 32 consecutive items: rows of one ray, whose neighbour lists overlap.
+    const int64_t jn = n_work - j0 < per ? n_work - j0 : per;
+    // half-wave `half` takes R consecutive items: rows of one ray, whose neighbour lists overlap.
     // A neighbour shared with the previous row carries its partial sum forward instead of being
     // flushed: the atomic goes out when it leaves the list (or at the end of the run).  Integer
     // sums: the result does not depend on which rows share a run, nor on the atomics' order.
@@ -1052,9 +1056,9 @@ __global__ __launch_bounds__(256) void k_gather_bwd(GatherBwdArgs a) {
       pid[kk] = -1;
       pacc[kk] = 0;
     }
-    const int64_t te = 32 * half + 32 < jn ? 32 * half + 32 : jn;
+    const int64_t te = (int64_t)R * half + R < jn ? (int64_t)R * half + R : jn;
 #pragma unroll 1
-    for (int64_t t = 32 * half; t < te; ++t) {  // uniform over each half-wave
+    for (int64_t t = (int64_t)R * half; t < te; ++t) {  // uniform over each half-wave
       const int64_t p = __float_as_int(a.wl.items[rl * a.wl.cap + j0 + t].w);
       // every load of the row issued at once: g_c / c rows, the k (index, weight) pairs (broadcast
       // within the half-wave), then the k feature rows and atomics predicated, no dependent branches
@@ -1339,7 +1343,14 @@ int launch_gather(const pnr_points& pts, const PointSrc& src, int mode, int64_t 
   int rc = scan_exclusive(a.gcnt, gv.gstart, G, gv.scratch, st);
   if (rc) return rc;
   hipLaunchKernelGGL(k_group_scatter, dim3((unsigned)(kLists * ((a.wl.cap + 255) / 256))), dim3(256), 0, st, a);
-  const int64_t tasks = (P + 63) / 64;  // upper bound on the chunks (the kernel reads the real count)
+  // Items per chunk: a chunk's segments (probe blocks) run one after another in its wave, each a few
+  // dependent round trips.  At the Mapper's real batches (1,000-5,000 rays) the items of a chunk rarely
+  // share a block, so 64-item chunks left ~200 waves each walking up to 64 segments in series
+  // (config C3: 209 + 320 us per iteration); smaller chunks spread the segments over the machine's
+  // ~5,000 wave slots.  The S-map batches (> 2.6M samples: 80 per block) keep 64.
+  a.chunk = 64;
+  while (a.chunk > 4 && (P + a.chunk - 1) / a.chunk < 5 * 1024 * 8) a.chunk >>= 1;
+  const int64_t tasks = (P + a.chunk - 1) / a.chunk;  // upper bound on the chunks (the kernel reads the real count)
   auto kern = pts.mode == PNR_GATHER_IDW
                   ? (a.feat_half ? k_gather_search<PNR_GATHER_IDW, true> : k_gather_search<PNR_GATHER_IDW, false>)
                   : (a.feat_half ? k_gather_search<PNR_GATHER_TRILINEAR, true>
@@ -1401,6 +1412,12 @@ int launch_gather_bwd(const pnr_points& pts, const PointSrc* src, int mode, cons
   int guard = 1;
   while (guard < 40 && (1ll << guard) <= P) ++guard;
   a.guard = guard;
+  // Items per half-wave run: each run's rows are serial (every row a few dependent loads and its
+  // atomics); the S-map batches keep 32 (long runs carry shared neighbours between a ray's rows), the
+  // Mapper's real batches shorter runs so the rows spread over the machine (config C3: 92 us per
+  // backward with 32-row runs over ~600 half-waves)
+  a.run = 32;
+  while (a.run > 2 && P / a.run < 2 * 5 * 1024 * 8) a.run >>= 1;
   if (hipMemsetAsync(a.wl.cnt, 0, kLists * 32 * 4, st) != hipSuccess) return (int)hipGetLastError();
   if (feats) {
     if (hipMemsetAsync(v.ctl, 0, 256, st) != hipSuccess) return (int)hipGetLastError();
@@ -1411,8 +1428,9 @@ int launch_gather_bwd(const pnr_points& pts, const PointSrc* src, int mode, cons
   hipLaunchKernelGGL(k_gather_bwd_probe, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, st, a);
   const int64_t tasks = kLists * ((a.wl.cap + 255) / 256);
   if (feats) hipLaunchKernelGGL(k_gather_bwd_gmax, dim3(resident_grid(k_gather_bwd_gmax, 256, tasks)), dim3(256), 0, st, a);
-  if (pts.mode == PNR_GATHER_IDW) gather_bwd_mode<PNR_GATHER_IDW>(mode, tasks, st, a);
-  else gather_bwd_mode<PNR_GATHER_TRILINEAR>(mode, tasks, st, a);
+  const int64_t rtasks = kLists * ((a.wl.cap + 8 * a.run - 1) / (8 * a.run));
+  if (pts.mode == PNR_GATHER_IDW) gather_bwd_mode<PNR_GATHER_IDW>(mode, rtasks, st, a);
+  else gather_bwd_mode<PNR_GATHER_TRILINEAR>(mode, rtasks, st, a);
   if (feats && pts.n_points > 0) {
     const int64_t n = pts.n_points * kCDim;
     hipLaunchKernelGGL(k_gather_bwd_fin, dim3((unsigned)((n / 4 + 255) / 256 + 1)), dim3(256), 0, st, v.facc, pts.g_feats,

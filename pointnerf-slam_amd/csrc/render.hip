@@ -1284,10 +1284,12 @@ int launch_adam_multi(float* p, const float* g, int nseg, const int64_t* off, co
     S.v[q] = v[q];
     S.lr[q] = lr[q];
     S.first[q] = blocks;
-    // grid-stride over at most 128 blocks per segment: every block takes one ticket, and a ticket per
-    // 256 elements (870 for the decoder) queued on one address for ~10 us
+    // a block per 1,024 elements (one pass of four loads per thread), at most 1,024 blocks per segment:
+    // every block takes one ticket (a ticket per 256 elements -- 870 for the decoder -- queued on one
+    // address for ~10 us), and 128 blocks left the 6.4M point features of config C3 latency-bound
+    // (49 dependent passes per thread: 88 us)
     const int64_t nb = nblk(n[q] > 0 ? n[q] : 1, 1024);
-    blocks += (int)(nb < 128 ? nb : 128);
+    blocks += (int)(nb < 1024 ? nb : 1024);
   }
   S.first[nseg] = blocks;
   S.nseg = nseg;

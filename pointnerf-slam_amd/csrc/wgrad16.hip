@@ -169,15 +169,12 @@ __device__ __forceinline__ void wx_stage_b(const WxRegs<NTB, WB>& R, char* slot,
           v[e] = c + e < kFourier ? fourier_sc<false>(arg) : 0.f;
         }
       }
-      f16x4 hi, lo;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        hi[e] = (_Float16)v[e];
-        lo[e] = (_Float16)(v[e] - (float)hi[e]);
-      }
+      uint32_t h0, l0, h1, l1;  // packed f16 hi / lo pairs (dev_common.h split2)
+      split2(v[0], v[1], h0, l0);
+      split2(v[2], v[3], h1, l1);
       char* base = slot + (c >> 5) * kTileB + r * 64 + (c & 31) * 2;
-      *reinterpret_cast<f16x4*>(base) = hi;
-      *reinterpret_cast<f16x4*>(base + Cfg::kPlane) = lo;
+      *reinterpret_cast<uint2*>(base) = make_uint2(h0, h1);
+      *reinterpret_cast<uint2*>(base + Cfg::kPlane) = make_uint2(l0, l1);
     }
   }
 }
@@ -279,14 +276,9 @@ __device__ __forceinline__ void wgrad16_body(const WxArgs& a, const int bid, cha
     }
     f16x8 ah[2], al[2];
 #pragma unroll
-    for (int s = 0; s < 2; ++s)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float x = R.a[8 * s + j] * sc;
-        const _Float16 h = (_Float16)x;
-        ah[s][j] = h;
-        al[s][j] = (_Float16)(x - (float)h);
-      }
+    for (int s = 0; s < 2; ++s) {
+      split8(R.a + 8 * s, sc, ah[s], al[s]);
+    }
     {  // next tile into the (now free) registers; the last tile is re-read (keeps the loop uniform)
       const int64_t tn = t + 1 < ntile ? t + 1 : t;
       wx_load<NTB, WB, SYN, FOUR, MSK>(a, kb + 32 * tn, R);
@@ -317,13 +309,7 @@ __device__ __forceinline__ void wgrad16_body(const WxArgs& a, const int bid, cha
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         f16x8 bh, bl;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float x = bv[8 * s + j] * sb;
-          const _Float16 h = (_Float16)x;
-          bh[j] = h;
-          bl[j] = (_Float16)(x - (float)h);
-        }
+        split8(bv + 8 * s, sb, bh, bl);
         acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[s], bh, acc[0], 0, 0, 0);
         acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[s], bl, acc[0], 0, 0, 0);
         acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[s], bh, acc[0], 0, 0, 0);
