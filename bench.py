@@ -201,6 +201,7 @@ def gather_roofline(dev, voxel=0.001, k=8, reps=5, feat_dtype='float32'):
     sb, _ = pts.descriptor(g_feats=gf)
     bws = torch.empty(lib.pnr_point_gather_bwd_workspace_bytes(ctypes.byref(sb), P), dtype=torch.uint8, device=dev)
     rows = int((idx[:, 0] >= 0).sum().item())
+    touched = int(torch.unique(idx[idx >= 0]).numel())  # feature rows some sample names
     lib.pnr_timing_enable(1)
     timing_read(5)
     for _ in range(reps):
@@ -216,17 +217,20 @@ def gather_roofline(dev, voxel=0.001, k=8, reps=5, feat_dtype='float32'):
                    'gather_bwd_atomics')
     M = int(xyz.shape[0])
     # HBM: per sample 4 B (its first neighbour index, the probe); per row with neighbours 128 B g_c
-    # read twice (max |g_c| pass, then the sums) + k x 8 B idx/w; the accumulators zeroed (M x 256 B),
-    # read once and the features' gradient read + written by the conversion (M x (256 + 256) B).
-    # Atomics: the 64-bit add instructions the kernel counted as it issued them (256 B each: 32 lanes x 8 B;
-    # shared neighbours are carried between a ray's rows, so far fewer go out than rows x neighbours)
-    b_hbm = P * 4 + rows * (2 * 128 + k * 8) + M * (256 + 256 + 256)
+    # read twice (max |g_c| pass, then the sums) + k x 8 B idx/w (read twice: the max pass marks the
+    # rows it names); per touched feature row its int64 accumulators zeroed, read once, and the
+    # features' gradient read + written by the conversion (256 + 256 + 256 B); the M-bit touched map
+    # zeroed and read.  Atomics: the 64-bit add instructions the kernel counted as it issued them (256 B
+    # each: 32 lanes x 8 B; shared neighbours are carried between a ray's rows, so far fewer go out than
+    # rows x neighbours)
+    b_hbm = P * 4 + rows * (2 * 128 + 2 * k * 8) + touched * (256 + 256 + 256) + 2 * (M // 8)
     b_atomic = int(n_instr.value) * 256
     t_floor = (b_hbm / (HBM_PEAK_GBS * 1e9) + b_atomic / 1.3e12) * 1e3
     bwd = {'kernel': 'k_gather_bwd_probe + k_gather_bwd_gmax + k_gather_bwd + k_gather_bwd_fin (feature gradients, '
                      'the Mapper case; deterministic int64 fixed point)',
            'avg_launch_ms': round(bavg, 4), 'bytes_hbm': b_hbm, 'bytes_atomic_issued': b_atomic,
            'atomic_instructions': int(n_instr.value), 'neighbour_terms': nb, 'rows': rows,
+           'touched_feature_rows': touched,
            'achieved_gbs': round((b_hbm + b_atomic) / (bavg * 1e-3) / 1e9, 1),
            'floor_ms': round(t_floor, 4), 'frac_of_floor': round(t_floor / bavg, 4),
            'floor_basis': 'HBM bytes at 8 TB/s + the issued 64-bit atomic bytes (counted in the kernel) at the '

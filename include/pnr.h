@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define PNR_ABI_VERSION 11
+#define PNR_ABI_VERSION 12
 #define PNR_N_PARAMS 11
 #define PNR_MAX_SAMPLES 64      /* N_samples + N_importance per ray */
 #define PNR_C_DIM 32            /* neural-point feature width (decoder.py:122-125 fc_c input) */
@@ -221,7 +221,8 @@ int pnr_point_gather(const pnr_points* pts, const double* p, int64_t P, float* c
  * no sum overflows), the terms are added exactly with 64-bit integer atomics, and the sum is
  * converted once into g_feats.  Any order of the additions gives the same bits.  The absolute error
  * of an element is at most (its term count) x 2^-(63 - guard) x max |dL/dc|: fp32-class for any
- * element above ~2^-14 of the largest term.  A non-finite dL/dc makes every g_feats element NaN. */
+ * element above ~2^-14 of the largest term.  A non-finite dL/dc makes every element of the feature
+ * rows the call's samples name NaN; rows no sample names are left untouched (ABI 12). */
 size_t pnr_point_gather_bwd_workspace_bytes(const pnr_points* pts, int64_t P);
 int pnr_point_gather_bwd(const pnr_points* pts, const double* p, int64_t P, const int32_t* idx, const float* w,
                          const float* c, const float* g_c, float* g_p, void* ws, size_t ws_bytes, void* stream);
@@ -331,6 +332,14 @@ int pnr_step_advance(int32_t* step_count, void* stream);
 int pnr_adam_multi_dev(float* p, const float* g, int32_t n_seg, const int64_t* seg_offset, const int64_t* seg_n,
                        float* const* m, float* const* v, const float* seg_lr, float beta1, float beta2, float eps,
                        int32_t* step2, void* stream);
+/* ABI 12: pnr_adam_multi_dev that also writes float16(p) of every updated element of segment q into
+ * half_copy[q][0 .. seg_n[q]) when half_copy (host array of n_seg device pointers) and half_copy[q]
+ * are non-NULL: the float16 feature copy the gather reads (pnr_points.feat_half), refreshed in the
+ * same pass instead of a separate conversion of the whole table (round to nearest even, as torch's
+ * float16 copy). */
+int pnr_adam_multi_dev_h(float* p, const float* g, int32_t n_seg, const int64_t* seg_offset, const int64_t* seg_n,
+                         float* const* m, float* const* v, const float* seg_lr, float beta1, float beta2, float eps,
+                         uint16_t* const* half_copy, int32_t* step2, void* stream);
 
 /* Mapper loss terms and their gradients (src/Mapper.py:628-655, the loss of Mapper.optimize_map
  * built from render_batch_ray's depth / colour and regulation's sigma), in one pass (ABI 9):

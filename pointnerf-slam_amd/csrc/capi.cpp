@@ -58,7 +58,7 @@ int launch_adam_dev(float*, const float*, float*, float*, int64_t, float, float,
                     hipStream_t);
 int launch_step_advance(int32_t*, hipStream_t);
 int launch_adam_multi(float*, const float*, int, const int64_t*, const int64_t*, float* const*, float* const*,
-                      const float*, float, float, float, int32_t*, hipStream_t);
+                      const float*, float, float, float, int32_t*, hipStream_t, uint16_t* const* half = nullptr);
 int launch_map_loss(const float*, const double*, const float*, const float*, int64_t, float, const float*, int64_t,
                     float, double*, double*, double*, float*, float*, hipStream_t);
 
@@ -1006,8 +1006,7 @@ int pnr_fc_pack(const float* const* fc_params, float* fc_packed, void* stream) {
   if (!fc_params || !fc_packed) return PNR_E_ARG;
   for (int i = 0; i < PNR_N_FC_PARAMS; ++i)
     if (!fc_params[i]) return PNR_E_ARG;
-  const int rc = launch_fc_pack(fc_params, fc_packed, (hipStream_t)stream);
-  return rc ? rc : launch_fc_pack_bf(fc_params, fc_packed, (hipStream_t)stream);
+  return launch_fc_pack_all(fc_params, fc_packed, (hipStream_t)stream);
 }
 
 int pnr_eval_points_c(const float* packed, const float* fc_packed, const double* p, const float* c, int64_t P,
@@ -1143,6 +1142,16 @@ int pnr_adam_multi_dev(float* p, const float* g, int32_t n_seg, const int64_t* s
     if (seg_n[q] < 0 || seg_offset[q] < 0 || (seg_n[q] > 0 && (!m[q] || !v[q]))) return PNR_E_ARG;
   return launch_adam_multi(p, g, n_seg, seg_offset, seg_n, m, v, seg_lr, beta1, beta2, eps, step2,
                            (hipStream_t)stream);
+}
+
+int pnr_adam_multi_dev_h(float* p, const float* g, int32_t n_seg, const int64_t* seg_offset, const int64_t* seg_n,
+                         float* const* m, float* const* v, const float* seg_lr, float beta1, float beta2, float eps,
+                         uint16_t* const* half_copy, int32_t* step2, void* stream) {
+  if (!p || !g || !seg_offset || !seg_n || !m || !v || !seg_lr || !step2 || n_seg < 1 || n_seg > 4) return PNR_E_ARG;
+  for (int q = 0; q < n_seg; ++q)
+    if (seg_n[q] < 0 || seg_offset[q] < 0 || (seg_n[q] > 0 && (!m[q] || !v[q]))) return PNR_E_ARG;
+  return launch_adam_multi(p, g, n_seg, seg_offset, seg_n, m, v, seg_lr, beta1, beta2, eps, step2,
+                           (hipStream_t)stream, half_copy);
 }
 
 int pnr_step_advance(int32_t* step_count, void* stream) {

@@ -353,6 +353,28 @@ struct BfFwd {
     }
   }
 
+  // Spread DMA (eval kernel): the 8 pieces of a hidden step's DMA go out one per MFMA group -- pieces
+  // 0..2 after the barrier in groups 5..7 of step g, pieces 3..7 in groups 0..4 of step g+1 -- instead
+  // of a burst after the barrier.  Only VMEM ops of the eval kernel are these DMAs, and all 8 pieces
+  // of DMA(i+1) are still issued before barrier B_i: the vmcnt counts stay those of the burst.
+#if defined(PNR_EXP_DMA_SPREAD)
+  static constexpr bool SPREAD = !HASC && SV == 0 && NP == 2;
+#else
+  static constexpr bool SPREAD = false;
+#endif
+  template <int g, int i>
+  static __device__ __forceinline__ void stage_piece(const BfFwdArgs& a, const char* lds, int sb) {
+    if constexpr (g < G::kSteps || (PST && g < 2 * G::kSteps)) {
+      constexpr int st = g < G::kSteps ? g : g - G::kSteps;
+      static_assert(G::main_n(st) == 8 && G::fc_n(st) == 0, "spread: hidden steps only");
+      const int w = wave_id(), lane = threadIdx.x & 63;
+      const uint32_t slot =
+          lds_addr(reinterpret_cast<const float*>(lds + ((g + sb) % G::kNbuf) * G::kSlot)) + w * 1024;
+      const char* src = a.wmain + G::main_off(st) + w * 1024;
+      glds16s(src + i * 4096, lane * 16, slot + i * 4096);
+    }
+  }
+
   static __device__ __forceinline__ const float* raw_lds(const char* lds) {
     return reinterpret_cast<const float*>(lds + G::kNbuf * G::kSlot);
   }
@@ -559,6 +581,7 @@ struct BfFwd {
       if constexpr (HASC && CONV && T == clamp_t(1, g)) load_frag<PR>(slot + G::kMainH, S.FC);
       if constexpr (HASC && CONV && T == clamp_t(3, g)) preload_fc<CL, CT>(S, lds);
       if constexpr (T + kPf < NT) load_frag<PR>(slot + (T + kPf) * 2 * NP * 1024, S.F[(b + T + kPf) % kRing]);
+      if constexpr (SPREAD && g >= 1 && T < NT - sync_t(g) + 2 && T + 3 < 8) stage_piece<g + kD, T + 3>(a, lds, S.sb);
       __builtin_amdgcn_sched_barrier(0);  // prefetch first, then the group's MFMAs
       if constexpr (NT == 1) {
         if constexpr (kc == 0) mfma_frag<PR, true>(S.F[b], act, S.out);
@@ -579,9 +602,10 @@ struct BfFwd {
           sync_chunk<0>();
 #else
           sync_chunk<younger_b(g + 1)>();
-          stage_step<g + 1 + kD>(a, lds, S.sb);
+          if constexpr (!SPREAD) stage_step<g + 1 + kD>(a, lds, S.sb);
 #endif
         }
+        if constexpr (SPREAD && T >= sync_t(g)) stage_piece<g + 1 + kD, T - sync_t(g)>(a, lds, S.sb);
         if constexpr (T == next_grp(g, 0)) next_frag<g + 1, 0>(S, lds);
         if constexpr (T == next_grp(g, 1)) next_frag<g + 1, 1>(S, lds);
         if constexpr (T == next_grp(g, 2)) next_frag<g + 1, 2>(S, lds);

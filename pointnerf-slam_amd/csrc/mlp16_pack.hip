@@ -230,9 +230,8 @@ struct FcRaw16 {
 };
 
 // fc entry e = 8L + t: A[row = unit 32t + (lane&31)][k = channel perm(8s+j, lane>>5)] of Wc_L
-__global__ void k_fc_pack16(FcRaw16 fc, uint16_t* __restrict__ bf2, uint16_t* __restrict__ bf1,
-                            uint16_t* __restrict__ h2, float* __restrict__ raw) {
-  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void fc_pack16_at(const FcRaw16& fc, uint16_t* __restrict__ bf2, uint16_t* __restrict__ bf1,
+                                             uint16_t* __restrict__ h2, float* __restrict__ raw, int64_t idx) {
   const int64_t n = kBfFcBytes / 2;  // elements per image
   if (idx < 3 * n) {
     const int img = (int)(idx / n);
@@ -262,8 +261,8 @@ __global__ void k_fc_pack16(FcRaw16 fc, uint16_t* __restrict__ bf2, uint16_t* __
 
 // fc backward entry e = 8(3 - l) + t: A[row = channel (lane&31)][k = unit 32t + perm(8s+j, lane>>5)]
 // = Wc_l[unit][channel], f16x3 scaled like the forward image (raw[kFcRawScl + l])
-__global__ void k_fc_pack16_bwd(FcRaw16 fc, uint16_t* __restrict__ out, const float* __restrict__ raw) {
-  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void fc_pack16_bwd_at(const FcRaw16& fc, uint16_t* __restrict__ out,
+                                                 const float* __restrict__ raw, int64_t e) {
   if (e >= kBfFcBytes / 2) return;
   const int ent = (int)(e / 2048);
   int64_t r = e % 2048;
@@ -276,9 +275,34 @@ __global__ void k_fc_pack16_bwd(FcRaw16 fc, uint16_t* __restrict__ out, const fl
   out[e] = part_bits<_Float16>(fc.at(2 * l)[unit * kCDim + (lane & 31)] * raw[kFcRawScl + l], part);
 }
 
-int launch_fc_pack_bf(const float* const* fcp, float* out, hipStream_t st) {
+// The fc_c images in two launches, as the main images (launch_pack_all): stage 1 the four fc weight
+// scales (blocks 0..3) and the fp32 image, stage 2 the forward 16-bit images with the fc raw table and
+// the transposed f16x3 backward image (both read stage 1's scales).  Four launches before: ~10 us of
+// latency per Mapper iteration at the neural-point configs' real batches.
+constexpr int64_t kFc16N = 3 * (kBfFcBytes / 2) + kFcRawInv;  // stage-2 elements of the forward images
+__global__ __launch_bounds__(1024) void k_fc_stage1(ScaleArgs sa, FcRaw fr, float* __restrict__ out) {
+  if (blockIdx.x < 4) {
+    wscale_block(sa, blockIdx.x);
+    return;
+  }
+  const int64_t stride = (int64_t)(gridDim.x - 4) * 1024;
+  for (int64_t i = (int64_t)(blockIdx.x - 4) * 1024 + threadIdx.x; i < kFcPackedFloats; i += stride)
+    fc_pack_fp32_at(fr, out, i);
+}
+__global__ __launch_bounds__(256) void k_fc_stage2(FcRaw16 fc, float* __restrict__ out) {
+  float* raw = out + kOffFcRaw;
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx < kFc16N)
+    fc_pack16_at(fc, reinterpret_cast<uint16_t*>(out + kOffFcBf2), reinterpret_cast<uint16_t*>(out + kOffFcBf1),
+                 reinterpret_cast<uint16_t*>(out + kOffFcH2), raw, idx);
+  else
+    fc_pack16_bwd_at(fc, reinterpret_cast<uint16_t*>(out + kOffFcBwd), raw, idx - kFc16N);
+}
+
+int launch_fc_pack_all(const float* const* fcp, float* out, hipStream_t st) {
   FcRaw16 r;
-  for (int i = 0; i < PNR_N_FC_PARAMS; ++i) r.p[i] = fcp[i];
+  FcRaw fr;
+  for (int i = 0; i < PNR_N_FC_PARAMS; ++i) r.p[i] = fr.p[i] = fcp[i];
   float* raw = out + kOffFcRaw;
   ScaleArgs sa{};
   for (int i = 0; i < 4; ++i) {
@@ -287,14 +311,10 @@ int launch_fc_pack_bf(const float* const* fcp, float* out, hipStream_t st) {
   }
   sa.inv = raw + kFcRawInv;
   sa.scl = raw + kFcRawScl;
-  hipLaunchKernelGGL(k_wscale, dim3(4), dim3(1024), 0, st, sa);
-  const int64_t n = 3 * (kBfFcBytes / 2) + kFcRawInv;
-  const int threads = 256;
-  hipLaunchKernelGGL(k_fc_pack16, dim3((unsigned)((n + threads - 1) / threads)), dim3(threads), 0, st, r,
-                     reinterpret_cast<uint16_t*>(out + kOffFcBf2), reinterpret_cast<uint16_t*>(out + kOffFcBf1),
-                     reinterpret_cast<uint16_t*>(out + kOffFcH2), raw);
-  hipLaunchKernelGGL(k_fc_pack16_bwd, dim3((unsigned)((kBfFcBytes / 2 + 255) / 256)), dim3(256), 0, st, r,
-                     reinterpret_cast<uint16_t*>(out + kOffFcBwd), raw);
+  const int nb1 = 4 + (int)std::min<int64_t>(64, (kFcPackedFloats + 1023) / 1024);
+  hipLaunchKernelGGL(k_fc_stage1, dim3(nb1), dim3(1024), 0, st, sa, fr, out);
+  const int64_t n2 = kFc16N + kBfFcBytes / 2;
+  hipLaunchKernelGGL(k_fc_stage2, dim3((unsigned)((n2 + 255) / 256)), dim3(256), 0, st, r, out);
   return hip_status(hipGetLastError());
 }
 

@@ -75,4 +75,28 @@ __device__ __forceinline__ void pack_fp32_at(const RawParams& rp, float* __restr
   out[idx] = v;
 }
 
+// fc_c fp32 image element idx (pnr_internal.h "fc_c image"): fc[2l] = fc_c.l.weight (256,32),
+// fc[2l+1] = bias; segments 0..3 CF_l, 4..7 CB_l, 8..11 CT (reversed)
+struct FcRaw {
+  const float* p[PNR_N_FC_PARAMS];
+};
+__device__ __forceinline__ void fc_pack_fp32_at(const FcRaw& fc, float* __restrict__ out, int64_t idx) {
+  if (idx >= kFcPackedFloats) return;
+  const int seg = (int)(idx / kChunkFloats);
+  const int i = (int)(idx % kChunkFloats);
+  const int blk = i / 1024, rem = i % 1024;   // blk = tile t (CF, CB) or k-chunk kc (CT)
+  const int rq = rem / 256, lane = (rem % 256) / 4, r = rq * 4 + rem % 4;
+  const int hh = lane >> 5, i32 = lane & 31;
+  float v;
+  if (seg < 4) {
+    v = fc.p[2 * seg][(32 * blk + i32) * kCDim + perm(r, hh)];
+  } else if (seg < 8) {
+    v = fc.p[2 * (seg - 4) + 1][32 * blk + perm(r, hh)];
+  } else {
+    const int l = 3 - (seg - 8);  // the backward visits l = 3, 2, 1, 0
+    v = fc.p[2 * l][(32 * blk + perm(r, hh)) * kCDim + i32];
+  }
+  out[idx] = v;
+}
+
 }  // namespace pnr

@@ -195,7 +195,7 @@ int launch_fc_pack(const float* const* fc, float* out, hipStream_t st);
 int64_t packed_floats_all();
 int64_t fc_packed_floats_all();
 
-int launch_fc_pack_bf(const float* const* fc, float* out, hipStream_t st);
+int launch_fc_pack_all(const float* const* fc, float* out, hipStream_t st);  // fp32 + 16-bit images, 2 launches
 // prec = PNR_PREC_BF16X3 / PNR_PREC_BF16 / PNR_PREC_F16X3
 // status: PNR_STATUS_* bits ORed in on the device (f16 range check of F16X3), or null
 int launch_mlp_fwd_bf(int prec, const float* packed, const PointSrc& src, int mode, int64_t P, float* raw,

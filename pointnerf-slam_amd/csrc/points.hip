@@ -207,8 +207,45 @@ __global__ void k_scan_add(int32_t* __restrict__ out, int64_t n, const int32_t* 
   else if (i == n) out[n] = offs[nb];
 }
 
+// One-block exclusive scan for n <= kScanSmall: thread t sums its run of consecutive elements, the
+// block scans the run sums, each thread writes its run (one launch where the tiled scan takes three:
+// the gather's group table at the Mapper's 1,000-ray batch has ~4 k entries; larger tables take the tiled scan:
+// one block over 16 k entries took 29 us at config C5)
+constexpr int64_t kScanSmall = 4096;
+__global__ __launch_bounds__(1024) void k_scan_small(const int32_t* __restrict__ in, int32_t* __restrict__ out,
+                                                     int64_t n) {
+  __shared__ int32_t wsum[16];
+  const int per = (int)((n + 1023) / 1024);
+  const int64_t b = (int64_t)threadIdx.x * per;
+  int t = 0;
+  for (int e = 0; e < per; ++e) t += b + e < n ? in[b + e] : 0;
+  int incl = t;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int o = __shfl_up(incl, d);
+    if (lane >= d) incl += o;
+  }
+  if (lane == 63) wsum[w] = incl;
+  __syncthreads();
+  int woff = 0;
+  for (int k = 0; k < w; ++k) woff += wsum[k];
+  int run = woff + incl - t;
+  for (int e = 0; e < per; ++e) {
+    if (b + e < n) {
+      out[b + e] = run;
+      run += in[b + e];
+    }
+  }
+  if (threadIdx.x == 1023) out[n] = woff + incl;
+}
+
 // out[0..n] = exclusive scan of in[0..n), out[n] = total.  scratch: scan_scratch_ints(n) ints.
 static int scan_exclusive(const int32_t* in, int32_t* out, int64_t n, int32_t* scratch, hipStream_t st) {
+  if (n > 0 && n <= kScanSmall) {
+    hipLaunchKernelGGL(k_scan_small, dim3(1), dim3(1024), 0, st, in, out, n);
+    return hip_status(hipGetLastError());
+  }
   const int64_t nb = (n + 1023) / 1024;
   int32_t* sums = scratch;
   hipLaunchKernelGGL(k_scan_tile, dim3((unsigned)nb), dim3(256), 0, st, in, out, n, sums);
@@ -976,7 +1013,8 @@ struct GatherBwdArgs {
   // Feature gradients in exact fixed point (order-independent, hence deterministic): every term
   // w dL/dc becomes an int64 multiple of 2^-s, s from max |dL/dc| over the rows and the guard bits
   // (a sum of <= 2^guard terms never overflows); k_gather_bwd_fin converts once into g_feats
-  long long* facc;       // [M][32] int64 accumulators (zeroed by the launcher)
+  long long* facc;       // [M][32] int64 accumulators: only the rows a work-list row names are used
+  uint32_t* touched;     // [M bits] rows of facc in use: set (and the row zeroed) by k_gather_bwd_gmax
   uint32_t* gmax;        // bits of max |dL/dc| over the work list's rows (NaN / inf propagate)
   unsigned long long* n_flush;  // int64 atomic instructions (256 B each) issued, for the roofline
   int guard;
@@ -1007,6 +1045,17 @@ __global__ __launch_bounds__(256) void k_gather_bwd_gmax(GatherBwdArgs a) {
       const int64_t p = __float_as_int(a.wl.items[rl * a.wl.cap + j0 + t].w);
       const uint32_t b = __float_as_uint(a.g_c[p * 32 + ch]) & 0x7FFFFFFFu;
       m = m > b ? m : b;
+      // the row's neighbours: the first lane to name a feature row zeroes its accumulators (the
+      // accumulating launch runs after this one, so no add can precede the zero fill)
+      const int id = ch < a.k ? a.idx[p * a.k + ch] : -1;
+      if (id >= 0) {
+        const uint32_t bit = 1u << (id & 31);
+        if (!(atomicOr(a.touched + (id >> 5), bit) & bit)) {
+          longlong2* row = reinterpret_cast<longlong2*>(a.facc + (int64_t)id * 32);
+#pragma unroll
+          for (int e = 0; e < 16; ++e) row[e] = make_longlong2(0, 0);
+        }
+      }
     }
   }
 #pragma unroll
@@ -1177,11 +1226,16 @@ __global__ __launch_bounds__(256) void k_gather_bwd(GatherBwdArgs a) {
   }
 }
 
-// g_feats += facc 2^-s (4 values per thread); a non-finite max |dL/dc| makes every element NaN
+// g_feats += facc 2^-s (4 values per thread) on the rows some sample named (the others received no
+// term: left as they are, their accumulators never zeroed); a non-finite max |dL/dc| makes the
+// elements of those rows NaN
 __global__ __launch_bounds__(256) void k_gather_bwd_fin(const long long* __restrict__ facc, float* __restrict__ g,
-                                                       int64_t n, const uint32_t* __restrict__ gmax, int guard) {
+                                                       int64_t n, const uint32_t* __restrict__ gmax, int guard,
+                                                       const uint32_t* __restrict__ touched) {
   const int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
   if (i >= n) return;
+  const int64_t row = i / 32;
+  if (!((touched[row >> 5] >> (row & 31)) & 1u)) return;
   const uint32_t gb = *gmax;
   const int s = fx_shift(gb, guard);
   const bool bad = gb >= 0x7F800000u;
@@ -1199,6 +1253,37 @@ __global__ __launch_bounds__(256) void k_gather_bwd_fin(const long long* __restr
     const int64_t e = i + 4 < n ? i + 4 : n;
     for (int64_t j = i; j < e; ++j) g[j] += bad ? __int_as_float(0x7FC00000) : (float)ldexp((double)facc[j], -s);
   }
+}
+
+// Up to four zero fills in one launch (the counters and accumulators a gather / gather backward
+// starts from): each hipMemsetAsync is a launch of its own, ~5 us apiece in the Mapper's captured
+// iteration at its real batch sizes.  Regions are 4-B aligned; 16-B stores where aligned.
+struct ZeroRegions {
+  char* p[4];
+  int64_t bytes[4];
+  int n;
+};
+__global__ __launch_bounds__(256) void k_zero_regions(ZeroRegions z) {
+  const int64_t tid = (int64_t)blockIdx.x * 256 + threadIdx.x, nth = (int64_t)gridDim.x * 256;
+  for (int r = 0; r < z.n; ++r) {
+    char* p = z.p[r];
+    const int64_t nb = z.bytes[r];
+    const int64_t head = ((16 - ((uintptr_t)p & 15)) & 15) < nb ? ((16 - ((uintptr_t)p & 15)) & 15) : nb;
+    for (int64_t i = tid * 4; i < head; i += nth * 4) *reinterpret_cast<uint32_t*>(p + i) = 0u;
+    const int64_t n16 = (nb - head) / 16;
+    uint4* q = reinterpret_cast<uint4*>(p + head);
+    for (int64_t i = tid; i < n16; i += nth) q[i] = make_uint4(0u, 0u, 0u, 0u);
+    for (int64_t i = head + n16 * 16 + tid * 4; i < nb; i += nth * 4) *reinterpret_cast<uint32_t*>(p + i) = 0u;
+  }
+}
+static int zero_regions(const ZeroRegions& z, hipStream_t st) {
+  int64_t total = 0;
+  for (int r = 0; r < z.n; ++r) total += z.bytes[r];
+  if (total <= 0) return PNR_OK;
+  const int64_t blocks = (total / 16 + 255) / 256;
+  hipLaunchKernelGGL(k_zero_regions, dim3((unsigned)(blocks < 2048 ? (blocks > 0 ? blocks : 1) : 2048)), dim3(256), 0,
+                     st, z);
+  return hip_status(hipGetLastError());
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1272,6 +1357,7 @@ struct GatherBwdView {
   uint32_t* gmax;
   unsigned long long* n_flush;
   long long* facc;
+  uint32_t* touched;
 };
 static GatherBwdView gather_bwd_view(void* ws, int64_t P, int64_t M, bool feats, size_t* bytes = nullptr) {
   GatherBwdView v{};
@@ -1285,6 +1371,8 @@ static GatherBwdView gather_bwd_view(void* ws, int64_t P, int64_t M, bool feats,
   if (feats) {
     v.facc = reinterpret_cast<long long*>(b ? b + off : nullptr);
     off += a256((size_t)(M > 0 ? M : 0) * kCDim * 8);
+    v.touched = reinterpret_cast<uint32_t*>(b ? b + off : nullptr);
+    off += a256((size_t)((M > 0 ? M : 0) + 31) / 32 * 4);
   }
   if (bytes) *bytes = off;
   return v;
@@ -1336,8 +1424,15 @@ int launch_gather(const pnr_points& pts, const PointSrc& src, int mode, int64_t 
   a.grouped = gv.grouped;
   a.gmask = (uint32_t)((1ll << gv.gbits) - 1);
   const int64_t G = 1ll << gv.gbits;
-  if (hipMemsetAsync(a.wl.cnt, 0, kLists * 32 * 4, st) != hipSuccess) return (int)hipGetLastError();
-  if (hipMemsetAsync(a.gcnt, 0, (size_t)G * 4, st) != hipSuccess) return (int)hipGetLastError();
+  {
+    ZeroRegions z{};
+    z.p[0] = reinterpret_cast<char*>(a.wl.cnt);
+    z.bytes[0] = kLists * 32 * 4;
+    z.p[1] = reinterpret_cast<char*>(a.gcnt);
+    z.bytes[1] = G * 4;
+    z.n = 2;
+    if (int rc = zero_regions(z, st)) return rc;
+  }
   TimingScope ts(kTimeGather, P, st);
   gather_probe(mode, dim3((unsigned)((rows + 255) / 256)), st, a);
   int rc = scan_exclusive(a.gcnt, gv.gstart, G, gv.scratch, st);
@@ -1406,6 +1501,7 @@ int launch_gather_bwd(const pnr_points& pts, const PointSrc* src, int mode, cons
   GatherBwdView v = gather_bwd_view(ws, P, pts.n_points, feats);
   a.wl = v.wl;
   a.facc = v.facc;
+  a.touched = v.touched;
   a.gmax = v.gmax;
   a.n_flush = v.n_flush;
   // a sum of at most P terms per element (the ids of a row are distinct): 2^guard > P
@@ -1418,12 +1514,22 @@ int launch_gather_bwd(const pnr_points& pts, const PointSrc* src, int mode, cons
   // backward with 32-row runs over ~600 half-waves)
   a.run = 32;
   while (a.run > 2 && P / a.run < 2 * 5 * 1024 * 8) a.run >>= 1;
-  if (hipMemsetAsync(a.wl.cnt, 0, kLists * 32 * 4, st) != hipSuccess) return (int)hipGetLastError();
-  if (feats) {
-    if (hipMemsetAsync(v.ctl, 0, 256, st) != hipSuccess) return (int)hipGetLastError();
-    if (hipMemsetAsync(v.facc, 0, (size_t)pts.n_points * kCDim * 8, st) != hipSuccess) return (int)hipGetLastError();
+  {
+    ZeroRegions z{};
+    z.p[z.n] = reinterpret_cast<char*>(a.wl.cnt);
+    z.bytes[z.n++] = kLists * 32 * 4;
+    if (feats) {
+      z.p[z.n] = v.ctl;
+      z.bytes[z.n++] = 256;
+      z.p[z.n] = reinterpret_cast<char*>(v.touched);  // (the accumulators: only the touched rows, by gmax)
+      z.bytes[z.n++] = (pts.n_points + 31) / 32 * 4;
+    }
+    if (g_p && !gp_accum) {
+      z.p[z.n] = reinterpret_cast<char*>(g_p);
+      z.bytes[z.n++] = P * 12;
+    }
+    if (int rc = zero_regions(z, st)) return rc;
   }
-  if (g_p && !gp_accum && hipMemsetAsync(g_p, 0, (size_t)P * 12, st) != hipSuccess) return (int)hipGetLastError();
   TimingScope ts(kTimeGatherBwd, P, st);
   hipLaunchKernelGGL(k_gather_bwd_probe, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, st, a);
   const int64_t tasks = kLists * ((a.wl.cap + 255) / 256);
@@ -1434,7 +1540,7 @@ int launch_gather_bwd(const pnr_points& pts, const PointSrc* src, int mode, cons
   if (feats && pts.n_points > 0) {
     const int64_t n = pts.n_points * kCDim;
     hipLaunchKernelGGL(k_gather_bwd_fin, dim3((unsigned)((n / 4 + 255) / 256 + 1)), dim3(256), 0, st, v.facc, pts.g_feats,
-                       n, v.gmax, guard);
+                       n, v.gmax, guard, v.touched);
   }
   return hip_status(hipGetLastError());
 }

@@ -1032,6 +1032,7 @@ struct AdamSegs {
   float* m[kAdamSegs];
   float* v[kAdamSegs];
   float lr[kAdamSegs];
+  uint16_t* h[kAdamSegs];    // ABI 12: float16 copy of the updated segment (the gather's f16 features) or null
   int first[kAdamSegs + 1];  // first block of each segment
   int nseg;
 };
@@ -1051,6 +1052,7 @@ __global__ __launch_bounds__(256) void k_adam_multi(float* __restrict__ p, const
   const int64_t nq = S.n[q], off = S.off[q];
   float* __restrict__ mq = S.m[q];
   float* __restrict__ vq = S.v[q];
+  uint16_t* __restrict__ hq = S.h[q];
   for (int64_t b = i0; b < nq; b += 4 * stride) {
     float gi[4], mi[4], vi[4], pi[4];
 #pragma unroll
@@ -1070,7 +1072,9 @@ __global__ __launch_bounds__(256) void k_adam_multi(float* __restrict__ p, const
         mq[i] = mn;
         vq[i] = vn;
         const float denom = sqrtf(vn) / bc2_sqrt + eps;
-        p[off + i] = pi[u] + (-step_size) * (mn / denom);
+        const float pn = pi[u] + (-step_size) * (mn / denom);
+        p[off + i] = pn;
+        if (hq) hq[i] = __builtin_bit_cast(uint16_t, (_Float16)pn);  // RNE, as torch's float16 copy
       }
     }
   }
@@ -1273,7 +1277,7 @@ int launch_adam_dev(float* p, const float* g, float* m, float* v, int64_t n, flo
 }
 int launch_adam_multi(float* p, const float* g, int nseg, const int64_t* off, const int64_t* n, float* const* m,
                       float* const* v, const float* lr, float beta1, float beta2, float eps, int32_t* step2,
-                      hipStream_t st) {
+                      hipStream_t st, uint16_t* const* half) {
   if (nseg < 1 || nseg > kAdamSegs) return PNR_E_ARG;
   AdamSegs S{};
   int blocks = 0;
@@ -1283,6 +1287,7 @@ int launch_adam_multi(float* p, const float* g, int nseg, const int64_t* off, co
     S.m[q] = m[q];
     S.v[q] = v[q];
     S.lr[q] = lr[q];
+    S.h[q] = half ? half[q] : nullptr;
     S.first[q] = blocks;
     // a block per 1,024 elements (one pass of four loads per thread), at most 1,024 blocks per segment:
     // every block takes one ticket (a ticket per 256 elements -- 870 for the decoder -- queued on one

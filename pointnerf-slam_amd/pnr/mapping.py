@@ -56,8 +56,14 @@ class Adam:
     segment and the step advance in one launch), so a step captured in a graph replays with the right
     bias corrections."""
 
-    def __init__(self, flat: FlatParams, lr: float, betas=(0.9, 0.999), eps=1e-8, on_update=None, segments=None):
+    def __init__(self, flat: FlatParams, lr: float, betas=(0.9, 0.999), eps=1e-8, on_update=None, segments=None,
+                 half=None):
+        """`half` (optional): {segment index: float16 device tensor of the segment's length} -- with the
+        device step counter, the Adam launch also writes float16 of the updated values there (the
+        gather's f16 feature copy, pnr_adam_multi_dev_h) and `wrote_half` is set after the step."""
         self.flat = flat
+        self.half = dict(half or {})
+        self.wrote_half = False
         self.on_update = on_update
         self.lr = lr
         self.segments = segments if segments is not None else [(0, flat.numel, lr)]
@@ -81,17 +87,28 @@ class Adam:
                               (ctypes.c_void_p * k)(*[m.data_ptr() for m, _ in self.mv]),
                               (ctypes.c_void_p * k)(*[v.data_ptr() for _, v in self.mv]),
                               (ctypes.c_float * k)(*[lr for _, _, lr in self.segments]))
+            self._half_arr = None
+            if self.half:
+                self._half_arr = (ctypes.c_void_p * k)(*[self.half[q].data_ptr() if q in self.half else None
+                                                         for q in range(k)])
 
     def step(self):
         self.step_count += 1
         lib = _lib.load()
         f = self.flat
         st = _lib.stream_of(f.data.device)
+        self.wrote_half = False
         if self.step_dev is not None:
             off, n, m, v, lr = self._seg_args
-            _lib.check(lib.pnr_adam_multi_dev(_lib.ptr(f.data), _lib.ptr(f.grad), len(self.segments), off, n, m, v, lr,
-                                              self.b1, self.b2, self.eps, _lib.ptr(self.step_dev), st),
-                       'adam_multi_dev')
+            if self._half_arr is not None:
+                _lib.check(lib.pnr_adam_multi_dev_h(_lib.ptr(f.data), _lib.ptr(f.grad), len(self.segments), off, n, m,
+                                                    v, lr, self.b1, self.b2, self.eps, self._half_arr,
+                                                    _lib.ptr(self.step_dev), st), 'adam_multi_dev_h')
+                self.wrote_half = True
+            else:
+                _lib.check(lib.pnr_adam_multi_dev(_lib.ptr(f.data), _lib.ptr(f.grad), len(self.segments), off, n, m,
+                                                  v, lr, self.b1, self.b2, self.eps, _lib.ptr(self.step_dev), st),
+                           'adam_multi_dev')
         else:
             for (a, n, lr), (m, v) in zip(self.segments, self.mv):
                 _lib.check(lib.pnr_adam_step(_lib.ptr(f.data[a:]), _lib.ptr(f.grad[a:]), _lib.ptr(m),
@@ -138,7 +155,12 @@ class MapStep:
                     segs.append((n_dec + a, b - a, flr))
             else:
                 segs.append((n_dec, points.feats.numel(), flr))
-        self.opt = Adam(self.flat, lr, on_update=self._invalidate, segments=segs)
+        # float16 features (C5): the captured step's Adam launch refreshes the gather's f16 copy itself
+        # (the whole-table conversion was a pass of its own); the sharded update all-gathers after Adam
+        half = None
+        if points is not None and points.feat_dtype == 'float16' and not self.shard and len(segs) == 2:
+            half = {1: points._feats_for_gather()}
+        self.opt = Adam(self.flat, lr, on_update=self._invalidate, segments=segs, half=half)
         self.c = {} if points is None else {'points_' + getattr(decoder, 'name', ''): points}
         self.w_color = w_color_loss
         self.w_reg = w_reg
@@ -178,7 +200,10 @@ class MapStep:
         self.decoder._packed.invalidate()
         if self.points is not None:
             self.decoder._packed_fc.invalidate()
-            self.points.invalidate_feats()  # the f16 feature copy, if any
+            if self.opt.wrote_half:  # Adam wrote the f16 feature copy with the fp32 master
+                self.points.mark_feats_fresh()
+            else:
+                self.points.invalidate_feats()  # the f16 feature copy, if any
 
     def _regulation_chain(self, views, rays_o, rays_d, gt_depth, t_rand):
         from .renderer import TrainPass, map_loss

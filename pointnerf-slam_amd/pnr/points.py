@@ -77,6 +77,11 @@ class NeuralPoints(nn.Module):
         pnr Adam kernel writing through a raw pointer)."""
         self._feats_h_key = None
 
+    def mark_feats_fresh(self):
+        """The f16 copy holds float16(feats) again (written by pnr_adam_multi_dev_h with the master)."""
+        if self._feats_h is not None:
+            self._feats_h_key = (self.feats.data_ptr(), self.feats._version)
+
     def _feats_for_gather(self):
         if self.feat_dtype == 'float32':
             return self.feats

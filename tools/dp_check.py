@@ -20,10 +20,11 @@ Checked on rank 0 after the first step, before Adam can amplify anything:
     MapSteps run on the shards with the same global far clamp (each rank's step is the 1-process
     step of its shard, and the 2-rank sum adds the two shard gradients once);
   * against the 1-process gradient of the whole batch it agrees elementwise to
-    |g_dp - g_1| <= 1e-6 |g_1| + 1e-5 max|g_1|: the two are float32 sums of the same terms in
-    different associations (rtol 1e-6, plus an association floor for elements whose terms cancel; the
-    f16x3 fc_c gradients, whose per-wave split scales follow the batch split, take the neural-point
-    floor 5e-4 max|g| of tests/test_gpu_points.py);
+    |g_dp - g_1| <= 1e-6 |g_1| + floor max|g_1|: the two are float32 sums of the same terms in
+    different associations (rtol 1e-6, plus an association floor for elements whose terms cancel:
+    floor = max(1e-5, 2 x the spread between the 1-process gradient of the batch and of the same
+    batch with its rays in a random order) -- the fc_c gradients (dL/dh)^T c cancel more, ~1e-5 measured; the
+    f16x3 split itself is batch-invariant to ~2e-7, tests/test_gpu_points_forced.py);
 and after all steps: every rank holds bit-identical parameters, a second 1-process run reproduces
 the first bit for bit, and the per-step losses agree.  Launched by torchrun before any GPU call; on
 a 1-GPU box both ranks share cuda:0 over gloo (RCCL needs one GPU per rank), on a node the same
@@ -175,12 +176,13 @@ def main():
         fa, fb, _ = ddp.feature_shard(pts.feats.numel())
         own_f = (n_dec + fa, n_dec + fb)
     if rank == 0:
-        def one_process(lo, hi, steps, clamp_ddp=True):
+        def one_process(lo, hi, steps, clamp_ddp=True, order=None):
             m1 = MapStep(mk_r(), mk_dec(), lr=2e-4, w_color_loss=0.05, points=mk_pts() if mk_pts else None,
                          ddp=FixedClamp(clamp) if clamp_ddp else None)
             ls, gf = [], None
+            sel = slice(lo, hi) if order is None else order
             for i, t in enumerate(t_rands[:steps]):
-                ls.append(float(m1(ro[lo:hi], rd[lo:hi], gt[lo:hi], col[lo:hi], t[lo:hi])))
+                ls.append(float(m1(ro[sel], rd[sel], gt[sel], col[sel], t[sel])))
                 if i == 0:
                     gf = m1.flat.grad.detach().clone()
             return ls, gf, m1.flat.data.detach().cpu().clone()
@@ -191,6 +193,11 @@ def main():
             g_sum += gk
         full, g_1, w1 = one_process(0, n, args.steps, clamp_ddp=False)
         full2, _, w2 = one_process(0, n, args.steps, clamp_ddp=False)
+        # the same batch with its rays in a random order: the same terms summed in another association
+        # (other rays share each 32-point weight-gradient tile and each workgroup's K range), the float32
+        # spread any re-partitioning of the batch (a shard split) is held to
+        perm = torch.randperm(n, generator=torch.Generator().manual_seed(77)).to(ro.device)
+        g_rev = one_process(0, n, 1, clamp_ddp=False, order=perm)[1]
         rerun_identical = full2 == full and torch.equal(w2, w1)
         parts = [slice(0, n_dec)] + ([slice(*own_f)] if shard else [])
         dp_eq_sum = all(torch.equal(g_first[p], g_sum[p]) for p in parts)
@@ -207,10 +214,11 @@ def main():
             cuts.append(slice(*own_f))
         per_part = {nm: float((g_first[c] - g_1[c]).abs().max() / g_1[c].abs().max().clamp_min(1e-30))
                     for nm, c in zip(names, cuts)}
-        # the fc_c weight gradients of the f16x3 split GEMMs take per-wave power-of-two scales of the
-        # point features, which depend on the points a wave sees (the batch split): the repository's
-        # neural-point gradient floor (tests/test_gpu_points.py FLIP_CAP, 5e-4 max|g|) applies there
-        floors = {'decoder': 1e-5, 'fc_c': 1e-5 if pnr._lib.DEFAULT_PRECISION == 'fp32' else 5e-4, 'features': 1e-5}
+        assoc = {nm: float((g_rev[c] - g_1[c]).abs().max() / g_1[c].abs().max().clamp_min(1e-30))
+                 for nm, c in zip(names, cuts)}
+        # floor per part: 1e-5 max|g| (float32 association), or twice the spread the same batch shows
+        # reordered where its sums cancel more (the fc_c gradients (dL/dh)^T c)
+        floors = {nm: max(1e-5, 2.0 * assoc[nm]) for nm in names}
         viol = max(float(((g_first[c] - g_1[c]).abs() / (1e-6 * g_1[c].abs() + floors[nm] * g_1[c].abs().max()
                                                           + 1e-30)).max()) for nm, c in zip(names, cuts))
         loss_rel = [abs(x - y) / abs(y) for x, y in zip(lt.tolist(), full)]
@@ -223,9 +231,10 @@ def main():
                    'max_abs_diff_vs_1proc': float(dg.max()), 'max_abs_grad': float(gref.max()),
                    'frac_elements_not_equal': float((dg > 0).float().mean()),
                    'worst_ratio_to_bound': viol, 'frac_beyond_rtol_1e-6_alone': strict,
-                   'bound': '|g_dp - g_1| <= 1e-6 |g_1| + floor max|g_1| per part (association floor 1e-5; '
-                            'f16x3 fc_c 5e-4, the neural-point floor)',
+                   'bound': '|g_dp - g_1| <= 1e-6 |g_1| + floor max|g_1| per part; floor = max(1e-5, 2 x the '
+                            'spread of the same batch in a random ray order)',
                    'max_abs_diff_over_max_abs_grad_per_part': per_part,
+                   'reordered_batch_spread_per_part': assoc, 'floor_per_part': floors,
                    'checked': 'decoder' + (' + fc_c, and rank 0 owned feature range' if shard else '')},
                'weights_max_abs_diff_after_steps': float(dw.max()),
                'far_clamp': 'device (far_mode 2), all_reduce MAX', 'precision': pnr._lib.DEFAULT_PRECISION,
