@@ -220,10 +220,12 @@ def gather_roofline(dev, voxel=0.001, k=8, reps=5, feat_dtype='float32'):
     # read twice (max |g_c| pass, then the sums) + k x 8 B idx/w (read twice: the max pass marks the
     # rows it names); per touched feature row its int64 accumulators zeroed, read once, and the
     # features' gradient read + written by the conversion (256 + 256 + 256 B); the M-bit touched map
-    # zeroed and read.  Atomics: the 64-bit add instructions the kernel counted as it issued them (256 B
+    # zeroed and read (sparse calls; dense ones -- this bench scene -- zero and convert all M rows).  Atomics: the 64-bit add instructions the kernel counted as it issued them (256 B
     # each: 32 lanes x 8 B; shared neighbours are carried between a ray's rows, so far fewer go out than
     # rows x neighbours)
-    b_hbm = P * 4 + rows * (2 * 128 + 2 * k * 8) + touched * (256 + 256 + 256) + 2 * (M // 8)
+    sparse = P * k < 4 * M  # points.hip launch_gather_bwd: touched rows only, else every row
+    b_hbm = P * 4 + rows * (2 * 128 + (2 if sparse else 1) * k * 8) + \
+        ((touched * (256 + 256 + 256) + 2 * (M // 8)) if sparse else M * (256 + 256 + 256))
     b_atomic = int(n_instr.value) * 256
     t_floor = (b_hbm / (HBM_PEAK_GBS * 1e9) + b_atomic / 1.3e12) * 1e3
     bwd = {'kernel': 'k_gather_bwd_probe + k_gather_bwd_gmax + k_gather_bwd + k_gather_bwd_fin (feature gradients, '

@@ -669,18 +669,24 @@ struct SearchLds {
 #endif
 // HALF: float16 features (pnr_points.feat_half), its own instantiation (a run-time dtype branch in the
 // feature rounds added register pressure that spilled)
-template <int KER, bool HALF>
+// PAR (candidate-parallel, small chunks of ncs <= 8 items): lane l works for item l mod ncs and
+// visits every (64 / ncs)-th staged candidate, keeping a partial top-k; after the segments the
+// partial lists of an item's lanes are merged by a butterfly of bitonic merges.  A segment's serial
+// scan then runs over 1 / (64 / ncs) of its candidates (the Mapper's real batches: chunks of 4 items,
+// each a segment of its own, whose scan over a dense block dominated the search).  Keys are unique
+// (d^2, index) pairs, so the merged list is the oracle's whatever lane visited which candidate.
+template <int KER, bool HALF, bool PAR>
 __global__ __launch_bounds__(64, PNR_SEARCH_WAVES) void k_gather_search(GatherArgs a) {
   PNR_FP_STRICT
   __shared__ SearchLds L;
   const int lane = threadIdx.x, gq = lane >> 3, q = lane & 7;
   const double kInf = __longlong_as_double(0x7FF0000000000000ll);
   const int64_t n_items = a.gstart[(int64_t)a.gmask + 1];
-  const int cs = a.chunk;  // items per chunk (lanes >= cs idle in the scan, still stage and sum)
-  const int64_t nchunk = (n_items + cs - 1) / cs;
+  const int ncs = PAR ? a.chunk : 64;  // items per chunk
+  const int64_t nchunk = (n_items + ncs - 1) / ncs;
   for (int64_t chunk = blockIdx.x; chunk < nchunk; chunk += gridDim.x) {
-    const int64_t it = chunk * cs + lane;
-    const bool has = lane < cs && it < n_items;
+    const int64_t it = chunk * ncs + (PAR ? (lane & (ncs - 1)) : lane);
+    const bool has = (PAR || lane < ncs) && it < n_items;
     float x0 = 0.f, x1 = 0.f, x2 = 0.f;
     int row = -1, bx = 0, by = 0, bz = 0;
     if (has) {
@@ -778,21 +784,54 @@ __global__ __launch_bounds__(64, PNR_SEARCH_WAVES) void k_gather_search(GatherAr
           }
         }
         __syncthreads();
-#if !defined(PNR_SEARCH_SERIAL)
-        if (!coll_any) {
-          // two candidates per trip: both LDS reads in flight before the first test
-          for (int j = 0; j < cnt; j += 2) {
-            const float4 q0 = L.cand[j], q1 = L.cand[j + 1];
-            visit(q0, 0, false);
-            visit(q1, 0, false);
+        if constexpr (PAR) {
+          const int stride = 64 / ncs;
+          if (!coll_any) {
+            for (int j = lane / ncs; j < cnt; j += stride) visit(L.cand[j], 0, false);
+          } else {
+            for (int j = lane / ncs; j < cnt; j += stride) visit(L.cand[j], L.tag[j], true);
           }
-        } else
+        } else {
+#if !defined(PNR_SEARCH_SERIAL)
+          if (!coll_any) {
+            // two candidates per trip: both LDS reads in flight before the first test
+            for (int j = 0; j < cnt; j += 2) {
+              const float4 q0 = L.cand[j], q1 = L.cand[j + 1];
+              visit(q0, 0, false);
+              visit(q1, 0, false);
+            }
+          } else
 #endif
-        {
-          for (int j = 0; j < cnt; ++j) visit(L.cand[j], L.tag[j], true);
+          {
+            for (int j = 0; j < cnt; ++j) visit(L.cand[j], L.tag[j], true);
+          }
         }
         __syncthreads();  // the next batch overwrites the staged list
       }
+    }
+    if constexpr (PAR) {
+      // merge the partial lists of each item's lanes (lanes equal mod ncs): the k smallest of two
+      // ascending lists as min(a_i, b_{k-1-i}) (bitonic), sorted by a bitonic merge network
+      for (int d = ncs; d < 64; d <<= 1) {
+        double r[PNR_MAX_K];
+#pragma unroll
+        for (int t = 0; t < PNR_MAX_K; ++t) {
+          const double pk = __shfl_xor(key[PNR_MAX_K - 1 - t], d);
+          r[t] = fmin(key[t], pk);
+        }
+#pragma unroll
+        for (int h = PNR_MAX_K / 2; h >= 1; h >>= 1)
+#pragma unroll
+          for (int t = 0; t < PNR_MAX_K; ++t)
+            if ((t & h) == 0) {
+              const double lo = fmin(r[t], r[t + h]), hi = fmax(r[t], r[t + h]);
+              r[t] = lo;
+              r[t + h] = hi;
+            }
+#pragma unroll
+        for (int t = 0; t < PNR_MAX_K; ++t) key[t] = r[t];
+      }
+      if (lane >= ncs) row = -1;  // one lane per item carries it on
     }
     // weights of the first k, normalised by their sequential sum (ascending distance)
     float wv_[PNR_MAX_K];
@@ -1047,7 +1086,7 @@ __global__ __launch_bounds__(256) void k_gather_bwd_gmax(GatherBwdArgs a) {
       m = m > b ? m : b;
       // the row's neighbours: the first lane to name a feature row zeroes its accumulators (the
       // accumulating launch runs after this one, so no add can precede the zero fill)
-      const int id = ch < a.k ? a.idx[p * a.k + ch] : -1;
+      const int id = a.touched && ch < a.k ? a.idx[p * a.k + ch] : -1;
       if (id >= 0) {
         const uint32_t bit = 1u << (id & 31);
         if (!(atomicOr(a.touched + (id >> 5), bit) & bit)) {
@@ -1235,7 +1274,7 @@ __global__ __launch_bounds__(256) void k_gather_bwd_fin(const long long* __restr
   const int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
   if (i >= n) return;
   const int64_t row = i / 32;
-  if (!((touched[row >> 5] >> (row & 31)) & 1u)) return;
+  if (touched && !((touched[row >> 5] >> (row & 31)) & 1u)) return;
   const uint32_t gb = *gmax;
   const int s = fx_shift(gb, guard);
   const bool bad = gb >= 0x7F800000u;
@@ -1443,13 +1482,19 @@ int launch_gather(const pnr_points& pts, const PointSrc& src, int mode, int64_t 
   // share a block, so 64-item chunks left ~200 waves each walking up to 64 segments in series
   // (config C3: 209 + 320 us per iteration); smaller chunks spread the segments over the machine's
   // ~5,000 wave slots.  The S-map batches (> 2.6M samples: 80 per block) keep 64.
-  a.chunk = 64;
-  while (a.chunk > 4 && (P + a.chunk - 1) / a.chunk < 5 * 1024 * 8) a.chunk >>= 1;
+  // (64 items from 2.6M samples up: the S-map batches; below, candidate-parallel chunks of 8 or 4)
+  a.chunk = P >= 64 * 5 * 1024 * 8 ? 64 : (P >= 160 * 1024 ? 8 : 4);
   const int64_t tasks = (P + a.chunk - 1) / a.chunk;  // upper bound on the chunks (the kernel reads the real count)
+  const bool par = a.chunk <= 8;  // candidate-parallel scan for small chunks
   auto kern = pts.mode == PNR_GATHER_IDW
-                  ? (a.feat_half ? k_gather_search<PNR_GATHER_IDW, true> : k_gather_search<PNR_GATHER_IDW, false>)
-                  : (a.feat_half ? k_gather_search<PNR_GATHER_TRILINEAR, true>
-                                 : k_gather_search<PNR_GATHER_TRILINEAR, false>);
+                  ? (a.feat_half ? (par ? k_gather_search<PNR_GATHER_IDW, true, true>
+                                        : k_gather_search<PNR_GATHER_IDW, true, false>)
+                                 : (par ? k_gather_search<PNR_GATHER_IDW, false, true>
+                                        : k_gather_search<PNR_GATHER_IDW, false, false>))
+                  : (a.feat_half ? (par ? k_gather_search<PNR_GATHER_TRILINEAR, true, true>
+                                        : k_gather_search<PNR_GATHER_TRILINEAR, true, false>)
+                                 : (par ? k_gather_search<PNR_GATHER_TRILINEAR, false, true>
+                                        : k_gather_search<PNR_GATHER_TRILINEAR, false, false>));
   hipLaunchKernelGGL(kern, dim3(resident_grid(kern, 64, tasks)), dim3(64), 0, st, a);
   return hip_status(hipGetLastError());
 }
@@ -1501,7 +1546,7 @@ int launch_gather_bwd(const pnr_points& pts, const PointSrc* src, int mode, cons
   GatherBwdView v = gather_bwd_view(ws, P, pts.n_points, feats);
   a.wl = v.wl;
   a.facc = v.facc;
-  a.touched = v.touched;
+  a.touched = P * (int64_t)pts.k < 4 * pts.n_points ? v.touched : nullptr;  // sparse: touched rows only
   a.gmax = v.gmax;
   a.n_flush = v.n_flush;
   // a sum of at most P terms per element (the ids of a row are distinct): 2^guard > P
@@ -1521,8 +1566,17 @@ int launch_gather_bwd(const pnr_points& pts, const PointSrc* src, int mode, cons
     if (feats) {
       z.p[z.n] = v.ctl;
       z.bytes[z.n++] = 256;
-      z.p[z.n] = reinterpret_cast<char*>(v.touched);  // (the accumulators: only the touched rows, by gmax)
-      z.bytes[z.n++] = (pts.n_points + 31) / 32 * 4;
+      // Sparse calls (the Mapper's real batches: a few neighbour slots per point of the cloud) zero
+      // and convert only the rows their samples name (the touched map, set by the max pass); dense
+      // ones (S-map: 15M neighbour slots over 182k points, where marking took 1.1 ms of same-word
+      // atomics) zero every accumulator and convert every row
+      if (!a.touched) {
+        z.p[z.n] = reinterpret_cast<char*>(v.facc);
+        z.bytes[z.n++] = pts.n_points * kCDim * 8;
+      } else {
+        z.p[z.n] = reinterpret_cast<char*>(v.touched);
+        z.bytes[z.n++] = (pts.n_points + 31) / 32 * 4;
+      }
     }
     if (g_p && !gp_accum) {
       z.p[z.n] = reinterpret_cast<char*>(g_p);
@@ -1540,7 +1594,7 @@ int launch_gather_bwd(const pnr_points& pts, const PointSrc* src, int mode, cons
   if (feats && pts.n_points > 0) {
     const int64_t n = pts.n_points * kCDim;
     hipLaunchKernelGGL(k_gather_bwd_fin, dim3((unsigned)((n / 4 + 255) / 256 + 1)), dim3(256), 0, st, v.facc, pts.g_feats,
-                       n, v.gmax, guard, v.touched);
+                       n, v.gmax, guard, a.touched);
   }
   return hip_status(hipGetLastError());
 }
