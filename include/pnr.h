@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define PNR_ABI_VERSION 12
+#define PNR_ABI_VERSION 13
 #define PNR_N_PARAMS 11
 #define PNR_MAX_SAMPLES 64      /* N_samples + N_importance per ray */
 #define PNR_C_DIM 32            /* neural-point feature width (decoder.py:122-125 fc_c input) */
@@ -358,6 +358,22 @@ size_t pnr_map_loss_workspace_bytes(void);
 int pnr_map_loss(const float* gt_depth, const double* depth, const float* gt_color, const float* color, int64_t n,
                  float w_color, const float* sigma, int64_t n_sigma, float w_reg, double* loss, double* g_depth,
                  float* g_color, float* g_sigma, void* workspace, void* stream);
+
+/* One Mapper iteration's loss and decoder / fc_c / point-feature gradients in ONE call (ABI 13;
+ * src/Mapper.py:623-655): pnr_map_fwd, pnr_map_loss and pnr_map_bwd on the same inputs.  Up to
+ * 32,768 rays the final compositing, the loss terms and the compositing backward run as ONE fused
+ * wave-per-ray launch (k_fine_loss_w): the gradients are bit for bit those of the three-call form,
+ * the loss differs from pnr_map_loss's only in summation order (fixed: deterministic).  Larger
+ * batches run the three calls' kernels.  No depth / colour / sigma outputs.
+ *   workspace: pnr_map_step_workspace_bytes(prm, n); bwd_ws: pnr_map_bwd_workspace_bytes(prm, n);
+ *   loss_ws: a pnr_map_loss workspace (zero-filled before its first use, left zero-filled);
+ *   grads / prm->grads_overwrite / prm->points as pnr_map_bwd; *loss float64 on the device.
+ * n = 0: *loss = 0 and (grads_overwrite) zero decoder / fc_c gradients. */
+size_t pnr_map_step_workspace_bytes(const pnr_render_params* prm, int64_t n_rays);
+int pnr_map_step(const pnr_render_params* prm, const float* packed, const float* rays_o, const float* rays_d,
+                 const float* gt_depth, const float* gt_color, const float* t_rand, int64_t n, float w_color,
+                 float w_reg, double* loss, float* const* grads, void* workspace, size_t ws_bytes, void* bwd_ws,
+                 size_t bwd_bytes, void* loss_ws, void* stream);
 
 /* ---- diagnostics (not on the reference API) ----------------------------------------------- */
 /* Kernel timing: while enabled, every launch of the timed kernels is bracketed by hipEvents on

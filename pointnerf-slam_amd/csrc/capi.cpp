@@ -61,6 +61,12 @@ int launch_adam_multi(float*, const float*, int, const int64_t*, const int64_t*,
                       const float*, float, float, float, int32_t*, hipStream_t, uint16_t* const* half = nullptr);
 int launch_map_loss(const float*, const double*, const float*, const float*, int64_t, float, const float*, int64_t,
                     float, double*, double*, double*, float*, float*, hipStream_t);
+int64_t fine_loss_max_rays();
+int64_t fine_loss_parts(int64_t n);
+int launch_fine_loss(const pnr_render_params&, const float*, const double*, const double*, const float*, const float*,
+                     const float4*, const float4*, int64_t, const float*, const float*, float, float, const float*,
+                     const float4*, float*, float*, float*, float*, float*, int, float*, int, float*, int, double*,
+                     uint32_t*, double*, hipStream_t);
 
 }  // namespace pnr
 
@@ -850,17 +856,12 @@ size_t pnr_map_workspace_bytes(const pnr_render_params* prm, int64_t n_rays) {
   return b;
 }
 
-int pnr_map_fwd(const pnr_render_params* prm, const float* packed, const float* rays_o, const float* rays_d,
-                const float* gt_depth, const float* t_rand, int64_t n, double* depth, double* var, float* rgb,
-                float* sigma, void* workspace, size_t ws_bytes, void* stream) {
-  if (!valid_map_prm(prm) || !packed || n < 0) return PNR_E_ARG;
-  if (n == 0) return PNR_OK;
-  if (!rays_o || !rays_d || !gt_depth || !t_rand || !depth || !var || !rgb || !sigma || !workspace) return PNR_E_ARG;
-  if (prm->points && !prm->points->fc_packed) return PNR_E_ARG;
-  size_t need = 0;
-  MapWS w = carve_map(prm, n, workspace, &need);
-  if (ws_bytes < need) return PNR_E_WORKSPACE;
-  hipStream_t st = (hipStream_t)stream;
+namespace {
+// The map pass's forward on a carved workspace: launches A and B with the pdf between them, then the
+// final compositing into depth / var / rgb unless `fine` is false (pnr_map_step's fused tail runs it)
+int map_fwd_core(const pnr_render_params* prm, const float* packed, const float* rays_o, const float* rays_d,
+                 const float* gt_depth, const float* t_rand, int64_t n, const MapWS& w, double* depth, double* var,
+                 float* rgb, float* sigma, bool fine, hipStream_t st) {
   const int S = prm->n_samples, I = prm->n_importance;
   int rc = 0;
   if (prm->far_mode == 0) rc = launch_gt_max(gt_depth, n, w.gmax, st);
@@ -899,8 +900,73 @@ int pnr_map_fwd(const pnr_render_params* prm, const float* packed, const float* 
     fa.c = w.c + w.r1 * kCDim;
   }
   rc = mlp_fwd(prm->precision, packed, src2, kPtsX4, n * I, w.raw + w.r1 * 4, &s2, st, pts ? &fa : nullptr, status);
-  if (rc) return rc;
+  if (rc || !fine) return rc;
   return launch_fine(*prm, rays_d, w.z, zi, w.raw + w.pr * 4, w.raw + w.r1 * 4, n, depth, var, rgb, w.ord, st);
+}
+
+// The map pass's backward on carved workspaces: the compositing backward into b.g_out (unless the
+// fused tail already wrote it: `fine_done`), the delta chain / weight gradients and the gather backward
+int map_bwd_core(const pnr_render_params* prm, const float* packed, const float* rays_d, int64_t n, const MapWS& w,
+                 BwdWS& b, const double* g_depth, const float* g_rgb, const float* g_sigma, float* const* grads,
+                 bool fine_done, hipStream_t st) {
+  const int S = prm->n_samples, I = prm->n_importance;
+  const double* zi = w.z + n * S;
+  const float4* x4 = w.save.xP;
+  const pnr_points* pts = prm->points;
+  int rc = 0;
+  if (!fine_done) {
+    // dL/draw of every row: render rows from the compositing backward, regulation rows from dL/dsigma,
+    // zeros on the three segments' padding rows -- one launch
+    rc = launch_fine_bwd(*prm, rays_d, w.z, zi, w.raw + w.pr * 4, w.raw + w.r1 * 4, x4 + w.pr, x4 + w.r1, w.ord, n,
+                         g_depth, nullptr, g_rgb, b.g_out + w.pr * 4, b.g_out + w.r1 * 4, b.g_nrm,
+                         b.g_out + (n * S) * 4, (int)(w.pr - n * S), b.g_out + (w.pr + n * S) * 4,
+                         (int)(w.r1 - w.pr - n * S), st, g_sigma, x4, b.g_out, b.g_out + (w.r1 + n * I) * 4,
+                         (int)(w.ld - w.r1 - n * I));
+    if (rc) return rc;
+  }
+  FeatBwd fb{pts ? pts->fc_packed : nullptr, w.c, pts ? pts->g_fc : nullptr};
+  rc = mlp_backward_core(prm->precision, packed, w.save, w.ld, b, grads, false, st, pts ? &fb : nullptr,
+                         prm->grads_overwrite != 0);
+  if (rc) return rc;
+  if (pts)
+    rc = launch_gather_bwd(*pts, nullptr, kPtsX4, x4, w.ld, w.nidx, w.nw, w.c, b.g_c, nullptr, true, b.gws, b.gws_bytes,
+                           st);
+  return rc;
+}
+
+// pnr_map_step's per-ray scratch after the map workspace: the unfused tail's depth / var / rgb /
+// sigma and upstream gradients, and the fused tail's block partial losses
+struct StepWS {
+  double *depth, *var, *g_depth, *part;
+  float *rgb, *sigma, *g_rgb, *g_sigma;
+};
+StepWS carve_step(const pnr_render_params* prm, int64_t n, Carver& c) {
+  StepWS s{};
+  const int64_t S = prm->n_samples;
+  s.depth = c.take<double>(n);
+  s.var = c.take<double>(n);
+  s.g_depth = c.take<double>(n);
+  s.part = c.take<double>(fine_loss_parts(n) > 0 ? fine_loss_parts(n) : 1);
+  s.rgb = c.take<float>(n * 3);
+  s.sigma = c.take<float>(n * S);
+  s.g_rgb = c.take<float>(n * 3);
+  s.g_sigma = c.take<float>(n * S);
+  return s;
+}
+}  // namespace
+
+int pnr_map_fwd(const pnr_render_params* prm, const float* packed, const float* rays_o, const float* rays_d,
+                const float* gt_depth, const float* t_rand, int64_t n, double* depth, double* var, float* rgb,
+                float* sigma, void* workspace, size_t ws_bytes, void* stream) {
+  if (!valid_map_prm(prm) || !packed || n < 0) return PNR_E_ARG;
+  if (n == 0) return PNR_OK;
+  if (!rays_o || !rays_d || !gt_depth || !t_rand || !depth || !var || !rgb || !sigma || !workspace) return PNR_E_ARG;
+  if (prm->points && !prm->points->fc_packed) return PNR_E_ARG;
+  size_t need = 0;
+  MapWS w = carve_map(prm, n, workspace, &need);
+  if (ws_bytes < need) return PNR_E_WORKSPACE;
+  return map_fwd_core(prm, packed, rays_o, rays_d, gt_depth, t_rand, n, w, depth, var, rgb, sigma, true,
+                      (hipStream_t)stream);
 }
 
 size_t pnr_map_bwd_workspace_bytes(const pnr_render_params* prm, int64_t n_rays) {
@@ -931,26 +997,60 @@ int pnr_map_bwd(const pnr_render_params* prm, const float* packed, const float* 
   const pnr_points* pts = prm->points;
   BwdWS b = carve_bwd(w.ld, n, bwd_ws, &bneed, pts != nullptr, true, n_pts(prm));
   if (ws_bytes < need || bwd_bytes < bneed) return PNR_E_WORKSPACE;
+  return map_bwd_core(prm, packed, rays_d, n, w, b, g_depth, g_rgb, g_sigma, grads, false, (hipStream_t)stream);
+}
+
+size_t pnr_map_step_workspace_bytes(const pnr_render_params* prm, int64_t n_rays) {
+  if (!valid_map_prm(prm) || n_rays < 0) return 0;
+  Carver c(nullptr);
+  carve_map(prm, n_rays, nullptr, &c.off);
+  carve_step(prm, n_rays, c);
+  return c.off;
+}
+
+int pnr_map_step(const pnr_render_params* prm, const float* packed, const float* rays_o, const float* rays_d,
+                 const float* gt_depth, const float* gt_color, const float* t_rand, int64_t n, float w_color,
+                 float w_reg, double* loss, float* const* grads, void* workspace, size_t ws_bytes, void* bwd_ws,
+                 size_t bwd_bytes, void* loss_ws, void* stream) {
+  if (!valid_map_prm(prm) || !packed || n < 0 || !loss || !loss_ws) return PNR_E_ARG;
   hipStream_t st = (hipStream_t)stream;
-  const int S = prm->n_samples, I = prm->n_importance;
-  const double* zi = w.z + n * S;
-  const float4* x4 = w.save.xP;
-  // dL/draw of every row: render rows from the compositing backward, regulation rows from dL/dsigma,
-  // zeros on the three segments' padding rows -- one launch
-  int rc = launch_fine_bwd(*prm, rays_d, w.z, zi, w.raw + w.pr * 4, w.raw + w.r1 * 4, x4 + w.pr, x4 + w.r1, w.ord, n,
-                           g_depth, nullptr, g_rgb, b.g_out + w.pr * 4, b.g_out + w.r1 * 4, b.g_nrm,
-                           b.g_out + (n * S) * 4, (int)(w.pr - n * S), b.g_out + (w.pr + n * S) * 4,
-                           (int)(w.r1 - w.pr - n * S), st, g_sigma, x4, b.g_out, b.g_out + (w.r1 + n * I) * 4,
-                           (int)(w.ld - w.r1 - n * I));
+  if (grads)
+    for (int i = 0; i < PNR_N_PARAMS; ++i)
+      if (!grads[i]) return PNR_E_ARG;
+  if (n == 0) {  // no rays: loss 0 and (store semantics) zero weight gradients
+    if (int rc = hip_status(hipMemsetAsync(loss, 0, sizeof(double), st))) return rc;
+    if (!prm->grads_overwrite) return PNR_OK;
+    return zero_weight_grads(grads, prm->points ? prm->points->g_fc : nullptr, st);
+  }
+  if (!rays_o || !rays_d || !gt_depth || !gt_color || !t_rand || !workspace || !bwd_ws) return PNR_E_ARG;
+  if (prm->points && !prm->points->fc_packed) return PNR_E_ARG;
+  size_t need = 0, bneed = 0;
+  MapWS w = carve_map(prm, n, workspace, &need);
+  Carver c(workspace);
+  c.off = need;
+  StepWS sw = carve_step(prm, n, c);
+  const pnr_points* pts = prm->points;
+  BwdWS b = carve_bwd(w.ld, n, bwd_ws, &bneed, pts != nullptr, true, n_pts(prm));
+  if (ws_bytes < c.off || bwd_bytes < bneed) return PNR_E_WORKSPACE;
+  const bool fuse = n <= fine_loss_max_rays();
+  int rc = map_fwd_core(prm, packed, rays_o, rays_d, gt_depth, t_rand, n, w, sw.depth, sw.var, sw.rgb,
+                        fuse ? nullptr : sw.sigma, !fuse, st);
   if (rc) return rc;
-  FeatBwd fb{pts ? pts->fc_packed : nullptr, w.c, pts ? pts->g_fc : nullptr};
-  rc = mlp_backward_core(prm->precision, packed, w.save, w.ld, b, grads, false, st, pts ? &fb : nullptr,
-                         prm->grads_overwrite != 0);
+  const int64_t S = prm->n_samples, I = prm->n_importance;
+  double* lws = static_cast<double*>(loss_ws);
+  if (fuse) {
+    const float4* x4 = w.save.xP;
+    rc = launch_fine_loss(*prm, rays_d, w.z, w.z + n * S, w.raw + w.pr * 4, w.raw + w.r1 * 4, x4 + w.pr, x4 + w.r1, n,
+                          gt_depth, gt_color, w_color, w_reg, w.raw, x4, b.g_out, b.g_out + w.pr * 4,
+                          b.g_out + w.r1 * 4, b.g_nrm, b.g_out + (n * S) * 4, (int)(w.pr - n * S),
+                          b.g_out + (w.pr + n * S) * 4, (int)(w.r1 - w.pr - n * S), b.g_out + (w.r1 + n * I) * 4,
+                          (int)(w.ld - w.r1 - n * I), sw.part, reinterpret_cast<uint32_t*>(lws + 256), loss, st);
+  } else {
+    rc = launch_map_loss(gt_depth, sw.depth, gt_color, sw.rgb, n, w_color, sw.sigma, n * S, w_reg, lws, loss,
+                         sw.g_depth, sw.g_rgb, sw.g_sigma, st);
+  }
   if (rc) return rc;
-  if (pts)
-    rc = launch_gather_bwd(*pts, nullptr, kPtsX4, x4, w.ld, w.nidx, w.nw, w.c, b.g_c, nullptr, true, b.gws, b.gws_bytes,
-                           st);
-  return rc;
+  return map_bwd_core(prm, packed, rays_d, n, w, b, sw.g_depth, sw.g_rgb, sw.g_sigma, grads, fuse, st);
 }
 
 // ---- neural points ---------------------------------------------------------------------------

@@ -849,6 +849,171 @@ __global__ __launch_bounds__(256) void k_map_loss(const float* __restrict__ gt, 
 }
 
 // ---------------------------------------------------------------------------------------------
+// The tail of a Mapper iteration at wave-per-ray batches (pnr_map_step), fused: k_fine_w's final
+// compositing, k_map_loss's loss terms and gradients (render rays and the ray's regulation samples)
+// and k_fine_bwd_w's compositing backward in ONE launch, a wave per ray and four rays per block.
+// Every value is formed by the same expressions as in those three kernels (the backward reuses the
+// forward's weights and sums instead of recomputing them from the stored order: the same bits), so
+// the dL/draw rows are identical to the three-launch sequence; only the loss's summation order
+// differs (per ray, the four rays of a block, then the blocks in order, added by the block that takes
+// the last ticket).  Two launch boundaries and the compositing recompute leave the critical path.
+struct FineLoss {
+  const float* gt;      // (n) gt depth
+  const float* gtc;     // (n, 3) gt colour
+  float w_color, w_reg;
+  const float4* rawr;   // regulation rows of launch A (sigma = .w)
+  const float4* insr;   // their kPtsX4 rows (inside flags)
+  float4* gor;          // their dL/draw rows
+  float4* pad2;         // importance padding rows
+  int np2;
+  double* part;         // [gridDim.x] block partial losses
+  uint32_t* ticket;     // zero on entry, left zero
+  double* loss;
+};
+template <int SS, int II>
+__global__ __launch_bounds__(256) void k_fine_loss_w(pnr_render_params prm, const float* __restrict__ rd,
+                                                     const double* __restrict__ zc, const double* __restrict__ zi,
+                                                     const float4* __restrict__ rawc, const float4* __restrict__ rawi,
+                                                     const float4* __restrict__ insc, const float4* __restrict__ insi,
+                                                     int64_t n_rays, float4* __restrict__ goc, float4* __restrict__ goi,
+                                                     float* __restrict__ g_nrm, float4* __restrict__ pad0, int np0,
+                                                     float4* __restrict__ pad1, int np1, FineLoss fl) {
+  __shared__ double zn_[4][PNR_MAX_SAMPLES];
+  __shared__ uint8_t os_[4][PNR_MAX_SAMPLES + 4];
+  __shared__ double red[4];
+  __shared__ uint32_t last;
+  const int l = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  {  // the segments' padding rows: dL/draw = 0 (as k_fine_bwd_w)
+    const int64_t gi = (int64_t)blockIdx.x * 256 + threadIdx.x, gs = (int64_t)gridDim.x * 256;
+    for (int64_t i = gi; i < np0; i += gs) pad0[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int64_t i = gi; i < np1; i += gs) pad1[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int64_t i = gi; i < fl.np2; i += gs) fl.pad2[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  // a wave past the batch works on the last ray and stores nothing (the block barriers stay uniform)
+  const bool live = (int64_t)blockIdx.x * 4 + wv < n_rays;
+  const int64_t n = live ? (int64_t)blockIdx.x * 4 + wv : n_rays - 1;
+  double* zn = zn_[wv];
+  uint8_t* os = os_[wv];
+  const int S = SS > 0 ? SS : prm.n_samples, I = II > 0 ? II : prm.n_importance, M = S + I;
+  // ---- k_fine_w: rank sort and compositing
+  const int lq = l < M ? l : M - 1;
+  const double zl = *(lq < S ? zc + n * S + lq : zi + n * I + (lq - S));
+  zn[l] = zl;
+  os[l] = 0;
+  if (l < 4) os[64 + l] = 0;
+  __syncthreads();
+  if (l < M) {
+    int r = 0;
+    for (int m = 0; m < M; ++m) {
+      const double v = zn[m];
+      r += (lt_nan(v, zl) || (eq_nan(v, zl) && m < l)) ? 1 : 0;
+    }
+    os[r] = (uint8_t)l;
+  }
+  __syncthreads();
+  const int s = os[l];
+  const double zq = zn[s];
+  const double znx = l + 1 < M ? zn[os[l + 1]] : 0.0;
+  const float4 c = *(s < S ? rawc + n * S + s : rawi + n * I + (s - S));  // lanes >= M: s = 0, never read
+  const float nrm = ray_norm(rd + n * 3);
+  const float dz = l < M - 1 ? (float)(znx - zq) : 1e10f;
+  const float delta = dz * nrm;
+  const float sr = relu(c.w);
+  const float ex = expf(-sr * delta);
+  const float a = 1.f - ex;
+  const float Tf = (float)excl_cumprod((double)(1.f - a + 1e-10f), M, l);
+  const float w = a * Tf;
+  const float p0 = w * c.x, p1 = w * c.y, p2 = w * c.z;
+  const double pD = (double)w * zq;
+  float r0 = 0.f, r1 = 0.f, r2 = 0.f;
+  double D = 0.0;
+  for (int q = 0; q < M; ++q) {
+    r0 += rlf(p0, q); r1 += rlf(p1, q); r2 += rlf(p2, q);
+    D += rld(pD, q);
+  }
+  // ---- k_map_loss: this ray's terms and the upstream gradients (wave-uniform)
+  const float g = fl.gt[n];
+  const double e = (double)g - D;
+  const bool msk = g > 0.f;
+  double Lr = msk ? fabs(e) : 0.0;
+  const double gd = msk ? -sgn(e) : 0.0;
+  const float col[3] = {r0, r1, r2};
+  float gr[3];
+  float cs = 0.f;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const float ec = fl.gtc[n * 3 + k] - col[k];
+    cs += fabsf(ec);
+    gr[k] = -fl.w_color * sgnf(ec);
+  }
+  Lr += (double)(fl.w_color * cs);
+  {  // the ray's regulation samples: w_reg |sigma| and dL/draw = (0, 0, 0, w_reg sign(sigma) [inside])
+    const int64_t rr = n * S + (l < S ? l : S - 1);
+    const float sg = fl.rawr[rr].w;
+    const float gsg = fl.w_reg * sgnf(sg);
+    if (live && l < S) fl.gor[rr] = make_float4(0.f, 0.f, 0.f, fl.insr[rr].w != 0.f ? gsg : 0.f);
+    const double ls = (double)(fl.w_reg * fabsf(sg));
+    for (int q = 0; q < S; ++q) Lr += rld(ls, q);
+  }
+  // ---- k_fine_bwd_w with g_var = 0, from the forward's values
+  const bool act = l < M;
+  const bool inside = act && (s < S ? insc + n * S + s : insi + n * I + (s - S))->w != 0.f;
+  const double gv = 0.0;
+  const float gr0 = gr[0], gr1 = gr[1], gr2 = gr[2];
+  const double pS = (double)(a * Tf) * (zq - D);
+  double sdev = 0.0;
+  for (int q = 0; q < M; ++q) sdev += rld(pS, q);
+  const double gD = gd - 2.0 * gv * sdev;
+  const double dd = zq - D;
+  const float gw = (gr0 * c.x + gr1 * c.y + gr2 * c.z) + (float)(gD * zq) + (float)(gv * dd * dd);
+  const float pa = gw * a, g1 = 1.f - a + 1e-10f;
+  float R = 0.f, Rl = 0.f;
+  for (int q = M - 1; q >= 0; --q) {
+    Rl = l == q ? R : Rl;
+    R = rlf(pa, q) + rlf(g1, q) * R;
+  }
+  const float ga = Tf * (gw - Rl);
+  float gs = c.w > 0.f ? ga * ex * delta : 0.f;
+  if (!inside) gs = 0.f;
+  const float pg = (ga * ex * sr) * dz;
+  float gn = 0.f;
+  for (int q = M - 1; q >= 0; --q) gn += rlf(pg, q);
+  if (live && act) {
+    const float4 go = make_float4(gr0 * w, gr1 * w, gr2 * w, gs);
+    if (s < S) goc[n * S + s] = go; else goi[n * I + (s - S)] = go;
+  }
+  if (live && g_nrm && l == 0) g_nrm[n] = gn;
+  // ---- the loss: block partial, then the last block adds the partials in order (k_map_loss's hand-off)
+  if (l == 0) red[wv] = live ? Lr : 0.0;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    fl.part[blockIdx.x] = ((red[0] + red[1]) + red[2]) + red[3];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t t = atomicAdd(fl.ticket, 1u);
+    last = t == gridDim.x - 1 ? 1u : 0u;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  __syncthreads();
+  if (!last) return;
+  double v = 0.0;
+  for (int i = (int)threadIdx.x; i < (int)gridDim.x; i += 256) v += fl.part[i];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  __syncthreads();
+  if (l == 0) red[wv] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    fl.loss[0] = (red[0] + red[1]) + (red[2] + red[3]);
+    *fl.ticket = 0u;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // rays: dirs = [(i-cx)/fx, -(j-cy)/fy, -1]; rays_d = sum(dirs * c2w[:3,:3], -1); rays_o = c2w[:3,3]
 __device__ __forceinline__ void make_ray(float i, float j, float fx, float fy, float cx, float cy,
                                          const float* __restrict__ c2w, int ld, float* o, float* d) {
@@ -1190,6 +1355,29 @@ int launch_fine_bwd(const pnr_render_params& prm, const float* rd, const double*
     hipLaunchKernelGGL((k_fine_bwd<0, 0>), dim3(nblk(n, 64)), dim3(64), sh, st, prm, rd, zc, zi, (const float4*)rawc,
                        (const float4*)rawi, insc, insi, ord, n, gd, gv, grgb, (float4*)goc, (float4*)goi, g_nrm,
                        (float4*)pad0, np0, (float4*)pad1, np1, mb);
+  return hip_status(hipGetLastError());
+}
+// the fused compositing + loss + compositing backward (k_fine_loss_w); n <= fine_loss_max_rays()
+int64_t fine_loss_max_rays() { return kWaveRays; }
+int64_t fine_loss_parts(int64_t n) { return (n + 3) / 4; }
+int launch_fine_loss(const pnr_render_params& prm, const float* rd, const double* zc, const double* zi,
+                     const float* rawc, const float* rawi, const float4* insc, const float4* insi, int64_t n,
+                     const float* gt, const float* gtc, float w_color, float w_reg, const float* rawr,
+                     const float4* insr, float* gor, float* goc, float* goi, float* g_nrm, float* pad0, int np0,
+                     float* pad1, int np1, float* pad2, int np2, double* part, uint32_t* ticket, double* loss,
+                     hipStream_t st) {
+  if (n <= 0 || n > kWaveRays) return PNR_E_ARG;
+  const FineLoss fl{gt, gtc, w_color, w_reg, reinterpret_cast<const float4*>(rawr), insr,
+                    reinterpret_cast<float4*>(gor), reinterpret_cast<float4*>(pad2), np2, part, ticket, loss};
+  const unsigned nb = (unsigned)fine_loss_parts(n);
+  if (prm.n_samples == 32 && prm.n_importance == 12)
+    hipLaunchKernelGGL((k_fine_loss_w<32, 12>), dim3(nb), dim3(256), 0, st, prm, rd, zc, zi, (const float4*)rawc,
+                       (const float4*)rawi, insc, insi, n, (float4*)goc, (float4*)goi, g_nrm, (float4*)pad0, np0,
+                       (float4*)pad1, np1, fl);
+  else
+    hipLaunchKernelGGL((k_fine_loss_w<0, 0>), dim3(nb), dim3(256), 0, st, prm, rd, zc, zi, (const float4*)rawc,
+                       (const float4*)rawi, insc, insi, n, (float4*)goc, (float4*)goi, g_nrm, (float4*)pad0, np0,
+                       (float4*)pad1, np1, fl);
   return hip_status(hipGetLastError());
 }
 int launch_ray_grads_f64(const float* rd, const double* za, int sa, const double* zb, int sb, const float* gxa,

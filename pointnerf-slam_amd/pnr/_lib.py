@@ -25,7 +25,7 @@ PRECISIONS = {'fp32': 0, 'bf16x3': 1, 'bf16': 2, 'f16x3': 3}
 # f16x3: fp32-class forward AND backward (every GEMM on 22-bit split operands with fp32
 # accumulation; tests/test_gpu_parity.py runs every case under fp32 and f16x3 at the same tolerances)
 DEFAULT_PRECISION = os.environ.get('PNR_PRECISION', 'f16x3')
-ABI_VERSION = 12
+ABI_VERSION = 13
 STATUS_F16_RANGE = 1  # include/pnr.h PNR_STATUS_F16_RANGE
 
 
@@ -102,6 +102,10 @@ _SIGS = {
     'pnr_map_bwd_workspace_bytes': (c_size_t, [ctypes.POINTER(RenderParams), c_int64]),
     'pnr_map_bwd': (ctypes.c_int, [ctypes.POINTER(RenderParams), c_void_p, c_void_p, c_int64, c_void_p, c_void_p,
                                    c_void_p, c_void_p, c_void_p, c_size_t, c_void_p, c_size_t, c_void_p]),
+    'pnr_map_step_workspace_bytes': (c_size_t, [ctypes.POINTER(RenderParams), c_int64]),
+    'pnr_map_step': (ctypes.c_int, [ctypes.POINTER(RenderParams), c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                    c_void_p, c_int64, c_float, c_float, c_void_p, c_void_p, c_void_p, c_size_t,
+                                    c_void_p, c_size_t, c_void_p, c_void_p]),
     'pnr_get_rays': (ctypes.c_int, [c_int32, c_int32, c_float, c_float, c_float, c_float, c_void_p, c_void_p,
                                     c_void_p, c_void_p]),
     'pnr_rays_from_uv': (ctypes.c_int, [c_void_p, c_void_p, c_int64, c_float, c_float, c_float, c_float, c_void_p,

@@ -131,6 +131,8 @@ class MapStep:
     fixed order).  No path goes through autograd (MapStep.loss is the autograd drop-in form)."""
 
     OVERLAP_MAX_RAYS = 32768
+    # the fused path as one pnr_map_step call (ABI 13) rather than pnr_map_fwd + pnr_map_loss + pnr_map_bwd
+    one_call = True
 
     def __init__(self, renderer, decoder, lr=2e-4, w_color_loss=0.05, w_reg=0.0005, ddp=None, points=None,
                  feat_lr=None, overlap='auto', fused=True):
@@ -244,6 +246,12 @@ class MapStep:
         if self.fused:  # render + regulation as ONE decoder pass (pnr_map_fwd / pnr_map_bwd)
             from .renderer import MapPass
             mp = MapPass(r, self.c, self.decoder)
+            views = self._views['main']
+            if self.one_call:  # pnr_map_step: forward, loss and backward in one C call, fused tail
+                loss = mp.step(rays_o, rays_d, gt_depth, gt_color, t_rand, self.w_color, self.w_reg,
+                               self._loss_ws('main'), views[0], g_fc=views[1], g_feats=views[2],
+                               far_clamp=far_clamp, overwrite=True)
+                return self._finish(loss)
             d, _, c, sigma = mp.forward(rays_o, rays_d, gt_depth, t_rand, far_clamp=far_clamp)
             loss, g_d, g_c, g_s = map_loss(gt_depth, d, gt_color, c, self.w_color, sigma=sigma, w_reg=self.w_reg,
                                            ws=self._loss_ws('main'))

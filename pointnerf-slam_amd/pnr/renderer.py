@@ -366,6 +366,40 @@ class MapPass:
                                    bws.numel(), _lib.stream_of(dev)), 'map_bwd')
         self.ws = self.packed = None
 
+    def step(self, rays_o, rays_d, gt_depth, gt_color, t_rand, w_color, w_reg, loss_ws, grads, g_fc=None,
+             g_feats=None, far_clamp=None, overwrite=False):
+        """forward + map_loss + backward in ONE C call (pnr_map_step, ABI 13): at batches up to 32,768 rays
+        the compositing, the loss and the compositing backward are one fused launch.  Same gradients as
+        the three-call form bit for bit; returns the float64 loss (0-dim, on the device)."""
+        lib = _lib.load()
+        r = self.r
+        dev = rays_o.device
+        n = rays_o.shape[0]
+        prm = r.params()
+        prm.status = r.status_word(dev).data_ptr()
+        prm.save_for_backward = 1
+        prm.need_ray_grads = 0
+        prm.grads_overwrite = 1 if overwrite else 0
+        packed = self.packer.image(self.feat.params)
+        self.feat.attach(prm, g_feats, g_fc)
+        if isinstance(far_clamp, torch.Tensor):
+            far_clamp = far_clamp.reshape(-1)[:1].float().contiguous()
+            prm.far_mode = 2
+            prm.far_clamp_dev = far_clamp.data_ptr()
+        elif far_clamp is not None:
+            prm.far_mode = 1
+            prm.far_clamp = float(far_clamp)
+        ws = torch.empty(lib.pnr_map_step_workspace_bytes(ctypes_ref(prm), n), dtype=torch.uint8, device=dev)
+        bws = torch.empty(lib.pnr_map_bwd_workspace_bytes(ctypes_ref(prm), n), dtype=torch.uint8, device=dev)
+        loss = torch.empty((), dtype=torch.float64, device=dev)
+        arr = _lib.PtrArray(*[g.data_ptr() for g in grads])
+        _lib.check(lib.pnr_map_step(ctypes_ref(prm), _lib.ptr(packed), _lib.ptr(rays_o), _lib.ptr(rays_d),
+                                    _lib.ptr(gt_depth), _lib.ptr(gt_color), _lib.ptr(t_rand), n, float(w_color),
+                                    float(w_reg), _lib.ptr(loss), arr, _lib.ptr(ws), ws.numel(), _lib.ptr(bws),
+                                    bws.numel(), _lib.ptr(loss_ws), _lib.stream_of(dev)), 'map_step')
+        prm.points = None
+        return loss
+
 
 def map_loss_workspace(device):
     """A zero-filled pnr_map_loss workspace (each call leaves it zero-filled: reuse it for the calls of

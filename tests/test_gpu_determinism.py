@@ -284,3 +284,47 @@ def test_map_step_multi_chunk_store(pnr_mod, dev, precision):
     diff = (g1 - g2).abs()
     floor = 1e-6 if precision == 'fp32' else 1e-5
     assert bool((diff <= 1e-6 * g2.abs() + floor * g2.abs().max()).all()), float(diff.max())
+
+
+@pytest.mark.parametrize('points,n', [(True, 512), (False, 512), (False, 33000)])
+def test_map_step_one_call_matches_three_calls(pnr_mod, dev, points, n, precision):
+    """pnr_map_step (ABI 13: forward, loss and backward in one C call; up to 32,768 rays the final
+    compositing, the loss and the compositing backward are ONE fused launch, k_fine_loss_w) against
+    pnr_map_fwd + pnr_map_loss + pnr_map_bwd: every gradient bit for bit (the fused kernel forms each
+    value with the same expressions), the loss to its summation order.  33,000 rays: the unfused tail."""
+    from pnr.mapping import MapStep
+    make, batches = _setup(pnr_mod, dev, points=points)
+    ro, rd, gt, col, t_rand = batches[0]
+    if n > ro.shape[0]:
+        reps = -(-n // ro.shape[0])
+        gen = torch.Generator().manual_seed(12)
+        ro, rd, gt = [t.repeat(reps, *([1] * (t.dim() - 1)))[:n].contiguous() for t in (ro, rd, gt)]
+        col = torch.rand((n, 3), generator=gen).to(dev)
+        t_rand = torch.rand((n, 32), generator=gen).to(dev)
+    out = []
+    for one in (True, False):
+        r, dec, pts = make()
+        ms = MapStep(r, dec, points=pts, feat_lr=1e-2, lr=0.0)
+        ms.one_call = one
+        ms.flat.grad.copy_(torch.randn_like(ms.flat.grad))
+        if points:
+            ms.flat.grad[ms.n_dec:].zero_()
+        loss = float(ms(ro, rd, gt, col, t_rand))
+        torch.cuda.synchronize()
+        out.append((loss, ms.flat.grad.clone()))
+    assert abs(out[0][0] - out[1][0]) <= 1e-12 * abs(out[1][0]), (out[0][0], out[1][0])
+    assert torch.equal(out[0][1], out[1][1])
+
+
+def test_map_step_empty_batch(pnr_mod, dev, precision):
+    """pnr_map_step with n = 0: loss 0 and (grads_overwrite) zero decoder gradients."""
+    from pnr.mapping import MapStep
+    make, _ = _setup(pnr_mod, dev, points=False)
+    r, dec, _ = make()
+    ms = MapStep(r, dec, lr=0.0)
+    ms.flat.grad.fill_(7.0)
+    e3 = torch.empty((0, 3), device=dev)
+    loss = ms(e3, e3, torch.empty(0, device=dev), e3, torch.empty((0, 32), device=dev))
+    torch.cuda.synchronize()
+    assert float(loss) == 0.0
+    assert bool((ms.flat.grad == 0).all())

@@ -58,6 +58,12 @@ for step in "$@"; do
     gather)
       run 300 ${O}_gather.log python3 tools/gather_bench.py
       tail -8 ${O}_gather.log ;;
+    timeline)
+      run 200 gpurun_out/prof_${TAG}_tl.log rocprofv3 --kernel-trace --output-format csv \
+        -d gpurun_out/prof_${TAG}_tl -o t -- python3 bench.py --workload room0 --steps 30 --warmup 3 --no-extras \
+        --no-cpu-baseline
+      python3 tools/timeline.py gpurun_out/prof_${TAG}_tl --period-kernel k_adam_multi > ${O}_room0_timeline.txt
+      cat ${O}_room0_timeline.txt ;;
     aux)
       run 200 ${O}_track.json python3 tools/track_bench.py
       run 200 ${O}_render.json python3 tools/render_bench.py
