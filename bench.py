@@ -354,7 +354,7 @@ def timed(step, steps, warmup, ddp, lib):
     ddp.barrier()
     torch.cuda.synchronize()
     lib.pnr_timing_enable(1)
-    for kind in range(6):
+    for kind in range(7):
         timing_read(kind)
     t0 = time.perf_counter()
     for _ in range(steps):
@@ -364,7 +364,7 @@ def timed(step, steps, warmup, ddp, lib):
     el = time.perf_counter() - t0
     lib.pnr_timing_enable(0)
     kt = {'mlp_fwd': timing_read(0), 'mlp_bwd': timing_read(1), 'wgrad': timing_read(3), 'gather': timing_read(4),
-          'gather_bwd': timing_read(5)}
+          'gather_bwd': timing_read(5), 'wgrad_group': timing_read(6)}
     kt = {k: v for k, v in kt.items() if v[0] > 0}
     if ddp.world > 1:
         t = torch.tensor([el], device='cuda', dtype=torch.float64)
@@ -374,17 +374,23 @@ def timed(step, steps, warmup, ddp, lib):
 
 
 def kernel_roofline(kt, prec, el_s, traffic_units=True):
-    """Roofline of the dominant hand-written MLP kernel (fused forward or delta chain), per launch:
-    algorithmic fp32-equivalent FLOP per point x points per launch / mean launch time."""
+    """Roofline of the dominant hand-written kernel of the step -- the one with the most device time
+    among the fused forward, the delta chain and the grouped weight-gradient launch -- per launch:
+    algorithmic fp32-equivalent FLOP per launch / mean launch time.  The MLP kernels count FLOP per
+    point x points; the grouped launch counts its GEMMs' multiply-adds (pnr_timing_read kind 6: units
+    of 65,536 MACs = 131,072 FLOP)."""
     best = None
     for name, (launches, ms, units) in kt.items():
-        if name not in ('mlp_fwd', 'mlp_bwd'):
+        if name not in ('mlp_fwd', 'mlp_bwd', 'wgrad_group'):
             continue
-        fl = FLOP_PER_POINT_FWD if name == 'mlp_fwd' else FLOP_PER_POINT_BWD
-        # the delta chain is fp32 in the fp32 mode and the f16x3 split in every other mode
-        kprec = prec if name == 'mlp_fwd' else ('fp32' if prec == 'fp32' else 'f16x3')
-        kname = ('k_mlp_fwd16' if prec != 'fp32' else 'k_mlp_fwd') if name == 'mlp_fwd' else \
-            ('k_mlp_bwd16' if prec != 'fp32' else 'k_mlp_bwd')
+        if name == 'wgrad_group':  # f16x3 GEMMs in every split precision
+            fl, kprec, kname = 131072, 'f16x3', 'k_wgrad16_group'
+        else:
+            fl = FLOP_PER_POINT_FWD if name == 'mlp_fwd' else FLOP_PER_POINT_BWD
+            # the delta chain is fp32 in the fp32 mode and the f16x3 split in every other mode
+            kprec = prec if name == 'mlp_fwd' else ('fp32' if prec == 'fp32' else 'f16x3')
+            kname = ('k_mlp_fwd16' if prec != 'fp32' else 'k_mlp_fwd') if name == 'mlp_fwd' else \
+                ('k_mlp_bwd16' if prec != 'fp32' else 'k_mlp_bwd')
         cand = {'kernel': kname, 'launches': launches, 'prec': kprec, 'peak': ALGO_PEAK_TF[kprec],
                 'avg_ms': ms / launches, 'share_of_step': ms / (el_s * 1e3), 'units': units / launches,
                 'achieved': fl * units / launches / (ms / launches * 1e-3) / 1e12, '_ms': ms}
@@ -394,18 +400,20 @@ def kernel_roofline(kt, prec, el_s, traffic_units=True):
         return None
     tkey = {'k_mlp_fwd': 'k_mlp_fwd_train', 'k_mlp_fwd16': 'k_mlp_fwd16_train', 'k_mlp_bwd': 'k_mlp_bwd',
             'k_mlp_bwd16': 'k_mlp_bwd16'}
-    traffic = pmc_traffic(tkey[best['kernel']], best['units']) if traffic_units else None
+    traffic = pmc_traffic(tkey[best['kernel']], best['units']) if traffic_units and best['kernel'] in tkey else None
     return {'bound': 'mfma', 'achieved': round(best['achieved'], 2), 'peak': round(best['peak'], 1),
             'unit': 'TFLOP/s', 'frac': round(best['achieved'] / best['peak'], 4), 'traffic': traffic,
             'kernel': best['kernel'], 'avg_launch_ms': round(best['avg_ms'], 3), 'launches': best['launches'],
             'kernel_share_of_step': round(best['share_of_step'], 3),
-            'flop_basis': 'algorithmic fp32-equivalent FLOP (443,438 fwd / 442,880 bwd per point); peak = '
+            'flop_basis': ('algorithmic fp32-equivalent FLOP (2 x the multiply-adds of the launch\'s weight-gradient '
+                           'GEMMs); peak = ' if best['kernel'] == 'k_wgrad16_group' else
+                           'algorithmic fp32-equivalent FLOP (443,438 fwd / 442,880 bwd per point); peak = ')
                           + ('fp32 MFMA 157.3 TF' if best['prec'] == 'fp32' else
                              'f16/bf16 MFMA 2.5 PF dense / 3 products per fp32 product'
                              if best['prec'] != 'bf16' else 'bf16 MFMA 2.5 PF dense')}
 
 
-def kernel_table(kt, prec, el_s, steps):
+def kernel_table(kt, prec, el_s, steps, fc=False):
     """Every timed MLP kernel family of the step on its MFMA roofline (algorithmic fp32-equivalent
     FLOP / measured time; the split modes against 833 TF, fp32 against 157.3 TF), with the MFMA-busy
     fraction of the newest committed rocprofv3 PMC pass (profiles/r*_mfma_busy_map.json)."""
@@ -417,14 +425,20 @@ def kernel_table(kt, prec, el_s, steps):
             busy[k] = v.get('mfma_busy_frac')
     peak = ALGO_PEAK_TF['fp32' if prec == 'fp32' else 'f16x3']
     out = {}
+    kt = dict(kt)
+    if 'wgrad_group' in kt or 'wgrad' in kt:  # every weight-gradient launch: the group + dWo / dB (or fp32 GEMMs)
+        g = kt.get('wgrad_group', (0, 0.0, 0))
+        w = kt.get('wgrad', (0, 0.0, 0))
+        kt['wgrad_all'] = (g[0] + w[0], g[1] + w[1], 0)
     for name, fl, kname in (('mlp_fwd', FLOP_PER_POINT_FWD, 'k_mlp_fwd16 (training, saves)'),
                             ('mlp_bwd', FLOP_PER_POINT_BWD, 'k_mlp_bwd16 (delta chain)'),
-                            ('wgrad', 443430, 'k_wgrad16 + k_wgrad_skinny (all weight gradients)')):
+                            ('wgrad_all', 443430 + (65536 if fc else 0),
+                             'k_wgrad16_group + k_wgrad_skinny (all weight gradients)')):
         if name not in kt:
             continue
         launches, ms, units = kt[name]
-        # wgrad units count each layer's launch over its K points: 6 launches per chunk
-        pts = units / 6 if name == 'wgrad' else units
+        # the weight gradients over the delta chain's points (fc: + the four 256 x 32 fc_c GEMMs)
+        pts = kt['mlp_bwd'][2] if name == 'wgrad_all' and 'mlp_bwd' in kt else units
         tf = fl * pts / (ms * 1e-3) / 1e12
         out[kname] = {'achieved_tf': round(tf, 1), 'peak_tf': round(peak, 1), 'frac': round(tf / peak, 4),
                       'ms_per_step': round(ms / steps, 3),
@@ -668,6 +682,7 @@ def map_points_extra(pnr, plib, slam, params, bound, pose, dev, ddp, lib, n=W * 
                        'feature + decoder Adam', 'rays': n, 'points': int(xyz.shape[0]),
            'value': round(n * steps / el, 1), 'unit': 'rays/s', 'ms_per_step': round(el / steps * 1e3, 3),
            'steps': steps, 'roofline': kernel_roofline(kt, prec, el, traffic_units=False),
+           'kernel_rooflines': kernel_table(kt, prec, el, steps, fc=True),
            'kernels': {k: {'launches': v[0], 'ms': round(v[1], 3), 'units': v[2]} for k, v in kt.items()}}
     if 'gather_bwd' in kt:
         launches, ms, units = kt['gather_bwd']
@@ -902,7 +917,8 @@ def main():
                        'graph': bool(args.graph and args.workload == 'map'),
                        **({'point_features': args.feat_dtype} if args.workload == 'map-points' else {})},
             'roofline': roofline, 'cpu_baseline': cpu,
-            'kernel_rooflines': kernel_table(kt, prec, el, args.steps) if args.workload != 'fwd' else None,
+            'kernel_rooflines': kernel_table(kt, prec, el, args.steps, fc=args.workload == 'map-points')
+            if args.workload != 'fwd' else None,
             'kernels': {k: {'launches': v[0], 'ms': round(v[1], 3), 'units': v[2]} for k, v in kt.items()},
         }
         if dist_info:

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define PNR_ABI_VERSION 13
+#define PNR_ABI_VERSION 14
 #define PNR_N_PARAMS 11
 #define PNR_MAX_SAMPLES 64      /* N_samples + N_importance per ray */
 #define PNR_C_DIM 32            /* neural-point feature width (decoder.py:122-125 fc_c input) */
@@ -163,6 +163,12 @@ size_t pnr_mlp_packed_floats(void);
 /* Builds the packed image from the 11 reference tensors (params: host array of device ptrs).
  * Must be re-run after every optimizer step (the image is a pure function of the weights). */
 int pnr_mlp_pack(const float* const* params, float* packed, void* stream);
+/* ABI 14: pnr_mlp_pack with flags.  PNR_PACK_F16X3_ONLY: only the images the PNR_PREC_F16X3 kernels
+ * read (the weight scales, the forward and delta-chain images and the raw table; the fp32 and bf16
+ * images are left as they were) -- a Mapper iteration's repack after its Adam step, on the critical
+ * path.  Those images are bit for bit those of pnr_mlp_pack.  flags 0 = pnr_mlp_pack. */
+#define PNR_PACK_F16X3_ONLY 2
+int pnr_mlp_pack2(const float* const* params, float* packed, int32_t flags, void* stream);
 
 /* Renderer.eval_points (src/utils/Renderer.py:23-61): raw[P,4] = MLP(p) with raw[:,3] := 100
  * where p is not strictly inside `bound6`.  p float64 (P,3).  `precision`: PNR_PREC_*. */
@@ -233,6 +239,8 @@ int pnr_point_gather_bwd_atomics(const pnr_points* pts, const void* ws, int64_t 
  * fc_c.0.weight, fc_c.0.bias, ..., fc_c.3.bias (contiguous float32). */
 size_t pnr_fc_packed_floats(void);
 int pnr_fc_pack(const float* const* fc_params, float* fc_packed, void* stream);
+/* ABI 14: pnr_fc_pack with the pnr_mlp_pack2 flags. */
+int pnr_fc_pack2(const float* const* fc_params, float* fc_packed, int32_t flags, void* stream);
 /* MLP.forward with per-point features c (P,32): eval (bound6 may be NULL) and training
  * variants.  pnr_mlp_bwd_c also writes g_c (P,32) and accumulates the 8 fc_c grads. */
 int pnr_eval_points_c(const float* packed, const float* fc_packed, const double* p, const float* c, int64_t P,
@@ -386,6 +394,9 @@ int pnr_map_step(const pnr_render_params* prm, const float* packed, const float*
  *   4 = neural-point gather (pnr_point_gather and the render's gathers: probe, group scan /
  *       scatter and search as one bracket), units = samples
  *   5 = neural-point gather backward (k_gather_bwd_probe + k_gather_bwd), units = samples
+ *   6 = the grouped split weight-gradient launch (k_wgrad16_group: every f16x3 GEMM of a backward
+ *       chunk but dWo / dB), units = multiply-adds / 65,536 (one 256 x 256 layer over one point = 1)
+ *       -- kind 3 then holds the dWo / dB launches and the fp32-mode GEMMs
  * the launch count, the summed device milliseconds and the summed units, then clears that
  * kernel's record.  Process-global, mutex-protected; off by default. */
 int pnr_timing_enable(int on);

@@ -324,15 +324,12 @@ int mlp_backward_core(int prec, const float* packed, const SaveArgs& sv, int64_t
     };
     const bool want_fc = fb && fb->g_fc;
     int rc = 0;
-    // output layer (split precisions): dWo (4x256) += g_out^T h4 ; dbo += colsum(g_out).  It needs only
-    // g_out and the forward's h4, so it streams its 1 KB/point BEFORE the delta chain, not behind the
-    // chain's 3 KB/point of stores (measured at the 1,000-ray Mapper batch: 32 us after the chain)
-    if (split && grads) {
-      rc = launch_wgrad_out16(b.g_out + p0 * 4, sv.hP + p0 * kHidden + 3 * hstride, C, grads[9], grads[10], pp, pb,
-                              st, &jobs[nj]);
-      if (rc) return rc;
-      took();
-    }
+    // The skinny fp32 GEMMs of the split precisions -- dWo (4x256) += g_out^T h4, dbo += colsum(g_out)
+    // and dB (3x93) += x^T g_arg -- are jobs of the grouped weight-gradient launch: its GEMMs are sized to
+    // leave them 1/8 of the CUs when they fill the chip once (the Mapper's 1,000-ray batch), so the two
+    // bandwidth-bound streams run beside the GEMMs instead of as launches of their own (dWo ahead of the
+    // delta chain, dB behind the GEMMs: 30 us of the iteration's critical path).
+    const bool skinny_in_group = split && grads;
     // the delta chain: exact fp32 MFMA for PNR_PREC_FP32, f16x3 split MFMA otherwise
     rc = prec == PNR_PREC_FP32 ? launch_mlp_bwd(packed, a, C, st) : launch_mlp_bwd_bf(packed, a, C, st);
     if (rc) return rc;
@@ -343,8 +340,8 @@ int mlp_backward_core(int prec, const float* packed, const SaveArgs& sv, int64_t
       // is not stored by k_mlp_bwd16 (rank 4: rebuilt from g_out and the h4 masks inside the GEMM).
       // These GEMMs (and the fc_c ones below) are independent: prepared here, launched as one group.
       WgradSyn syn{reinterpret_cast<const float4*>(b.g_out + p0 * 4), sv.masks + 3 * (sv.ld / 32) * 64, p0 / 32,
-                   packed + packed_raw_wo_offset(), sv.xP + p0, packed + kOffFB, pp, pb, nullptr,
-                   (grads ? 4 : 0) + (want_fc ? 4 : 0)};
+                   packed + packed_raw_wo_offset(), sv.xP + p0, packed + packed_raw_fb_offset(), pp, pb, nullptr,
+                   (grads ? 4 : 0) + (want_fc ? 4 : 0), skinny_in_group ? device_cu_count() / 8 : 0};
       // with the feature branch k_mlp_bwd16 stores dL/dh_l only: delta_l = dL/dh_l masked in the GEMM
       const bool fmask = fb != nullptr;
       const int64_t mstride = (sv.ld / 32) * 64;
@@ -377,12 +374,22 @@ int mlp_backward_core(int prec, const float* packed, const SaveArgs& sv, int64_t
         for (int l = 0; l < 4; ++l)
           prep(l == 3 ? kWgradFcOut : kWgradFc, b.gH + l * dstride, fb->c + p0 * kCDim, fb->g_fc[2 * l], kCDim,
                fb->g_fc[2 * l + 1], nullptr);
-      if (rc == 0) rc = launch_wgrad16_group(gjobs, ng, st);
-      // Fourier: dB (3x93) += x^T g_arg
-      if (rc == 0 && grads) {
-        rc = launch_wgrad_fourier16(sv.xP + p0, b.gargP, C, grads[0], pp, st, &jobs[nj]);
-        if (rc == 0) took();
+      // the skinny jobs last in the grid: their workgroups take the CUs the GEMMs leave
+      if (rc == 0 && skinny_in_group) {
+        rc = wgrad_skinny_prepare(1, b.g_out + p0 * 4, hp + 3 * hstride, C, grads[9], grads[10], pp, pb, &gjobs[ng],
+                                  &jobs[nj]);
+        if (rc == 0) {
+          ++ng;
+          took();
+          rc = wgrad_skinny_prepare(0, reinterpret_cast<const float*>(sv.xP + p0), b.gargP, C, grads[0], nullptr,
+                                    pp, pb, &gjobs[ng], &jobs[nj]);
+        }
+        if (rc == 0) {
+          ++ng;
+          took();
+        }
       }
+      if (rc == 0) rc = launch_wgrad16_group(gjobs, ng, st);
     } else if (grads) {
       const float* hp = sv.hP + p0 * kHidden;
       rc = launch_wgrad(kWgradOut, b.g_out + p0 * 4, 4, hp + 3 * hstride, kHidden, C, grads[9], kHidden, grads[10],
@@ -473,6 +480,13 @@ int pnr_mlp_pack(const float* const* params, float* packed, void* stream) {
   RawParams rp;
   for (int i = 0; i < PNR_N_PARAMS; ++i) rp.p[i] = params[i];
   return launch_pack_all(rp, packed, (hipStream_t)stream);
+}
+
+int pnr_mlp_pack2(const float* const* params, float* packed, int32_t flags, void* stream) {
+  if (!check_params(params) || !packed || (flags & ~PNR_PACK_F16X3_ONLY)) return PNR_E_ARG;
+  RawParams rp;
+  for (int i = 0; i < PNR_N_PARAMS; ++i) rp.p[i] = params[i];
+  return launch_pack_all(rp, packed, (hipStream_t)stream, flags);
 }
 
 int pnr_eval_points(const float* packed, const double* p, int64_t P, const double* bound6, float* raw_out,
@@ -1107,6 +1121,13 @@ int pnr_fc_pack(const float* const* fc_params, float* fc_packed, void* stream) {
   for (int i = 0; i < PNR_N_FC_PARAMS; ++i)
     if (!fc_params[i]) return PNR_E_ARG;
   return launch_fc_pack_all(fc_params, fc_packed, (hipStream_t)stream);
+}
+
+int pnr_fc_pack2(const float* const* fc_params, float* fc_packed, int32_t flags, void* stream) {
+  if (!fc_params || !fc_packed || (flags & ~PNR_PACK_F16X3_ONLY)) return PNR_E_ARG;
+  for (int i = 0; i < PNR_N_FC_PARAMS; ++i)
+    if (!fc_params[i]) return PNR_E_ARG;
+  return launch_fc_pack_all(fc_params, fc_packed, (hipStream_t)stream, flags);
 }
 
 int pnr_eval_points_c(const float* packed, const float* fc_packed, const double* p, const float* c, int64_t P,

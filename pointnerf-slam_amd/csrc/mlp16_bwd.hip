@@ -477,7 +477,7 @@ static __device__ __forceinline__ void bwd16_tile(const float* __restrict__ W, c
   // g_arg = g_e * cos(x@B), g_x = B g_arg (the k_mlp_bwd epilogue on set 0, tiles 0..2)
   if (!K::PST && valid) xv = a.xP[col];
   const float x0 = xv.x, x1 = xv.y, x2 = xv.z;
-  const float* FB = W + kOffFB;
+  const float* FB = W + kOffRaw + kRawFB;  // the raw table's copy (an f16x3-only pack has no fp32 image)
   float s0 = 0.f, s1 = 0.f, s2 = 0.f;
 #pragma unroll
   for (int t = 0; t < 3; ++t) {

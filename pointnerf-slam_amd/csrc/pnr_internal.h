@@ -186,16 +186,17 @@ int launch_mlp_bwd_bf(const float* packed, const BwdArgs& a, int64_t P, hipStrea
 
 int launch_pack(const RawParams& rp, float* packed, hipStream_t st);
 // every image (fp32, 16-bit forward, delta chain, raw table) in two launches (mlp16_pack.hip)
-int launch_pack_all(const RawParams& rp, float* packed, hipStream_t st);
+int launch_pack_all(const RawParams& rp, float* packed, hipStream_t st, int flags = 0);  // PNR_PACK_* flags
 // float offset of Wo [4][256] fp32 in the packed buffer (the raw table's copy, mlp16.h kRawWo)
 int64_t packed_raw_wo_offset();
+int64_t packed_raw_fb_offset();  // the raw table's Fourier B [3][96] (f16x3 path: no fp32 image)
 int launch_fc_pack(const float* const* fc, float* out, hipStream_t st);
 
 // bf16 split forward (mlp_bf.hip): images appended to the fp32 images in the same buffers
 int64_t packed_floats_all();
 int64_t fc_packed_floats_all();
 
-int launch_fc_pack_all(const float* const* fc, float* out, hipStream_t st);  // fp32 + 16-bit images, 2 launches
+int launch_fc_pack_all(const float* const* fc, float* out, hipStream_t st, int flags = 0);  // fp32 + 16-bit images, 2 launches
 // prec = PNR_PREC_BF16X3 / PNR_PREC_BF16 / PNR_PREC_F16X3
 // status: PNR_STATUS_* bits ORed in on the device (f16 range check of F16X3), or null
 int launch_mlp_fwd_bf(int prec, const float* packed, const PointSrc& src, int mode, int64_t P, float* raw,
@@ -258,7 +259,7 @@ struct WgradSyn {
   int64_t mgrp0;        // saved row of A row 0, / 32
   const float* wo;      // Wo [4][256] fp32
   const float4* xP;     // kWgradFirstX: saved inputs of the chunk rows
-  const float* fb;      // kWgradFirstX: Fourier B padded [3][96] (packed + kOffFB)
+  const float* fb;      // kWgradFirstX: Fourier B padded [3][96] (the raw table copy, packed_raw_fb_offset)
   // every kind: per-workgroup partial tiles (wgrad_part_floats + wgrad_part_bias_floats of scratch),
   // added into C / bias in a fixed order by k_part_reduce -- no float atomics, deterministic
   float* part;
@@ -269,6 +270,8 @@ struct WgradSyn {
   // GEMMs that will share one grouped launch (launch_wgrad16_group), 0 = a launch of its own (see
   // wgrad16_prepare's grid rule)
   int group_jobs;
+  // CUs left to the grouped launch's skinny jobs (dWo / dB) when the GEMMs are sized to fill the chip once
+  int reserve_cus;
 };
 // Arguments of one split weight-gradient GEMM (wgrad16.hip k_wgrad16)
 struct WxArgs {
@@ -302,7 +305,7 @@ struct Wgrad16Job {
   int var;   // kernel variant (wgrad16.hip kVar*)
   int nwg;   // workgroups (split-K)
 };
-constexpr int kMaxGemmJobs = 8;
+constexpr int kMaxGemmJobs = 10;  // 4 hidden + 4 fc_c GEMMs + the skinny dWo / dB
 constexpr int kWgradMaxWg = 512;    // fp32 k_wgrad grid cap
 constexpr int kWgrad16MaxWg = 256;  // split k_wgrad16 grid cap
 constexpr int kSkinnyMaxWg = 1024;  // k_wgrad_skinny grid cap
@@ -359,6 +362,10 @@ int launch_wgrad16(int kind, const float* A, const float* B, int64_t K, int64_t 
 int wgrad16_prepare(int kind, const float* A, const float* B, int64_t K, int64_t kb_rows, float* C, int64_t ldc,
                     float* bias, const WgradSyn* syn, Wgrad16Job* job, ReduceJob* red);
 int launch_wgrad16_group(const Wgrad16Job* jobs, int n, hipStream_t st);
+// the skinny dWo (out = 1: A = g_out rows, B = h4, + dbo) / dB (out = 0: A = x rows, B = g_arg) as a job
+// of a grouped launch
+int wgrad_skinny_prepare(int out, const float* A4, const float* B, int64_t K, float* C, float* bias, float* part,
+                         float* part_bias, Wgrad16Job* job, ReduceJob* red);
 int launch_wgrad_out16(const float* g_out, const float* h4, int64_t K, float* C, float* bias, float* part,
                        float* part_bias, hipStream_t st, ReduceJob* defer = nullptr);
 int launch_wgrad_fourier16(const float4* xP, const float* garg, int64_t K, float* C, float* part, hipStream_t st,
@@ -374,7 +381,7 @@ int device_cu_count();
 // Diagnostics: bracket a launch with hipEvents when pnr_timing_enable(1) (capi.cpp).
 enum TimedKernel : int {
   kTimeMlpFwd = 0, kTimeMlpBwd = 1, kTimeRay = 2, kTimeWgrad = 3, kTimeGather = 4, kTimeGatherBwd = 5,
-  kTimeKinds = 6
+  kTimeWgradGroup = 6, kTimeKinds = 7
 };
 struct TimingScope {
   hipEvent_t a = nullptr, b = nullptr;

@@ -652,6 +652,7 @@ __device__ __forceinline__ double kstage(double& key, double kn) {
 // broadcast LDS reads.  Against a thread per sample walking its own candidates through global
 // memory, a candidate costs one global load per block instead of one per sample.
 constexpr int kCandBatch = 128;
+typedef int v4i32 __attribute__((ext_vector_type(4)));
 struct SearchLds {
   float4 cand[kCandBatch + 1];   // staged candidate points (x, y, z, index bits) + pair padding
   uint8_t tag[kCandBatch + 1];   // probe cell n | 8 if its bucket collides
@@ -707,6 +708,42 @@ __global__ __launch_bounds__(64, PNR_SEARCH_WAVES) void k_gather_search(GatherAr
                 lbz = __builtin_amdgcn_readlane(bz, leader);
       const bool member = ((pending >> lane) & 1ull) && bx == lbx && by == lby && bz == lbz;
       pending &= ~__ballot(member);
+      int cs[8], ce[8], cb[8], cf[8];  // wave-uniform: list start / end, bucket start, tag per cell
+#if !defined(PNR_VECTOR_HDR)
+      // the 8 probe cells' bucket headers by SCALAR loads (one s_load_dwordx4 each, one wait): the
+      // cell coordinates are wave-uniform, so the headers land in SGPRs and the per-cell ranges, their
+      // running sum and the collision tags are scalar arithmetic (no lane loads, scan or readlanes)
+      {
+        const int4* hp[8];
+#pragma unroll
+        for (int n = 0; n < 8; ++n)
+          hp[n] = a.hdr + cell_hash(lbx + (n & 1), lby + ((n >> 1) & 1), lbz + (n >> 2), a.g.mask);
+        v4i32 h[8];
+        asm volatile(
+            "s_load_dwordx4 %0, %8, 0x0\n\ts_load_dwordx4 %1, %9, 0x0\n\t"
+            "s_load_dwordx4 %2, %10, 0x0\n\ts_load_dwordx4 %3, %11, 0x0\n\t"
+            "s_load_dwordx4 %4, %12, 0x0\n\ts_load_dwordx4 %5, %13, 0x0\n\t"
+            "s_load_dwordx4 %6, %14, 0x0\n\ts_load_dwordx4 %7, %15, 0x0\n\t"
+            "s_waitcnt lgkmcnt(0)"
+            : "=&s"(h[0]), "=&s"(h[1]), "=&s"(h[2]), "=&s"(h[3]), "=&s"(h[4]), "=&s"(h[5]), "=&s"(h[6]), "=&s"(h[7])
+            : "s"(hp[0]), "s"(hp[1]), "s"(hp[2]), "s"(hp[3]), "s"(hp[4]), "s"(hp[5]), "s"(hp[6]), "s"(hp[7])
+            : "memory");
+        int run = 0;
+#pragma unroll
+        for (int n = 0; n < 8; ++n) {
+          const int cx = lbx + (n & 1), cy = lby + ((n >> 1) & 1), cz = lbz + (n >> 2);
+          const uint64_t hk = (uint64_t)(uint32_t)h[n].z | ((uint64_t)(uint32_t)h[n].w << 32);
+          const bool coll = (hk & kCollision) != 0;
+          const bool own = (hk & ~kCollision) == cell_key(cx, cy, cz);
+          const int len = (coll || own) ? h[n].y - h[n].x : 0;
+          cb[n] = (coll || own) ? h[n].x : 0;
+          cs[n] = run;
+          run += len;
+          ce[n] = run;
+          cf[n] = n | (coll ? 8 : 0);
+        }
+      }
+#else
       // the 8 probe cells' candidate ranges, lane n < 8 for cell n
       int s0 = 0, len = 0, fl = 0;
       if (lane < 8) {
@@ -727,7 +764,6 @@ __global__ __launch_bounds__(64, PNR_SEARCH_WAVES) void k_gather_search(GatherAr
         const int t = __shfl_up(incl, d);
         if (lane >= d) incl += t;
       }
-      int cs[8], ce[8], cb[8], cf[8];  // wave-uniform: list start / end, bucket start, tag per cell
 #pragma unroll
       for (int n = 0; n < 8; ++n) {
         ce[n] = __builtin_amdgcn_readlane(incl, n);
@@ -735,6 +771,7 @@ __global__ __launch_bounds__(64, PNR_SEARCH_WAVES) void k_gather_search(GatherAr
         cb[n] = __builtin_amdgcn_readlane(s0, n);
         cf[n] = __builtin_amdgcn_readlane(fl, n);
       }
+#endif
       const int total = ce[7];
       // no colliding bucket among the 8 (the common case): no tag reads, no per-point cell test
       const bool coll_any = ((cf[0] | cf[1] | cf[2] | cf[3] | cf[4] | cf[5] | cf[6] | cf[7]) & 8) != 0;

@@ -879,6 +879,8 @@ __global__ __launch_bounds__(256) void k_fine_loss_w(pnr_render_params prm, cons
                                                      float* __restrict__ g_nrm, float4* __restrict__ pad0, int np0,
                                                      float4* __restrict__ pad1, int np1, FineLoss fl) {
   __shared__ double zn_[4][PNR_MAX_SAMPLES];
+  __shared__ float4 cr_[4][PNR_MAX_SAMPLES];   // raw of each sample, by its unsorted index
+  __shared__ float ci_[4][PNR_MAX_SAMPLES];    // its inside flag
   __shared__ uint8_t os_[4][PNR_MAX_SAMPLES + 4];
   __shared__ double red[4];
   __shared__ uint32_t last;
@@ -895,10 +897,21 @@ __global__ __launch_bounds__(256) void k_fine_loss_w(pnr_render_params prm, cons
   double* zn = zn_[wv];
   uint8_t* os = os_[wv];
   const int S = SS > 0 ? SS : prm.n_samples, I = II > 0 ? II : prm.n_importance, M = S + I;
-  // ---- k_fine_w: rank sort and compositing
+  // every global input of the ray in ONE round trip: the depths, the raw outputs and inside flags by
+  // unsorted sample (read through LDS by rank below, instead of two dependent loads after the sort),
+  // the ray's gt depth / colour and its regulation rows
   const int lq = l < M ? l : M - 1;
   const double zl = *(lq < S ? zc + n * S + lq : zi + n * I + (lq - S));
+  const float4 cl = *(lq < S ? rawc + n * S + lq : rawi + n * I + (lq - S));
+  const float il = (lq < S ? insc + n * S + lq : insi + n * I + (lq - S))->w;
+  const float g = fl.gt[n];
+  const float gtc0 = fl.gtc[n * 3 + 0], gtc1 = fl.gtc[n * 3 + 1], gtc2 = fl.gtc[n * 3 + 2];
+  const int64_t rr = n * S + (l < S ? l : S - 1);
+  const float sg = fl.rawr[rr].w;
+  const float ir = fl.insr[rr].w;
   zn[l] = zl;
+  cr_[wv][l] = cl;
+  ci_[wv][l] = il;
   os[l] = 0;
   if (l < 4) os[64 + l] = 0;
   __syncthreads();
@@ -914,7 +927,7 @@ __global__ __launch_bounds__(256) void k_fine_loss_w(pnr_render_params prm, cons
   const int s = os[l];
   const double zq = zn[s];
   const double znx = l + 1 < M ? zn[os[l + 1]] : 0.0;
-  const float4 c = *(s < S ? rawc + n * S + s : rawi + n * I + (s - S));  // lanes >= M: s = 0, never read
+  const float4 c = cr_[wv][s];  // lanes >= M: s = 0, never read
   const float nrm = ray_norm(rd + n * 3);
   const float dz = l < M - 1 ? (float)(znx - zq) : 1e10f;
   const float delta = dz * nrm;
@@ -932,32 +945,29 @@ __global__ __launch_bounds__(256) void k_fine_loss_w(pnr_render_params prm, cons
     D += rld(pD, q);
   }
   // ---- k_map_loss: this ray's terms and the upstream gradients (wave-uniform)
-  const float g = fl.gt[n];
   const double e = (double)g - D;
   const bool msk = g > 0.f;
   double Lr = msk ? fabs(e) : 0.0;
   const double gd = msk ? -sgn(e) : 0.0;
-  const float col[3] = {r0, r1, r2};
+  const float col[3] = {r0, r1, r2}, gtc[3] = {gtc0, gtc1, gtc2};
   float gr[3];
   float cs = 0.f;
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
-    const float ec = fl.gtc[n * 3 + k] - col[k];
+    const float ec = gtc[k] - col[k];
     cs += fabsf(ec);
     gr[k] = -fl.w_color * sgnf(ec);
   }
   Lr += (double)(fl.w_color * cs);
   {  // the ray's regulation samples: w_reg |sigma| and dL/draw = (0, 0, 0, w_reg sign(sigma) [inside])
-    const int64_t rr = n * S + (l < S ? l : S - 1);
-    const float sg = fl.rawr[rr].w;
     const float gsg = fl.w_reg * sgnf(sg);
-    if (live && l < S) fl.gor[rr] = make_float4(0.f, 0.f, 0.f, fl.insr[rr].w != 0.f ? gsg : 0.f);
+    if (live && l < S) fl.gor[rr] = make_float4(0.f, 0.f, 0.f, ir != 0.f ? gsg : 0.f);
     const double ls = (double)(fl.w_reg * fabsf(sg));
     for (int q = 0; q < S; ++q) Lr += rld(ls, q);
   }
   // ---- k_fine_bwd_w with g_var = 0, from the forward's values
   const bool act = l < M;
-  const bool inside = act && (s < S ? insc + n * S + s : insi + n * I + (s - S))->w != 0.f;
+  const bool inside = act && ci_[wv][s] != 0.f;
   const double gv = 0.0;
   const float gr0 = gr[0], gr1 = gr[1], gr2 = gr[2];
   const double pS = (double)(a * Tf) * (zq - D);
@@ -987,21 +997,19 @@ __global__ __launch_bounds__(256) void k_fine_loss_w(pnr_render_params prm, cons
   if (l == 0) red[wv] = live ? Lr : 0.0;
   __syncthreads();
   if (threadIdx.x == 0) {
-    fl.part[blockIdx.x] = ((red[0] + red[1]) + red[2]) + red[3];
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    // the partial as an 8-B agent atomic, read back by 8-B agent atomics (MI355X_MICROARCH.md, valid
+    // hand-off forms): no L2 write-back per block, which a release fence would cost
+    const double pb = ((red[0] + red[1]) + red[2]) + red[3];
+    atomicExch(reinterpret_cast<unsigned long long*>(fl.part) + blockIdx.x, __double_as_longlong(pb));
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const uint32_t t = atomicAdd(fl.ticket, 1u);
     last = t == gridDim.x - 1 ? 1u : 0u;
-    if (last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
   }
   __syncthreads();
   if (!last) return;
   double v = 0.0;
-  for (int i = (int)threadIdx.x; i < (int)gridDim.x; i += 256) v += fl.part[i];
+  for (int i = (int)threadIdx.x; i < (int)gridDim.x; i += 256)
+    v += __longlong_as_double(atomicAdd(reinterpret_cast<unsigned long long*>(fl.part) + i, 0ull));
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
   __syncthreads();

@@ -350,6 +350,91 @@ __global__ __launch_bounds__(512, 1) void k_wgrad16(WxArgs a) {
   wgrad16_body<NTB, WB, SYN, FOUR, BSC, MSK>(a, blockIdx.x, lds);
 }
 
+// Skinny weight-gradient GEMMs (fp32 FMAs), bandwidth-bound on B:
+//   C[m][n] += sum_k A[k][m] B[k][n]   m < M (<= 4), n < N      (bias[m] += sum_k A[k][m])
+// A fp32 rows of 4 (float4: g_out, or x = (x0, x1, x2, inside) with M = 3), B fp32 rows of WB.
+//   dWo (4 x 256) = g_out^T h4 (+ dbo)       dB (3 x 93) = x^T g_arg
+// A block streams its K range: thread (r, c) = (tid / CPR, tid % CPR) loads 32 B (8 columns) of row
+// r and the row's float4 of A, keeping 4 x 8 partial sums; the RPI row groups are then added in
+// row-group order through LDS and the block's M x N sums go to the partials (part[block][m N + n],
+// pbias[block][m]) that k_part_reduce adds into C / bias in a fixed order.
+// (NT threads: 256 as a launch of its own, 512 as a job of the grouped launch; `lds` holds the
+// RPI x 4 x WB row-group sums and the RPI x 4 bias sums)
+template <int WB, int NT>
+struct SkinnyGeo {
+  static constexpr int CPR = WB / 8;   // threads per row (32 for 256, 12 for 96)
+  static constexpr int RPI = NT / CPR; // rows per iteration (8 / 21 at 256 threads, 16 / 42 at 512)
+  static constexpr int kLds = RPI * 4 * WB * 4 + RPI * 4 * 4;
+};
+template <int WB, int NT>
+__device__ __forceinline__ void skinny_body(const float4* __restrict__ A, const float* __restrict__ B, int64_t K,
+                                            int64_t ks, int M, int N, float* __restrict__ part,
+                                            float* __restrict__ pbias, int bid, char* lds) {
+  constexpr int CPR = SkinnyGeo<WB, NT>::CPR;
+  constexpr int RPI = SkinnyGeo<WB, NT>::RPI;
+  float (*red)[4][WB] = reinterpret_cast<float (*)[4][WB]>(lds);
+  float (*redb)[4] = reinterpret_cast<float (*)[4]>(lds + RPI * 4 * WB * 4);
+  const int tid = threadIdx.x;
+  const int r = tid / CPR, c = tid % CPR;
+  const bool act = r < RPI;
+  const int64_t kb = (int64_t)bid * ks;
+  const int64_t ke = kb + ks < K ? kb + ks : K;
+  float acc[4][8];
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[m][j] = 0.f;
+  float bs[4] = {0.f, 0.f, 0.f, 0.f};
+  if (act) {
+    constexpr int U = 8;  // rows in flight per thread (HBM latency: bytes in flight per CU)
+    for (int64_t k = kb + r; k < ke; k += U * RPI) {
+      float4 av[U], b0[U], b1[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t ku = k + u * RPI;
+        const int64_t kc = ku < ke ? ku : k;  // rows past the range: re-read row k, weighted 0
+        av[u] = A[kc];
+        b0[u] = *reinterpret_cast<const float4*>(B + kc * WB + 8 * c);
+        b1[u] = *reinterpret_cast<const float4*>(B + kc * WB + 8 * c + 4);
+        if (ku >= ke) av[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const float a4[4] = {av[u].x, av[u].y, av[u].z, av[u].w};
+        const float bv[8] = {b0[u].x, b0[u].y, b0[u].z, b0[u].w, b1[u].x, b1[u].y, b1[u].z, b1[u].w};
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+#pragma unroll
+          for (int m = 0; m < 4; ++m) acc[m][j] = __builtin_fmaf(a4[m], bv[j], acc[m][j]);
+        if (c == 0) {
+#pragma unroll
+          for (int m = 0; m < 4; ++m) bs[m] += a4[m];
+        }
+      }
+    }
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) red[r][m][8 * c + j] = acc[m][j];
+    if (c == 0)
+#pragma unroll
+      for (int m = 0; m < 4; ++m) redb[r][m] = bs[m];
+  }
+  __syncthreads();
+  for (int i = tid; i < M * N; i += NT) {
+    const int m = i / N, n = i % N;
+    float s = red[0][m][n];
+#pragma unroll
+    for (int q = 1; q < RPI; ++q) s += red[q][m][n];
+    part[(int64_t)bid * M * N + i] = s;
+  }
+  if (pbias && tid < M) {
+    float s = redb[0][tid];
+#pragma unroll
+    for (int q = 1; q < RPI; ++q) s += redb[q][tid];
+    pbias[(int64_t)bid * M + tid] = s;
+  }
+}
 // Every split weight-gradient GEMM of a backward chunk in ONE launch (they are independent): block b
 // runs workgroup b - first[q] of job q.  At the Mapper's 1,000-ray batch each GEMM fills ~170 CUs
 // for ~30 us and five of them ran back to back; grouped they share the chip, and the launch gaps go.
@@ -360,7 +445,8 @@ struct Wgrad16Group {
   int first[kMaxGemmJobs + 1];
   int n;
 };
-enum : int { kVarHidden = 0, kVarHiddenM, kVarSyn, kVarFirstX, kVarFirstXM, kVarFc, kVarFcOut };
+enum : int { kVarHidden = 0, kVarHiddenM, kVarSyn, kVarFirstX, kVarFirstXM, kVarFc, kVarFcOut, kVarSkinnyOut,
+              kVarSkinnyFour };
 __global__ __launch_bounds__(512, 1) void k_wgrad16_group(Wgrad16Group G) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   int q = 0;
@@ -373,6 +459,15 @@ __global__ __launch_bounds__(512, 1) void k_wgrad16_group(Wgrad16Group G) {
     case kVarFirstX: wgrad16_body<3, 96, false, true, false, false>(G.a[q], bid, lds); break;
     case kVarFirstXM: wgrad16_body<3, 96, false, true, false, true>(G.a[q], bid, lds); break;
     case kVarFcOut: wgrad16_body<1, 32, true, false, true, false>(G.a[q], bid, lds); break;
+    // the skinny fp32 GEMMs (dWo, dB) as jobs of the same launch (skinny_body below; A = float4 rows)
+    case kVarSkinnyOut:
+      skinny_body<256, 512>(reinterpret_cast<const float4*>(G.a[q].A), G.a[q].B, G.a[q].K, G.a[q].ks, 4, kHidden,
+                            G.a[q].part, G.a[q].part_bias, bid, lds);
+      break;
+    case kVarSkinnyFour:
+      skinny_body<96, 512>(reinterpret_cast<const float4*>(G.a[q].A), G.a[q].B, G.a[q].K, G.a[q].ks, 3, kFourier,
+                           G.a[q].part, nullptr, bid, lds);
+      break;
     default: wgrad16_body<1, 32, false, false, true, false>(G.a[q], bid, lds); break;
   }
 }
@@ -528,7 +623,7 @@ int wgrad16_prepare(int kind, const float* A, const float* B, int64_t K, int64_t
   const int64_t tiles = K / 32;
   int64_t per = 8;
   if (syn->group_jobs > 0) {
-    const int64_t cus = device_cu_count();
+    const int64_t cus = device_cu_count() - syn->reserve_cus;
     const int64_t fill = (tiles * syn->group_jobs + cus - 1) / cus;
     if (fill <= 256) per = fill > per ? fill : per;
   }
@@ -590,22 +685,23 @@ int launch_wgrad16_group(const Wgrad16Job* jobs, int n, hipStream_t st) {
   if (n > kMaxGemmJobs) return PNR_E_ARG;
   constexpr int kLds = Wx3<8, 256>::kLds;  // the largest variant
   static_assert(Wx3<3, 96>::kLds <= kLds && Wx3<1, 32>::kLds <= kLds, "group LDS");
+  static_assert(SkinnyGeo<256, 512>::kLds <= kLds && SkinnyGeo<96, 512>::kLds <= kLds, "group LDS (skinny jobs)");
   static const bool attr = hipFuncSetAttribute((const void*)k_wgrad16_group, hipFuncAttributeMaxDynamicSharedMemorySize,
                                                kLds) == hipSuccess;
   if (!attr) return PNR_E_ARG;
   Wgrad16Group G{};
   int blocks = 0;
-  int64_t units = 0;
+  int64_t macs = 0;  // timing units (pnr_timing_read kind 6): multiply-adds / 65,536
   for (int i = 0; i < n; ++i) {
     G.a[i] = jobs[i].a;
     G.var[i] = jobs[i].var;
     G.first[i] = blocks;
     blocks += jobs[i].nwg;
-    units += jobs[i].a.K;
+    macs += jobs[i].a.K * 256 * jobs[i].a.nb;
   }
   G.first[n] = blocks;
   G.n = n;
-  TimingScope ts(kTimeWgrad, units, st);
+  TimingScope ts(kTimeWgradGroup, macs / 65536, st);
   hipLaunchKernelGGL(k_wgrad16_group, dim3((unsigned)blocks), dim3(512), kLds, st, G);
   return hip_status(hipGetLastError());
 }
@@ -647,88 +743,41 @@ int launch_wgrad16(int kind, const float* A, const float* B, int64_t K, int64_t 
   return launch_part_reduce(red.part, red.pbias, red.nwg, red.nr, red.pw, red.nb, red.C, red.ldc, red.bias, st);
 }
 
-// Skinny weight-gradient GEMMs (fp32 FMAs), bandwidth-bound on B:
-//   C[m][n] += sum_k A[k][m] B[k][n]   m < M (<= 4), n < N      (bias[m] += sum_k A[k][m])
-// A fp32 rows of 4 (float4: g_out, or x = (x0, x1, x2, inside) with M = 3), B fp32 rows of WB.
-//   dWo (4 x 256) = g_out^T h4 (+ dbo)       dB (3 x 93) = x^T g_arg
-// A block streams its K range: thread (r, c) = (tid / CPR, tid % CPR) loads 32 B (8 columns) of row
-// r and the row's float4 of A, keeping 4 x 8 partial sums; the RPI row groups are then added in
-// row-group order through LDS and the block's M x N sums go to the partials (part[block][m N + n],
-// pbias[block][m]) that k_part_reduce adds into C / bias in a fixed order.
 template <int WB>
 __global__ __launch_bounds__(256) void k_wgrad_skinny(const float4* __restrict__ A, const float* __restrict__ B,
                                                       int64_t K, int64_t ks, int M, int N, float* __restrict__ part,
                                                       float* __restrict__ pbias) {
-  constexpr int CPR = WB / 8;          // threads per row (32 for 256, 12 for 96)
-  constexpr int RPI = 256 / CPR;       // rows per iteration (8 or 21)
-  __shared__ float red[RPI][4][WB];
-  __shared__ float redb[RPI][4];
-  const int tid = threadIdx.x;
-  const int r = tid / CPR, c = tid % CPR;
-  const bool act = r < RPI;
-  const int64_t kb = (int64_t)blockIdx.x * ks;
-  const int64_t ke = kb + ks < K ? kb + ks : K;
-  float acc[4][8];
-#pragma unroll
-  for (int m = 0; m < 4; ++m)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[m][j] = 0.f;
-  float bs[4] = {0.f, 0.f, 0.f, 0.f};
-  if (act) {
-    constexpr int U = 8;  // rows in flight per thread (HBM latency: bytes in flight per CU)
-    for (int64_t k = kb + r; k < ke; k += U * RPI) {
-      float4 av[U], b0[U], b1[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int64_t ku = k + u * RPI;
-        const int64_t kc = ku < ke ? ku : k;  // rows past the range: re-read row k, weighted 0
-        av[u] = A[kc];
-        b0[u] = *reinterpret_cast<const float4*>(B + kc * WB + 8 * c);
-        b1[u] = *reinterpret_cast<const float4*>(B + kc * WB + 8 * c + 4);
-        if (ku >= ke) av[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const float a4[4] = {av[u].x, av[u].y, av[u].z, av[u].w};
-        const float bv[8] = {b0[u].x, b0[u].y, b0[u].z, b0[u].w, b1[u].x, b1[u].y, b1[u].z, b1[u].w};
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-#pragma unroll
-          for (int m = 0; m < 4; ++m) acc[m][j] = __builtin_fmaf(a4[m], bv[j], acc[m][j]);
-        if (c == 0) {
-#pragma unroll
-          for (int m = 0; m < 4; ++m) bs[m] += a4[m];
-        }
-      }
-    }
-#pragma unroll
-    for (int m = 0; m < 4; ++m)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) red[r][m][8 * c + j] = acc[m][j];
-    if (c == 0)
-#pragma unroll
-      for (int m = 0; m < 4; ++m) redb[r][m] = bs[m];
-  }
-  __syncthreads();
-  for (int i = tid; i < M * N; i += 256) {
-    const int m = i / N, n = i % N;
-    float s = red[0][m][n];
-#pragma unroll
-    for (int q = 1; q < RPI; ++q) s += red[q][m][n];
-    part[(int64_t)blockIdx.x * M * N + i] = s;
-  }
-  if (pbias && tid < M) {
-    float s = redb[0][tid];
-#pragma unroll
-    for (int q = 1; q < RPI; ++q) s += redb[q][tid];
-    pbias[(int64_t)blockIdx.x * M + tid] = s;
-  }
+  __shared__ __attribute__((aligned(16))) char lds[SkinnyGeo<WB, 256>::kLds];
+  skinny_body<WB, 256>(A, B, K, ks, M, N, part, pbias, blockIdx.x, lds);
 }
 
-static int skinny_blocks(int64_t K, int64_t* ks) {
+// rows per workgroup: >= 256 (a 256-thread launch) / >= 512 (a grouped job), at most kSkinnyMaxWg groups
+static int skinny_blocks(int64_t K, int64_t* ks, int64_t min_rows = 256) {
   *ks = (K + kSkinnyMaxWg - 1) / kSkinnyMaxWg;
-  if (*ks < 256) *ks = 256;
+  if (*ks < min_rows) *ks = min_rows;
   return (int)((K + *ks - 1) / *ks);
+}
+
+// dWo / dB as jobs of a grouped launch (512-thread workgroups of >= 512 rows): arguments in the job's
+// WxArgs (A = the float4 rows, B, K, ks, partials), reduction into *red
+int wgrad_skinny_prepare(int out, const float* A4, const float* B, int64_t K, float* C, float* bias, float* part,
+                         float* part_bias, Wgrad16Job* job, ReduceJob* red) {
+  if (K <= 0 || !part || (out && !part_bias)) return PNR_E_ARG;
+  int64_t ks;
+  const int nb = skinny_blocks(K, &ks, 512);
+  WxArgs a{};
+  a.A = A4;
+  a.B = B;
+  a.K = K;
+  a.ks = ks;
+  a.part = part;
+  a.part_bias = out && bias ? part_bias : nullptr;
+  job->a = a;
+  job->var = out ? kVarSkinnyOut : kVarSkinnyFour;
+  job->nwg = nb;
+  *red = out ? ReduceJob{part, part_bias, nb, 4, kHidden, kHidden, C, (int64_t)kHidden, bias}
+             : ReduceJob{part, nullptr, nb, 3, kFourier, kFourier, C, (int64_t)kFourier, nullptr};
+  return 0;
 }
 
 // dWo (4 x 256) += g_out^T h4, dbo += colsum(g_out)

@@ -25,7 +25,7 @@ PRECISIONS = {'fp32': 0, 'bf16x3': 1, 'bf16': 2, 'f16x3': 3}
 # f16x3: fp32-class forward AND backward (every GEMM on 22-bit split operands with fp32
 # accumulation; tests/test_gpu_parity.py runs every case under fp32 and f16x3 at the same tolerances)
 DEFAULT_PRECISION = os.environ.get('PNR_PRECISION', 'f16x3')
-ABI_VERSION = 13
+ABI_VERSION = 14
 STATUS_F16_RANGE = 1  # include/pnr.h PNR_STATUS_F16_RANGE
 
 
@@ -67,6 +67,7 @@ class RenderParams(ctypes.Structure):
 PtrArray = c_void_p * N_PARAMS
 FcPtrArray = c_void_p * N_FC_PARAMS
 PPoints = ctypes.POINTER(Points)
+PACK_F16X3_ONLY = 2  # include/pnr.h PNR_PACK_F16X3_ONLY
 
 # name -> (restype, argtypes)
 _SIGS = {
@@ -74,6 +75,7 @@ _SIGS = {
     'pnr_build_info': (ctypes.c_char_p, []),
     'pnr_mlp_packed_floats': (c_size_t, []),
     'pnr_mlp_pack': (ctypes.c_int, [PtrArray, c_void_p, c_void_p]),
+    'pnr_mlp_pack2': (ctypes.c_int, [PtrArray, c_void_p, c_int32, c_void_p]),
     'pnr_eval_points': (ctypes.c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_int32, c_void_p]),
     'pnr_eval_points_f32': (ctypes.c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_int32, c_void_p]),
     'pnr_mlp_train_workspace_bytes': (c_size_t, [c_int64]),
@@ -140,6 +142,7 @@ _SIGS = {
     'pnr_point_gather_bwd_atomics': (ctypes.c_int, [PPoints, c_void_p, c_int64, ctypes.POINTER(c_int64), c_void_p]),
     'pnr_fc_packed_floats': (c_size_t, []),
     'pnr_fc_pack': (ctypes.c_int, [FcPtrArray, c_void_p, c_void_p]),
+    'pnr_fc_pack2': (ctypes.c_int, [FcPtrArray, c_void_p, c_int32, c_void_p]),
     'pnr_eval_points_c': (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p,
                                          c_int32, c_void_p]),
     'pnr_mlp_fwd_train_c': (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p,

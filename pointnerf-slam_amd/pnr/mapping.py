@@ -238,9 +238,10 @@ class MapStep:
         ren = TrainPass(r, self.c, self.decoder, 'render')
         # the weight images, the point index and the f16 feature copy: built on this stream before the
         # chains fork (both read them)
-        ren.packer.image(ren.feat.params)
+        prec = _lib.precision_code(r.precision)
+        ren.packer.image(ren.feat.params, prec=prec)
         if self.points is not None:
-            ren.feat.fc_owner.image(ren.feat.fc)
+            ren.feat.fc_owner.image(ren.feat.fc, prec=prec)
             self.points.index()
             self.points._feats_for_gather()
         if self.fused:  # render + regulation as ONE decoder pass (pnr_map_fwd / pnr_map_bwd)

@@ -71,6 +71,7 @@ class _Feat:
         self.params = tensors[:_lib.N_PARAMS]
         self.fc = tensors[_lib.N_PARAMS:_lib.N_PARAMS + _lib.N_FC_PARAMS] if pts is not None else ()
         self.keep = []
+        self.prec = None  # PNR_PREC_* of the call when only that precision's images are needed
         # grad mode of the CALLER (inside Function.forward it is always off, and needs_input_grad
         # only reflects requires_grad): an eval call under no_grad saves no activations
         self.train = torch.is_grad_enabled()
@@ -78,7 +79,7 @@ class _Feat:
     def attach(self, prm, g_feats=None, g_fc=None):
         if self.pts is None:
             return
-        s, keep = self.pts.descriptor(self.fc_owner.image(self.fc), g_feats, g_fc)
+        s, keep = self.pts.descriptor(self.fc_owner.image(self.fc, prec=self.prec), g_feats, g_fc)
         self.keep = [s, keep]
         prm.points = ctypes.pointer(s)
 
@@ -249,7 +250,8 @@ class TrainPass:
         prm.status = r.status_word(dev).data_ptr()
         prm.save_for_backward = 1
         prm.need_ray_grads = 0
-        packed = self.packer.image(self.feat.params)
+        packed = self.packer.image(self.feat.params, prec=prm.precision)
+        self.feat.prec = prm.precision
         self.feat.attach(prm)
         if isinstance(far_clamp, torch.Tensor):
             far_clamp = far_clamp.reshape(-1)[:1].float().contiguous()
@@ -327,7 +329,8 @@ class MapPass:
         prm.status = r.status_word(dev).data_ptr()
         prm.save_for_backward = 1
         prm.need_ray_grads = 0
-        packed = self.packer.image(self.feat.params)
+        packed = self.packer.image(self.feat.params, prec=prm.precision)
+        self.feat.prec = prm.precision
         self.feat.attach(prm)
         if isinstance(far_clamp, torch.Tensor):
             far_clamp = far_clamp.reshape(-1)[:1].float().contiguous()
@@ -380,7 +383,8 @@ class MapPass:
         prm.save_for_backward = 1
         prm.need_ray_grads = 0
         prm.grads_overwrite = 1 if overwrite else 0
-        packed = self.packer.image(self.feat.params)
+        packed = self.packer.image(self.feat.params, prec=prm.precision)
+        self.feat.prec = prm.precision
         self.feat.attach(prm, g_feats, g_fc)
         if isinstance(far_clamp, torch.Tensor):
             far_clamp = far_clamp.reshape(-1)[:1].float().contiguous()

@@ -43,7 +43,7 @@ def test_python_binding_covers_header():
 
 def test_host_only_calls(lib):
     lib.pnr_abi_version.restype = ctypes.c_int
-    assert lib.pnr_abi_version() == 13
+    assert lib.pnr_abi_version() == 14
     lib.pnr_mlp_packed_floats.restype = ctypes.c_size_t
     # fp32 images 486,688 + bf16x3 / bf16 / f16x3 forward streams 229,376 / 118,784 / 229,376
     # + f16x3 delta-chain stream 225,280 + raw table 2,048 + fp32 Wo 1,024

@@ -328,3 +328,36 @@ def test_map_step_empty_batch(pnr_mod, dev, precision):
     torch.cuda.synchronize()
     assert float(loss) == 0.0
     assert bool((ms.flat.grad == 0).all())
+
+
+@pytest.mark.parametrize('points', [True, False])
+def test_f16x3_only_pack_matches_full(pnr_mod, dev, points):
+    """ABI 14: the Mapper's repack asks for the f16x3 images only (pnr_mlp_pack2 / pnr_fc_pack2
+    PNR_PACK_F16X3_ONLY: no fp32 / bf16 images).  After a few MapSteps, its images of the final weights
+    equal a fresh full pack's bit for bit on everything the f16x3 kernels read: the f16x3 forward and
+    delta-chain images and the raw table (biases, Fourier B, scales, Wo)."""
+    from pnr import _lib
+    from pnr.mapping import MapStep
+    from pnr.packing import PackedFC, PackedMLP
+    make, batches = _setup(pnr_mod, dev, points=points)
+    r, dec, pts = make()
+    ms = MapStep(r, dec, points=pts, feat_lr=1e-2)
+    for b in batches[:2]:
+        ms(*b)
+    torch.cuda.synchronize()
+    lib = _lib.load()
+    f16 = _lib.PRECISIONS['f16x3']
+    # (compared as int32 words: two f16 parts in a float32 word can spell a NaN)
+    img = dec._packed.image(list(dec.ordered_params()), prec=f16).clone().view(torch.int32)
+    ref = PackedMLP().image([p.detach().clone() for p in dec.ordered_params()]).view(torch.int32)
+    raw0 = lib.pnr_mlp_packed_floats() - 3072   # kOffRaw: the raw table is the last 12 KiB
+    lo = raw0 - (917504 + 901120) // 4          # kOffH2: f16x3 main image, then the delta-chain image
+    # raw words: biases / bo / Fourier B [0, 1344), inverse scales [1344, 1349), scales [1352, 1357), Wo [2048, 3072)
+    for a, b in ((lo, raw0 + 1349), (raw0 + 1352, raw0 + 1357), (raw0 + 2048, raw0 + 3072)):
+        assert torch.equal(img[a:b], ref[a:b]), (a, b)
+    if points:
+        fimg = dec._packed_fc.image(list(dec.ordered_fc_params()), prec=f16).clone().view(torch.int32)
+        fref = PackedFC().image([p.detach().clone() for p in dec.ordered_fc_params()]).view(torch.int32)
+        fraw0 = lib.pnr_fc_packed_floats() - 2048  # kOffFcRaw
+        flo = fraw0 - 2 * 32768                    # kOffFcH2: f16x3 fc image, then the fc backward image
+        assert torch.equal(fimg[flo:fraw0 + 1032], fref[flo:fraw0 + 1032])  # (bc, inverse [4], forward [4])

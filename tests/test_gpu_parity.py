@@ -84,7 +84,7 @@ def grad_elementwise(g, cr, f32, rel_f32, what):
 
 def test_library_info(pnr_mod):
     lib = pnr_mod.library()
-    assert lib.pnr_abi_version() == 13
+    assert lib.pnr_abi_version() == 14
     assert lib.pnr_mlp_packed_floats() > 0
 
 

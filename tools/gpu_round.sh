@@ -10,6 +10,9 @@
 #   points      the neural-point S-map alone
 #   gather      tools/gather_bench.py (forward + backward gather timing)
 #   aux         the auxiliary benches: Tracker, render_img, Mesher grid, configs C3 / C5
+#   timeline    rocprofv3 kernel trace of the replayed room0 iteration -> ${TAG}_room0_timeline.txt
+#   pmcsearch   the gather search's stall counters (tools/pmc_search.sh)
+#   npf         the faithful-size neural-point iterations C3 / C5 (tools/np_faithful.py) + their kernel stats
 #   prof        the round profile: rocprofv3 kernel stats + FETCH/WRITE and MFMA-busy PMC passes
 #               (tools/prof_round.sh), the gather's traffic passes and kernel stats, the faithful
 #               iteration's kernel stats
@@ -64,6 +67,18 @@ for step in "$@"; do
         --no-cpu-baseline
       python3 tools/timeline.py gpurun_out/prof_${TAG}_tl --period-kernel k_adam_multi > ${O}_room0_timeline.txt
       cat ${O}_room0_timeline.txt ;;
+    pmcsearch)
+      bash tools/pmc_search.sh ${TAG} > ${O}_pmcsearch.log 2>&1 || { echo "FAILED pmcsearch"; tail -5 ${O}_pmcsearch.log; exit 1; }
+      tail -12 ${O}_pmcsearch.log ;;
+    npf)
+      run 200 ${O}_c3.log python3 tools/np_faithful.py --case C3 --iters 50
+      run 200 ${O}_c5.log python3 tools/np_faithful.py --case C5 --iters 30
+      tail -1 ${O}_c3.log; tail -1 ${O}_c5.log
+      run 300 gpurun_out/prof_${TAG}_c3.log rocprofv3 --kernel-trace --stats --output-format csv \
+        -d gpurun_out/prof_${TAG}_c3 -o c3 -- python3 tools/np_faithful.py --case C3 --iters 30
+      run 300 gpurun_out/prof_${TAG}_c5.log rocprofv3 --kernel-trace --stats --output-format csv \
+        -d gpurun_out/prof_${TAG}_c5 -o c5 -- python3 tools/np_faithful.py --case C5 --iters 20
+      echo npf-prof ;;
     aux)
       run 200 ${O}_track.json python3 tools/track_bench.py
       run 200 ${O}_render.json python3 tools/render_bench.py

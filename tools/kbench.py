@@ -80,14 +80,16 @@ def main():
             continue
         # forward with save + backward (MLP autograd path)
         x = pts.float().requires_grad_(False)
-        timing_read(0), timing_read(1), timing_read(3)
+        timing_read(0), timing_read(1), timing_read(3), timing_read(6)
         for _ in range(args.reps):
             out = dec(x)
             out.sum().backward()
         torch.cuda.synchronize()
         report(f'[{prec}] k_mlp_fwd train (save)', 0, 443438)
         report(f'[{prec}] k_mlp_bwd delta chain', 1, 442880)
-        n, ms, u = timing_read(3)  # weight-gradient GEMMs: 10 launches per backward, units = K points
+        n, ms, u = timing_read(3)  # dWo / dB (or the fp32 GEMMs) ...
+        n6, ms6, _ = timing_read(6)  # ... and the grouped split GEMMs (pnr_timing_read kind 6)
+        n, ms = n + n6, ms + ms6
         print(f'[{prec}] k_wgrad* (all shapes)            launches={n:3d} ms/backward={ms / args.reps:9.3f}', flush=True)
         lib.pnr_timing_enable(0)
 
