@@ -71,15 +71,8 @@ __device__ __forceinline__ uint16_t part_bits(float x, int part) {
 
 // element (T, s, part, lane, j) of a weight fragment image for a layer with A[row][k]:
 // row = 32T + (lane&31), k = 32kc + perm(8s+j, lane>>5).  img 0: BF16X3, 1: BF16, 2: F16X3.
-__device__ __forceinline__ float pick5(const float (&sc)[5], int t) {  // sc[t] without dynamic register indexing
-  float v = sc[0];
-#pragma unroll
-  for (int k = 1; k < 5; ++k) v = t == k ? sc[k] : v;
-  return v;
-}
 __device__ __forceinline__ void pack16_at(const RawParams& rp, uint16_t* __restrict__ bf2, uint16_t* __restrict__ bf1,
-                                          uint16_t* __restrict__ h2, float* __restrict__ raw, const int64_t idx64,
-                                          const float (&scl)[5]) {
+                                          uint16_t* __restrict__ h2, float* __restrict__ raw, const int64_t idx64) {
   constexpr int n2 = (int)(bf_main_bytes(2) / 2), n1 = (int)(bf_main_bytes(1) / 2);
   static_assert(2LL * n2 + n1 < (1LL << 30), "32-bit pack indices");
   if (idx64 < 2 * n2 + n1) {
@@ -121,7 +114,7 @@ __device__ __forceinline__ void pack16_at(const RawParams& rp, uint16_t* __restr
         v = row < 4 ? rp.p[9][row * kHidden + k] : 0.f;
       }
     }
-    if (img == 2) h2[e0] = part_bits<_Float16>(v * pick5(scl, tensor), part);
+    if (img == 2) h2[e0] = part_bits<_Float16>(v * raw[kRawScl + tensor], part);
     else (img == 0 ? bf2 : bf1)[e0] = part_bits<__bf16>(v, part);
     return;
   }
@@ -146,8 +139,8 @@ __device__ __forceinline__ void pack16_at(const RawParams& rp, uint16_t* __restr
 
 // Transposed f16x3 images of the delta chain (element e of the backward stream), each tensor
 // scaled by the forward image's power of two (raw[kRawScl + tensor], k_wscale)
-__device__ __forceinline__ void pack16_bwd_at(const RawParams& rp, uint16_t* __restrict__ out, const int64_t e,
-                                              const float (&scl)[5]) {
+__device__ __forceinline__ void pack16_bwd_at(const RawParams& rp, uint16_t* __restrict__ out,
+                                              const float* __restrict__ raw, const int64_t e) {
   if (e >= kBwdBytes / 2) return;
   static_assert(kBwdBytes < (1LL << 31), "32-bit pack indices");
   const int byte = 2 * (int)e;
@@ -178,7 +171,7 @@ __device__ __forceinline__ void pack16_bwd_at(const RawParams& rp, uint16_t* __r
       tensor = 0;
     }
   }
-  out[e] = part_bits<_Float16>(v * pick5(scl, tensor), part);
+  out[e] = part_bits<_Float16>(v * raw[kRawScl + tensor], part);
 }
 
 // The weight images of every precision in two launches (the Mapper repacks once per iteration, and
@@ -201,21 +194,15 @@ __global__ __launch_bounds__(1024) void k_pack_stage1(ScaleArgs sa, RawParams rp
   for (int64_t i = (int64_t)(blockIdx.x - nscale) * 1024 + threadIdx.x; i < kPackedFloats; i += stride)
     pack_fp32_at(rp, packed, i);
 }
-// (the scales come in through their own restrict pointer: uniform reads the compiler can prove
-// unclobbered become scalar loads; as vector loads of one line by every wave of the launch they
-// queued on one L2 channel -- measured 5.7 -> 18.7 us per launch for five per thread)
 __global__ __launch_bounds__(256) void k_pack_stage2(RawParams rp, float* __restrict__ packed, int nb_bwd,
-                                                     int64_t base16, const float* __restrict__ scl) {
+                                                     int64_t base16) {
   float* raw = packed + kOffRaw;
-  float sc[5];  // stage 1's scales
-#pragma unroll
-  for (int t = 0; t < 5; ++t) sc[t] = scl[t];
   if ((int)blockIdx.x < nb_bwd)
-    pack16_bwd_at(rp, reinterpret_cast<uint16_t*>(packed + kOffBwd), (int64_t)blockIdx.x * 256 + threadIdx.x, sc);
+    pack16_bwd_at(rp, reinterpret_cast<uint16_t*>(packed + kOffBwd), raw, (int64_t)blockIdx.x * 256 + threadIdx.x);
   else
     pack16_at(rp, reinterpret_cast<uint16_t*>(packed + kOffBf2), reinterpret_cast<uint16_t*>(packed + kOffBf1),
               reinterpret_cast<uint16_t*>(packed + kOffH2), raw,
-              base16 + (int64_t)(blockIdx.x - nb_bwd) * 256 + threadIdx.x, sc);
+              base16 + (int64_t)(blockIdx.x - nb_bwd) * 256 + threadIdx.x);
 }
 
 int launch_pack_all(const RawParams& rp, float* packed, hipStream_t st, int flags) {
@@ -236,8 +223,7 @@ int launch_pack_all(const RawParams& rp, float* packed, hipStream_t st, int flag
   const int64_t n16 = 2 * n2 + n1 + kRawWo + 4 * kHidden;
   const int64_t base16 = (flags & PNR_PACK_F16X3_ONLY) ? n2 + n1 : 0;  // from the f16x3 main image on
   const int nb2 = nb_bwd + (int)((n16 - base16 + 255) / 256);
-  hipLaunchKernelGGL(k_pack_stage2, dim3(nb2), dim3(256), 0, st, rp, packed, nb_bwd, base16,
-                     (const float*)(raw + kRawScl));
+  hipLaunchKernelGGL(k_pack_stage2, dim3(nb2), dim3(256), 0, st, rp, packed, nb_bwd, base16);
   return hip_status(hipGetLastError());
 }
 
@@ -253,8 +239,7 @@ struct FcRaw16 {
 
 // fc entry e = 8L + t: A[row = unit 32t + (lane&31)][k = channel perm(8s+j, lane>>5)] of Wc_L
 __device__ __forceinline__ void fc_pack16_at(const FcRaw16& fc, uint16_t* __restrict__ bf2, uint16_t* __restrict__ bf1,
-                                             uint16_t* __restrict__ h2, float* __restrict__ raw, int64_t idx,
-                                             const float (&scl)[5]) {
+                                             uint16_t* __restrict__ h2, float* __restrict__ raw, int64_t idx) {
   const int64_t n = kBfFcBytes / 2;  // elements per image
   if (idx < 3 * n) {
     const int img = (int)(idx / n);
@@ -274,7 +259,7 @@ __device__ __forceinline__ void fc_pack16_at(const FcRaw16& fc, uint16_t* __rest
       const int ch = perm(8 * s + j, lane >> 5);
       v = fc.at(2 * L)[unit * kCDim + ch];
     }
-    if (img == 2) h2[e] = part_bits<_Float16>(v * pick5(scl, L), part);
+    if (img == 2) h2[e] = part_bits<_Float16>(v * raw[kFcRawScl + L], part);
     else (img == 0 ? bf2 : bf1)[e] = part_bits<__bf16>(v, part);
     return;
   }
@@ -284,8 +269,8 @@ __device__ __forceinline__ void fc_pack16_at(const FcRaw16& fc, uint16_t* __rest
 
 // fc backward entry e = 8(3 - l) + t: A[row = channel (lane&31)][k = unit 32t + perm(8s+j, lane>>5)]
 // = Wc_l[unit][channel], f16x3 scaled like the forward image (raw[kFcRawScl + l])
-__device__ __forceinline__ void fc_pack16_bwd_at(const FcRaw16& fc, uint16_t* __restrict__ out, int64_t e,
-                                                 const float (&scl)[5]) {
+__device__ __forceinline__ void fc_pack16_bwd_at(const FcRaw16& fc, uint16_t* __restrict__ out,
+                                                 const float* __restrict__ raw, int64_t e) {
   if (e >= kBfFcBytes / 2) return;
   const int ent = (int)(e / 2048);
   int64_t r = e % 2048;
@@ -295,7 +280,7 @@ __device__ __forceinline__ void fc_pack16_bwd_at(const FcRaw16& fc, uint16_t* __
   const int s = (int)(r / 2);
   const int l = 3 - ent / 8, t = ent % 8;
   const int unit = 32 * t + perm(8 * s + j, lane >> 5);
-  out[e] = part_bits<_Float16>(fc.at(2 * l)[unit * kCDim + (lane & 31)] * pick5(scl, l), part);
+  out[e] = part_bits<_Float16>(fc.at(2 * l)[unit * kCDim + (lane & 31)] * raw[kFcRawScl + l], part);
 }
 
 // The fc_c images in two launches, as the main images (launch_pack_all): stage 1 the four fc weight
@@ -312,18 +297,14 @@ __global__ __launch_bounds__(1024) void k_fc_stage1(ScaleArgs sa, FcRaw fr, floa
   for (int64_t i = (int64_t)(blockIdx.x - nscale) * 1024 + threadIdx.x; i < kFcPackedFloats; i += stride)
     fc_pack_fp32_at(fr, out, i);
 }
-__global__ __launch_bounds__(256) void k_fc_stage2(FcRaw16 fc, float* __restrict__ out, int64_t base,
-                                                   const float* __restrict__ scl) {
+__global__ __launch_bounds__(256) void k_fc_stage2(FcRaw16 fc, float* __restrict__ out, int64_t base) {
   float* raw = out + kOffFcRaw;
-  float sc[5];  // stage 1's scales of Wc_0..Wc_3 (scalar loads: see k_pack_stage2)
-#pragma unroll
-  for (int t = 0; t < 5; ++t) sc[t] = t < 4 ? scl[t] : 1.f;
   const int64_t idx = base + (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (idx < kFc16N)
     fc_pack16_at(fc, reinterpret_cast<uint16_t*>(out + kOffFcBf2), reinterpret_cast<uint16_t*>(out + kOffFcBf1),
-                 reinterpret_cast<uint16_t*>(out + kOffFcH2), raw, idx, sc);
+                 reinterpret_cast<uint16_t*>(out + kOffFcH2), raw, idx);
   else
-    fc_pack16_bwd_at(fc, reinterpret_cast<uint16_t*>(out + kOffFcBwd), idx - kFc16N, sc);
+    fc_pack16_bwd_at(fc, reinterpret_cast<uint16_t*>(out + kOffFcBwd), raw, idx - kFc16N);
 }
 
 int launch_fc_pack_all(const float* const* fcp, float* out, hipStream_t st, int flags) {
@@ -343,8 +324,7 @@ int launch_fc_pack_all(const float* const* fcp, float* out, hipStream_t st, int 
   hipLaunchKernelGGL(k_fc_stage1, dim3(nscale + nimg), dim3(1024), 0, st, sa, fr, out, nscale);
   const int64_t n2 = kFc16N + kBfFcBytes / 2;
   const int64_t base = (flags & PNR_PACK_F16X3_ONLY) ? 2 * (kBfFcBytes / 2) : 0;  // from the f16x3 image on
-  hipLaunchKernelGGL(k_fc_stage2, dim3((unsigned)((n2 - base + 255) / 256)), dim3(256), 0, st, r, out, base,
-                     (const float*)(raw + kFcRawScl));
+  hipLaunchKernelGGL(k_fc_stage2, dim3((unsigned)((n2 - base + 255) / 256)), dim3(256), 0, st, r, out, base);
   return hip_status(hipGetLastError());
 }
 
