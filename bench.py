@@ -391,16 +391,18 @@ def kernel_roofline(kt, prec, el_s, traffic_units=True):
             kprec = prec if name == 'mlp_fwd' else ('fp32' if prec == 'fp32' else 'f16x3')
             kname = ('k_mlp_fwd16' if prec != 'fp32' else 'k_mlp_fwd') if name == 'mlp_fwd' else \
                 ('k_mlp_bwd16' if prec != 'fp32' else 'k_mlp_bwd')
+        # PMC traffic is kept per training point: the grouped launch's points are the delta chain's
+        pts = (kt['mlp_bwd'][2] / launches if 'mlp_bwd' in kt else None) if name == 'wgrad_group' else units / launches
         cand = {'kernel': kname, 'launches': launches, 'prec': kprec, 'peak': ALGO_PEAK_TF[kprec],
                 'avg_ms': ms / launches, 'share_of_step': ms / (el_s * 1e3), 'units': units / launches,
-                'achieved': fl * units / launches / (ms / launches * 1e-3) / 1e12, '_ms': ms}
+                'points': pts, 'achieved': fl * units / launches / (ms / launches * 1e-3) / 1e12, '_ms': ms}
         if best is None or ms > best['_ms']:
             best = cand
     if best is None:
         return None
     tkey = {'k_mlp_fwd': 'k_mlp_fwd_train', 'k_mlp_fwd16': 'k_mlp_fwd16_train', 'k_mlp_bwd': 'k_mlp_bwd',
-            'k_mlp_bwd16': 'k_mlp_bwd16'}
-    traffic = pmc_traffic(tkey[best['kernel']], best['units']) if traffic_units and best['kernel'] in tkey else None
+            'k_mlp_bwd16': 'k_mlp_bwd16', 'k_wgrad16_group': 'k_wgrad16_group'}
+    traffic = pmc_traffic(tkey[best['kernel']], best['points']) if traffic_units and best['points'] else None
     return {'bound': 'mfma', 'achieved': round(best['achieved'], 2), 'peak': round(best['peak'], 1),
             'unit': 'TFLOP/s', 'frac': round(best['achieved'] / best['peak'], 4), 'traffic': traffic,
             'kernel': best['kernel'], 'avg_launch_ms': round(best['avg_ms'], 3), 'launches': best['launches'],

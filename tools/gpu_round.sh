@@ -12,6 +12,7 @@
 #   aux         the auxiliary benches: Tracker, render_img, Mesher grid, configs C3 / C5
 #   timeline    rocprofv3 kernel trace of the replayed room0 iteration -> ${TAG}_room0_timeline.txt
 #   pmcsearch   the gather search's stall counters (tools/pmc_search.sh)
+#   mpstats     rocprofv3 kernel stats of the neural-point S-map (--workload map-points)
 #   npf         the faithful-size neural-point iterations C3 / C5 (tools/np_faithful.py) + their kernel stats
 #   prof        the round profile: rocprofv3 kernel stats + FETCH/WRITE and MFMA-busy PMC passes
 #               (tools/prof_round.sh), the gather's traffic passes and kernel stats, the faithful
@@ -79,6 +80,11 @@ for step in "$@"; do
       run 300 gpurun_out/prof_${TAG}_c5.log rocprofv3 --kernel-trace --stats --output-format csv \
         -d gpurun_out/prof_${TAG}_c5 -o c5 -- python3 tools/np_faithful.py --case C5 --iters 20
       echo npf-prof ;;
+    mpstats)
+      run 300 gpurun_out/prof_${TAG}_mp.log rocprofv3 --kernel-trace --stats --output-format csv \
+        -d gpurun_out/prof_${TAG}_mp -o mp -- python3 bench.py --workload map-points --steps 3 --warmup 1 \
+        --no-cpu-baseline --no-gather
+      echo mpstats ;;
     aux)
       run 200 ${O}_track.json python3 tools/track_bench.py
       run 200 ${O}_render.json python3 tools/render_bench.py
