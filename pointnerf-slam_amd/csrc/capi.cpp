@@ -16,6 +16,7 @@
 #include <cmath>
 #include <cstddef>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <vector>
@@ -341,7 +342,11 @@ int mlp_backward_core(int prec, const float* packed, const SaveArgs& sv, int64_t
       // These GEMMs (and the fc_c ones below) are independent: prepared here, launched as one group.
       WgradSyn syn{reinterpret_cast<const float4*>(b.g_out + p0 * 4), sv.masks + 3 * (sv.ld / 32) * 64, p0 / 32,
                    packed + packed_raw_wo_offset(), sv.xP + p0, packed + packed_raw_fb_offset(), pp, pb, nullptr,
-                   (grads ? 4 : 0) + (want_fc ? 4 : 0), skinny_in_group ? device_cu_count() / 8 : 0};
+                   (grads ? 4 : 0) + (want_fc ? 4 : 0), skinny_in_group ? device_cu_count() / 8 : 0, 0.f};
+      if (grads)
+        syn.group_weight += wgrad16_job_weight(kWgradOutDelta, false) + 2 * wgrad16_job_weight(kWgradHidden, false) +
+                            wgrad16_job_weight(kWgradFirstX, false);
+      if (want_fc) syn.group_weight += 3 * wgrad16_job_weight(kWgradFc, false) + wgrad16_job_weight(kWgradFcOut, false);
       // with the feature branch k_mlp_bwd16 stores dL/dh_l only: delta_l = dL/dh_l masked in the GEMM
       const bool fmask = fb != nullptr;
       const int64_t mstride = (sv.ld / 32) * 64;
@@ -389,7 +394,14 @@ int mlp_backward_core(int prec, const float* packed, const SaveArgs& sv, int64_t
           took();
         }
       }
-      if (rc == 0) rc = launch_wgrad16_group(gjobs, ng, st);
+      // diagnostics (PNR_WGRAD_SPLIT=1): each job as a launch of its own, so a kernel trace times every
+      // GEMM kind at its grouped grid (the per-kind costs behind wgrad16_prepare's sizing weights)
+      static const bool split_jobs = getenv("PNR_WGRAD_SPLIT") && getenv("PNR_WGRAD_SPLIT")[0] == '1';
+      if (rc == 0 && split_jobs) {
+        for (int i = 0; i < ng && rc == 0; ++i) rc = launch_wgrad16_group(gjobs + i, 1, st);
+      } else if (rc == 0) {
+        rc = launch_wgrad16_group(gjobs, ng, st);
+      }
     } else if (grads) {
       const float* hp = sv.hP + p0 * kHidden;
       rc = launch_wgrad(kWgradOut, b.g_out + p0 * 4, 4, hp + 3 * hstride, kHidden, C, grads[9], kHidden, grads[10],

@@ -270,9 +270,15 @@ struct WgradSyn {
   // GEMMs that will share one grouped launch (launch_wgrad16_group), 0 = a launch of its own (see
   // wgrad16_prepare's grid rule)
   int group_jobs;
+  // the group's summed per-tile cost weights (wgrad16_job_weight): a GEMM kind that costs less per
+  // tile gets more tiles per workgroup, so the grouped launch's workgroups finish together
   // CUs left to the grouped launch's skinny jobs (dWo / dB) when the GEMMs are sized to fill the chip once
   int reserve_cus;
+  float group_weight;
 };
+// relative cost per 32-point tile of a split weight-gradient GEMM kind in a grouped launch (measured
+// one job per launch at its grouped grid, PNR_WGRAD_SPLIT=1: room0 and C3 batches)
+float wgrad16_job_weight(int kind, bool masked);
 // Arguments of one split weight-gradient GEMM (wgrad16.hip k_wgrad16)
 struct WxArgs {
   const float* A;      // [K][256]

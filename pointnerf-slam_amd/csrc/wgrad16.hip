@@ -607,6 +607,20 @@ static int launch_k(const WxArgs& a, hipStream_t st, ReduceJob* defer) {
 // K is rounded up to 32 (the A rows up to it exist and carry zero deltas).  Fills the job's
 // arguments, its kernel variant and its reduction (the partials go to the backward's scratch:
 // WgradSyn part / part_bias).
+// per-tile costs measured with PNR_WGRAD_SPLIT=1 (one job per launch, 28-56 workgroups, 43-85 tiles each):
+// dW3 (delta4 rebuilt) 2.79-2.85 us, dW2 / dW1 2.50-2.85, dW0 (e recomputed) 1.74-2.14, dWc 1.00-1.09 per
+// tile: relative to a plain hidden GEMM
+float wgrad16_job_weight(int kind, bool masked) {
+  (void)masked;
+  switch (kind) {
+    case kWgradOutDelta: return 1.05f;
+    case kWgradFirstX: return 0.72f;
+    case kWgradFc: return 0.38f;
+    case kWgradFcOut: return 0.40f;
+    default: return 1.0f;
+  }
+}
+
 int wgrad16_prepare(int kind, const float* A, const float* B, int64_t K, int64_t kb_rows, float* C, int64_t ldc,
                     float* bias, const WgradSyn* syn, Wgrad16Job* job, ReduceJob* red) {
   if (kb_rows <= 0) return PNR_E_ARG;
@@ -625,7 +639,14 @@ int wgrad16_prepare(int kind, const float* A, const float* B, int64_t K, int64_t
   if (syn->group_jobs > 0) {
     const int64_t cus = device_cu_count() - syn->reserve_cus;
     const int64_t fill = (tiles * syn->group_jobs + cus - 1) / cus;
-    if (fill <= 256) per = fill > per ? fill : per;
+    if (fill <= 256) {
+      // one round of workgroups: tiles per workgroup so that every job's workgroups take about the same
+      // time (the group's summed cost over the CUs, divided by this kind's cost per tile)
+      const float w = wgrad16_job_weight(kind, syn->amasks != nullptr);
+      const float gw = syn->group_weight > 0.f ? syn->group_weight : (float)syn->group_jobs;
+      const int64_t wfill = (int64_t)((double)tiles * gw / ((double)cus * w) + 0.999);
+      per = wfill > per ? wfill : per;
+    }
   }
   int64_t nwg = (tiles + per - 1) / per;
   nwg = nwg < 4 ? 4 : (nwg > kWgrad16MaxWg ? kWgrad16MaxWg : nwg);
