@@ -92,6 +92,19 @@ def test_workspace_queries_and_arg_errors(lib):
     assert L.pnr_adam_step(None, None, None, None, 5, 1e-3, 0.9, 0.999, 1e-8, 0, None) == -1
     assert L.pnr_adam_step_dev(None, None, None, None, 5, 1e-3, 0.9, 0.999, 1e-8, None, None) == -1
     assert L.pnr_step_advance(None, None) == -1
+    # ABI 13 / 14: the one-call map step (workspace = the map workspace + its per-ray scratch; a missing
+    # loss or loss workspace is an argument error) and the flagged repacks (unknown flag bits refused)
+    mp = _lib.RenderParams()
+    mp.n_samples, mp.n_importance, mp.precision = 32, 12, 3
+    assert L.pnr_map_step_workspace_bytes(ctypes.byref(mp), 1000) > L.pnr_map_workspace_bytes(ctypes.byref(mp), 1000)
+    assert L.pnr_map_step_workspace_bytes(ctypes.byref(bad), 1000) == 0
+    assert L.pnr_map_step(ctypes.byref(mp), ctypes.c_void_p(1), None, None, None, None, None, 10, 0.2, 5e-4, None,
+                          None, None, 0, None, 0, None, None) == -1
+    arr = _lib.PtrArray(*([1] * _lib.N_PARAMS))
+    assert L.pnr_mlp_pack2(arr, ctypes.c_void_p(1), 4, None) == -1
+    assert L.pnr_mlp_pack2(arr, None, _lib.PACK_F16X3_ONLY, None) == -1
+    farr = _lib.FcPtrArray(*([1] * _lib.N_FC_PARAMS))
+    assert L.pnr_fc_pack2(farr, ctypes.c_void_p(1), 1, None) == -1
     # zero-sized calls are no-ops
     assert L.pnr_eval_points(ctypes.c_void_p(1), None, 0, None, None, 0, None) == 0
 
