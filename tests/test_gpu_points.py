@@ -54,11 +54,14 @@ def pnr_mod():
 # fraction of the elements, each by about one sample's share: ~max|g| / n for n samples (~2.7e4 here).
 # FLIP_CAP = 5e-4 max|g| admits about a dozen such terms, and only on a bounded share of the elements:
 # at most FLIP_FRAC of a tensor's elements (at least one) may use the allowance, i.e. lie beyond the
-# strict bound.  Measured maxima (round 4): 1.42% of fc_c.1.weight and 0.95% of fc_c.0.weight (the
-# trilinear render: 2% there, see test_render_with_points_matches_oracle), 0.26% of dL/drays_o (IDW tracking), 0.15% of pts_linears.0.weight, one of C3's
-# 256 pts_linears.2.bias.
+# strict bound.  Measured maxima (round 5, per test and precision, tools/_flips.sh -> profiles/r05_flips.txt):
+# fp32 trilinear render 1.40% of fc_c.1.weight, 0.96% of fc_c.0.weight, 0.51% of pts_linears.1.weight (2%
+# there, see test_render_with_points_matches_oracle) and 0.19% of dL/dfeats; f16x3 trilinear render
+# 0.16% of pts_linears.0.weight; one element of dL/drays_o (fp32 IDW tracking, 1 of 384); every IDW
+# render / small-feature / regulation case 0.  FLIP_FRAC 3e-3 holds everything but the fp32 trilinear
+# weight gradients.
 FLIP_CAP = 5e-4
-FLIP_FRAC = 1e-2
+FLIP_FRAC = 3e-3
 # summation-magnitude floor, in ulps (u = 2^-24) of M = sum_p |t_p|: a gradient element is a sum over
 # samples of terms that each carry a few ulps from the forward / delta chain, and the sum itself
 # rounds in a blocked order; 64 u M bounds both (an element without cancellation has M ~ |g|, where
@@ -344,7 +347,7 @@ def make_renderer(pnr, scene_bound):
 
 
 @pytest.mark.parametrize('mode', ['idw', 'trilinear'])
-def test_render_with_points_matches_oracle(pnr_mod, dev, mode):
+def test_render_with_points_matches_oracle(pnr_mod, dev, mode, precision):
     scene = load_golden('scene.npz')
     bound = torch.from_numpy(scene['bound'])
     ro, rd, gt, xyz, feats = surface_cloud(dev)
@@ -382,9 +385,10 @@ def test_render_with_points_matches_oracle(pnr_mod, dev, mode):
             close(v, vr, 1e-8, 'var', rtol=2e-3)
     # the fc_c weight gradients (dL/dh_l)^T c are rank-1 sums in which every sample's feature row
     # enters every element, so one flipped sample moves all of them: measured 1.42% of fc_c.1.weight
-    # (fp32, trilinear, this seeded probe gc_), hence 2% for this test's tensors
+    # (fp32, trilinear, this seeded probe gc_), hence 2% for that case's weight tensors
+    wfrac = 2e-2 if (precision == 'fp32' and mode == 'trilinear') else FLIP_FRAC
     for k, t in dec.named_parameters():
-        grad_elementwise(t.grad, refs[True][0][k], refs[False][0][k], k, flips=True, mag=mags[k], flip_frac=2e-2)
+        grad_elementwise(t.grad, refs[True][0][k], refs[False][0][k], k, flips=True, mag=mags[k], flip_frac=wfrac)
     grad_elementwise(pts.feats.grad, refs[True][1], refs[False][1], 'dL/dfeats', flips=True, mag=mags['feats'])
 
 
