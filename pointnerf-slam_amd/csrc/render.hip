@@ -819,24 +819,22 @@ __global__ __launch_bounds__(256) void k_map_loss(const float* __restrict__ gt, 
   __syncthreads();
   // the block's partial, then a ticket: the block that takes the last one adds every partial in a
   // fixed order (one launch; the sum is the same whichever block finishes last).  Hand-off per
-  // MI355X_MICROARCH.md (Valid forms): store, vmcnt(0), agent release, vmcnt(0), ticket atomic;
-  // the last block: agent acquire, vmcnt(0), barrier, plain loads.
+  // MI355X_MICROARCH.md (Valid forms): the partial as an 8-B agent atomic, vmcnt(0), ticket atomic;
+  // the last block reads the partials by 8-B agent atomics (no per-block L2 write-back, which a
+  // release fence costs)
   __shared__ uint32_t last;
   if (threadIdx.x == 0) {
-    part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    atomicExch(reinterpret_cast<unsigned long long*>(part) + blockIdx.x,
+               (unsigned long long)__double_as_longlong((red[0] + red[1]) + (red[2] + red[3])));
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const uint32_t t = atomicAdd(ticket, 1u);
     last = t == gridDim.x - 1 ? 1u : 0u;
-    if (last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
   }
   __syncthreads();
   if (!last) return;
-  double v = (int)threadIdx.x < (int)gridDim.x ? part[threadIdx.x] : 0.0;
+  double v = (int)threadIdx.x < (int)gridDim.x
+                 ? __longlong_as_double((long long)atomicAdd(reinterpret_cast<unsigned long long*>(part) + threadIdx.x, 0ull))
+                 : 0.0;
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
   __syncthreads();
@@ -1088,9 +1086,9 @@ struct SampleState {
   int64_t batch;
   uint32_t ticket;
   uint32_t pad;
-  float part[kSampleParts];
+  uint64_t part[kSampleParts];  // per-block gt maxima (float bits), written and read by 8-B atomics
 };
-static_assert(sizeof(SampleState) == 16 + 4 * kSampleParts, "sampler state layout");
+static_assert(sizeof(SampleState) == 16 + 8 * kSampleParts, "sampler state layout");
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {
   z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
   z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
@@ -1136,23 +1134,19 @@ __global__ __launch_bounds__(256) void k_window_sample(uint64_t seed, SampleStat
     }
   }
   m = block_max_256(m, red);
-  // ticket hand-off as k_map_loss; the last block reduces the maxima and advances the batch
+  // ticket hand-off as k_map_loss (8-B agent atomics both sides); the last block reduces the maxima
+  // and advances the batch
   if (threadIdx.x == 0) {
-    if ((int)blockIdx.x < nbr) stt->part[blockIdx.x] = m;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    if ((int)blockIdx.x < nbr) atomicExch(stt->part + blockIdx.x, (unsigned long long)__float_as_uint(m));
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const uint32_t t = atomicAdd(&stt->ticket, 1u);
     last = t == gridDim.x - 1 ? 1u : 0u;
-    if (last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
   }
   __syncthreads();
   if (!last) return;
   __shared__ float red2[4];
-  const float v = block_max_256((int)threadIdx.x < nbr ? stt->part[threadIdx.x] : -INFINITY, red2);
+  const float v = block_max_256(
+      (int)threadIdx.x < nbr ? __uint_as_float((uint32_t)atomicAdd(stt->part + threadIdx.x, 0ull)) : -INFINITY, red2);
   if (threadIdx.x == 0) {
     if (far_out) far_out[0] = v;
     stt->batch = batch + 1;
