@@ -74,6 +74,10 @@ int launch_fine_loss(const pnr_render_params&, const float*, const double*, cons
 using namespace pnr;
 
 // ---- diagnostics: kernel timing --------------------------------------------------------------
+// CUs left to the skinny dWo / dB jobs of a grouped weight-gradient launch that fills the chip once: 1/8
+#ifndef PNR_SKINNY_CU_DIV
+#define PNR_SKINNY_CU_DIV 8
+#endif
 namespace {
 struct TimedLaunch {
   hipEvent_t a, b;
@@ -342,7 +346,7 @@ int mlp_backward_core(int prec, const float* packed, const SaveArgs& sv, int64_t
       // These GEMMs (and the fc_c ones below) are independent: prepared here, launched as one group.
       WgradSyn syn{reinterpret_cast<const float4*>(b.g_out + p0 * 4), sv.masks + 3 * (sv.ld / 32) * 64, p0 / 32,
                    packed + packed_raw_wo_offset(), sv.xP + p0, packed + packed_raw_fb_offset(), pp, pb, nullptr,
-                   (grads ? 4 : 0) + (want_fc ? 4 : 0), skinny_in_group ? device_cu_count() / 8 : 0, 0.f};
+                   (grads ? 4 : 0) + (want_fc ? 4 : 0), skinny_in_group ? device_cu_count() / PNR_SKINNY_CU_DIV : 0, 0.f};
       if (grads)
         syn.group_weight += wgrad16_job_weight(kWgradOutDelta, false) + 2 * wgrad16_job_weight(kWgradHidden, false) +
                             wgrad16_job_weight(kWgradFirstX, false);
