@@ -73,11 +73,14 @@ int launch_fine_loss(const pnr_render_params&, const float*, const double*, cons
 
 using namespace pnr;
 
-// ---- diagnostics: kernel timing --------------------------------------------------------------
-// CUs left to the skinny dWo / dB jobs of a grouped weight-gradient launch that fills the chip once: 1/8
+// CUs left to the skinny dWo / dB jobs of a grouped weight-gradient launch that fills the chip once: 1/16
+// (A/B, room0 / C3 graph ms: 1/8 0.521-0.523 / 0.854-0.859, 1/16 0.518-0.519 / 0.833-0.842, 1/32 and
+// 1/64 the same as 1/16 within noise, 1/4 0.526)
 #ifndef PNR_SKINNY_CU_DIV
-#define PNR_SKINNY_CU_DIV 8
+#define PNR_SKINNY_CU_DIV 16
 #endif
+
+// ---- diagnostics: kernel timing --------------------------------------------------------------
 namespace {
 struct TimedLaunch {
   hipEvent_t a, b;
@@ -331,7 +334,7 @@ int mlp_backward_core(int prec, const float* packed, const SaveArgs& sv, int64_t
     int rc = 0;
     // The skinny fp32 GEMMs of the split precisions -- dWo (4x256) += g_out^T h4, dbo += colsum(g_out)
     // and dB (3x93) += x^T g_arg -- are jobs of the grouped weight-gradient launch: its GEMMs are sized to
-    // leave them 1/8 of the CUs when they fill the chip once (the Mapper's 1,000-ray batch), so the two
+    // leave them 1/16 of the CUs (PNR_SKINNY_CU_DIV) when they fill the chip once (the Mapper's 1,000-ray batch), so the two
     // bandwidth-bound streams run beside the GEMMs instead of as launches of their own (dWo ahead of the
     // delta chain, dB behind the GEMMs: 30 us of the iteration's critical path).
     const bool skinny_in_group = split && grads;
