@@ -610,11 +610,16 @@ static int launch_k(const WxArgs& a, hipStream_t st, ReduceJob* defer) {
 // per-tile costs measured with PNR_WGRAD_SPLIT=1 (one job per launch, 28-56 workgroups, 43-85 tiles each):
 // dW3 (delta4 rebuilt) 2.79-2.85 us, dW2 / dW1 2.50-2.85, dW0 (e recomputed) 1.74-2.14, dWc 1.00-1.09 per
 // tile: relative to a plain hidden GEMM
+// (the first-layer weight as a build knob; A/B at the end of round 5, room0 / C3 graph ms: 0.60 -> C3
+// 0.863-0.864, 0.85 -> 0.514-0.516 / 0.835-0.837, 0.72 -> 0.516-0.518 / 0.832-0.839: kept)
+#ifndef PNR_W_FIRSTX
+#define PNR_W_FIRSTX 0.72f
+#endif
 float wgrad16_job_weight(int kind, bool masked) {
   (void)masked;
   switch (kind) {
     case kWgradOutDelta: return 1.05f;
-    case kWgradFirstX: return 0.72f;
+    case kWgradFirstX: return PNR_W_FIRSTX;
     case kWgradFc: return 0.38f;
     case kWgradFcOut: return 0.40f;
     default: return 1.0f;
