@@ -25,9 +25,11 @@ Extra keys of the default line (measured after the timed region, never part of `
                   the oracle's CPU rate
   fp32            the S-map step with fp32-MFMA decoder arithmetic
   gather_roofline the neural-point gather (A15) on its HBM roofline
-N>1 lines (one rank per GPU, RCCL) carry `smap` (weak: 307,200 rays per GPU) and `fixed_global_batch`
-(ONE 307,200-ray batch split over the ranks: strong scaling) and `distributed` (the
-backend and world size the ranks saw).
+  room0_iter_fp32 the headline's room0 iteration (graph replay) in strict fp32 MFMA (config C2's precision)
+N>1 lines (one rank per GPU, RCCL) carry `smap` (weak: 307,200 rays per GPU), `fixed_global_batch`
+(ONE 307,200-ray batch split over the ranks: strong scaling), `sfwd` (weak: 640x480 x 64
+samples per GPU) and `sfwd_fixed_global` (one 640x480 batch split over the ranks), rank 0's
+`gather_roofline`, and `distributed` (the backend and world size the ranks saw).
 
 Data: synthetic.  Decoder = the trained room0 weights committed as a golden fixture
 (tests/golden/weights.npz, from the reference's own checkpoint) -- random init if absent.  room0: renders
@@ -489,27 +491,40 @@ def map_step_fn(pnr, renderer, dec, cfg, ro, rd, gt, col, dev, ddp=None, points=
     return step
 
 
-def sfwd_extra(pnr, plib, slam, params, bound, pose, dev, ddp, lib, steps=10, cpu=True):
+def sfwd_extra(pnr, plib, slam, params, bound, pose, dev, ddp, lib, steps=10, cpu=True, rank=0, world=1,
+               fixed_global=False):
     """S-fwd: render_batch_ray forward over the 640x480 batch at 64 stratified
-    samples, no importance, gt_depth None; roofline of k_mlp_fwd16 (eval) and the oracle CPU rate."""
+    samples, no importance, gt_depth None; roofline of k_mlp_fwd16 (eval) and the oracle CPU rate.
+    Data parallel: every rank renders its own 640x480 batch (weak, seed = rank), or -- fixed_global --
+    its contiguous share of ONE 640x480 batch (strong).  gt_depth None leaves no batch-global coupling
+    (the far clamp of src/utils/Renderer.py:112 needs gt), so the ranks exchange nothing."""
     import copy
     cfg = copy.deepcopy(pnr.ROOM0_CFG)
     cfg['rendering']['N_samples'], cfg['rendering']['N_importance'] = 64, 0
     r = pnr.Renderer(cfg, None, slam)
     dec = make_decoder(pnr, cfg, params, dev)
-    ro, rd, _, _ = synth_batch(W * H, 0, pose, dev)
+    if fixed_global:
+        from pnr import dist as pdist
+        a, b = pdist.shard_bounds(W * H, rank, world)
+        ro, rd = [t[a:b].contiguous() for t in synth_batch(W * H, 0, pose, dev)[:2]]
+    else:
+        ro, rd, _, _ = synth_batch(W * H, rank, pose, dev)
+    total = W * H if fixed_global else W * H * world
 
     def step():
         with torch.no_grad():
             r.render_batch_ray({}, dec, rd, ro, dev, 'color', gt_depth=None)
     el, kt = timed(step, steps, 2, ddp, lib)
     prec = plib.DEFAULT_PRECISION
-    out = {'workload': 'S-fwd: render_batch_ray forward, 640x480 rays x 64 stratified samples, gt_depth None',
-           'value': round(W * H * steps / el, 1), 'unit': 'rays/s', 'ms_per_step': round(el / steps * 1e3, 3),
-           'steps': steps, 'roofline': kernel_roofline(kt, prec, el, traffic_units=False)}
+    out = {'workload': 'S-fwd: render_batch_ray forward, 640x480 rays x 64 stratified samples, gt_depth None'
+                       + (' (ONE batch split over the ranks)' if fixed_global else ' per GPU'),
+           'value': round(total * steps / el, 1), 'unit': 'rays/s', 'ms_per_step': round(el / steps * 1e3, 3),
+           'steps': steps, 'n_gpus': world, 'scaling': 'strong' if fixed_global else 'weak',
+           'rays_per_gpu': int(ro.shape[0]), 'global_batch': total,
+           'roofline': kernel_roofline(kt, prec, el, traffic_units=False)}
     if out['roofline'] is not None:
         out['roofline']['kernel'] += ' (eval, no activation saves)'
-    if cpu and params is not None:
+    if cpu and params is not None and world == 1:
         def gpu_render(ro_c, rd_c, gt_c):
             with torch.no_grad():
                 d, _, c = r.render_batch_ray({}, dec, rd_c.to(dev), ro_c.to(dev), dev, 'color', gt_depth=None)
@@ -610,7 +625,8 @@ def room0_window(pnr, params, bound, dev):
     return slam, frames
 
 
-def room0_extra(pnr, params, bound, pose, dev, ddp, lib, steps=100, warmup=5, cpu=True, graph=True, rank=0):
+def room0_extra(pnr, params, bound, pose, dev, ddp, lib, steps=100, warmup=5, cpu=True, graph=True, rank=0,
+                prec='f16x3'):
     """The metric's own workload: ONE room0 Mapper iteration (src/Mapper.py:507-662) at its real size,
     1,000 rays over the 5-frame window (200 per frame) of the room0 camera, gt = the decoder's own
     rendered depth / colour.  Timed per iteration: the window batch (pnr_window_sample: pixels, jitter
@@ -642,19 +658,21 @@ def room0_extra(pnr, params, bound, pose, dev, ddp, lib, steps=100, warmup=5, cp
     # a graph replay has no per-launch host hook): the MLP kernels' rooflines at this batch size
     el_e, kt = timed(lambda: mstep(*sampler()), 20, 3, ddp, lib)
     tf = MAP_FLOP_PER_RAY * rate / 1e12
-    peak = ALGO_PEAK_TF['f16x3']
+    peak = ALGO_PEAK_TF['fp32' if prec == 'fp32' else 'f16x3']
     out = {'workload': 'room0 Mapper iteration: 1,000 rays = 5-frame window x 200 uniform pixels on the 680x1200 '
                        'fx=fy=600 camera, gt = rendered depth / colour (S-ref); window sampling + render (32+12) + '
                        'regulation (32) + L1 losses + backward + Adam in one replayed HIP graph',
            'rays_per_iter': n, 'ms_per_iter': round(el / steps * 1e3, 4), 'rays_per_s': round(rate, 1),
            'graph': graph, 'iters': steps, 'achieved_tflops': round(tf, 2), 'frac_of_split_peak': round(tf / peak, 4),
-           'flop_basis': '115.29 MFLOP per ray per mapping iteration (SURVEY.md 8(d)); peak 833 TF (f16 MFMA / 3)',
+           'flop_basis': '115.29 MFLOP per ray per mapping iteration (SURVEY.md 8(d)); peak '
+                         + ('157.3 TF (fp32 MFMA)' if prec == 'fp32' else '833 TF (f16 MFMA / 3)'),
+           'decoder_precision': prec, 'dtype': DTYPE[prec],
            'eager_ms_per_iter': round(el_e / 20 * 1e3, 4),
-           'roofline': kernel_roofline(kt, 'f16x3', el_e, traffic_units=True),
-           'kernel_rooflines': kernel_table(kt, 'f16x3', el_e, 20),
-           'kernel_profile': 'profiles/r05_room0_timeline.txt, profiles/r05_room0_kernel_stats.csv (rocprofv3 of '
+           'roofline': kernel_roofline(kt, prec, el_e, traffic_units=prec != 'fp32'),
+           'kernel_rooflines': kernel_table(kt, prec, el_e, 20) if prec != 'fp32' else None,
+           'kernel_profile': 'profiles/r06_room0_timeline.txt, profiles/r06_room0_kernel_stats.csv (rocprofv3 of '
                              'the graph replay)'}
-    if cpu:
+    if cpu and prec != 'fp32':
         rays = sampler()[:4]
         cr = oracle_map_rate(bound, pose, params, n, rays=rays)
         out['cpu_baseline'] = {'value': round(cr, 1), 'unit': 'rays/s', 'cores': cpu_threads(), 'kind': 'port',
@@ -823,6 +841,11 @@ def main():
             if world > 1:
                 extras['fixed_global_batch'] = fixed_global_run(pnr, slam, params, pose, dev, ddp, lib, rank, world,
                                                                 steps=5, warmup=2)
+                # the north star's S-fwd curve (640x480 x 64 samples) at every N: weak and fixed-global forms
+                extras['sfwd'] = sfwd_extra(pnr, plib, slam, params, bound, pose, dev, ddp, lib, cpu=False, rank=rank,
+                                            world=world)
+                extras['sfwd_fixed_global'] = sfwd_extra(pnr, plib, slam, params, bound, pose, dev, ddp, lib,
+                                                         cpu=False, rank=rank, world=world, fixed_global=True)
             elif params is not None:
                 extras.update(n1_extras(pnr, plib, slam, params, bound, pose, dev, ddp, lib, prec, args, cpu_ok))
         if rank == 0:
@@ -841,10 +864,12 @@ def main():
             if 'smap' in extras:  # the S-map rays/s next to the headline (SURVEY.md 8(d) throughput batch)
                 out['smap_value'] = extras['smap']['value']
             out.update(extras)
-            if world == 1 and not args.no_gather and not args.no_extras and params is not None:
+            if not args.no_gather and not args.no_extras and params is not None:
+                # single-GPU kernel line (rank 0's GPU at N > 1, after every rank's timed regions)
                 out['gather_roofline'] = gather_roofline(dev, feat_dtype=args.feat_dtype)
             print(json.dumps(out), flush=True)
         if world > 1:
+            ddp.barrier()
             torch.distributed.destroy_process_group()
         return
 
@@ -1013,6 +1038,13 @@ def n1_extras(pnr, plib, slam, params, bound, pose, dev, ddp, lib, prec, args, c
         extras['fp32'] = {'value': round(n * 3 / fel, 1), 'unit': 'rays/s',
                           'ms_per_step': round(fel / 3 * 1e3, 3), 'steps': 3, 'dtype': DTYPE['fp32'],
                           'roofline': kernel_roofline(fkt, 'fp32', fel, traffic_units=False)}
+        # the headline's own iteration (room0, 1,000 rays, graph replay) in strict fp32 (config C2's precision)
+        plib.DEFAULT_PRECISION = 'fp32'
+        try:
+            extras['room0_iter_fp32'] = room0_extra(pnr, params, bound, pose, dev, ddp, lib, steps=100, warmup=5,
+                                                    cpu=False, prec='fp32')
+        finally:
+            plib.DEFAULT_PRECISION = saved
     return extras
 
 

@@ -79,6 +79,7 @@ using namespace pnr;
 #ifndef PNR_SKINNY_CU_DIV
 #define PNR_SKINNY_CU_DIV 16
 #endif
+static_assert(PNR_SKINNY_CU_DIV >= 2, "the skinny jobs' CU share leaves the GEMMs at least half the chip");
 
 // ---- diagnostics: kernel timing --------------------------------------------------------------
 namespace {

@@ -642,7 +642,8 @@ int wgrad16_prepare(int kind, const float* A, const float* B, int64_t K, int64_t
   const int64_t tiles = K / 32;
   int64_t per = 8;
   if (syn->group_jobs > 0) {
-    const int64_t cus = device_cu_count() - syn->reserve_cus;
+    int64_t cus = device_cu_count() - syn->reserve_cus;
+    cus = cus < 1 ? 1 : cus;
     const int64_t fill = (tiles * syn->group_jobs + cus - 1) / cus;
     if (fill <= 256) {
       // one round of workgroups: tiles per workgroup so that every job's workgroups take about the same

@@ -366,6 +366,11 @@ class MapGraph:
                 if src.data_ptr() != dst.data_ptr():
                     dst.copy_(src, non_blocking=True)
         self.graph.replay()
+        # the replay moved the weights through Adam's raw pointers (no _version bump) and repacked only
+        # the f16x3 images: a later eager call must not reuse a cached image of any precision
+        self.mstep.decoder._packed.invalidate()
+        if self.mstep.points is not None:
+            self.mstep.decoder._packed_fc.invalidate()
         return self.loss
 
 

@@ -30,6 +30,7 @@ class PackedMLP:
     def invalidate(self):
         """Force a re-pack (weights were written in place outside autograd, e.g. pnr_adam_step)."""
         self._key = None
+        self._cover_all = False
 
     def image(self, params, prec=None) -> torch.Tensor:
         """The packed image of `params`; prec = PNR_PREC_F16X3 (int): only the f16x3 kernels will read it."""

@@ -45,3 +45,21 @@ def trained_params():
 @pytest.fixture(scope='session')
 def random_params():
     return golden_params('random')
+
+
+def maybe_dump_grads(what, g, cr, f32, mag, d32, rtol, atol, a):
+    """Diagnostics (tools/flip_dump.sh, env PNR_DUMP_GRADS=<dir>): save the HIP gradient, the
+    correctly-rounded and float32 references and the summation magnitudes of any tensor with an
+    element beyond the strict elementwise bound (a = its absolute term), one .npz per test and tensor."""
+    import os
+    dump = os.environ.get('PNR_DUMP_GRADS')
+    if not dump:
+        return
+    g, cr, f32 = (np.asarray(x, dtype=np.float64) for x in (g, cr, f32))
+    if (np.abs(g - cr) > rtol * np.abs(cr) + a).any() or (np.abs(g - f32) > rtol * np.abs(f32) + a).any():
+        os.makedirs(dump, exist_ok=True)
+        tag = (os.environ.get('PYTEST_CURRENT_TEST', 'x').split(' ')[0] + '__' + what)
+        for ch in '/:[]':
+            tag = tag.replace(ch, '_')
+        np.savez_compressed(os.path.join(dump, tag + '.npz'), g=g.astype(np.float32), cr=cr, f32=f32.astype(np.float32),
+                            mag=np.asarray(0.0 if mag is None else mag), d32=d32, rtol=rtol, atol=atol)

@@ -25,7 +25,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import golden_params
+from conftest import golden_params, maybe_dump_grads
 from oracle import ref_points as RP
 from oracle import ref_render as RR
 
@@ -186,6 +186,7 @@ def map_grad_parity(pnr, ms, params, bound, xyz, feats, ro, rd, gt, radius, prec
         d32 = np.abs(b - bcr).max() / scale
         atol = (1e-6 + d32) * scale + MAG_ULPS * 2.0 ** -24 * mags[k]
         viol = np.abs(a - bcr) / (1e-3 * np.abs(bcr) + atol)
+        maybe_dump_grads(k, a, bcr, b, mags[k], d32, 1e-3, 1e-6, atol)
         print(f'{precision} {k}: d32 {d32:.2e}, worst |g - g_cr| / (rtol |g_cr| + atol) = {viol.max():.3f}, '
               f'beyond: {float(np.mean(viol > 1)):.1e}')
         np.testing.assert_array_less(np.abs(a - bcr), 1e-3 * np.abs(bcr) + atol + FLIP_CAP * scale + 1e-45, err_msg=k)

@@ -17,7 +17,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import load_golden, golden_params
+from conftest import load_golden, golden_params, maybe_dump_grads
 from oracle import ref_points as RP
 from oracle import ref_render as RR
 
@@ -81,6 +81,7 @@ def grad_elementwise(g, cr, f32, what, rel_f32=None, rtol=1e-3, atol=1e-6, flips
     mfloor = 0.0 if mag is None else MAG_ULPS * 2.0 ** -24 * np.asarray(mag)
     scale = max(np.abs(cr).max(), 1e-30)
     d32 = float(rel_f32) if rel_f32 is not None else float(np.abs(f32 - cr).max() / scale)
+    maybe_dump_grads(what, g, cr, f32, mag, d32, rtol, atol, (atol + d32) * scale + mfloor)
     for ref, tag in ((cr, 'correctly rounded'), (f32, 'float32')):
         m = max(np.abs(ref).max(), 1e-30)
         a = (atol + d32) * m + mfloor
@@ -186,6 +187,61 @@ def test_gather_many_tasks_per_block(pnr_mod, dev):
     assert np.array_equal(idx[sel.to(dev)].cpu().numpy(), idx_ref.numpy().astype(np.int32))
     close(w[sel.to(dev)], w_ref, 1e-6, 'weights')
     close(c[sel.to(dev)], c_ref, 1e-5 * c_ref.abs().max().item(), 'c')
+
+
+def test_gather_large_batch_paths(pnr_mod, dev, precision):
+    """P = 2,700,000 >= 2,621,440 samples along 45,000 short rays: the paths the S-map and map-points
+    batches take -- the forward search in 64-item chunks (csrc/points.hip launch: a.chunk = 64, the
+    scalar bucket-header loads) and the backward in 32-row half-wave runs that carry a neighbour shared
+    with the previous row of the ray forward (a.run = 32).  Forward: a random row subset against the
+    oracle.  Backward: dL/dfeats against a float64 scatter of the gather's own (index, weight) rows (the
+    forward check pins those), dL/dp elementwise on a row subset against the float64 gradient."""
+    if precision == 'fp32':
+        pytest.skip('the gather has no decoder precision: run once')
+    import ctypes
+    lib = pnr_mod.library()
+    xyz, feats, _ = random_cloud(seed=31)
+    gen = torch.Generator().manual_seed(32)
+    n_rays, S = 45_000, 60
+    P = n_rays * S
+    assert P >= 64 * 5 * 1024 * 8 and P // 32 >= 2 * 5 * 1024 * 8, 'the large-batch thresholds of points.hip'
+    o = xyz[torch.randint(0, xyz.shape[0], (n_rays,), generator=gen)] + 0.02 * torch.randn((n_rays, 3), generator=gen)
+    d = torch.nn.functional.normalize(torch.randn((n_rays, 3), generator=gen), dim=1)
+    t = torch.linspace(-0.03, 0.03, S)
+    q = (o[:, None, :] + t[None, :, None] * d[:, None, :]).reshape(-1, 3).double()
+    pts = pnr_mod.NeuralPoints(xyz.to(dev), feats.to(dev), mode='idw', radius=0.03, k=8).to(dev)
+    c, idx, w = _gather_c_abi(pnr_mod, dev, pts, q, 8)
+    assert not torch.isnan(c).any() and not (idx == -7).any(), 'every row written'
+    frac = (idx[:, 0] >= 0).float().mean().item()
+    assert 0.05 < frac < 0.95, f'a mix of samples with and without neighbours ({frac:.2f})'
+    sel = torch.randint(0, P, (4096,), generator=gen)
+    c_ref, idx_ref, w_ref = RP.point_gather(q[sel], xyz, feats, 'idw', radius=0.03, k=8, return_idx=True)
+    assert np.array_equal(idx[sel.to(dev)].cpu().numpy(), idx_ref.numpy().astype(np.int32))
+    close(w[sel.to(dev)], w_ref, 1e-6, 'weights')
+    close(c[sel.to(dev)], c_ref, 1e-5 * c_ref.abs().max().item(), 'c')
+    del c
+    # backward through the autograd op (pnr_point_gather_backward)
+    dgen = torch.Generator(device=dev).manual_seed(33)
+    gc = torch.randn((P, 32), generator=dgen, device=dev)
+    qd = q.to(dev).requires_grad_(True)
+    pts.feats.grad = None
+    (pts.gather(qd) * gc).sum().backward()
+    torch.cuda.synchronize()
+    valid = idx >= 0
+    rows = torch.arange(P, device=dev)[:, None].expand(-1, 8)[valid]
+    ref = torch.zeros((xyz.shape[0], 32), dtype=torch.float64, device=dev)
+    ref.index_add_(0, idx[valid].long(), w[valid].double()[:, None] * gc[rows].double())
+    mag = torch.zeros_like(ref).index_add_(0, idx[valid].long(), w[valid].double()[:, None] * gc[rows].double().abs())
+    err = (pts.feats.grad.double() - ref).abs()
+    bound = 1e-5 * ref.abs() + 2.0 ** -20 * mag + 1e-7 * ref.abs().max()
+    print(f'dL/dfeats: worst |g - g64| / bound = {(err / bound).max().item():.3f}')
+    assert bool((err <= bound).all()), 'dL/dfeats vs the float64 scatter of the gather rows'
+    sub = sel[:1024]
+    gsub = gc[sub.to(dev)].cpu()
+    qr = q[sub].clone().requires_grad_(True)
+    (RP.point_gather(qr, xyz, feats, 'idw', radius=0.03, k=8) * gsub).sum().backward()
+    gcr, mag_p = idw_grad_p_cr(q[sub].float().double(), xyz.double(), feats.double(), idx_ref[:1024], gsub.double())
+    grad_elementwise(qd.grad[sub.to(dev)], gcr, qr.grad, 'dL/dp (large batch)', mag=mag_p)
 
 
 def _gather_c_abi(pnr_mod, dev, pts, q, k):

@@ -6,10 +6,19 @@ the other side of a decision edge (a neighbour radius, a ReLU threshold) and tho
 allowance for them.  Here the HIP gather + decoder are fed the ORACLE's own sample positions (the
 coarse, importance and regulation points its render_batch_ray / regulation evaluated for the golden
 rays), so the inputs are identical; the samples that still sit on a decision edge are identified in
-float64 and left out of BOTH sides:
-  * a ReLU pre-activation within 1e-5 of its layer's largest |pre-activation| (a float32 order can
-    take either branch there), and
-  * a candidate point within 1e-5 relative of the neighbourhood radius (IDW) or of the box (trilinear).
+float64 and left out of BOTH sides.  The edges are tied to rounding bounds, per element:
+  * a ReLU pre-activation z_j = sum_i W_ji h_i + b_j with |z_j| <= RELU_ULPS u M_j, M_j = sum_i |W_ji h_i|
+    + |b_j| its own summation magnitude (u = 2^-24): no float32 order of the sum (the torch CPU order,
+    the MFMA's blocked fp32 order), nor the f16x3 split (3 x 2^-22 per product), moves z_j by more
+    (measured: the oracle's float32 forward stays within 44 u M_j of the float64 one, inputs' own
+    rounding included), and
+  * a candidate point within NB_ULPS u of the neighbourhood radius (|d^2 - r^2| <= NB_ULPS u r^2, IDW)
+    or of the box (||dx| - h| <= NB_ULPS u h, trilinear): float32 point coordinates and a three-term
+    float32 distance.
+The filter is checked against the kernel itself: the HIP training forward's saved ReLU masks are read
+back, and every HIP decision that differs from the float64 one must lie inside the filter; on the
+kept samples the HIP and float64 decisions are identical.  The dropped share is printed; the keep
+floor is 0.9.
 On the remaining samples the neighbour sets are asserted identical, and every gradient -- the 11
 decoder tensors, the 8 fc_c tensors, the point features and dL/dp -- is held ELEMENTWISE at rtol 1e-3
 against the correctly-rounded gradient (float64 GEMMs, rounded per layer: oracle.ref_points
@@ -31,7 +40,9 @@ from test_gpu_points import grad_elementwise, mag_arrays, surface_cloud
 
 pytestmark = pytest.mark.gpu
 
-EDGE_TAU = 1e-5
+RELU_ULPS = 64.0
+NB_ULPS = 16.0
+U32 = 2.0 ** -24
 
 
 @pytest.fixture(autouse=True, params=['fp32', 'f16x3'])
@@ -70,8 +81,10 @@ def oracle_samples(params, ro, rd, gt, bound, pdict):
     return torch.cat(seen).double()
 
 
-def edge_free(params, q, xyz, pdict):
-    """Samples with no ReLU pre-activation and no candidate distance on a decision edge (float64)."""
+def edge_free(params, q, xyz, pdict, return_z=False):
+    """Samples with no ReLU pre-activation and no candidate distance on a decision edge (float64, the
+    rounding bounds of the module docstring).  return_z: also the float64 pre-activations z (4, P, 256),
+    their edge flags and the samples off every neighbourhood edge."""
     keep = torch.ones(q.shape[0], dtype=torch.bool)
     # neighbourhood edge: a point at the radius (IDW) or on the box faces (trilinear)
     for a in range(0, q.shape[0], 4096):
@@ -80,21 +93,63 @@ def edge_free(params, q, xyz, pdict):
         if pdict['mode'] == 'idw':
             d2 = (dl * dl).sum(-1)
             r2 = pdict['radius'] ** 2
-            bad = ((d2 - r2).abs() <= EDGE_TAU * r2).any(1)
+            bad = ((d2 - r2).abs() <= NB_ULPS * U32 * r2).any(1)
         else:
             h = torch.tensor(pdict['spacing'], dtype=torch.float64)
-            bad = (((dl.abs() - h).abs() <= EDGE_TAU * h).any(-1)).any(1)
+            bad = (((dl.abs() - h).abs() <= NB_ULPS * U32 * h).any(-1)).any(1)
         keep[a:a + 4096] &= ~bad
-    # ReLU edges: pre-activations of every hidden layer in float64 on the float32 inputs
+    nb_ok = keep.clone()
+    nb_keep = int(keep.sum())
+    # ReLU edges: pre-activations of every hidden layer in float64 on the float32 inputs, each against
+    # its own summation magnitude
     c = RP.point_gather(q, xyz, pdict['feats'].detach(), pdict['mode'], pdict.get('radius', 0.0),
                         pdict.get('spacing'), pdict['k'], pdict['eps']).double()
     x = q.float().double()
     h = torch.sin(x @ params['embedder._B'].double())
+    zs, es = [], []
     for li in range(4):
-        z = h @ params[f'pts_linears.{li}.weight'].double().t() + params[f'pts_linears.{li}.bias'].double()
-        keep &= ~((z.abs() <= EDGE_TAU * z.abs().max()).any(1))
-        h = torch.relu(z) + c @ params[f'fc_c.{li}.weight'].double().t() + params[f'fc_c.{li}.bias'].double()
+        W, b = params[f'pts_linears.{li}.weight'].double(), params[f'pts_linears.{li}.bias'].double()
+        z = h @ W.t() + b
+        M = h.abs() @ W.abs().t() + b.abs()
+        e = z.abs() <= RELU_ULPS * U32 * M
+        keep &= ~e.any(1)
+        zs.append(z)
+        es.append(e)
+        h = (torch.relu(z) + c @ params[f'fc_c.{li}.weight'].double().t() + params[f'fc_c.{li}.bias'].double()).float()
+        h = h.double()
+    print(f'decision edges: {q.shape[0] - nb_keep} samples at a neighbourhood edge, '
+          f'{nb_keep - int(keep.sum())} more at a ReLU edge; {q.shape[0] - int(keep.sum())} of {q.shape[0]} dropped')
+    if return_z:
+        return keep, torch.stack(zs), torch.stack(es), nb_ok
     return keep
+
+
+def hip_relu_decisions(pnr_mod, dec, x, c, prec):
+    """The ReLU decisions [z > 0] of the HIP training forward (pnr_mlp_fwd_train_c) for points x (P,3)
+    float32 and features c (P,32): its saved mask words (capi.cpp carve_save: e [ld][96], h [4][ld][256]
+    fp32, x [ld] float4, then the masks [4][ld/32][64 lanes] uint4; unit u of lane half (u >> 2) & 1,
+    word u >> 6, bit 16 ((u >> 5) & 1) + 4 ((u >> 3) & 3) + (u & 3): k_mlp_fwd16 conv1 / mlp.hip
+    save_mask), decoded to a bool (4, P, 256)."""
+    from pnr import _lib
+    lib = pnr_mod.library()
+    P = x.shape[0]
+    ld = -(-P // 128) * 128
+    dev = x.device
+    ws = torch.empty(lib.pnr_mlp_train_workspace_bytes(P), dtype=torch.uint8, device=dev)
+    raw = torch.empty((P, 4), device=dev)
+    packed = dec._packed.image(dec.ordered_params())
+    fcp = dec._packed_fc.image(dec.ordered_fc_params())
+    _lib.check(lib.pnr_mlp_fwd_train_c(_lib.ptr(packed), _lib.ptr(fcp), _lib.ptr(x), _lib.ptr(c), P, _lib.ptr(raw),
+                                       _lib.ptr(ws), ws.numel(), _lib.precision_code(prec), _lib.stream_of(dev)),
+               'mlp_fwd_train_c')
+    torch.cuda.synchronize()
+    off = (96 + 4 * 256) * 4 * ld + 16 * ld
+    words = ws[off:off + 128 * ld].view(torch.int32).view(4, ld // 32, 2, 32, 4).cpu().long() & 0xFFFFFFFF
+    u = torch.arange(256)
+    hh, wi, bit = (u >> 2) & 1, u >> 6, 16 * ((u >> 5) & 1) + 4 * ((u >> 3) & 3) + (u & 3)
+    p = torch.arange(P)
+    w = words[:, (p >> 5)[:, None], hh[None, :], (p & 31)[:, None], wi[None, :]]  # (4, P, 256)
+    return ((w >> bit[None, None, :]) & 1).bool()
 
 
 @pytest.mark.parametrize('mode', ['idw', 'trilinear'])
@@ -108,10 +163,11 @@ def test_decoder_with_points_teacher_forced(pnr_mod, dev, mode, precision):
     kw = dict(mode=mode, k=8, radius=0.04, eps=1e-6, spacing=[0.03, 0.03, 0.03])
     pdict = dict(xyz=xyz, feats=feats, **kw)
     q_all = oracle_samples(params, ro, rd, gt, bound, pdict)
-    keep = edge_free(params, q_all, xyz, pdict)
+    keep, z64, edge, nb_ok = edge_free(params, q_all, xyz, pdict, return_z=True)
     q = q_all[keep].contiguous()
-    print(f'{mode}: {q_all.shape[0]} oracle samples, {q.shape[0]} off every decision edge')
-    assert q.shape[0] > 0.7 * q_all.shape[0]
+    print(f'{mode}: {q_all.shape[0]} oracle samples, {q.shape[0]} off every decision edge, '
+          f'{q_all.shape[0] - q.shape[0]} dropped ({1 - q.shape[0] / q_all.shape[0]:.2%})')
+    assert q.shape[0] >= 0.9 * q_all.shape[0]
     G = torch.randn((q.shape[0], 4), generator=torch.Generator().manual_seed(23), dtype=torch.float64).float()
 
     # HIP: gather + decoder with fc_c injection on the oracle's points (float64 in, as the renderer)
@@ -123,6 +179,22 @@ def test_decoder_with_points_teacher_forced(pnr_mod, dev, mode, precision):
     raw = dec(qd, c_grid={'points_color': pts})
     (raw * G.to(dev)).sum().backward()
     torch.cuda.synchronize()
+
+    # the filter against the kernel's own ReLU decisions on ALL oracle samples off a neighbourhood edge
+    # (where the neighbour sets, hence the features, agree): a HIP decision that differs from the
+    # float64 one lies on a filtered ReLU edge, and none survives on a kept sample
+    xa = q_all.float().to(dev).contiguous()
+    with torch.no_grad():
+        ca = pts.gather(q_all.to(dev)).contiguous()
+    dec_hip = hip_relu_decisions(pnr_mod, dec, xa, ca, precision)
+    dec64 = z64 > 0
+    diff = (dec_hip != dec64) & nb_ok[None, :, None]
+    clear = ~edge & (z64.abs() > 1e-3 * z64.abs().amax(-1, keepdim=True))
+    assert not diff[clear].any(), 'HIP ReLU decisions away from every edge equal the float64 ones (mask decode)'
+    print(f'HIP ReLU decisions differing from float64: {int(diff.sum())} of {diff.numel()}, on '
+          f'{int(diff.any(-1).any(0).sum())} samples; outside the filter: {int((diff & ~edge).sum())}')
+    assert not (diff & ~edge).any(), 'every HIP decision flip lies inside the rounding-bound filter'
+    assert not diff[:, keep].any()
 
     # identical neighbour sets on every kept sample
     from test_gpu_points import _gather_c_abi

@@ -218,7 +218,11 @@ def main():
                  for nm, c in zip(names, cuts)}
         # floor per part: 1e-5 max|g| (float32 association), or twice the spread the same batch shows
         # reordered where its sums cancel more (the fc_c gradients (dL/dh)^T c)
-        floors = {nm: max(1e-5, 2.0 * assoc[nm]) for nm in names}
+        # capped at 5e-4 (a regression that made the split sums order-sensitive must not loosen its own
+        # bound), and a reordered-batch spread above that cap fails the check outright
+        floors = {nm: min(max(1e-5, 2.0 * assoc[nm]), 5e-4) for nm in names}
+        if max(assoc.values()) > 2.5e-4:
+            raise SystemExit(f'dp_check: reordered-batch spread {assoc} above the 2.5e-4 limit')
         viol = max(float(((g_first[c] - g_1[c]).abs() / (1e-6 * g_1[c].abs() + floors[nm] * g_1[c].abs().max()
                                                           + 1e-30)).max()) for nm, c in zip(names, cuts))
         loss_rel = [abs(x - y) / abs(y) for x, y in zip(lt.tolist(), full)]
