@@ -73,6 +73,24 @@ __device__ __forceinline__ void glds16s_x8(const char* src, uint32_t voff, uint3
       : "memory");
 }
 
+// Four LDS-DMA pieces of 1 KB per wave, 8 KB apart in the source and in LDS (one weight step of the
+// 16-point-wave forward, mlp16w.h: 8 waves x 4 pieces), in one statement: two source bases, two lane
+// offsets (voff, voff + 8 KB), M0 stepped by s_add.
+__device__ __forceinline__ void glds16s_x4(const char* src, uint32_t voff, uint32_t lds_byte) {
+  unsigned keep;
+  const uint32_t voff2 = voff + 8192;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %5\n\ts_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, %3\n\ts_add_u32 m0, m0, 0x2000\n\ts_nop 0\n\t"
+      "global_load_lds_dwordx4 %2, %3\n\ts_add_u32 m0, m0, 0x2000\n\ts_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, %4\n\ts_add_u32 m0, m0, 0x2000\n\ts_nop 0\n\t"
+      "global_load_lds_dwordx4 %2, %4\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "v"(voff2), "s"(src), "s"(src + 16384), "s"(lds_byte)
+      : "memory");
+}
+
 // 16-B store of a training save (activations, deltas), read back only by a later kernel.
 // PNR_SAVE_SC1: write-through (sc1) -- the line is dropped from the XCD's L2 instead of kept
 // (MI355X_MICROARCH.md "stores of each flavour"), so the save stream does not evict the weight

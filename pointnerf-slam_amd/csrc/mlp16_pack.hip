@@ -1,13 +1,16 @@
 // mlp16_pack.hip -- 16-bit weight images of the split-precision decoder kernels (mlp16.h) and
 // the forward dispatch on PNR_PREC_*.
 #include <algorithm>
+#include <cstdlib>
 
 #include "mlp16.h"
+#include "mlp16u.h"
+#include "mlp16w.h"
 #include "pack_fp32.h"
 
 namespace pnr {
 
-int64_t packed_floats_all() { return kPackedFloatsAll; }
+int64_t packed_floats_all() { return kPackedFloatsW16; }
 int64_t fc_packed_floats_all() { return kFcPackedFloatsAll; }
 // ---------------------------------------------------------------------------------------------
 // Packing
@@ -174,6 +177,46 @@ __device__ __forceinline__ void pack16_bwd_at(const RawParams& rp, uint16_t* __r
   out[e] = part_bits<_Float16>(v * raw[kRawScl + tensor], part);
 }
 
+// The 16-point-wave forward image (mlp16w.h, element e of kW16Bytes / 2): 27 hidden steps of
+// A[row = 16T + (lane & 15)][k] over [T 16][part 2][lane 64][j 8], k = 32kc + 8(lane >> 4) + j for the
+// Fourier layer and 32kc + w16_kmap(8(lane >> 4) + j) for the hidden ones; then Wo (rows 0..3 of 16) per
+// h4 input tile [kc 8][part 2][lane 64][j 8].  f16x3 parts under the forward image's scales.
+__device__ __forceinline__ void pack16w_at(const RawParams& rp, uint16_t* __restrict__ out,
+                                           const float* __restrict__ raw, const int e) {
+  constexpr int hstep = (int)(kW16StepBytes / 2);
+  static_assert(kW16Bytes / 2 < (1LL << 31), "32-bit pack indices");
+  if (e >= (int)(kW16Bytes / 2)) return;
+  float v = 0.f;
+  int part, tensor;
+  if (e < kW16Steps * hstep) {
+    const int g = e / hstep;
+    int r = e - g * hstep;
+    const int j = r & 7; r >>= 3;
+    const int lane = r & 63; r >>= 6;
+    part = r & 1;
+    const int T = r >> 1;
+    const int layer = w16_layer(g), kc = w16_kc(g);
+    const int row = 16 * T + (lane & 15), s = 8 * (lane >> 4) + j;
+    const float* W = rp.at(1 + 2 * layer);
+    tensor = layer;
+    if (layer == 0) {
+      const int k = 32 * kc + s;
+      v = k < kFourier ? W[row * kFourier + k] : 0.f;
+    } else {
+      v = W[row * kHidden + 32 * kc + w16_kmap(s)];
+    }
+  } else {
+    int r = e - kW16Steps * hstep;
+    const int j = r & 7; r >>= 3;
+    const int lane = r & 63; r >>= 6;
+    part = r & 1;
+    const int kc = r >> 1, row = lane & 15;
+    v = row < 4 ? rp.p[9][row * kHidden + 32 * kc + w16_kmap(8 * (lane >> 4) + j)] : 0.f;
+    tensor = 4;
+  }
+  out[e] = part_bits<_Float16>(v * raw[kRawScl + tensor], part);
+}
+
 // The weight images of every precision in two launches (the Mapper repacks once per iteration, and
 // at its 1,000-ray batch each launch costs ~5 us of latency on the step's critical path):
 //   stage 1: blocks 0..4 the power-of-two weight scales (k_wscale), the rest the fp32 image (k_pack)
@@ -195,9 +238,11 @@ __global__ __launch_bounds__(1024) void k_pack_stage1(ScaleArgs sa, RawParams rp
     pack_fp32_at(rp, packed, i);
 }
 __global__ __launch_bounds__(256) void k_pack_stage2(RawParams rp, float* __restrict__ packed, int nb_bwd,
-                                                     int64_t base16) {
+                                                     int nb16, int64_t base16) {
   float* raw = packed + kOffRaw;
-  if ((int)blockIdx.x < nb_bwd)
+  if ((int)blockIdx.x >= nb_bwd + nb16)  // the 16-point-wave forward image (after the raw table)
+    pack16w_at(rp, reinterpret_cast<uint16_t*>(packed + kOffW16), raw, ((int)blockIdx.x - nb_bwd - nb16) * 256 + threadIdx.x);
+  else if ((int)blockIdx.x < nb_bwd)
     pack16_bwd_at(rp, reinterpret_cast<uint16_t*>(packed + kOffBwd), raw, (int64_t)blockIdx.x * 256 + threadIdx.x);
   else
     pack16_at(rp, reinterpret_cast<uint16_t*>(packed + kOffBf2), reinterpret_cast<uint16_t*>(packed + kOffBf1),
@@ -222,8 +267,9 @@ int launch_pack_all(const RawParams& rp, float* packed, hipStream_t st, int flag
   constexpr int64_t n2 = bf_main_bytes(2) / 2, n1 = bf_main_bytes(1) / 2;
   const int64_t n16 = 2 * n2 + n1 + kRawWo + 4 * kHidden;
   const int64_t base16 = (flags & PNR_PACK_F16X3_ONLY) ? n2 + n1 : 0;  // from the f16x3 main image on
-  const int nb2 = nb_bwd + (int)((n16 - base16 + 255) / 256);
-  hipLaunchKernelGGL(k_pack_stage2, dim3(nb2), dim3(256), 0, st, rp, packed, nb_bwd, base16);
+  const int nb16 = (int)((n16 - base16 + 255) / 256);
+  const int nbw = (int)((kW16Bytes / 2 + 255) / 256);
+  hipLaunchKernelGGL(k_pack_stage2, dim3(nb_bwd + nb16 + nbw), dim3(256), 0, st, rp, packed, nb_bwd, nb16, base16);
   return hip_status(hipGetLastError());
 }
 
@@ -328,6 +374,17 @@ int launch_fc_pack_all(const float* const* fcp, float* out, hipStream_t st, int 
   return hip_status(hipGetLastError());
 }
 
+// The f16x3 forward without features has three kernels: 0 k_mlp_fwd16 (32-point waves, one per SIMD),
+// 1 k_mlp_fwd16w (16-point waves, two per SIMD, mlp16w.h), 2 k_mlp_fwd16u (output units split over two
+// waves per SIMD, mlp16u.h).  PNR_FWD_VARIANT (environment, read per launch) picks one for A/B runs;
+// the default is measured (tools/w16_ab.py, 4.19M points, one process, interleaved rounds): the eval
+// forward runs k_mlp_fwd16w (4.38-4.49 ms against 4.71-4.83), the training forward k_mlp_fwd16
+// (6.18-6.29 ms against 6.29-6.47 for k_mlp_fwd16w and 6.99-7.37 for k_mlp_fwd16u).
+int fwd16_variant(int save) {
+  const char* e = getenv("PNR_FWD_VARIANT");
+  return e ? atoi(e) : (save == 0 ? 1 : 0);
+}
+
 int launch_mlp_fwd_bf(int prec, const float* packed, const PointSrc& src, int mode, int64_t P, float* raw,
                       const SaveArgs* save, hipStream_t st, const FeatArgs* feat, uint32_t* status) {
   if (P <= 0) return 0;
@@ -357,6 +414,15 @@ int launch_mlp_fwd_bf(int prec, const float* packed, const PointSrc& src, int mo
   }
   const dim3 grid((unsigned)nwg);
   TimingScope ts(kTimeMlpFwd, P, st);
+  if (prec == PNR_PREC_F16X3 && !hasc) {
+    const int var = fwd16_variant(sv);
+    if (var == 1) {  // 16-point waves (mlp16w.h)
+      BfFwdArgs b = a;
+      b.wmain = reinterpret_cast<const char*>(packed + kOffW16);
+      return launch_fwd16w(mode, grid, st, b, sv);
+    }
+    if (var == 2) return launch_fwd16u(mode, grid, st, a, sv);  // unit-split wave pairs (mlp16u.h)
+  }
   switch (prec) {
     case PNR_PREC_BF16X3: return launch_fwd16_bf16x3(mode, grid, st, a, hasc, sv);
     case PNR_PREC_BF16: return launch_fwd16_bf16(mode, grid, st, a, hasc, sv);

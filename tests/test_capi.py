@@ -47,7 +47,7 @@ def test_host_only_calls(lib):
     lib.pnr_mlp_packed_floats.restype = ctypes.c_size_t
     # fp32 images 486,688 + bf16x3 / bf16 / f16x3 forward streams 229,376 / 118,784 / 229,376
     # + f16x3 delta-chain stream 225,280 + raw table 2,048 + fp32 Wo 1,024
-    assert lib.pnr_mlp_packed_floats() == 486688 + 229376 + 118784 + 229376 + 225280 + 3072
+    assert lib.pnr_mlp_packed_floats() == 486688 + 229376 + 118784 + 229376 + 225280 + 3072 + 225280
     lib.pnr_build_info.restype = ctypes.c_char_p
     assert b'gfx950' in lib.pnr_build_info()
 

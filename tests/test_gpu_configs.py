@@ -36,7 +36,13 @@ OFFICE3 = [[-6.7, 5.1], [-7.5, 4.9], [-2.8, 3.5]]       # configs/Replica/office
 # decision-edge allowance (tests/test_gpu_points.py FLIP_CAP)
 MAG_ULPS = 64.0
 FLIP_CAP = 5e-4
-FLIP_FRAC = 1e-2  # the share of a tensor's elements that may use it, >= 1 (tests/test_gpu_points.py)
+# the share of a tensor's elements that may use it, >= 1.  Round 6: 3e-3 (was 1e-2).  Measured at the
+# round-6 code (tools/flip_dump.sh, profiles/r06_flip_rank.txt): C3 f16x3 fc_c.0 / fc_c.1.weight 2.4-2.8e-3
+# beyond the strict bound -- NOT a flipped sample's rank-1 term (flat singular spectrum, |dg| <= 1.8e-5
+# max|g|): the f16x3 split of dL/dh under the per-wave running scale of the dWc GEMM (wgrad16.hip BSC)
+# keeps 22 bits relative to the wave's largest |dL/dh|, not to each element's own terms; one element
+# of 256 in fc_c.2.bias / pts_linears.2.bias; pts_linears.2 / .3.weight one flipped sample's term.
+FLIP_FRAC = 3e-3
 APARTMENT = [[-5.8, 11.3], [-4.0, 4.5], [-7.9, 4.9]]    # configs/Apartment/apartment.yaml:27
 
 

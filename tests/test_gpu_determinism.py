@@ -350,10 +350,11 @@ def test_f16x3_only_pack_matches_full(pnr_mod, dev, points):
     # (compared as int32 words: two f16 parts in a float32 word can spell a NaN)
     img = dec._packed.image(list(dec.ordered_params()), prec=f16).clone().view(torch.int32)
     ref = PackedMLP().image([p.detach().clone() for p in dec.ordered_params()]).view(torch.int32)
-    raw0 = lib.pnr_mlp_packed_floats() - 3072   # kOffRaw: the raw table is the last 12 KiB
+    w16 = 225280                                # the 16-point-wave forward image (mlp16w.h), after the raw table
+    raw0 = lib.pnr_mlp_packed_floats() - w16 - 3072   # kOffRaw: the raw table's 12 KiB, then that image
     lo = raw0 - (917504 + 901120) // 4          # kOffH2: f16x3 main image, then the delta-chain image
     # raw words: biases / bo / Fourier B [0, 1344), inverse scales [1344, 1349), scales [1352, 1357), Wo [2048, 3072)
-    for a, b in ((lo, raw0 + 1349), (raw0 + 1352, raw0 + 1357), (raw0 + 2048, raw0 + 3072)):
+    for a, b in ((lo, raw0 + 1349), (raw0 + 1352, raw0 + 1357), (raw0 + 2048, raw0 + 3072 + w16)):
         assert torch.equal(img[a:b], ref[a:b]), (a, b)
     if points:
         fimg = dec._packed_fc.image(list(dec.ordered_fc_params()), prec=f16).clone().view(torch.int32)

@@ -49,19 +49,20 @@ def pnr_mod():
 
 # Render / regulation / tracking with IDW or trilinear features over a random cloud: a few samples sit
 # on a decision edge (a ReLU pre-activation, a neighbour's distance or a pdf bin boundary within
-# rounding of the threshold), where two float32 orders take different branches.  A flipped sample
-# changes one rank-1 term of a weight gradient (its delta times its activations), so it can move ANY
-# fraction of the elements, each by about one sample's share: ~max|g| / n for n samples (~2.7e4 here).
-# FLIP_CAP = 5e-4 max|g| admits about a dozen such terms, and only on a bounded share of the elements:
-# at most FLIP_FRAC of a tensor's elements (at least one) may use the allowance, i.e. lie beyond the
-# strict bound.  Measured maxima (round 5, per test and precision, tools/_flips.sh -> profiles/r05_flips.txt):
-# fp32 trilinear render 1.40% of fc_c.1.weight, 0.96% of fc_c.0.weight, 0.51% of pts_linears.1.weight (2%
-# there, see test_render_with_points_matches_oracle) and 0.19% of dL/dfeats; f16x3 trilinear render
-# 0.16% of pts_linears.0.weight; one element of dL/drays_o (fp32 IDW tracking, 1 of 384); every IDW
-# render / small-feature / regulation case 0.  FLIP_FRAC 3e-3 holds everything but the fp32 trilinear
-# weight gradients.
+# rounding of the threshold), where two float32 orders take different branches (the end-to-end tests
+# let each side place its own importance samples: tests/test_gpu_points_forced.py feeds the oracle's
+# samples to the kernels and holds every kept sample to the strict bound with no allowance at all).
+# A flipped sample changes ONE rank-1 term of every weight gradient -- dW = sum_p delta_p h_p^T, and with
+# the bias as one more column [dW | db] = sum_p delta_p [h_p; 1]^T -- and of dL/dfeats and dL/drays
+# (its own rows), so what a flip may move is a rank-1 matrix, not a share of the elements.  The
+# allowance (round 6, replacing round 5's FLIP_FRAC share of elements and its 2% fp32-trilinear
+# exception): the deviation from each reference may exceed the strict elementwise bound only by at most
+# FLIP_RANK rank-1 terms -- after removing its best rank-k approximation (SVD, k <= FLIP_RANK) EVERY
+# element is inside the strict bound -- and the removed part stays within FLIP_CAP max|g| elementwise.
+# Measured (tools/flip_dump.sh + tools/flip_analysis.py, profiles/r06_flip_rank.txt): every tensor of
+# every end-to-end case that leaves the strict bound is brought inside it by ONE rank-1 term.
 FLIP_CAP = 5e-4
-FLIP_FRAC = 3e-3
+FLIP_RANK = 2
 # summation-magnitude floor, in ulps (u = 2^-24) of M = sum_p |t_p|: a gradient element is a sum over
 # samples of terms that each carry a few ulps from the forward / delta chain, and the sum itself
 # rounds in a blocked order; 64 u M bounds both (an element without cancellation has M ~ |g|, where
@@ -69,33 +70,72 @@ FLIP_FRAC = 3e-3
 MAG_ULPS = 64.0
 
 
-def grad_elementwise(g, cr, f32, what, rel_f32=None, rtol=1e-3, atol=1e-6, flips=False, mag=None,
-                     flip_frac=FLIP_FRAC):
+def strict_bound(ref, cr, d32, mfloor, rtol, atol):
+    """rtol |ref| + (atol + d32) max|g_cr| + the summation floor: the elementwise bound of grad_elementwise."""
+    return rtol * np.abs(ref) + (atol + d32) * max(np.abs(cr).max(), 1e-30) + mfloor
+
+
+def flip_rank(D, B, cap, kmax=FLIP_RANK):
+    """Smallest k <= kmax such that D minus its best rank-k approximation lies inside B everywhere and
+    the removed rank-k part inside cap (2-D D), else None (see FLIP_RANK)."""
+    if (np.abs(D) <= B).all():
+        return 0
+    if D.ndim != 2:  # (a 1-D gradient has no rank structure to name a flip by: no relief)
+        return None
+    D2, B2 = D, np.broadcast_to(B, D.shape)
+    u, s, vt = np.linalg.svd(D2, full_matrices=False)
+    for k in range(1, min(kmax, len(s)) + 1):
+        Rk = (u[:, :k] * s[:k]) @ vt[:k]
+        if (np.abs(D2 - Rk) <= B2).all() and (np.abs(Rk) <= cap).all():
+            return k
+    return None
+
+
+def _np(t):
+    return t.detach().cpu().numpy().astype(np.float64) if isinstance(t, torch.Tensor) else np.asarray(t, np.float64)
+
+
+def grad_elementwise(g, cr, f32, what, rel_f32=None, rtol=1e-3, atol=1e-6, flips=False, mag=None):
     """|g - g_cr| <= rtol |g_cr| + (atol + d32) max|g_cr| + MAG_ULPS u M and |g - g_f32| <= the same
     with g_f32 elementwise, d32 = rel_f32 or max |g_f32 - g_cr| / max |g_cr|, M = the element's
     summation magnitude sum_p |t_p| (oracle.ref_points.magnitudes; 0 when not given): the float32
-    rounding floor of a sum that cancels.  flips: up to a share flip_frac of the elements may exceed
-    that by up to FLIP_CAP max|g| (decision-edge samples, see above)."""
-    g = g.detach().cpu().numpy() if isinstance(g, torch.Tensor) else np.asarray(g)
-    cr, f32 = (t.detach().cpu().numpy() if isinstance(t, torch.Tensor) else np.asarray(t) for t in (cr, f32))
+    rounding floor of a sum that cancels.  flips: beyond that bound only by at most FLIP_RANK rank-1
+    terms of at most FLIP_CAP max|g| (decision-edge samples, see above)."""
+    g, cr, f32 = _np(g), _np(cr), _np(f32)
     mfloor = 0.0 if mag is None else MAG_ULPS * 2.0 ** -24 * np.asarray(mag)
     scale = max(np.abs(cr).max(), 1e-30)
     d32 = float(rel_f32) if rel_f32 is not None else float(np.abs(f32 - cr).max() / scale)
     maybe_dump_grads(what, g, cr, f32, mag, d32, rtol, atol, (atol + d32) * scale + mfloor)
     for ref, tag in ((cr, 'correctly rounded'), (f32, 'float32')):
-        m = max(np.abs(ref).max(), 1e-30)
-        a = (atol + d32) * m + mfloor
-        viol = np.abs(g - ref) / (rtol * np.abs(ref) + a)
-        out = float(np.mean(viol > 1))
-        print(f'{what} vs {tag} (d32 {d32:.2e}): worst |g - g_ref| / (rtol |g_ref| + atol) = {viol.max():.3f}, '
-              f'beyond: {out:.1e}')
+        B = strict_bound(ref, cr, d32, mfloor, rtol, atol)
+        viol = np.abs(g - ref) / B
+        print(f'{what} vs {tag} (d32 {d32:.2e}): worst |g - g_ref| / bound = {viol.max():.3f}, '
+              f'beyond: {float(np.mean(viol > 1)):.1e}')
         if flips:
-            np.testing.assert_array_less(np.abs(g - ref), rtol * np.abs(ref) + np.maximum(a, FLIP_CAP * m) + 1e-45,
-                                         err_msg=f'{what} vs {tag}')
-            assert int(np.sum(viol > 1)) <= max(1.0, flip_frac * g.size), \
-                f'{what} vs {tag}: {out:.2e} of the elements use the flip allowance'
+            k = flip_rank(g - ref, B, FLIP_CAP * max(np.abs(ref).max(), 1e-30))
+            print(f'    flipped-sample terms needed: {k}')
+            assert k is not None, f'{what} vs {tag}: the deviation beyond the strict bound is not {FLIP_RANK} rank-1 terms'
         else:
-            np.testing.assert_array_less(np.abs(g - ref), rtol * np.abs(ref) + a + 1e-45, err_msg=f'{what} vs {tag}')
+            np.testing.assert_array_less(np.abs(g - ref), B + 1e-45, err_msg=f'{what} vs {tag}')
+
+
+def grad_layers(named, cr, f32, mags, flips=True):
+    """grad_elementwise over a decoder's parameter gradients (named: name -> tensor), each weight held
+    together with its bias as one more column ([dW | db]: one flipped sample is one rank-1 term of it)."""
+    done = set()
+    for k, t in named.items():
+        if k in done:
+            continue
+        if k.endswith('.weight') and k[:-7] + '.bias' in named:
+            kb = k[:-7] + '.bias'
+            cat = lambda a, b: np.concatenate([_np(a), _np(b)[:, None]], 1)  # noqa: E731
+            m = None if mags is None else np.concatenate([np.asarray(mags[k]), np.asarray(mags[kb])[:, None]], 1)
+            grad_elementwise(cat(t, named[kb]), cat(cr[k], cr[kb]), cat(f32[k], f32[kb]), k + ' | bias',
+                             flips=flips, mag=m)
+            done.update((k, kb))
+        elif not k.endswith('.bias') or k[:-5] + '.weight' not in named:
+            grad_elementwise(t, cr[k], f32[k], k, flips=flips, mag=None if mags is None else mags[k])
+            done.add(k)
 
 
 def mag_arrays(mag, params):
@@ -439,12 +479,9 @@ def test_render_with_points_matches_oracle(pnr_mod, dev, mode, precision):
             close(d, dr, 0, 'depth', rtol=1e-4)
             close(col, cr, 2e-5, 'rgb', rtol=1e-4)
             close(v, vr, 1e-8, 'var', rtol=2e-3)
-    # the fc_c weight gradients (dL/dh_l)^T c are rank-1 sums in which every sample's feature row
-    # enters every element, so one flipped sample moves all of them: measured 1.42% of fc_c.1.weight
-    # (fp32, trilinear, this seeded probe gc_), hence 2% for that case's weight tensors
-    wfrac = 2e-2 if (precision == 'fp32' and mode == 'trilinear') else FLIP_FRAC
-    for k, t in dec.named_parameters():
-        grad_elementwise(t.grad, refs[True][0][k], refs[False][0][k], k, flips=True, mag=mags[k], flip_frac=wfrac)
+    # (round 5 allowed 2% of the fc_c weight elements here (fp32, trilinear): one flipped sample's rank-1
+    # term, which FLIP_RANK now names as such)
+    grad_layers({k: t.grad for k, t in dec.named_parameters()}, refs[True][0], refs[False][0], mags)
     grad_elementwise(pts.feats.grad, refs[True][1], refs[False][1], 'dL/dfeats', flips=True, mag=mags['feats'])
 
 
@@ -486,8 +523,7 @@ def test_render_with_small_features_matches_oracle(pnr_mod, dev):
             mags = mag_arrays(mag, params)
             close(d, dr, 0, 'depth', rtol=1e-4)
             close(col, cr, 2e-5, 'rgb', rtol=1e-4)
-    for k, t in dec.named_parameters():
-        grad_elementwise(t.grad, refs[True][0][k], refs[False][0][k], k, flips=True, mag=mags[k])
+    grad_layers({k: t.grad for k, t in dec.named_parameters()}, refs[True][0], refs[False][0], mags)
     grad_elementwise(pts.feats.grad, refs[True][1], refs[False][1], 'dL/dfeats', flips=True, mag=mags['feats'])
 
 
@@ -550,8 +586,7 @@ def test_regulation_with_points(pnr_mod, dev):
             mags = mag_arrays(mag, params)
             close(s, sr, 2e-5 * sr.abs().max().item(), 'sigma')
     grad_elementwise(pts.feats.grad, refs[True][1], refs[False][1], 'dL/dfeats', flips=True, mag=mags['feats'])
-    for k, t in dec.named_parameters():
-        grad_elementwise(t.grad, refs[True][0][k], refs[False][0][k], k, flips=True, mag=mags[k])
+    grad_layers({k: t.grad for k, t in dec.named_parameters()}, refs[True][0], refs[False][0], mags)
 
 
 def test_gather_f16_features_equal_rounded_fp32(pnr_mod, dev):
