@@ -522,8 +522,9 @@ def sfwd_extra(pnr, plib, slam, params, bound, pose, dev, ddp, lib, steps=10, cp
            'steps': steps, 'n_gpus': world, 'scaling': 'strong' if fixed_global else 'weak',
            'rays_per_gpu': int(ro.shape[0]), 'global_batch': total,
            'roofline': kernel_roofline(kt, prec, el, traffic_units=False)}
-    if out['roofline'] is not None:
-        out['roofline']['kernel'] += ' (eval, no activation saves)'
+    if out['roofline'] is not None:  # the eval forward (f16x3): 16-point waves, two per SIMD (csrc/mlp16w.h)
+        out['roofline']['kernel'] = ('k_mlp_fwd16w' if prec == 'f16x3' else out['roofline']['kernel']) + \
+            ' (eval, no activation saves)'
     if cpu and params is not None and world == 1:
         def gpu_render(ro_c, rd_c, gt_c):
             with torch.no_grad():

@@ -4,7 +4,6 @@
 #include <cstdlib>
 
 #include "mlp16.h"
-#include "mlp16u.h"
 #include "mlp16w.h"
 #include "pack_fp32.h"
 
@@ -374,15 +373,16 @@ int launch_fc_pack_all(const float* const* fcp, float* out, hipStream_t st, int 
   return hip_status(hipGetLastError());
 }
 
-// The f16x3 forward without features has three kernels: 0 k_mlp_fwd16 (32-point waves, one per SIMD),
-// 1 k_mlp_fwd16w (16-point waves, two per SIMD, mlp16w.h), 2 k_mlp_fwd16u (output units split over two
-// waves per SIMD, mlp16u.h).  PNR_FWD_VARIANT (environment, read per launch) picks one for A/B runs;
-// the default is measured (tools/w16_ab.py, 4.19M points, one process, interleaved rounds): the eval
-// forward runs k_mlp_fwd16w (4.38-4.49 ms against 4.71-4.83), the training forward k_mlp_fwd16
-// (6.18-6.29 ms against 6.29-6.47 for k_mlp_fwd16w and 6.99-7.37 for k_mlp_fwd16u).
+// The f16x3 forward without features: k_mlp_fwd16w (16-point waves, two per SIMD, mlp16w.h) by
+// default, k_mlp_fwd16 (32-point waves, one per SIMD) with PNR_FWD_VARIANT=0 (environment, read per
+// launch: A/B runs).  Measured (tools/w16_ab.py, 4.19M points, one process, interleaved rounds,
+// profiles/r06_fwd_variants.txt): eval 4.34 against 4.69 ms, training 5.88 against 6.16 ms.  (The
+// output-unit split over two waves per SIMD, k_mlp_fwd16u, measured 5.08-5.16 / 7.20-7.37 ms and was
+// removed.)
 int fwd16_variant(int save) {
   const char* e = getenv("PNR_FWD_VARIANT");
-  return e ? atoi(e) : (save == 0 ? 1 : 0);
+  (void)save;
+  return e ? atoi(e) : 1;
 }
 
 int launch_mlp_fwd_bf(int prec, const float* packed, const PointSrc& src, int mode, int64_t P, float* raw,
@@ -421,7 +421,6 @@ int launch_mlp_fwd_bf(int prec, const float* packed, const PointSrc& src, int mo
       b.wmain = reinterpret_cast<const char*>(packed + kOffW16);
       return launch_fwd16w(mode, grid, st, b, sv);
     }
-    if (var == 2) return launch_fwd16u(mode, grid, st, a, sv);  // unit-split wave pairs (mlp16u.h)
   }
   switch (prec) {
     case PNR_PREC_BF16X3: return launch_fwd16_bf16x3(mode, grid, st, a, hasc, sv);

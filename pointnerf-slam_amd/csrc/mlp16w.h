@@ -60,13 +60,16 @@ struct W16Geo {
   static constexpr int kRawOff = kNbuf * kSlot;             // raw table (8 KiB: biases, Fourier B, scales)
   static constexpr int kWoOff = kRawOff + (int)kRawBytes;   // Wo hi / lo image (16 KiB)
   static constexpr int kLds = kWoOff + (int)kW16WoBytes;    // 152 KiB
+// the group that meets the next slot: 11 in the eval kernel, 13 with training saves (A/B at 4.19M
+// points, profiles/r06_fwd_variants.txt: eval 4.34 / 4.40 / 4.44 ms and training 6.37 / 5.88 / 6.54 ms at
+// 11 / 13 / 14)
 #ifndef PNR_W16_SYNC
-#define PNR_W16_SYNC 11
+#define PNR_W16_SYNC 0
 #endif
 #ifndef PNR_W16_RING
 #define PNR_W16_RING 3
 #endif
-  static constexpr int kSync = PNR_W16_SYNC;                // group of a step that meets the next slot
+  __host__ __device__ static constexpr int sync(int sv) { return PNR_W16_SYNC ? PNR_W16_SYNC : (sv == 0 ? 11 : 13); }
   static constexpr int kRing = PNR_W16_RING, kPf = kRing - 1;  // fragment ring, groups prefetched ahead
   // epilogue pieces of a converting step: conv1 (bias, ReLU, masks) and conv2 (save, split) of
   // output tile 2 ct + q
@@ -113,6 +116,7 @@ struct W16Fwd {
   static constexpr bool SAVE = SV != 0, SAVEH = SV == 1;
   using G = W16Geo;
   static constexpr int kSteps = G::kSteps, kD = G::kD, kPf = G::kPf, kRing = G::kRing;
+  static constexpr int kSync = G::sync(SV);
 
   __host__ __device__ static constexpr int n_glds(int g) { return g < kSteps ? 4 : 0; }
   // VMEM stores the epilogue of step g issues in group T
@@ -145,14 +149,14 @@ struct W16Fwd {
       int first = 0;
       if (i >= kD && i - kD >= 1) {
         const int p = i - kD;
-        n += stores_rng(p - 1, G::kSync + 1, G::kNT - 1, ph);
+        n += stores_rng(p - 1, kSync + 1, G::kNT - 1, ph);
         first = p;
       } else {
         if (i < kD) n += 1;  // DMA(i) issued in the prologue, before the x save
         first = 0;
       }
       for (int g = first; g <= i - 2; ++g) n += stores_rng(g, 0, G::kNT - 1, ph);
-      n += stores_rng(i - 1, 0, G::kSync, ph);
+      n += stores_rng(i - 1, 0, kSync, ph);
     }
     return n;
   }
@@ -346,7 +350,7 @@ struct W16Fwd {
         }
       }
       if constexpr (g + 1 < kSteps) {
-        if constexpr (T == G::kSync) {
+        if constexpr (T == kSync) {
           sync_chunk<younger_b(g + 1)>();
           stage_step<g + 1 + kD>(a.wmain, lds, S.sb);
         }

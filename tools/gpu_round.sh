@@ -18,7 +18,7 @@
 #               (tools/prof_round.sh), the gather's traffic passes and kernel stats, the faithful
 #               iteration's kernel stats
 set -o pipefail
-TAG=${PNR_TAG:-r05}
+TAG=${PNR_TAG:-r06}
 cd /tmp && export TMPDIR=/tmp
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out

@@ -58,7 +58,7 @@ def main():
 
     ref, gref = run('fp32', 0, True)
     ref_e, _ = run('fp32', 0, False)
-    for w16 in (0, 1, 2):
+    for w16 in (0, 1):
         o, _ = run('f16x3', w16, False)
         ot, gr = run('f16x3', w16, True)
         torch.cuda.synchronize()
@@ -68,9 +68,9 @@ def main():
         print(f'variant {w16}: eval max|d|/max vs fp32 {e:.3e}, training {et:.3e}, grads max rel (per tensor max) {eg:.3e}',
               flush=True)
     lib.pnr_timing_enable(1)
-    res = {v: {'eval': [], 'train': []} for v in (0, 1, 2)}
+    res = {v: {'eval': [], 'train': []} for v in (0, 1)}
     for rd in range(args.rounds):
-        for w16 in (0, 1, 2):
+        for w16 in (0, 1):
             for mode in ('eval', 'train'):
                 timing_read(0)
                 for _ in range(args.reps):
@@ -79,7 +79,7 @@ def main():
                 n, ms, u = timing_read(0)
                 res[w16][mode].append(ms / n)
     lib.pnr_timing_enable(0)
-    for w16 in (0, 1, 2):
+    for w16 in (0, 1):
         for mode in ('eval', 'train'):
             v = res[w16][mode]
             tf = 443438 * P / (np.median(v) * 1e-3) / 1e12
