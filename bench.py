@@ -391,8 +391,9 @@ def kernel_roofline(kt, prec, el_s, traffic_units=True):
             fl = FLOP_PER_POINT_FWD if name == 'mlp_fwd' else FLOP_PER_POINT_BWD
             # the delta chain is fp32 in the fp32 mode and the f16x3 split in every other mode
             kprec = prec if name == 'mlp_fwd' else ('fp32' if prec == 'fp32' else 'f16x3')
-            kname = ('k_mlp_fwd16' if prec != 'fp32' else 'k_mlp_fwd') if name == 'mlp_fwd' else \
-                ('k_mlp_bwd16' if prec != 'fp32' else 'k_mlp_bwd')
+            # (the f16x3 forward without features runs the 16-point-wave kernel, csrc/mlp16w.h)
+            kname = ({'fp32': 'k_mlp_fwd', 'f16x3': 'k_mlp_fwd16w'}.get(prec, 'k_mlp_fwd16') if name == 'mlp_fwd' else
+                     ('k_mlp_bwd16' if prec != 'fp32' else 'k_mlp_bwd'))
         # PMC traffic is kept per training point: the grouped launch's points are the delta chain's
         pts = (kt['mlp_bwd'][2] / launches if 'mlp_bwd' in kt else None) if name == 'wgrad_group' else units / launches
         cand = {'kernel': kname, 'launches': launches, 'prec': kprec, 'peak': ALGO_PEAK_TF[kprec],
@@ -402,7 +403,8 @@ def kernel_roofline(kt, prec, el_s, traffic_units=True):
             best = cand
     if best is None:
         return None
-    tkey = {'k_mlp_fwd': 'k_mlp_fwd_train', 'k_mlp_fwd16': 'k_mlp_fwd16_train', 'k_mlp_bwd': 'k_mlp_bwd',
+    tkey = {'k_mlp_fwd': 'k_mlp_fwd_train', 'k_mlp_fwd16': 'k_mlp_fwd16_train', 'k_mlp_fwd16w': 'k_mlp_fwd16_train',
+            'k_mlp_bwd': 'k_mlp_bwd',
             'k_mlp_bwd16': 'k_mlp_bwd16', 'k_wgrad16_group': 'k_wgrad16_group'}
     traffic = pmc_traffic(tkey[best['kernel']], best['points']) if traffic_units and best['points'] else None
     return {'bound': 'mfma', 'achieved': round(best['achieved'], 2), 'peak': round(best['peak'], 1),
@@ -434,7 +436,8 @@ def kernel_table(kt, prec, el_s, steps, fc=False):
         g = kt.get('wgrad_group', (0, 0.0, 0))
         w = kt.get('wgrad', (0, 0.0, 0))
         kt['wgrad_all'] = (g[0] + w[0], g[1] + w[1], 0)
-    for name, fl, kname in (('mlp_fwd', FLOP_PER_POINT_FWD, 'k_mlp_fwd16 (training, saves)'),
+    fwd_label = 'k_mlp_fwd16w (training, saves)' if prec == 'f16x3' else 'k_mlp_fwd16 (training, saves)'
+    for name, fl, kname in (('mlp_fwd', FLOP_PER_POINT_FWD, fwd_label),
                             ('mlp_bwd', FLOP_PER_POINT_BWD, 'k_mlp_bwd16 (delta chain)'),
                             ('wgrad_all', 443430 + (65536 if fc else 0),
                              'k_wgrad16_group + k_wgrad_skinny (all weight gradients)')):
@@ -448,6 +451,7 @@ def kernel_table(kt, prec, el_s, steps, fc=False):
                       'ms_per_step': round(ms / steps, 3),
                       'share_of_step': round(ms / (el_s * 1e3), 3)}
     pm = {'k_mlp_fwd16 (training, saves)': ('void pnr::k_mlp_fwd16<3, false, 1>', 'void pnr::k_mlp_fwd16<3, false, true>'),
+          'k_mlp_fwd16w (training, saves)': ('void pnr::k_mlp_fwd16w<1>',),
           'k_mlp_bwd16 (delta chain)': ('void pnr::k_mlp_bwd16<false>',)}
     for k, names in pm.items():
         for b in names:
@@ -522,9 +526,8 @@ def sfwd_extra(pnr, plib, slam, params, bound, pose, dev, ddp, lib, steps=10, cp
            'steps': steps, 'n_gpus': world, 'scaling': 'strong' if fixed_global else 'weak',
            'rays_per_gpu': int(ro.shape[0]), 'global_batch': total,
            'roofline': kernel_roofline(kt, prec, el, traffic_units=False)}
-    if out['roofline'] is not None:  # the eval forward (f16x3): 16-point waves, two per SIMD (csrc/mlp16w.h)
-        out['roofline']['kernel'] = ('k_mlp_fwd16w' if prec == 'f16x3' else out['roofline']['kernel']) + \
-            ' (eval, no activation saves)'
+    if out['roofline'] is not None:
+        out['roofline']['kernel'] += ' (eval, no activation saves)'
     if cpu and params is not None and world == 1:
         def gpu_render(ro_c, rd_c, gt_c):
             with torch.no_grad():

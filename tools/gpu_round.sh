@@ -73,6 +73,8 @@ for step in "$@"; do
       tail -12 ${O}_pmcsearch.log ;;
     npf)
       run 200 ${O}_c3.log python3 tools/np_faithful.py --case C3 --iters 50
+      run 200 ${O}_c3_bf16.log python3 tools/np_faithful.py --case C3 --iters 50 --precision bf16
+      tail -1 ${O}_c3_bf16.log
       run 200 ${O}_c5.log python3 tools/np_faithful.py --case C5 --iters 30
       tail -1 ${O}_c3.log; tail -1 ${O}_c5.log
       run 300 gpurun_out/prof_${TAG}_c3.log rocprofv3 --kernel-trace --stats --output-format csv \
