@@ -351,6 +351,7 @@ int mlp_backward_core(int prec, const float* packed, const SaveArgs& sv, int64_t
       WgradSyn syn{reinterpret_cast<const float4*>(b.g_out + p0 * 4), sv.masks + 3 * (sv.ld / 32) * 64, p0 / 32,
                    packed + packed_raw_wo_offset(), sv.xP + p0, packed + packed_raw_fb_offset(), pp, pb, nullptr,
                    (grads ? 4 : 0) + (want_fc ? 4 : 0), skinny_in_group ? device_cu_count() / PNR_SKINNY_CU_DIV : 0, 0.f};
+      syn.bsplit = hsave_is_split(sv.hP) ? 1 : 0;  // h1..h3 as f16 parts (the 16-point-wave forward)
       if (grads)
         syn.group_weight += wgrad16_job_weight(kWgradOutDelta, false) + 2 * wgrad16_job_weight(kWgradHidden, false) +
                             wgrad16_job_weight(kWgradFirstX, false);
@@ -411,6 +412,7 @@ int mlp_backward_core(int prec, const float* packed, const SaveArgs& sv, int64_t
         rc = launch_wgrad16_group(gjobs, ng, st);
       }
     } else if (grads) {
+      if (hsave_is_split(sv.hP)) return PNR_E_ARG;  // saved by the f16x3 forward: not fp32 activations
       const float* hp = sv.hP + p0 * kHidden;
       rc = launch_wgrad(kWgradOut, b.g_out + p0 * 4, 4, hp + 3 * hstride, kHidden, C, grads[9], kHidden, grads[10],
                         b.part, b.part_bias, st);

@@ -2,6 +2,8 @@
 // the forward dispatch on PNR_PREC_*.
 #include <algorithm>
 #include <cstdlib>
+#include <mutex>
+#include <unordered_map>
 
 #include "mlp16.h"
 #include "mlp16w.h"
@@ -383,6 +385,26 @@ int fwd16_variant(int save) {
   const char* e = getenv("PNR_FWD_VARIANT");
   (void)save;
   return e ? atoi(e) : 1;
+}
+
+// the f16x3 forward without the feature branch runs k_mlp_fwd16w (variant 1), whose saves are split
+bool fwd_saves_split(int prec, const FeatArgs* feat) {
+  return PNR_W16_HSPLIT != 0 && prec == PNR_PREC_F16X3 && !(feat && feat->fcw) && fwd16_variant(1) == 1;
+}
+
+namespace {
+std::mutex g_hsave_mu;
+std::unordered_map<const float*, bool> g_hsave;
+}  // namespace
+void hsave_set_split(const float* hP, bool split) {
+  std::lock_guard<std::mutex> lk(g_hsave_mu);
+  if (g_hsave.size() > 4096) g_hsave.clear();  // stale areas (freed workspaces): every forward re-marks its own
+  g_hsave[hP] = split;
+}
+bool hsave_is_split(const float* hP) {
+  std::lock_guard<std::mutex> lk(g_hsave_mu);
+  const auto it = g_hsave.find(hP);
+  return it != g_hsave.end() && it->second;
 }
 
 int launch_mlp_fwd_bf(int prec, const float* packed, const PointSrc& src, int mode, int64_t P, float* raw,

@@ -44,6 +44,20 @@ constexpr int64_t kOffW16 = kPackedFloatsAll;  // floats, after the raw table
 constexpr int64_t kPackedFloatsW16 = kOffW16 + kW16Bytes / 4;
 static_assert(kOffW16 % 4 == 0, "16-B aligned image");
 
+// PNR_W16_HSPLIT=1 (experiment, not the default): training saves of h1..h3 (L = 0..2) in split form --
+// each 16-B group of 4 values holds their f16 parts {hi(v0,v1), hi(v2,v3), lo(v0,v1), lo(v2,v3)}
+// (split2, unscaled), the B operand image the weight-gradient GEMMs otherwise form per tile
+// (wgrad16.hip PRE); h4 stays fp32 (dWo's fp32 FMAs).  Gradients bitwise equal to the fp32 saves
+// (tools/lib_ab.py), the grouped launch's VALU instructions -8.6 %, but its time unchanged at the
+// room0 batch (0.161 / 0.162 ms) and -1.4 % at 4.19M points, while this kernel's training variant
+// spills 35 registers instead of 15 and runs 3.7 % slower: room0 0.5109-0.5120 ms (fp32 saves)
+// against 0.5171-0.5189 (profiles/r06_hsplit_ab.txt).  Not kept.
+#ifndef PNR_W16_HSPLIT
+#define PNR_W16_HSPLIT 0
+#endif
+template <int L>
+constexpr bool kSplitSave = PNR_W16_HSPLIT != 0 && L < 3;
+
 __host__ __device__ constexpr int w16_layer(int g) { return g < 3 ? 0 : 1 + (g - 3) / 8; }
 __host__ __device__ constexpr int w16_kc(int g) { return g < 3 ? g : (g - 3) % 8; }
 // step g converts input tile w16_ct(g) of h_{w16_cl(g)} (tile 0 of a layer in its own last step)
@@ -293,15 +307,19 @@ struct W16Fwd {
     const float* v = S.v + 4 * q;
     (void)gq;
     typedef float v4f __attribute__((ext_vector_type(4)));
-    if constexpr (SAVEH)
-      *reinterpret_cast<__attribute__((address_space(1))) v4f*>(S.hrow + (int64_t)L * a.save.ld * kHidden +
-                                                                16 * (2 * ct + q)) = v4f{v[0], v[1], v[2], v[3]};
+    auto* dst = reinterpret_cast<__attribute__((address_space(1))) v4f*>(S.hrow + (int64_t)L * a.save.ld * kHidden +
+                                                                        16 * (2 * ct + q));
+    if constexpr (SAVEH && !kSplitSave<L>) *dst = v4f{v[0], v[1], v[2], v[3]};
     S.vmax = fmaxf(S.vmax, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
     // here, not sunk to the tile's end (which keeps every saved value alive: 232 spills)
     asm volatile("" : "+v"(S.vmax));
     uint32_t h0, l0, h1, l1;
     split2(v[0], v[1], h0, l0);
     split2(v[2], v[3], h1, l1);
+    // h1..h3 are only read again as the B operands of the weight-gradient GEMMs, which split them the
+    // same way (unscaled split2): the 16 B of 4 values hold their parts instead, {hi01, hi23, lo01, lo23}
+    if constexpr (SAVEH && kSplitSave<L>)
+      *reinterpret_cast<__attribute__((address_space(1))) u32x4*>(dst) = u32x4{h0, h1, l0, l1};
     u32x4 hv = __builtin_bit_cast(u32x4, S.nxt[0]);
     u32x4 lv = __builtin_bit_cast(u32x4, S.nxt[1]);
     hv[2 * q] = h0;

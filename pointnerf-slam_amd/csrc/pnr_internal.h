@@ -145,7 +145,7 @@ __device__ __forceinline__ void load_point(const PointSrc& s, int64_t p, float& 
 
 // Activation save area for training, POINT-major (row p = one point), ld = total points
 // (multiple of 128; padded points hold finite activations of x = 0 and get zero gradient).
-// fp32 in every precision (the split weight-gradient GEMMs split the values themselves).
+// fp32, except h1..h3 of the 16-point-wave f16x3 forward (f16 hi / lo parts: hsave_is_split below).
 struct SaveArgs {
   float* eP;       // [ld][96]        Fourier features sin(x@B)
   float* hP;       // [4][ld][256]    h1..h4
@@ -202,10 +202,18 @@ int launch_fc_pack_all(const float* const* fc, float* out, hipStream_t st, int f
 int launch_mlp_fwd_bf(int prec, const float* packed, const PointSrc& src, int mode, int64_t P, float* raw,
                       const SaveArgs* save, hipStream_t st, const FeatArgs* feat = nullptr,
                       uint32_t* status = nullptr);
+// Format of a save area's h1..h3 (host-side record keyed by SaveArgs::hP, set by every forward that
+// saves activations): fp32, or the f16 hi / lo parts the 16-point-wave forward stores (mlp16w.h
+// kSplitSave) -- the backward picks its weight-gradient B staging from it and refuses a split save
+// area on the fp32 path.  (Host order = stream order, also under graph capture.)
+bool fwd_saves_split(int prec, const FeatArgs* feat);  // mlp16_pack.hip: the dispatch's own rule
+void hsave_set_split(const float* hP, bool split);
+bool hsave_is_split(const float* hP);
 // forward dispatch on PNR_PREC_*
 inline int mlp_fwd(int prec, const float* packed, const PointSrc& src, int mode, int64_t P, float* raw,
                    const SaveArgs* save, hipStream_t st, const FeatArgs* feat = nullptr,
                    uint32_t* status = nullptr) {
+  if (save && save->hP) hsave_set_split(save->hP, prec != PNR_PREC_FP32 && fwd_saves_split(prec, feat));
   if (prec == PNR_PREC_FP32) return launch_mlp_fwd(packed, src, mode, P, raw, save, st, feat);
   return launch_mlp_fwd_bf(prec, packed, src, mode, P, raw, save, st, feat, status);
 }
@@ -275,6 +283,8 @@ struct WgradSyn {
   // CUs left to the grouped launch's skinny jobs (dWo / dB) when the GEMMs are sized to fill the chip once
   int reserve_cus;
   float group_weight;
+  // kWgradHidden / kWgradOutDelta: B (h1..h3) saved as f16 hi / lo parts (hsave_is_split)
+  int bsplit;
 };
 // relative cost per 32-point tile of a split weight-gradient GEMM kind in a grouped launch (measured
 // one job per launch at its grouped grid, PNR_WGRAD_SPLIT=1: room0 and C3 batches)

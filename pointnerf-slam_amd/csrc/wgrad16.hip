@@ -139,7 +139,7 @@ __device__ __forceinline__ void wx_load(const WxArgs& a, int64_t k0, WxRegs<NTB,
 // B tile -> hi / lo f16 planes of `slot` (SYN: + the next tile's g_out rows into the other slot;
 // BSC: fp32 rows of kBscRow floats)
 
-template <int NTB, int WB, bool SYN, bool FOUR, bool BSC = false>
+template <int NTB, int WB, bool SYN, bool FOUR, bool BSC = false, bool PRE = false>
 __device__ __forceinline__ void wx_stage_b(const WxRegs<NTB, WB>& R, char* slot, char* next_slot,
                                            const float (&fbr)[Wx3<NTB, WB>::kBPer][3][4]) {
   using Cfg = Wx3<NTB, WB>;
@@ -152,6 +152,13 @@ __device__ __forceinline__ void wx_stage_b(const WxRegs<NTB, WB>& R, char* slot,
       const int r = q / Cfg::kC4, c = 4 * (q % Cfg::kC4);
       if constexpr (BSC) {
         *reinterpret_cast<float4*>(slot + (r * kBscRow + c) * 4) = R.b[i];
+        continue;
+      }
+      char* base = slot + (c >> 5) * kTileB + r * 64 + (c & 31) * 2;
+      if constexpr (PRE) {  // the forward stored the parts: {hi01, hi23, lo01, lo23} (mlp16w.h kSplitSave)
+        const uint4 u = __builtin_bit_cast(uint4, R.b[i]);
+        *reinterpret_cast<uint2*>(base) = make_uint2(u.x, u.y);
+        *reinterpret_cast<uint2*>(base + Cfg::kPlane) = make_uint2(u.z, u.w);
         continue;
       }
       float v[4] = {R.b[i].x, R.b[i].y, R.b[i].z, R.b[i].w};
@@ -172,7 +179,6 @@ __device__ __forceinline__ void wx_stage_b(const WxRegs<NTB, WB>& R, char* slot,
       uint32_t h0, l0, h1, l1;  // packed f16 hi / lo pairs (dev_common.h split2)
       split2(v[0], v[1], h0, l0);
       split2(v[2], v[3], h1, l1);
-      char* base = slot + (c >> 5) * kTileB + r * 64 + (c & 31) * 2;
       *reinterpret_cast<uint2*>(base) = make_uint2(h0, h1);
       *reinterpret_cast<uint2*>(base + Cfg::kPlane) = make_uint2(l0, l1);
     }
@@ -196,8 +202,9 @@ __device__ __forceinline__ f16x8 tr_frag(const char* img, int T, int s) {
 
 // workgroup `bid` of one weight-gradient GEMM (k_wgrad16: bid = blockIdx.x; k_wgrad16_group: the
 // block's index within its job)
-template <int NTB, int WB, bool SYN, bool FOUR, bool BSC, bool MSK>
+template <int NTB, int WB, bool SYN, bool FOUR, bool BSC, bool MSK, bool PRE = false>
 __device__ __forceinline__ void wgrad16_body(const WxArgs& a, const int bid, char* lds) {
+  static_assert(!PRE || (WB == 256 && !FOUR && !BSC && !MSK), "PRE: B = split h1..h3 (hidden / dW3 GEMMs)");
   static_assert(!MSK || (!SYN && !BSC), "MSK: the hidden / first-layer GEMMs");
   static_assert(!BSC || (NTB == 1 && WB == 32 && !FOUR), "BSC: the fc_c shape");
   static_assert(!SYN || !BSC || !MSK, "SYN + BSC: dWc_3 on A = Wo^T g_out (unmasked)");
@@ -243,7 +250,7 @@ __device__ __forceinline__ void wgrad16_body(const WxArgs& a, const int bid, cha
     char* slot = lds + (t & 1) * Cfg::kSlot;
     // g_out rows of tile t + 1 go to the other slot: their last reader (synth of tile t - 1) ran
     // before the previous barrier
-    wx_stage_b<NTB, WB, SYN, FOUR, BSC>(R, slot, lds + ((t + 1) & 1) * Cfg::kSlot, fbr);
+    wx_stage_b<NTB, WB, SYN, FOUR, BSC, PRE>(R, slot, lds + ((t + 1) & 1) * Cfg::kSlot, fbr);
     if constexpr (SYN) {
       // delta4 = (Wo^T g_out) masked, fp32 FMAs (the tile's g_out rows from LDS, staged before the
       // previous barrier; broadcast reads)
@@ -344,10 +351,10 @@ __device__ __forceinline__ void wgrad16_body(const WxArgs& a, const int bid, cha
   if (a.bias && hh == 0) a.part_bias[(int64_t)bid * 256 + 32 * w + lane] = cs;
 }
 
-template <int NTB, int WB, bool SYN, bool FOUR, bool BSC, bool MSK>
+template <int NTB, int WB, bool SYN, bool FOUR, bool BSC, bool MSK, bool PRE = false>
 __global__ __launch_bounds__(512, 1) void k_wgrad16(WxArgs a) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
-  wgrad16_body<NTB, WB, SYN, FOUR, BSC, MSK>(a, blockIdx.x, lds);
+  wgrad16_body<NTB, WB, SYN, FOUR, BSC, MSK, PRE>(a, blockIdx.x, lds);
 }
 
 // Skinny weight-gradient GEMMs (fp32 FMAs), bandwidth-bound on B:
@@ -446,7 +453,7 @@ struct Wgrad16Group {
   int n;
 };
 enum : int { kVarHidden = 0, kVarHiddenM, kVarSyn, kVarFirstX, kVarFirstXM, kVarFc, kVarFcOut, kVarSkinnyOut,
-              kVarSkinnyFour };
+              kVarSkinnyFour, kVarHiddenP, kVarSynP };  // P: B pre-split by the forward (mlp16w.h kSplitSave)
 __global__ __launch_bounds__(512, 1) void k_wgrad16_group(Wgrad16Group G) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   int q = 0;
@@ -456,6 +463,8 @@ __global__ __launch_bounds__(512, 1) void k_wgrad16_group(Wgrad16Group G) {
     case kVarHidden: wgrad16_body<8, 256, false, false, false, false>(G.a[q], bid, lds); break;
     case kVarHiddenM: wgrad16_body<8, 256, false, false, false, true>(G.a[q], bid, lds); break;
     case kVarSyn: wgrad16_body<8, 256, true, false, false, false>(G.a[q], bid, lds); break;
+    case kVarHiddenP: wgrad16_body<8, 256, false, false, false, false, true>(G.a[q], bid, lds); break;
+    case kVarSynP: wgrad16_body<8, 256, true, false, false, false, true>(G.a[q], bid, lds); break;
     case kVarFirstX: wgrad16_body<3, 96, false, true, false, false>(G.a[q], bid, lds); break;
     case kVarFirstXM: wgrad16_body<3, 96, false, true, false, true>(G.a[q], bid, lds); break;
     case kVarFcOut: wgrad16_body<1, 32, true, false, true, false>(G.a[q], bid, lds); break;
@@ -669,7 +678,8 @@ int wgrad16_prepare(int kind, const float* A, const float* B, int64_t K, int64_t
   }
   int var, ntb;
   if (kind == kWgradHidden) {
-    var = msk ? kVarHiddenM : kVarHidden;
+    if (msk && syn->bsplit) return PNR_E_ARG;  // the feature-branch forward saves fp32
+    var = msk ? kVarHiddenM : (syn->bsplit ? kVarHiddenP : kVarHidden);
     ntb = 8;
   } else if (kind == kWgradOutDelta) {  // dW3 += delta4^T h3, delta4 rebuilt from g_out and the h4 masks
     if (!syn->g_out || !syn->masks || !syn->wo) return PNR_E_ARG;
@@ -677,7 +687,7 @@ int wgrad16_prepare(int kind, const float* A, const float* B, int64_t K, int64_t
     a.masks = syn->masks;
     a.mgrp0 = syn->mgrp0;
     a.wo = syn->wo;
-    var = kVarSyn;
+    var = syn->bsplit ? kVarSynP : kVarSyn;
     ntb = 8;
   } else if (kind == kWgradFc) {  // dWc_l (256 x 32) += gH_l^T c
     a.nb = kCDim;
@@ -733,10 +743,10 @@ int launch_wgrad16_group(const Wgrad16Job* jobs, int n, hipStream_t st) {
   return hip_status(hipGetLastError());
 }
 
-template <int NTB, int WB, bool SYN = false, bool FOUR = false, bool BSC = false, bool MSK = false>
+template <int NTB, int WB, bool SYN = false, bool FOUR = false, bool BSC = false, bool MSK = false, bool PRE = false>
 static int launch_k(const WxArgs& a, int nwg, hipStream_t st) {
   using Cfg = Wx3<NTB, WB>;
-  auto kern = k_wgrad16<NTB, WB, SYN, FOUR, BSC, MSK>;
+  auto kern = k_wgrad16<NTB, WB, SYN, FOUR, BSC, MSK, PRE>;
   static const bool attr = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                                                Cfg::kLds) == hipSuccess;
   if (!attr) return PNR_E_ARG;
@@ -757,6 +767,8 @@ int launch_wgrad16(int kind, const float* A, const float* B, int64_t K, int64_t 
     case kVarHidden: rc = launch_k<8, 256>(j.a, j.nwg, st); break;
     case kVarHiddenM: rc = launch_k<8, 256, false, false, false, true>(j.a, j.nwg, st); break;
     case kVarSyn: rc = launch_k<8, 256, true>(j.a, j.nwg, st); break;
+    case kVarHiddenP: rc = launch_k<8, 256, false, false, false, false, true>(j.a, j.nwg, st); break;
+    case kVarSynP: rc = launch_k<8, 256, true, false, false, false, true>(j.a, j.nwg, st); break;
     case kVarFirstX: rc = launch_k<3, 96, false, true>(j.a, j.nwg, st); break;
     case kVarFirstXM: rc = launch_k<3, 96, false, true, false, true>(j.a, j.nwg, st); break;
     case kVarFcOut: rc = launch_k<1, 32, true, false, true>(j.a, j.nwg, st); break;
