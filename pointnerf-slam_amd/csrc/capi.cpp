@@ -348,43 +348,60 @@ int mlp_backward_core(int prec, const float* packed, const SaveArgs& sv, int64_t
       // hidden layers: dW_l += delta_{l+1}^T h_l  (W3: delta4.h3, W2: delta3.h2, W1: delta2.h1); delta4
       // is not stored by k_mlp_bwd16 (rank 4: rebuilt from g_out and the h4 masks inside the GEMM).
       // These GEMMs (and the fc_c ones below) are independent: prepared here, launched as one group.
+      // PNR_WGRAD_FC_FUSE=1 (experiment, off by default): with both the decoder's and the feature
+      // branch's gradients, each layer's fc_c GEMM runs inside the dW GEMM that reads the same dL/dh_l
+      // tiles (FC jobs, k_wgrad16_group_fc: the A stream read once).  The fused 256-column jobs do not fit
+      // the 256 registers a wave has at two waves per SIMD (36-40 spilled, 76 in the group kernel): the grouped launch took
+      // 1.89 ms against 1.00 at C5, C5 3.81-3.85 against 3.02 ms, the neural-point S-map 185 against
+      // 154-156 ms (profiles/r06_fc_fuse_ab.txt)
+      static const bool fc_fuse_env = getenv("PNR_WGRAD_FC_FUSE") && getenv("PNR_WGRAD_FC_FUSE")[0] == '1';
+      const bool fc_fuse = fc_fuse_env && grads && want_fc;
       WgradSyn syn{reinterpret_cast<const float4*>(b.g_out + p0 * 4), sv.masks + 3 * (sv.ld / 32) * 64, p0 / 32,
                    packed + packed_raw_wo_offset(), sv.xP + p0, packed + packed_raw_fb_offset(), pp, pb, nullptr,
-                   (grads ? 4 : 0) + (want_fc ? 4 : 0), skinny_in_group ? device_cu_count() / PNR_SKINNY_CU_DIV : 0, 0.f};
+                   (grads ? 4 : 0) + (want_fc && !fc_fuse ? 4 : 0),
+                   skinny_in_group ? device_cu_count() / PNR_SKINNY_CU_DIV : 0, 0.f};
       syn.bsplit = hsave_is_split(sv.hP) ? 1 : 0;  // h1..h3 as f16 parts (the 16-point-wave forward)
       if (grads)
         syn.group_weight += wgrad16_job_weight(kWgradOutDelta, false) + 2 * wgrad16_job_weight(kWgradHidden, false) +
                             wgrad16_job_weight(kWgradFirstX, false);
-      if (want_fc) syn.group_weight += 3 * wgrad16_job_weight(kWgradFc, false) + wgrad16_job_weight(kWgradFcOut, false);
+      if (fc_fuse) syn.group_weight += 4 * kWgradFcFusedWeight;
+      else if (want_fc)
+        syn.group_weight += 3 * wgrad16_job_weight(kWgradFc, false) + wgrad16_job_weight(kWgradFcOut, false);
       // with the feature branch k_mlp_bwd16 stores dL/dh_l only: delta_l = dL/dh_l masked in the GEMM
       const bool fmask = fb != nullptr;
       const int64_t mstride = (sv.ld / 32) * 64;
       const float* dsrc = fmask ? b.gH : b.dP;
+      // fcl >= 0: fuse the fc_c GEMM of layer fcl (dWc_l += (dL/dh_l)^T c, dbc_l += colsum) into this job
       auto prep = [&](int kind, const float* A, const float* B, float* Cw, int64_t ldc, float* bias,
-                      const uint4* amasks) {
+                      const uint4* amasks, int fcl = -1) {
         if (rc) return;
         syn.part = pp;
         syn.part_bias = pb;
         syn.amasks = amasks;
-        rc = wgrad16_prepare(kind, A, B, C, C, Cw, ldc, bias, &syn, &gjobs[ng], &jobs[nj]);
+        syn.fc_c = fcl >= 0 ? fb->c + p0 * kCDim : nullptr;
+        syn.fc_C = fcl >= 0 ? fb->g_fc[2 * fcl] : nullptr;
+        syn.fc_bias = fcl >= 0 ? fb->g_fc[2 * fcl + 1] : nullptr;
+        rc = wgrad16_prepare(kind, A, B, C, C, Cw, ldc, bias, &syn, &gjobs[ng], &jobs[nj], &jobs[nj + 1]);
         syn.amasks = nullptr;
+        syn.fc_c = nullptr;
         if (rc == 0) {
           ++ng;
           took();
+          if (fcl >= 0) took();
         }
       };
       if (grads) {
-        prep(kWgradOutDelta, nullptr, hp + 2 * hstride, grads[7], kHidden, grads[8], nullptr);
+        prep(kWgradOutDelta, nullptr, hp + 2 * hstride, grads[7], kHidden, grads[8], nullptr, fc_fuse ? 3 : -1);
         for (int l = 2; l >= 1; --l)
           prep(kWgradHidden, dsrc + l * dstride, hp + (l - 1) * hstride, grads[1 + 2 * l], kHidden,
-               grads[2 + 2 * l], fmask ? sv.masks + l * mstride : nullptr);
+               grads[2 + 2 * l], fmask ? sv.masks + l * mstride : nullptr, fc_fuse ? l : -1);
         // first layer: dW0 (256x93) += delta1^T e ; db0 -- e = sin(x@B) recomputed from the saved x
         // (k_mlp_fwd16 saves no e)
-        prep(kWgradFirstX, dsrc, nullptr, grads[1], kFourier, grads[2], fmask ? sv.masks : nullptr);
+        prep(kWgradFirstX, dsrc, nullptr, grads[1], kFourier, grads[2], fmask ? sv.masks : nullptr, fc_fuse ? 0 : -1);
       }
       // feature branch: dWc_l (256x32) += (dL/dh_l)^T c ; dbc_l += colsum(dL/dh_l)
       // (dL/dh4 = Wo^T g_out is rank 4: k_mlp_bwd16 does not store it, the dWc_3 GEMM rebuilds it)
-      if (want_fc)
+      if (want_fc && !fc_fuse)
         for (int l = 0; l < 4; ++l)
           prep(l == 3 ? kWgradFcOut : kWgradFc, b.gH + l * dstride, fb->c + p0 * kCDim, fb->g_fc[2 * l], kCDim,
                fb->g_fc[2 * l + 1], nullptr);

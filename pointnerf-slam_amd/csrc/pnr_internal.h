@@ -285,6 +285,11 @@ struct WgradSyn {
   float group_weight;
   // kWgradHidden / kWgradOutDelta: B (h1..h3) saved as f16 hi / lo parts (hsave_is_split)
   int bsplit;
+  // non-null c: the job also runs the fc_c GEMM of its layer on its A tiles (FC): dWc += A^T c,
+  // dbc += colsum(A), A = dL/dh_l unmasked; its reduction goes to wgrad16_prepare's *red2
+  const float* fc_c;
+  float* fc_C;
+  float* fc_bias;
 };
 // relative cost per 32-point tile of a split weight-gradient GEMM kind in a grouped launch (measured
 // one job per launch at its grouped grid, PNR_WGRAD_SPLIT=1: room0 and C3 batches)
@@ -313,6 +318,11 @@ struct WxArgs {
   const float* fb;       // Fourier B padded [3][96]
   float* part;           // non-null: [grid][256][NTB 32] partial tiles + part_bias [grid][256]
   float* part_bias;      //   (plain stores; k_wgrad_reduce sums them into C / bias)
+  // FC (feature branch, wgrad16.hip): the fc_c GEMM dWc_l = (dL/dh_l)^T c on the same A tiles -- A
+  // unmasked there -- into a second partial region ([grid][256][32] + [grid][256])
+  const float* cB;       // c rows [K][32], chunk-local
+  float* part2;
+  float* part_bias2;
 };
 
 // a prepared GEMM of a grouped launch (wgrad16_prepare -> launch_wgrad16_group)
@@ -322,6 +332,9 @@ struct Wgrad16Job {
   int nwg;   // workgroups (split-K)
 };
 constexpr int kMaxGemmJobs = 10;  // 4 hidden + 4 fc_c GEMMs + the skinny dWo / dB
+// per-tile cost of a fused fc_c GEMM (FC) relative to a hidden GEMM: its A stream comes with the main
+// GEMM's (wgrad16_prepare's grid sizing)
+constexpr float kWgradFcFusedWeight = 0.22f;
 constexpr int kWgradMaxWg = 512;    // fp32 k_wgrad grid cap
 constexpr int kWgrad16MaxWg = 256;  // split k_wgrad16 grid cap
 constexpr int kSkinnyMaxWg = 1024;  // k_wgrad_skinny grid cap
@@ -375,8 +388,10 @@ int launch_wgrad(int kind, const float* A, int ma, const float* B, int nb, int64
 // defer: non-null = fill the reduction job instead of launching it (launch_part_reduce_multi later)
 int launch_wgrad16(int kind, const float* A, const float* B, int64_t K, int64_t kb_rows, float* C, int64_t ldc,
                    float* bias, hipStream_t st, const WgradSyn* syn = nullptr, ReduceJob* defer = nullptr);
+// syn->fc_c non-null (kWgradHidden / kWgradFirstX with syn->amasks, or kWgradOutDelta): the job also
+// runs its layer's fc_c GEMM (FC); that GEMM's reduction goes to *red2 (partials after the main ones)
 int wgrad16_prepare(int kind, const float* A, const float* B, int64_t K, int64_t kb_rows, float* C, int64_t ldc,
-                    float* bias, const WgradSyn* syn, Wgrad16Job* job, ReduceJob* red);
+                    float* bias, const WgradSyn* syn, Wgrad16Job* job, ReduceJob* red, ReduceJob* red2 = nullptr);
 int launch_wgrad16_group(const Wgrad16Job* jobs, int n, hipStream_t st);
 // the skinny dWo (out = 1: A = g_out rows, B = h4, + dbo) / dB (out = 0: A = x rows, B = g_arg) as a job
 // of a grouped launch

@@ -57,7 +57,8 @@ struct Wx3 {
   static constexpr int kPlane = NTB * kTileB;            // one plane (hi or lo) of a B tile
   // the tile's 32 g_out rows (SYN) follow the B image: the two planes, or BSC's fp32 rows
   static constexpr int kGo = 2 * kPlane > 32 * kBscRow * 4 ? 2 * kPlane : 32 * kBscRow * 4;
-  static constexpr int kSlot = kGo + 512;
+  static constexpr int kCOff = kGo + 512;                // FC: the tile's c rows (fp32, kBscRow floats)
+  static constexpr int kSlot = kCOff + 32 * kBscRow * 4;
   static constexpr int kLds = 2 * kSlot;                 // double-buffered
   static constexpr int kC4 = WB / 4;                     // float4 per B row
   static constexpr int kB4 = 32 * kC4;                   // float4 per B tile
@@ -71,6 +72,8 @@ struct WxRegs {
   float a[16];                                 // A element (k-step s, j) -> a[8s + j]  (SYN: mask words)
   float4 b[Wx3<NTB, WB>::kBPer];               // FOUR: the B row's point x (the values come in stage)
   float4 go;                                   // SYN: g_out row k0 + 32 + tid (threads < 32): the NEXT tile's
+  float4 cv;                                   // FC: c piece (row tid / 8, columns 4 (tid % 8)..), threads < 256
+  uint32_t mb;                                 // MSK + FC: the ReLU bits of a[0..15] (A itself stays unmasked)
 };
 
 // mask-word pointer of unit u = 32 w + (lane & 31) for the 32-point group of k0: the lane's 16
@@ -81,7 +84,7 @@ __device__ __forceinline__ const uint32_t* mask_words(const uint4* masks, int64_
 }
 __device__ __forceinline__ int mask_bit(int u) { return ((u >> 5) & 1) * 16 + ((u >> 3) & 3) * 4 + (u & 3); }
 
-template <int NTB, int WB, bool SYN, bool FOUR, bool MSK = false>
+template <int NTB, int WB, bool SYN, bool FOUR, bool MSK = false, bool FC = false>
 __device__ __forceinline__ void wx_load(const WxArgs& a, int64_t k0, WxRegs<NTB, WB>& R) {
   using Cfg = Wx3<NTB, WB>;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -112,7 +115,14 @@ __device__ __forceinline__ void wx_load(const WxArgs& a, int64_t k0, WxRegs<NTB,
     for (int s = 0; s < 2; ++s)
 #pragma unroll
       for (int j = 0; j < 8; ++j) R.a[8 * s + j] = Ab[(16 * s + j) * 256];
-    if constexpr (MSK) {  // delta = dL/dh where the forward's ReLU passed (bit sign-extended, ANDed)
+    if constexpr (MSK && FC) {  // the ReLU bits only: the fc_c GEMM needs A unmasked
+      const uint32_t* mw = mask_words(a.amasks, a.mgrp0 + k0 / 32);
+      const int bit = mask_bit(32 * wave_id() + (lane & 31));
+      uint32_t mb = 0u;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) mb |= ((mw[(8 * (lane >> 5) + 16 * (i >> 3) + (i & 7)) * 4] >> bit) & 1u) << i;
+      R.mb = mb;
+    } else if constexpr (MSK) {  // delta = dL/dh where the forward's ReLU passed (bit sign-extended, ANDed)
       const uint32_t* mw = mask_words(a.amasks, a.mgrp0 + k0 / 32);
       const int bit = mask_bit(32 * wave_id() + (lane & 31));
 #pragma unroll
@@ -122,6 +132,13 @@ __device__ __forceinline__ void wx_load(const WxArgs& a, int64_t k0, WxRegs<NTB,
           const int m = (int)(mw[(8 * (lane >> 5) + 16 * s + j) * 4] << (31 - bit)) >> 31;
           R.a[8 * s + j] = __int_as_float(__float_as_int(R.a[8 * s + j]) & m);
         }
+    }
+  }
+  if constexpr (FC) {
+    if (tid < 256) {
+      int64_t row = k0 + (tid >> 3);
+      row = row < a.kb_rows ? row : a.kb_rows - 1;
+      R.cv = *reinterpret_cast<const float4*>(a.cB + row * kCDim + 4 * (tid & 7));
     }
   }
 #pragma unroll
@@ -139,12 +156,14 @@ __device__ __forceinline__ void wx_load(const WxArgs& a, int64_t k0, WxRegs<NTB,
 // B tile -> hi / lo f16 planes of `slot` (SYN: + the next tile's g_out rows into the other slot;
 // BSC: fp32 rows of kBscRow floats)
 
-template <int NTB, int WB, bool SYN, bool FOUR, bool BSC = false, bool PRE = false>
+template <int NTB, int WB, bool SYN, bool FOUR, bool BSC = false, bool PRE = false, bool FC = false>
 __device__ __forceinline__ void wx_stage_b(const WxRegs<NTB, WB>& R, char* slot, char* next_slot,
                                            const float (&fbr)[Wx3<NTB, WB>::kBPer][3][4]) {
   using Cfg = Wx3<NTB, WB>;
   const int tid = threadIdx.x;
   if (SYN && tid < 32) reinterpret_cast<float4*>(next_slot + Cfg::kGo)[tid] = R.go;
+  if (FC && tid < 256)
+    *reinterpret_cast<float4*>(slot + Cfg::kCOff + ((tid >> 3) * kBscRow + 4 * (tid & 7)) * 4) = R.cv;
 #pragma unroll
   for (int i = 0; i < Cfg::kBPer; ++i) {
     const int q = tid + Cfg::kThreads * i;
@@ -200,15 +219,80 @@ __device__ __forceinline__ f16x8 tr_frag(const char* img, int T, int s) {
   return r;
 }
 
+// the fp32 B rows of a BSC tile (c: point features, 32 columns) as this lane's operand, split under
+// the wave's running B scale sb (lowered, with the accumulator, when this tile needs it), and the
+// tile's 6 MFMAs into acc
+__device__ __forceinline__ void bsc_tile(const char* rows, const f16x8 (&ah)[2], const f16x8 (&al)[2], f32x16& acc,
+                                         float& sb) {
+  const int lane = threadIdx.x & 63, hh = lane >> 5;
+  const float* tb = reinterpret_cast<const float*>(rows) + (lane & 31);
+  float bv[16];
+  float mb = 0.f;
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      bv[8 * s + j] = tb[(16 * s + 8 * hh + j) * kBscRow];
+      mb = fmaxf(mb, fabsf(bv[8 * s + j]));
+    }
+  if (__builtin_amdgcn_ballot_w64(mb * sb >= 32768.f) != 0) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mb = fmaxf(mb, __shfl_xor(mb, o));
+    const float ns = pt_scale(mb);
+    const float r = ns / sb;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] *= r;
+    sb = ns;
+  }
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    f16x8 bh, bl;
+    split8(bv + 8 * s, sb, bh, bl);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[s], bh, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[s], bl, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[s], bh, acc, 0, 0, 0);
+  }
+}
+
+// A's 16 values of this lane for one tile -> fp32 row sums, the running scale (accumulators rescaled
+// when the tile needs a smaller one) and the hi / lo operands
+template <int N>
+__device__ __forceinline__ void a_split(const float (&v)[16], float& cs, float& sc, f32x16 (&acc)[N], f16x8 (&ah)[2],
+                                        f16x8 (&al)[2]) {
+  float m = 0.f;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    m = fmaxf(m, fabsf(v[i]));
+    cs += v[i];
+  }
+  if (__builtin_amdgcn_ballot_w64(m * sc >= 32768.f) != 0) {  // this tile needs a smaller scale
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+    const float ns = pt_scale(m);
+    const float r = ns / sc;
+#pragma unroll
+    for (int y = 0; y < N; ++y)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[y][i] *= r;
+    sc = ns;
+  }
+#pragma unroll
+  for (int s = 0; s < 2; ++s) split8(v + 8 * s, sc, ah[s], al[s]);
+}
+
 // workgroup `bid` of one weight-gradient GEMM (k_wgrad16: bid = blockIdx.x; k_wgrad16_group: the
-// block's index within its job)
-template <int NTB, int WB, bool SYN, bool FOUR, bool BSC, bool MSK, bool PRE = false>
+// block's index within its job).  FC (feature branch): the same A tiles also feed the layer's fc_c
+// GEMM dWc += A^T c -- A unmasked there (MSK: the ReLU bits are applied for the main GEMM only; SYN:
+// dL/dh4 = Wo^T g_out before the h4 mask) -- with its own running scales, accumulator and partials
+// (a.part2 / a.part_bias2): the 1 KB / point A stream is read once for both GEMMs.
+template <int NTB, int WB, bool SYN, bool FOUR, bool BSC, bool MSK, bool PRE = false, bool FC = false>
 __device__ __forceinline__ void wgrad16_body(const WxArgs& a, const int bid, char* lds) {
   static_assert(!PRE || (WB == 256 && !FOUR && !BSC && !MSK), "PRE: B = split h1..h3 (hidden / dW3 GEMMs)");
   static_assert(!MSK || (!SYN && !BSC), "MSK: the hidden / first-layer GEMMs");
   static_assert(!BSC || (NTB == 1 && WB == 32 && !FOUR), "BSC: the fc_c shape");
   static_assert(!SYN || !BSC || !MSK, "SYN + BSC: dWc_3 on A = Wo^T g_out (unmasked)");
   static_assert(!BSC || 32 * kBscRow * 4 <= Wx3<NTB, WB>::kSlot, "BSC tile fits the slot");
+  static_assert(!FC || (!BSC && !PRE && (MSK || (SYN && WB == 256))), "FC: on a masked main GEMM");
   using Cfg = Wx3<NTB, WB>;
   const int lane = threadIdx.x & 63, hh = lane >> 5;
   const int w = wave_id();  // output row block of this wave
@@ -223,7 +307,13 @@ __device__ __forceinline__ void wgrad16_body(const WxArgs& a, const int bid, cha
     for (int r = 0; r < 16; ++r) acc[y][r] = 0.f;
   float cs = 0.f;          // fp32 row sums of A (bias) for row 32w + (lane & 31), this lane's points
   float sc = 0x1p100f;     // running scale of A (wave-uniform, <= 2^100 as pt_scale); lowered by a tile
-  float sb = 0x1p100f;     // BSC: the same for B
+  float sb = 0x1p100f;     // BSC / FC: the same for B = c
+  f32x16 accc[1];          // FC: the fc_c tile and its row sums (A scale: sc, shared)
+  float csc = 0.f;
+  if constexpr (FC) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) accc[0][r] = 0.f;
+  }
   WxRegs<NTB, WB> R;
   float wo[4];             // SYN: Wo[:, u] of this lane's unit, and its mask bit
   int mbit = 0;
@@ -241,7 +331,7 @@ __device__ __forceinline__ void wgrad16_body(const WxArgs& a, const int bid, cha
 #pragma unroll
       for (int e = 0; e < 4; ++e)
         fbr[i][d][e] = FOUR ? a.fb[d * kFourierPad + 4 * ((threadIdx.x + Cfg::kThreads * i) % Cfg::kC4) + e] : 0.f;
-  if (ntile > 0) wx_load<NTB, WB, SYN, FOUR, MSK>(a, kb, R);
+  if (ntile > 0) wx_load<NTB, WB, SYN, FOUR, MSK, FC>(a, kb, R);
   if (SYN && ntile > 0) {  // the first tile's g_out rows; later tiles' are staged one tile ahead
     if (threadIdx.x < 32) reinterpret_cast<float4*>(lds + Cfg::kGo)[threadIdx.x] = a.g_out[kb + threadIdx.x];
     __syncthreads();
@@ -250,7 +340,9 @@ __device__ __forceinline__ void wgrad16_body(const WxArgs& a, const int bid, cha
     char* slot = lds + (t & 1) * Cfg::kSlot;
     // g_out rows of tile t + 1 go to the other slot: their last reader (synth of tile t - 1) ran
     // before the previous barrier
-    wx_stage_b<NTB, WB, SYN, FOUR, BSC, PRE>(R, slot, lds + ((t + 1) & 1) * Cfg::kSlot, fbr);
+    wx_stage_b<NTB, WB, SYN, FOUR, BSC, PRE, FC>(R, slot, lds + ((t + 1) & 1) * Cfg::kSlot, fbr);
+    float au[16];  // FC: A unmasked
+    uint32_t keep = 0u;  // FC: the main GEMM's ReLU bits of au[0..15]
     if constexpr (SYN) {
       // delta4 = (Wo^T g_out) masked, fp32 FMAs (the tile's g_out rows from LDS, staged before the
       // previous barrier; broadcast reads)
@@ -261,78 +353,84 @@ __device__ __forceinline__ void wgrad16_body(const WxArgs& a, const int bid, cha
         for (int j = 0; j < 8; ++j) {
           const float4 g = go[16 * s + j];
           const float d = __builtin_fmaf(wo[3], g.w, __builtin_fmaf(wo[2], g.z, __builtin_fmaf(wo[1], g.y, wo[0] * g.x)));
-          R.a[8 * s + j] = BSC ? d : (((__float_as_uint(R.a[8 * s + j]) >> mbit) & 1u) ? d : 0.f);
+          if constexpr (FC) {
+            au[8 * s + j] = d;
+            keep |= ((__float_as_uint(R.a[8 * s + j]) >> mbit) & 1u) << (8 * s + j);
+          } else {
+            R.a[8 * s + j] = BSC ? d : (((__float_as_uint(R.a[8 * s + j]) >> mbit) & 1u) ? d : 0.f);
+          }
         }
-    }
-    float m = 0.f;
+    } else if constexpr (FC) {  // MSK + FC: A arrived unmasked, with its ReLU bits
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      m = fmaxf(m, fabsf(R.a[i]));
-      cs += R.a[i];
-    }
-    if (__builtin_amdgcn_ballot_w64(m * sc >= 32768.f) != 0) {  // this tile needs a smaller scale
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
-      const float ns = pt_scale(m);
-      const float r = ns / sc;
-#pragma unroll
-      for (int y = 0; y < NTB; ++y)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) acc[y][i] *= r;
-      sc = ns;
+      for (int i = 0; i < 16; ++i) au[i] = R.a[i];
+      keep = R.mb;
     }
     f16x8 ah[2], al[2];
+    if constexpr (FC) {
+      // one running scale for both GEMMs (from A unmasked): the main GEMM's operand is the fc_c one
+      // with the masked elements' parts zeroed (split8 of 0 is 0 / 0), so only one split is formed
+      // and the two hi / lo sets need not both stay live through the MFMAs
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      split8(R.a + 8 * s, sc, ah[s], al[s]);
+      for (int i = 0; i < 16; ++i) cs += ((keep >> i) & 1u) ? au[i] : 0.f;
+      float m = 0.f;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        m = fmaxf(m, fabsf(au[i]));
+        csc += au[i];
+      }
+      if (__builtin_amdgcn_ballot_w64(m * sc >= 32768.f) != 0) {
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+        const float ns = pt_scale(m);
+        const float r = ns / sc;
+#pragma unroll
+        for (int y = 0; y < NTB; ++y)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) acc[y][i] *= r;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) accc[0][i] *= r;
+        sc = ns;
+      }
+#pragma unroll
+      for (int s = 0; s < 2; ++s) split8(au + 8 * s, sc, ah[s], al[s]);
+    } else {
+      a_split<NTB>(R.a, cs, sc, acc, ah, al);
     }
     {  // next tile into the (now free) registers; the last tile is re-read (keeps the loop uniform)
       const int64_t tn = t + 1 < ntile ? t + 1 : t;
-      wx_load<NTB, WB, SYN, FOUR, MSK>(a, kb + 32 * tn, R);
+      wx_load<NTB, WB, SYN, FOUR, MSK, FC>(a, kb + 32 * tn, R);
     }
     __syncthreads();  // planes of tile t written; every wave is done with the slot of tile t - 2
     if constexpr (BSC) {
-      // the lane's B operand (column lane & 31, points 16 s + 8 hh + j) from the fp32 rows, split
-      // under the wave's running B scale (lowered, with the accumulator, when this tile needs it)
-      const float* tb = reinterpret_cast<const float*>(slot) + (lane & 31);
-      float bv[16];
-      float mb = 0.f;
-#pragma unroll
-      for (int s = 0; s < 2; ++s)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          bv[8 * s + j] = tb[(16 * s + 8 * hh + j) * kBscRow];
-          mb = fmaxf(mb, fabsf(bv[8 * s + j]));
-        }
-      if (__builtin_amdgcn_ballot_w64(mb * sb >= 32768.f) != 0) {
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) mb = fmaxf(mb, __shfl_xor(mb, o));
-        const float ns = pt_scale(mb);
-        const float r = ns / sb;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) acc[0][i] *= r;
-        sb = ns;
-      }
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        f16x8 bh, bl;
-        split8(bv + 8 * s, sb, bh, bl);
-        acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[s], bh, acc[0], 0, 0, 0);
-        acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[s], bl, acc[0], 0, 0, 0);
-        acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[s], bh, acc[0], 0, 0, 0);
-      }
+      bsc_tile(slot, ah, al, acc[0], sb);
     } else {
       const char* ph = slot;
       const char* pl = slot + Cfg::kPlane;
 #pragma unroll
-      for (int s = 0; s < 2; ++s)
+      for (int s = 0; s < 2; ++s) {
+        f16x8 mh = ah[s], ml = al[s];  // FC: the masked operand
+        if constexpr (FC) {
+          u32x4 hv = __builtin_bit_cast(u32x4, ah[s]), lv = __builtin_bit_cast(u32x4, al[s]);
+#pragma unroll
+          for (int d = 0; d < 4; ++d) {
+            const uint32_t km = (((keep >> (8 * s + 2 * d)) & 1u) ? 0xFFFFu : 0u) |
+                                (((keep >> (8 * s + 2 * d + 1)) & 1u) ? 0xFFFF0000u : 0u);
+            hv[d] &= km;
+            lv[d] &= km;
+          }
+          mh = __builtin_bit_cast(f16x8, hv);
+          ml = __builtin_bit_cast(f16x8, lv);
+        }
 #pragma unroll
         for (int y = 0; y < NTB; ++y) {
           const f16x8 bh = tr_frag(ph, y, s), bl = tr_frag(pl, y, s);
-          acc[y] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[s], bh, acc[y], 0, 0, 0);
-          acc[y] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[s], bl, acc[y], 0, 0, 0);
-          acc[y] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[s], bh, acc[y], 0, 0, 0);
+          acc[y] = __builtin_amdgcn_mfma_f32_32x32x16_f16(mh, bh, acc[y], 0, 0, 0);
+          acc[y] = __builtin_amdgcn_mfma_f32_32x32x16_f16(mh, bl, acc[y], 0, 0, 0);
+          acc[y] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ml, bh, acc[y], 0, 0, 0);
         }
+        if constexpr (FC) __builtin_amdgcn_sched_barrier(0);  // (register pressure: no reads hoisted across)
+      }
+      if constexpr (FC) bsc_tile(slot + Cfg::kCOff, ah, al, accc[0], sb);
     }
   }
   // two-phase flush: this workgroup's tile with plain stores (each instruction two 128-B row
@@ -349,12 +447,20 @@ __device__ __forceinline__ void wgrad16_body(const WxArgs& a, const int bid, cha
       P[(32 * w + perm(r, hh)) * (NTB * 32) + 32 * y + (lane & 31)] = BSC ? (acc[y][r] * inv) * invb : acc[y][r] * inv;
   cs += __shfl_xor(cs, 32);
   if (a.bias && hh == 0) a.part_bias[(int64_t)bid * 256 + 32 * w + lane] = cs;
+  if constexpr (FC) {
+    const float invc = 1.f / sc, invs = 1.f / sb;
+    float* P2 = a.part2 + (int64_t)bid * 256 * 32;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) P2[(32 * w + perm(r, hh)) * 32 + (lane & 31)] = (accc[0][r] * invc) * invs;
+    csc += __shfl_xor(csc, 32);
+    if (a.part_bias2 && hh == 0) a.part_bias2[(int64_t)bid * 256 + 32 * w + lane] = csc;
+  }
 }
 
-template <int NTB, int WB, bool SYN, bool FOUR, bool BSC, bool MSK, bool PRE = false>
+template <int NTB, int WB, bool SYN, bool FOUR, bool BSC, bool MSK, bool PRE = false, bool FC = false>
 __global__ __launch_bounds__(512, 1) void k_wgrad16(WxArgs a) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
-  wgrad16_body<NTB, WB, SYN, FOUR, BSC, MSK, PRE>(a, blockIdx.x, lds);
+  wgrad16_body<NTB, WB, SYN, FOUR, BSC, MSK, PRE, FC>(a, blockIdx.x, lds);
 }
 
 // Skinny weight-gradient GEMMs (fp32 FMAs), bandwidth-bound on B:
@@ -453,7 +559,35 @@ struct Wgrad16Group {
   int n;
 };
 enum : int { kVarHidden = 0, kVarHiddenM, kVarSyn, kVarFirstX, kVarFirstXM, kVarFc, kVarFcOut, kVarSkinnyOut,
-              kVarSkinnyFour, kVarHiddenP, kVarSynP };  // P: B pre-split by the forward (mlp16w.h kSplitSave)
+              kVarSkinnyFour, kVarHiddenP, kVarSynP,  // P: B pre-split by the forward (mlp16w.h kSplitSave)
+              kVarHiddenMF, kVarFirstXMF, kVarSynF };  // F: + the layer's fc_c GEMM on the same A tiles
+// the feature branch's fused jobs (FC) in a kernel of their own: their register pressure (spills) stays
+// out of the other jobs' code
+__device__ __forceinline__ bool group_skinny(const Wgrad16Group& G, int q, int bid, char* lds) {
+  switch (G.var[q]) {
+    case kVarSkinnyOut:
+      skinny_body<256, 512>(reinterpret_cast<const float4*>(G.a[q].A), G.a[q].B, G.a[q].K, G.a[q].ks, 4, kHidden,
+                            G.a[q].part, G.a[q].part_bias, bid, lds);
+      return true;
+    case kVarSkinnyFour:
+      skinny_body<96, 512>(reinterpret_cast<const float4*>(G.a[q].A), G.a[q].B, G.a[q].K, G.a[q].ks, 3, kFourier,
+                           G.a[q].part, nullptr, bid, lds);
+      return true;
+    default: return false;
+  }
+}
+__global__ __launch_bounds__(512, 1) void k_wgrad16_group_fc(Wgrad16Group G) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  int q = 0;
+  while (q + 1 < G.n && (int)blockIdx.x >= G.first[q + 1]) ++q;
+  const int bid = (int)blockIdx.x - G.first[q];
+  if (group_skinny(G, q, bid, lds)) return;
+  switch (G.var[q]) {
+    case kVarHiddenMF: wgrad16_body<8, 256, false, false, false, true, false, true>(G.a[q], bid, lds); break;
+    case kVarFirstXMF: wgrad16_body<3, 96, false, true, false, true, false, true>(G.a[q], bid, lds); break;
+    default: wgrad16_body<8, 256, true, false, false, false, false, true>(G.a[q], bid, lds); break;  // kVarSynF
+  }
+}
 __global__ __launch_bounds__(512, 1) void k_wgrad16_group(Wgrad16Group G) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   int q = 0;
@@ -636,7 +770,7 @@ float wgrad16_job_weight(int kind, bool masked) {
 }
 
 int wgrad16_prepare(int kind, const float* A, const float* B, int64_t K, int64_t kb_rows, float* C, int64_t ldc,
-                    float* bias, const WgradSyn* syn, Wgrad16Job* job, ReduceJob* red) {
+                    float* bias, const WgradSyn* syn, Wgrad16Job* job, ReduceJob* red, ReduceJob* red2) {
   if (kb_rows <= 0) return PNR_E_ARG;
   K = (K + 31) / 32 * 32;
   // split-K over at most one workgroup per CU, >= 8 tiles per workgroup (the flush of the partial
@@ -657,7 +791,7 @@ int wgrad16_prepare(int kind, const float* A, const float* B, int64_t K, int64_t
     if (fill <= 256) {
       // one round of workgroups: tiles per workgroup so that every job's workgroups take about the same
       // time (the group's summed cost over the CUs, divided by this kind's cost per tile)
-      const float w = wgrad16_job_weight(kind, syn->amasks != nullptr);
+      const float w = wgrad16_job_weight(kind, syn->amasks != nullptr) + (syn->fc_c ? kWgradFcFusedWeight : 0.f);
       const float gw = syn->group_weight > 0.f ? syn->group_weight : (float)syn->group_jobs;
       const int64_t wfill = (int64_t)((double)tiles * gw / ((double)cus * w) + 0.999);
       per = wfill > per ? wfill : per;
@@ -710,6 +844,17 @@ int wgrad16_prepare(int kind, const float* A, const float* B, int64_t K, int64_t
   } else {
     return PNR_E_ARG;
   }
+  if (syn->fc_c) {  // + the layer's fc_c GEMM on the same A tiles (A unmasked), partials after the main ones
+    if (!red2 || !syn->fc_C) return PNR_E_ARG;
+    if (var == kVarHiddenM) var = kVarHiddenMF;
+    else if (var == kVarFirstXM) var = kVarFirstXMF;
+    else if (var == kVarSyn) var = kVarSynF;
+    else return PNR_E_ARG;  // FC runs on a masked main GEMM (the feature branch's dW jobs)
+    a.cB = syn->fc_c;
+    a.part2 = a.part + nwg * 256 * ntb * 32;
+    a.part_bias2 = syn->fc_bias ? a.part_bias + nwg * 256 : nullptr;
+    *red2 = ReduceJob{a.part2, a.part_bias2, (int)nwg, 256, 32, kCDim, syn->fc_C, kCDim, syn->fc_bias};
+  }
   job->a = a;
   job->var = var;
   job->nwg = (int)nwg;
@@ -724,29 +869,39 @@ int launch_wgrad16_group(const Wgrad16Job* jobs, int n, hipStream_t st) {
   static_assert(Wx3<3, 96>::kLds <= kLds && Wx3<1, 32>::kLds <= kLds, "group LDS");
   static_assert(SkinnyGeo<256, 512>::kLds <= kLds && SkinnyGeo<96, 512>::kLds <= kLds, "group LDS (skinny jobs)");
   static const bool attr = hipFuncSetAttribute((const void*)k_wgrad16_group, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                               kLds) == hipSuccess;
+                                               kLds) == hipSuccess &&
+                           hipFuncSetAttribute((const void*)k_wgrad16_group_fc,
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, kLds) == hipSuccess;
   if (!attr) return PNR_E_ARG;
   Wgrad16Group G{};
   int blocks = 0;
   int64_t macs = 0;  // timing units (pnr_timing_read kind 6): multiply-adds / 65,536
+  int nfc = 0, nplain = 0;
   for (int i = 0; i < n; ++i) {
     G.a[i] = jobs[i].a;
     G.var[i] = jobs[i].var;
     G.first[i] = blocks;
     blocks += jobs[i].nwg;
-    macs += jobs[i].a.K * 256 * jobs[i].a.nb;
+    const bool fc = jobs[i].var == kVarHiddenMF || jobs[i].var == kVarFirstXMF || jobs[i].var == kVarSynF;
+    const bool skinny = jobs[i].var == kVarSkinnyOut || jobs[i].var == kVarSkinnyFour;
+    nfc += fc ? 1 : 0;
+    nplain += (fc || skinny) ? 0 : 1;
+    macs += jobs[i].a.K * 256 * (jobs[i].a.nb + (fc ? kCDim : 0));
   }
+  if (nfc > 0 && nplain > 0) return PNR_E_ARG;  // FC jobs run in k_wgrad16_group_fc, with the skinny ones only
   G.first[n] = blocks;
   G.n = n;
   TimingScope ts(kTimeWgradGroup, macs / 65536, st);
-  hipLaunchKernelGGL(k_wgrad16_group, dim3((unsigned)blocks), dim3(512), kLds, st, G);
+  if (nfc > 0) hipLaunchKernelGGL(k_wgrad16_group_fc, dim3((unsigned)blocks), dim3(512), kLds, st, G);
+  else hipLaunchKernelGGL(k_wgrad16_group, dim3((unsigned)blocks), dim3(512), kLds, st, G);
   return hip_status(hipGetLastError());
 }
 
-template <int NTB, int WB, bool SYN = false, bool FOUR = false, bool BSC = false, bool MSK = false, bool PRE = false>
+template <int NTB, int WB, bool SYN = false, bool FOUR = false, bool BSC = false, bool MSK = false, bool PRE = false,
+          bool FC = false>
 static int launch_k(const WxArgs& a, int nwg, hipStream_t st) {
   using Cfg = Wx3<NTB, WB>;
-  auto kern = k_wgrad16<NTB, WB, SYN, FOUR, BSC, MSK, PRE>;
+  auto kern = k_wgrad16<NTB, WB, SYN, FOUR, BSC, MSK, PRE, FC>;
   static const bool attr = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                                                Cfg::kLds) == hipSuccess;
   if (!attr) return PNR_E_ARG;
@@ -769,6 +924,9 @@ int launch_wgrad16(int kind, const float* A, const float* B, int64_t K, int64_t 
     case kVarSyn: rc = launch_k<8, 256, true>(j.a, j.nwg, st); break;
     case kVarHiddenP: rc = launch_k<8, 256, false, false, false, false, true>(j.a, j.nwg, st); break;
     case kVarSynP: rc = launch_k<8, 256, true, false, false, false, true>(j.a, j.nwg, st); break;
+    case kVarHiddenMF: rc = launch_k<8, 256, false, false, false, true, false, true>(j.a, j.nwg, st); break;
+    case kVarFirstXMF: rc = launch_k<3, 96, false, true, false, true, false, true>(j.a, j.nwg, st); break;
+    case kVarSynF: rc = launch_k<8, 256, true, false, false, false, false, true>(j.a, j.nwg, st); break;
     case kVarFirstX: rc = launch_k<3, 96, false, true>(j.a, j.nwg, st); break;
     case kVarFirstXM: rc = launch_k<3, 96, false, true, false, true>(j.a, j.nwg, st); break;
     case kVarFcOut: rc = launch_k<1, 32, true, false, true>(j.a, j.nwg, st); break;
