@@ -441,7 +441,7 @@ int launch_mlp_fwd_bf(int prec, const float* packed, const PointSrc& src, int mo
     if (var == 1) {  // 16-point waves (mlp16w.h)
       BfFwdArgs b = a;
       b.wmain = reinterpret_cast<const char*>(packed + kOffW16);
-      return launch_fwd16w(mode, grid, st, b, sv);
+      return launch_fwd16w(mode, st, b, sv);
     }
   }
   switch (prec) {

@@ -125,14 +125,18 @@ struct W16State {
 };
 
 // SV: 0 eval, 1 training saves (x, masks, h1..h4), 2 masks + x only (the Tracker's camera step)
-template <int SV>
+// NW: waves per workgroup -- 8 (128-point tiles, two waves per SIMD) or 4 (64-point tiles, one wave per
+// SIMD: the small batches whose 128-point tiles would leave most CUs idle, k_mlp_fwd16w's launcher)
+template <int SV, int NW = 8>
 struct W16Fwd {
+  static_assert(NW == 8 || NW == 4, "8 or 4 waves");
+  static constexpr int kPer = 8 / NW;  // 4-piece DMA rounds per wave and step
   static constexpr bool SAVE = SV != 0, SAVEH = SV == 1;
   using G = W16Geo;
   static constexpr int kSteps = G::kSteps, kD = G::kD, kPf = G::kPf, kRing = G::kRing;
   static constexpr int kSync = G::sync(SV);
 
-  __host__ __device__ static constexpr int n_glds(int g) { return g < kSteps ? 4 : 0; }
+  __host__ __device__ static constexpr int n_glds(int g) { return g < kSteps ? 4 * kPer : 0; }
   // VMEM stores the epilogue of step g issues in group T
   __host__ __device__ static constexpr int stores_grp(int g, int T, int ph) {
     if (!SAVE || !w16_conv(g)) return 0;
@@ -188,16 +192,19 @@ struct W16Fwd {
   static __device__ __forceinline__ const char* slot_of(const char* lds, int g, int sb) {
     return lds + ((g + sb) % G::kNbuf) * G::kSlot;
   }
-  // DMA of step g (>= kSteps: the next tile's step g - kSteps): wave w copies 1-KiB pieces w + 8i
+  // DMA of step g (>= kSteps: the next tile's step g - kSteps): wave w copies 1-KiB pieces w + NW i
   template <int g>
   static __device__ __forceinline__ void stage_step(const char* wimg, const char* lds, int sb) {
     if constexpr (g < 2 * kSteps) {
       constexpr int st = g < kSteps ? g : g - kSteps;
       const int w = wave_id();
-      const uint32_t slot = lds_addr(reinterpret_cast<const float*>(slot_of(lds, g, sb))) + w * 1024;
-      const char* base = wimg;  // opaque per call: 27 steps' source pairs hoisted out of the tile loop spill SGPRs
-      asm volatile("" : "+s"(base));
-      glds16s_x4(base + st * kW16StepBytes + w * 1024, (threadIdx.x & 63) * 16, slot);
+#pragma unroll
+      for (int r = 0; r < kPer; ++r) {
+        const uint32_t slot = lds_addr(reinterpret_cast<const float*>(slot_of(lds, g, sb))) + (w + NW * r) * 1024;
+        const char* base = wimg;  // opaque per call: 27 steps' source pairs hoisted out of the tile loop spill SGPRs
+        asm volatile("" : "+s"(base));
+        glds16s_x4(base + st * kW16StepBytes + (w + NW * r) * 1024, (threadIdx.x & 63) * 16, slot);
+      }
     }
   }
   // 16 B of LDS at a 32-bit LDS byte address (an opaque base stays an LDS access: ds_read_b128)
@@ -436,14 +443,14 @@ struct W16Fwd {
   }
 };
 
-// one 128-point tile of k_mlp_fwd16w (it: the workgroup's tile count so far, sb: its ring slot base)
-template <int SV>
+// one tile of k_mlp_fwd16w, 16 NW points (it: the workgroup's tile count so far, sb: its ring slot base)
+template <int SV, int NW>
 static __device__ __forceinline__ void fwd16w_tile(const BfFwdArgs& a, int mode, const char* lds, int64_t tile,
                                                   int it, int sb) {
-  using K = W16Fwd<SV>;
+  using K = W16Fwd<SV, NW>;
   using G = W16Geo;
   const int lane = threadIdx.x & 63, w = wave_id(), gq = lane >> 4;
-  const int64_t p = tile * 128 + w * 16 + (lane & 15);
+  const int64_t p = tile * (16 * NW) + w * 16 + (lane & 15);
   W16State S;
   S.sb = sb;
   S.ph = G::kPhased ? (w >> 2) : 0;
@@ -461,7 +468,7 @@ static __device__ __forceinline__ void fwd16w_tile(const BfFwdArgs& a, int mode,
   }
   S.inside = inside;
   S.col = a.save.p0 + p;
-  S.mgrp = (a.save.p0 + tile * 128) / 32 + (w >> 1);
+  S.mgrp = (a.save.p0 + tile * (16 * NW)) / 32 + (w >> 1);
   // opaque per tile: the save addresses of 64 store sites derive from it (hoisted out of the tile loop
   // as separate 64-bit addresses they would take 128 registers)
   // (a global-address-space pointer: through the asm a generic one would turn the saves into flat
@@ -472,8 +479,8 @@ static __device__ __forceinline__ void fwd16w_tile(const BfFwdArgs& a, int mode,
   S.mw[0] = S.mw[1] = S.mw[2] = S.mw[3] = 0u;
   S.vmax = 0.f;
   // the raw tables must have landed (older than the step DMAs) before the Fourier features
-  // (prologue order: raw 1 piece, Wo 2, steps 0 .. kD-1 4 each)
-  if (it == 0) sync_chunk<2 + 4 * G::kD>();
+  // (prologue order per wave: raw kPer pieces, Wo 2 kPer, steps 0 .. kD-1 4 kPer each)
+  if (it == 0) sync_chunk<2 * K::kPer + 4 * K::kPer * G::kD>();
   S.x0 = x0;
   S.x1 = x1;
   S.x2 = x2;
@@ -498,32 +505,39 @@ static __device__ __forceinline__ void fwd16w_tile(const BfFwdArgs& a, int mode,
   }
 }
 
-template <int SV>
-__global__ __launch_bounds__(512, 1) void k_mlp_fwd16w(BfFwdArgs a, int mode) {
-  using K = W16Fwd<SV>;
+template <int SV, int NW>
+__global__ __launch_bounds__(64 * NW, 1) void k_mlp_fwd16w(BfFwdArgs a, int mode) {
+  using K = W16Fwd<SV, NW>;
   using G = W16Geo;
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int lane = threadIdx.x & 63, w = wave_id();
-  // raw table (8 KiB: one piece per wave) and the Wo image (16 KiB: two), then the first kD steps
-  {
-    const uint32_t base = lds_addr(reinterpret_cast<const float*>(lds)) + w * 1024;
-    glds16(reinterpret_cast<const float*>(a.raw + w * 1024 + lane * 16), base + G::kRawOff);
+  // raw table (8 KiB: 1-KiB pieces w + NW r) and the Wo image (16 KiB), then the first kD steps
+#pragma unroll
+  for (int r = 0; r < K::kPer; ++r) {
+    const int pc = w + NW * r;
+    const uint32_t base = lds_addr(reinterpret_cast<const float*>(lds)) + pc * 1024;
+    glds16(reinterpret_cast<const float*>(a.raw + pc * 1024 + lane * 16), base + G::kRawOff);
+  }
+#pragma unroll
+  for (int r = 0; r < K::kPer; ++r) {
+    const int pc = w + NW * r;
+    const uint32_t base = lds_addr(reinterpret_cast<const float*>(lds)) + pc * 1024;
     const char* wo = a.wmain + kW16Steps * kW16StepBytes;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
-      glds16(reinterpret_cast<const float*>(wo + i * 8192 + w * 1024 + lane * 16), base + G::kWoOff + i * 8192);
+      glds16(reinterpret_cast<const float*>(wo + i * 8192 + pc * 1024 + lane * 16), base + G::kWoOff + i * 8192);
   }
   K::template prologue<0>(a.wmain, lds);
-  const int64_t ntiles = (a.P + 127) / 128;
+  const int64_t ntiles = (a.P + 16 * NW - 1) / (16 * NW);
   int sb = 0, it = 0;
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x, ++it) {
-    fwd16w_tile<SV>(a, mode, lds, tile, it, sb);
+    fwd16w_tile<SV, NW>(a, mode, lds, tile, it, sb);
     sb = (sb + G::kSteps) % G::kNbuf;
   }
   // the last tile's prefetch of a next tile must land before the workgroup exits
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-int launch_fwd16w(int mode, dim3 grid, hipStream_t st, const BfFwdArgs& a, int save);
+int launch_fwd16w(int mode, hipStream_t st, const BfFwdArgs& a, int save);  // picks the grid and NW
 
 }  // namespace pnr
