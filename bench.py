@@ -451,7 +451,7 @@ def kernel_table(kt, prec, el_s, steps, fc=False):
                       'ms_per_step': round(ms / steps, 3),
                       'share_of_step': round(ms / (el_s * 1e3), 3)}
     pm = {'k_mlp_fwd16 (training, saves)': ('void pnr::k_mlp_fwd16<3, false, 1>', 'void pnr::k_mlp_fwd16<3, false, true>'),
-          'k_mlp_fwd16w (training, saves)': ('void pnr::k_mlp_fwd16w<1>',),
+          'k_mlp_fwd16w (training, saves)': ('void pnr::k_mlp_fwd16w<1, 8>', 'void pnr::k_mlp_fwd16w<1>'),
           'k_mlp_bwd16 (delta chain)': ('void pnr::k_mlp_bwd16<false>',)}
     for k, names in pm.items():
         for b in names:

@@ -920,10 +920,18 @@ int map_fwd_core(const pnr_render_params* prm, const float* packed, const float*
   if (prm->far_mode == 0) rc = launch_gt_max(gt_depth, n, w.gmax, st);
   if (rc) return rc;
   float* x4 = reinterpret_cast<float*>(w.save.xP);
-  rc = launch_map_pts(*prm, rays_o, rays_d, gt_depth, t_rand, prm->far_mode == 2 ? prm->far_clamp_dev : w.gmax, n, w.pr,
-                      w.r1, w.z, w.far, x4, st);
-  if (rc) return rc;
   const pnr_points* pts = prm->points;
+  const float* gmax = prm->far_mode == 2 ? prm->far_clamp_dev : w.gmax;
+  // Launch A's rows (regulation + coarse samples) are formed by k_map_pts into the x4 rows, which the
+  // gather and the forward read; without the feature branch the 16-point-wave forward forms them itself
+  // (kMapRows: the same arithmetic, map_row_point, its x save is the x4 row) and the launch and its
+  // boundary go (PNR_MAP_ROWS_FUSE=0: always k_map_pts)
+  static const bool fuse_env = !(getenv("PNR_MAP_ROWS_FUSE") && getenv("PNR_MAP_ROWS_FUSE")[0] == '0');
+  const bool fuse = fuse_env && !pts && fwd_map_rows_ok(prm->precision, nullptr);
+  if (!fuse) {
+    rc = launch_map_pts(*prm, rays_o, rays_d, gt_depth, t_rand, gmax, n, w.pr, w.r1, w.z, w.far, x4, st);
+    if (rc) return rc;
+  }
   PointSrc src{};
   src.pts = x4;
   FeatArgs fa{pts ? pts->fc_packed : nullptr, w.c};
@@ -934,7 +942,12 @@ int map_fwd_core(const pnr_render_params* prm, const float* packed, const float*
     rc = launch_gather(*pts, src, kPtsX4, w.r1, w.r1, w.c, w.nidx, w.nw, w.gws, w.gws_bytes, st);
     if (rc) return rc;
   }
-  rc = mlp_fwd(prm->precision, packed, src, kPtsX4, w.r1, w.raw, &w.save, st, pts ? &fa : nullptr, status);
+  if (fuse) {
+    const MapRowsArgs mr = map_rows_args(*prm, rays_o, rays_d, gt_depth, t_rand, gmax, n, w.pr, w.z, w.far);
+    rc = mlp_fwd(prm->precision, packed, src, kMapRows, w.r1, w.raw, &w.save, st, nullptr, status, &mr);
+  } else {
+    rc = mlp_fwd(prm->precision, packed, src, kPtsX4, w.r1, w.raw, &w.save, st, pts ? &fa : nullptr, status);
+  }
   if (rc) return rc;
   // importance depths and points from the coarse weights; the regulation densities out of launch A
   double* zi = w.z + n * S;

@@ -407,10 +407,16 @@ bool hsave_is_split(const float* hP) {
   return it != g_hsave.end() && it->second;
 }
 
+bool fwd_map_rows_ok(int prec, const FeatArgs* feat) {
+  return prec == PNR_PREC_F16X3 && !(feat && feat->fcw) && fwd16_variant(1) == 1;
+}
+
 int launch_mlp_fwd_bf(int prec, const float* packed, const PointSrc& src, int mode, int64_t P, float* raw,
-                      const SaveArgs* save, hipStream_t st, const FeatArgs* feat, uint32_t* status) {
+                      const SaveArgs* save, hipStream_t st, const FeatArgs* feat, uint32_t* status,
+                      const MapRowsArgs* mr) {
   if (P <= 0) return 0;
-  if (mode < kPtsF64 || mode > kPtsX4) return PNR_E_ARG;
+  if (mode < kPtsF64 || mode > kMapRows) return PNR_E_ARG;
+  if (mode == kMapRows && !fwd_map_rows_ok(prec, feat)) return PNR_E_ARG;  // k_mlp_fwd16w only
   if (prec != PNR_PREC_BF16X3 && prec != PNR_PREC_BF16 && prec != PNR_PREC_F16X3) return PNR_E_ARG;
   BfFwdArgs a;
   a.wmain = reinterpret_cast<const char*>(packed + main_off_floats(prec));
@@ -441,7 +447,7 @@ int launch_mlp_fwd_bf(int prec, const float* packed, const PointSrc& src, int mo
     if (var == 1) {  // 16-point waves (mlp16w.h)
       BfFwdArgs b = a;
       b.wmain = reinterpret_cast<const char*>(packed + kOffW16);
-      return launch_fwd16w(mode, st, b, sv);
+      return launch_fwd16w(mode, st, b, sv, mode == kMapRows ? mr : nullptr);
     }
   }
   switch (prec) {

@@ -506,11 +506,30 @@ static __device__ __forceinline__ void fwd16w_tile(const BfFwdArgs& a, int mode,
 }
 
 template <int SV, int NW>
-__global__ __launch_bounds__(64 * NW, 1) void k_mlp_fwd16w(BfFwdArgs a, int mode) {
+__global__ __launch_bounds__(64 * NW, 1) void k_mlp_fwd16w(BfFwdArgs a, int mode, MapRowsArgs mr) {
   using K = W16Fwd<SV, NW>;
   using G = W16Geo;
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int lane = threadIdx.x & 63, w = wave_id();
+  const int64_t ntiles = (a.P + 16 * NW - 1) / (16 * NW);
+  if (SV == 1 && mode == kMapRows) {  // (training only: launch_fwd16w refuses kMapRows otherwise)
+    // the map pass's launch-A rows (map_row_point, k_map_pts's arithmetic) of this workgroup's tiles
+    // into the x4 rows (src.pts, the x save), by the lanes that load them below (every lane group
+    // writes its point's row: a lane reads back its own store), then the usual kPtsX4 loads.  Done
+    // and drained before the first DMA, so the step program's vmcnt counts stay as they are.
+    const int gq = lane >> 4;
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+      const int64_t p = tile * (16 * NW) + w * 16 + (lane & 15);
+      if (p < a.P) {
+        float x0, x1, x2;
+        bool inside;
+        map_row_point(mr, p, gq == 0, x0, x1, x2, inside);
+        const_cast<float4*>(reinterpret_cast<const float4*>(a.src.pts))[p] = make_float4(x0, x1, x2, inside ? 1.f : 0.f);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    mode = kPtsX4;
+  }
   // raw table (8 KiB: 1-KiB pieces w + NW r) and the Wo image (16 KiB), then the first kD steps
 #pragma unroll
   for (int r = 0; r < K::kPer; ++r) {
@@ -528,7 +547,6 @@ __global__ __launch_bounds__(64 * NW, 1) void k_mlp_fwd16w(BfFwdArgs a, int mode
       glds16(reinterpret_cast<const float*>(wo + i * 8192 + pc * 1024 + lane * 16), base + G::kWoOff + i * 8192);
   }
   K::template prologue<0>(a.wmain, lds);
-  const int64_t ntiles = (a.P + 16 * NW - 1) / (16 * NW);
   int sb = 0, it = 0;
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x, ++it) {
     fwd16w_tile<SV, NW>(a, mode, lds, tile, it, sb);
@@ -538,6 +556,7 @@ __global__ __launch_bounds__(64 * NW, 1) void k_mlp_fwd16w(BfFwdArgs a, int mode
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-int launch_fwd16w(int mode, hipStream_t st, const BfFwdArgs& a, int save);  // picks the grid and NW
+// picks the grid and NW; mr: the map rows of mode kMapRows (else null)
+int launch_fwd16w(int mode, hipStream_t st, const BfFwdArgs& a, int save, const MapRowsArgs* mr);
 
 }  // namespace pnr

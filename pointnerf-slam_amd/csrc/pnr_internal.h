@@ -84,7 +84,89 @@ enum PointMode : int {
   kRaysZ32 = 3,     // p = o + d * z, z float32 (regulation)
   kPtsX4 = 4,       // float4 (x, y, z, inside) rows written by the ray kernels of the map pass (k_map_pts,
                     // k_pdf): the point and its bound test already evaluated in the reference's dtype
+  kMapRows = 5,     // the map pass's launch-A rows formed in the forward itself (map_row_point; k_mlp_fwd16w
+                    // only): k_map_pts fused into the MLP launch
 };
+
+// Launch A of the map pass (pnr_map_fwd / pnr_map_step): row e < n S is regulation sample e % S of ray
+// e / S (Renderer.regulation, Renderer.py:284-298: float32 z in [0, 0.85 gt], jittered), rows
+// [pr, pr + n S) the coarse samples (Renderer.py:86-116, 157-179: near = 0.01 gt, far = the ray's box
+// exit + 0.01 clamped to [0, far clamp], float64 z and points), every other row the zero point outside
+// the bound.  k_map_pts evaluates it per row into the kPtsX4 rows; with kMapRows the forward does.
+struct MapRowsArgs {
+  const float* ro;
+  const float* rd;
+  const float* gt;
+  const float* t_rand;  // (n, S) regulation jitter
+  const float* gmax;    // far clamp (device), used unless far_mode == 1
+  int64_t n_rays, pr;
+  double* zc;           // (n, S) coarse z out
+  double* far_out;      // (n) per-ray far out, or null
+  double bound[6];
+  double far_clamp;
+  int far_mode, lindisp, n_samples;
+  float t_vals[PNR_MAX_SAMPLES];
+};
+__device__ __forceinline__ void map_row_point(const MapRowsArgs& m, int64_t e, bool write, float& x0, float& x1,
+                                              float& x2, bool& inside) {
+#pragma clang fp contract(off)  // (render.hip's rule: the reference's unfused float / double arithmetic)
+  auto mx = [](double a, double b) { return (a != a || b != b) ? NAN : (a > b ? a : b); };
+  auto mn = [](double a, double b) { return (a != a || b != b) ? NAN : (a < b ? a : b); };
+  const int S = m.n_samples;
+  x0 = x1 = x2 = 0.f;
+  inside = false;
+  if (e < m.n_rays * S) {  // regulation (k_reg_z, load_point<kRaysZ32>)
+    const int64_t n = e / S;
+    const int s = (int)(e - n * S);
+    const float far = m.gt[n] * 0.85f;
+    auto z0 = [&](int k) { return (0.0f * (1.f - m.t_vals[k])) + far * m.t_vals[k]; };
+    const float zs = z0(s);
+    const float lower = s > 0 ? .5f * (zs + z0(s - 1)) : zs;
+    const float upper = s < S - 1 ? .5f * (z0(s + 1) + zs) : zs;
+    const float z = lower + (upper - lower) * m.t_rand[e];
+    x0 = m.ro[n * 3 + 0] + m.rd[n * 3 + 0] * z;
+    x1 = m.ro[n * 3 + 1] + m.rd[n * 3 + 1] * z;
+    x2 = m.ro[n * 3 + 2] + m.rd[n * 3 + 2] * z;
+    inside = (x0 < (float)m.bound[1]) && (x0 > (float)m.bound[0]) && (x1 < (float)m.bound[3]) &&
+             (x1 > (float)m.bound[2]) && (x2 < (float)m.bound[5]) && (x2 > (float)m.bound[4]);
+  } else if (e >= m.pr && e < m.pr + m.n_rays * S) {  // render coarse (k_coarse_z, load_point<kRaysZ64>)
+    const int64_t q = e - m.pr;
+    const int64_t n = q / S;
+    const int s = (int)(q - n * S);
+    double fb = 0.0;
+    for (int a = 0; a < 3; ++a) {
+      const double o = (double)m.ro[n * 3 + a], d = (double)m.rd[n * 3 + a];
+      const double t0 = (m.bound[2 * a] - o) / d;
+      const double t1 = (m.bound[2 * a + 1] - o) / d;
+      const double tm = mx(t0, t1);
+      fb = a == 0 ? tm : mn(fb, tm);
+    }
+    fb = fb + 0.01;
+    const double hi = m.far_mode == 1 ? m.far_clamp : (double)(*m.gmax);
+    double far = fb != fb ? fb : (fb < 0.0 ? 0.0 : fb);  // clamp(min=0)
+    far = far != far ? far : (far > hi ? hi : far);
+    const float nearf = m.gt[n] * 0.01f;
+    if (write && s == 0 && m.far_out) m.far_out[n] = far;
+    const float t = m.t_vals[s];
+    double zz;
+    if (!m.lindisp) {
+      zz = (double)(nearf * (1.f - t)) + far * (double)t;
+    } else {
+      zz = 1.0 / ((double)((1.f / nearf) * (1.f - t)) + (1.0 / far) * (double)t);
+    }
+    if (write) m.zc[q] = zz;
+    const double q0 = (double)m.ro[n * 3 + 0] + (double)m.rd[n * 3 + 0] * zz;
+    const double q1 = (double)m.ro[n * 3 + 1] + (double)m.rd[n * 3 + 1] * zz;
+    const double q2 = (double)m.ro[n * 3 + 2] + (double)m.rd[n * 3 + 2] * zz;
+    inside = (q0 < m.bound[1]) && (q0 > m.bound[0]) && (q1 < m.bound[3]) && (q1 > m.bound[2]) && (q2 < m.bound[5]) &&
+             (q2 > m.bound[4]);
+    x0 = (float)q0;
+    x1 = (float)q1;
+    x2 = (float)q2;
+  }
+}
+MapRowsArgs map_rows_args(const pnr_render_params& prm, const float* ro, const float* rd, const float* gt,
+                          const float* t_rand, const float* gmax, int64_t n, int64_t pr, double* zc, double* far_out);
 
 struct PointSrc {
   const void* pts;      // kPtsF64/kPtsF32: (P,3)
@@ -201,7 +283,9 @@ int launch_fc_pack_all(const float* const* fc, float* out, hipStream_t st, int f
 // status: PNR_STATUS_* bits ORed in on the device (f16 range check of F16X3), or null
 int launch_mlp_fwd_bf(int prec, const float* packed, const PointSrc& src, int mode, int64_t P, float* raw,
                       const SaveArgs* save, hipStream_t st, const FeatArgs* feat = nullptr,
-                      uint32_t* status = nullptr);
+                      uint32_t* status = nullptr, const MapRowsArgs* mr = nullptr);
+// mode kMapRows is served (the forward runs k_mlp_fwd16w): f16x3 without the feature branch
+bool fwd_map_rows_ok(int prec, const FeatArgs* feat);
 // Format of a save area's h1..h3 (host-side record keyed by SaveArgs::hP, set by every forward that
 // saves activations): fp32, or the f16 hi / lo parts the 16-point-wave forward stores (mlp16w.h
 // kSplitSave) -- the backward picks its weight-gradient B staging from it and refuses a split save
@@ -212,10 +296,10 @@ bool hsave_is_split(const float* hP);
 // forward dispatch on PNR_PREC_*
 inline int mlp_fwd(int prec, const float* packed, const PointSrc& src, int mode, int64_t P, float* raw,
                    const SaveArgs* save, hipStream_t st, const FeatArgs* feat = nullptr,
-                   uint32_t* status = nullptr) {
+                   uint32_t* status = nullptr, const MapRowsArgs* mr = nullptr) {
   if (save && save->hP) hsave_set_split(save->hP, prec != PNR_PREC_FP32 && fwd_saves_split(prec, feat));
-  if (prec == PNR_PREC_FP32) return launch_mlp_fwd(packed, src, mode, P, raw, save, st, feat);
-  return launch_mlp_fwd_bf(prec, packed, src, mode, P, raw, save, st, feat, status);
+  if (prec == PNR_PREC_FP32) return mode == kMapRows ? PNR_E_ARG : launch_mlp_fwd(packed, src, mode, P, raw, save, st, feat);
+  return launch_mlp_fwd_bf(prec, packed, src, mode, P, raw, save, st, feat, status, mr);
 }
 
 // ---- neural-point gather (points.hip) --------------------------------------------------------

@@ -109,63 +109,13 @@ __global__ void k_coarse_z(pnr_render_params prm, const float* __restrict__ ro, 
 //                        float64 points and bound test;
 //   other rows < rows    padding: (0, 0, 0, outside).
 // x4 row = (x, y, z, inside ? 1 : 0) float32: the MLP input (kPtsX4) and its saved copy at once.
-__global__ void k_map_pts(pnr_render_params prm, const float* __restrict__ ro, const float* __restrict__ rd,
-                          const float* __restrict__ gt, const float* __restrict__ t_rand,
-                          const float* __restrict__ gmax, int64_t n_rays, int64_t pr, int64_t rows,
-                          double* __restrict__ zc, double* __restrict__ far_out, float4* __restrict__ x4) {
+__global__ void k_map_pts(MapRowsArgs m, int64_t rows, float4* __restrict__ x4) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= rows) return;
-  const int S = prm.n_samples;
-  float4 out = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (e < n_rays * S) {  // regulation (k_reg_z, load_point<kRaysZ32>)
-    const int64_t n = e / S;
-    const int s = (int)(e - n * S);
-    const float far = gt[n] * 0.85f;
-    auto z0 = [&](int k) { return (0.0f * (1.f - prm.t_vals[k])) + far * prm.t_vals[k]; };
-    const float zs = z0(s);
-    const float lower = s > 0 ? .5f * (zs + z0(s - 1)) : zs;
-    const float upper = s < S - 1 ? .5f * (z0(s + 1) + zs) : zs;
-    const float z = lower + (upper - lower) * t_rand[e];
-    const float x0 = ro[n * 3 + 0] + rd[n * 3 + 0] * z;
-    const float x1 = ro[n * 3 + 1] + rd[n * 3 + 1] * z;
-    const float x2 = ro[n * 3 + 2] + rd[n * 3 + 2] * z;
-    const bool inside = (x0 < (float)prm.bound[1]) && (x0 > (float)prm.bound[0]) && (x1 < (float)prm.bound[3]) &&
-                        (x1 > (float)prm.bound[2]) && (x2 < (float)prm.bound[5]) && (x2 > (float)prm.bound[4]);
-    out = make_float4(x0, x1, x2, inside ? 1.f : 0.f);
-  } else if (e >= pr && e < pr + n_rays * S) {  // render coarse (k_coarse_z, load_point<kRaysZ64>)
-    const int64_t q = e - pr;
-    const int64_t n = q / S;
-    const int s = (int)(q - n * S);
-    double fb = 0.0;
-    for (int a = 0; a < 3; ++a) {
-      const double o = (double)ro[n * 3 + a], d = (double)rd[n * 3 + a];
-      const double t0 = (prm.bound[2 * a] - o) / d;
-      const double t1 = (prm.bound[2 * a + 1] - o) / d;
-      const double mx = max_nan(t0, t1);
-      fb = a == 0 ? mx : min_nan(fb, mx);
-    }
-    fb = fb + 0.01;
-    const double hi = prm.far_mode == 1 ? prm.far_clamp : (double)(*gmax);
-    double far = fb != fb ? fb : (fb < 0.0 ? 0.0 : fb);  // clamp(min=0)
-    far = far != far ? far : (far > hi ? hi : far);
-    const float nearf = gt[n] * 0.01f;
-    if (s == 0 && far_out) far_out[n] = far;
-    const float t = prm.t_vals[s];
-    double zz;
-    if (!prm.lindisp) {
-      zz = (double)(nearf * (1.f - t)) + far * (double)t;
-    } else {
-      zz = 1.0 / ((double)((1.f / nearf) * (1.f - t)) + (1.0 / far) * (double)t);
-    }
-    zc[q] = zz;
-    const double q0 = (double)ro[n * 3 + 0] + (double)rd[n * 3 + 0] * zz;
-    const double q1 = (double)ro[n * 3 + 1] + (double)rd[n * 3 + 1] * zz;
-    const double q2 = (double)ro[n * 3 + 2] + (double)rd[n * 3 + 2] * zz;
-    const bool inside = (q0 < prm.bound[1]) && (q0 > prm.bound[0]) && (q1 < prm.bound[3]) && (q1 > prm.bound[2]) &&
-                        (q2 < prm.bound[5]) && (q2 > prm.bound[4]);
-    out = make_float4((float)q0, (float)q1, (float)q2, inside ? 1.f : 0.f);
-  }
-  x4[e] = out;
+  float x0, x1, x2;
+  bool inside;
+  map_row_point(m, e, true, x0, x1, x2, inside);
+  x4[e] = make_float4(x0, x1, x2, inside ? 1.f : 0.f);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1299,12 +1249,32 @@ int launch_pdf(const pnr_render_params& prm, const float* rd, const double* zc, 
     hipLaunchKernelGGL((k_pdf<0, 0>), dim3(nblk(n, 64)), dim3(64), 0, st, prm, rd, zc, (const float4*)rawc, n, zi, mp);
   return hip_status(hipGetLastError());
 }
+MapRowsArgs map_rows_args(const pnr_render_params& prm, const float* ro, const float* rd, const float* gt,
+                          const float* t_rand, const float* gmax, int64_t n, int64_t pr, double* zc, double* far_out) {
+  MapRowsArgs m{};
+  m.ro = ro;
+  m.rd = rd;
+  m.gt = gt;
+  m.t_rand = t_rand;
+  m.gmax = gmax;
+  m.n_rays = n;
+  m.pr = pr;
+  m.zc = zc;
+  m.far_out = far_out;
+  for (int i = 0; i < 6; ++i) m.bound[i] = prm.bound[i];
+  m.far_clamp = prm.far_clamp;
+  m.far_mode = prm.far_mode;
+  m.lindisp = prm.lindisp;
+  m.n_samples = prm.n_samples;
+  for (int i = 0; i < PNR_MAX_SAMPLES; ++i) m.t_vals[i] = prm.t_vals[i];
+  return m;
+}
 int launch_map_pts(const pnr_render_params& prm, const float* ro, const float* rd, const float* gt, const float* t_rand,
                    const float* gmax, int64_t n, int64_t pr, int64_t rows, double* zc, double* far_out, float* x4,
                    hipStream_t st) {
   if (rows <= 0) return 0;
-  hipLaunchKernelGGL(k_map_pts, dim3(nblk(rows, 256)), dim3(256), 0, st, prm, ro, rd, gt, t_rand, gmax, n, pr, rows, zc,
-                     far_out, (float4*)x4);
+  const MapRowsArgs m = map_rows_args(prm, ro, rd, gt, t_rand, gmax, n, pr, zc, far_out);
+  hipLaunchKernelGGL(k_map_pts, dim3(nblk(rows, 256)), dim3(256), 0, st, m, rows, (float4*)x4);
   return hip_status(hipGetLastError());
 }
 int launch_fine(const pnr_render_params& prm, const float* rd, const double* zc, const double* zi,

@@ -34,8 +34,8 @@ def per_launch(d):
 
 
 def family(name):
-    if 'k_mlp_fwd16w<' in name:  # the 16-point-wave forward (csrc/mlp16w.h): template argument = save mode
-        sv = name.split('<')[1].split('>')[0].strip()
+    if 'k_mlp_fwd16w<' in name:  # the 16-point-wave forward (csrc/mlp16w.h): <save mode, waves>
+        sv = name.split('<')[1].split('>')[0].split(',')[0].strip()
         return {'1': 'k_mlp_fwd16_train', '2': 'k_mlp_fwd16_masks'}.get(sv, 'k_mlp_fwd16_eval')
     if 'k_mlp_fwd16<' in name:  # last template argument: save mode (true / 1 training, 2 masks only)
         sv = name.split('>')[0].split(',')[-1].strip()
