@@ -478,9 +478,18 @@ __global__ __launch_bounds__(64) void k_pdf_w(pnr_render_params prm, const float
   const int lq = l < S ? l : S - 1;  // clamped, unconditional loads (lanes >= S are never read)
   const double z = zc[n * S + lq];
   const float sg = rawc[n * S + lq].w;
+  // the ray's own rows in the same round trip (after the barrier they would wait alone)
+  const float nrm = ray_norm(rd + n * 3);
+  double ro3[3] = {0.0, 0.0, 0.0}, rd3[3] = {0.0, 0.0, 0.0};
+  if (mp.x4i) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      ro3[k] = (double)mp.ro[n * 3 + k];
+      rd3[k] = (double)rd[n * 3 + k];
+    }
+  }
   zs[l] = z;
   __syncthreads();
-  const float nrm = ray_norm(rd + n * 3);
   const float dz = l < S - 1 ? (float)(zs[l + 1] - z) : 1e10f;
   const float delta = dz * nrm;
   const float a = 1.f - expf(-relu(sg) * delta);
@@ -519,9 +528,9 @@ __global__ __launch_bounds__(64) void k_pdf_w(pnr_render_params prm, const float
   const double zz = b0 + (double)t * (b1 - b0);
   zi[n * I + l] = zz;
   if (mp.x4i) {
-    const double q0 = (double)mp.ro[n * 3 + 0] + (double)rd[n * 3 + 0] * zz;
-    const double q1 = (double)mp.ro[n * 3 + 1] + (double)rd[n * 3 + 1] * zz;
-    const double q2 = (double)mp.ro[n * 3 + 2] + (double)rd[n * 3 + 2] * zz;
+    const double q0 = ro3[0] + rd3[0] * zz;
+    const double q1 = ro3[1] + rd3[1] * zz;
+    const double q2 = ro3[2] + rd3[2] * zz;
     const bool inside = (q0 < prm.bound[1]) && (q0 > prm.bound[0]) && (q1 < prm.bound[3]) && (q1 > prm.bound[2]) &&
                         (q2 < prm.bound[5]) && (q2 > prm.bound[4]);
     mp.x4i[n * I + l] = make_float4((float)q0, (float)q1, (float)q2, inside ? 1.f : 0.f);
@@ -857,6 +866,7 @@ __global__ __launch_bounds__(256) void k_fine_loss_w(pnr_render_params prm, cons
   const int64_t rr = n * S + (l < S ? l : S - 1);
   const float sg = fl.rawr[rr].w;
   const float ir = fl.insr[rr].w;
+  const float nrm = ray_norm(rd + n * 3);  // (in this round trip: after the barriers below it would wait alone)
   zn[l] = zl;
   cr_[wv][l] = cl;
   ci_[wv][l] = il;
@@ -876,7 +886,6 @@ __global__ __launch_bounds__(256) void k_fine_loss_w(pnr_render_params prm, cons
   const double zq = zn[s];
   const double znx = l + 1 < M ? zn[os[l + 1]] : 0.0;
   const float4 c = cr_[wv][s];  // lanes >= M: s = 0, never read
-  const float nrm = ray_norm(rd + n * 3);
   const float dz = l < M - 1 ? (float)(znx - zq) : 1e10f;
   const float delta = dz * nrm;
   const float sr = relu(c.w);
@@ -913,6 +922,19 @@ __global__ __launch_bounds__(256) void k_fine_loss_w(pnr_render_params prm, cons
     const double ls = (double)(fl.w_reg * fabsf(sg));
     for (int q = 0; q < S; ++q) Lr += rld(ls, q);
   }
+  // ---- the loss hand-off, issued now so its round trips run under the compositing backward: the
+  // block partial as an 8-B agent atomic, read back by 8-B agent atomics (MI355X_MICROARCH.md, valid
+  // hand-off forms: no L2 write-back per block, which a release fence would cost), then the ticket;
+  // the block that takes the last ticket adds the partials in order at the end
+  if (l == 0) red[wv] = live ? Lr : 0.0;
+  __syncthreads();
+  uint32_t tk = 0u;
+  if (threadIdx.x == 0) {
+    const double pb = ((red[0] + red[1]) + red[2]) + red[3];
+    atomicExch(reinterpret_cast<unsigned long long*>(fl.part) + blockIdx.x, __double_as_longlong(pb));
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    tk = atomicAdd(fl.ticket, 1u);
+  }
   // ---- k_fine_bwd_w with g_var = 0, from the forward's values
   const bool act = l < M;
   const bool inside = act && ci_[wv][s] != 0.f;
@@ -941,18 +963,8 @@ __global__ __launch_bounds__(256) void k_fine_loss_w(pnr_render_params prm, cons
     if (s < S) goc[n * S + s] = go; else goi[n * I + (s - S)] = go;
   }
   if (live && g_nrm && l == 0) g_nrm[n] = gn;
-  // ---- the loss: block partial, then the last block adds the partials in order (k_map_loss's hand-off)
-  if (l == 0) red[wv] = live ? Lr : 0.0;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    // the partial as an 8-B agent atomic, read back by 8-B agent atomics (MI355X_MICROARCH.md, valid
-    // hand-off forms): no L2 write-back per block, which a release fence would cost
-    const double pb = ((red[0] + red[1]) + red[2]) + red[3];
-    atomicExch(reinterpret_cast<unsigned long long*>(fl.part) + blockIdx.x, __double_as_longlong(pb));
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const uint32_t t = atomicAdd(fl.ticket, 1u);
-    last = t == gridDim.x - 1 ? 1u : 0u;
-  }
+  // ---- the loss: the last block adds the partials in order (k_map_loss's hand-off)
+  if (threadIdx.x == 0) last = tk == gridDim.x - 1 ? 1u : 0u;
   __syncthreads();
   if (!last) return;
   double v = 0.0;
