@@ -66,6 +66,16 @@ ALGO_PEAK_TF = {'fp32': FP32_MFMA_PEAK_TF, 'f16x3': F16_MFMA_PEAK_TF / 3, 'bf16x
 HBM_PEAK_GBS = 8000.0
 FLOP_PER_POINT_FWD = 443438        # 2 x (279 + 23,808 + 3 x 65,536 + 1,024) MAC
 FLOP_PER_POINT_BWD = 442880        # delta chain: 2 x (1,024 + 3 x 65,536 + 23,808) MAC
+# the grouped weight-gradient launch (k_wgrad16_group, with the skinny dWo / dB jobs): algorithmic fp32
+# operand bytes per training point (profiles/r06_traffic.json: W3 h3 1,024 + g_out 16 + h4 mask words 32;
+# W2, W1 delta 1,024 + h 1,024 each; W0 delta1 1,024 + x 16; dWo h4 1,024 + g_out 16; dB g_arg 384 + x 16)
+# and with the feature branch + the four fc_c GEMMs (dL/dh_l 1,024 + c 128 for l < 3; dWc_3 rebuilds its
+# A from g_out: 16 + 128).  Its FLOP per point over those bytes (58.5; 45.5 with fc_c) is below the
+# machine balance (833 TF / 8 TB/s = 104 FLOP/B): the launch sits on the HBM side of the roofline
+WGRAD_B_PER_POINT = 7580
+WGRAD_FC_B_PER_POINT = 3 * (1024 + 128) + (16 + 128)
+WGRAD_FLOP_PER_POINT = 443430
+WGRAD_FC_FLOP_PER_POINT = 4 * 2 * 256 * 32
 W, H = 640, 480
 FX, FY, CX, CY = 577.59, 578.73, 318.91, 242.68   # configs/ScanNet/scannet.yaml:30-35
 
@@ -375,12 +385,15 @@ def timed(step, steps, warmup, ddp, lib):
     return el, kt
 
 
-def kernel_roofline(kt, prec, el_s, traffic_units=True):
+def kernel_roofline(kt, prec, el_s, traffic_units=True, fc=False):
     """Roofline of the dominant hand-written kernel of the step -- the one with the most device time
-    among the fused forward, the delta chain and the grouped weight-gradient launch -- per launch:
-    algorithmic fp32-equivalent FLOP per launch / mean launch time.  The MLP kernels count FLOP per
-    point x points; the grouped launch counts its GEMMs' multiply-adds (pnr_timing_read kind 6: units
-    of 65,536 MACs = 131,072 FLOP)."""
+    among the fused forward, the delta chain and the grouped weight-gradient launch -- per launch.
+    The MLP kernels (arithmetic intensity above the machine balance) on the MFMA roof: algorithmic
+    fp32-equivalent FLOP per point x points / mean launch time.  The grouped weight-gradient launch
+    (58.5 FLOP per byte of fp32 operands, 45.5 with fc_c: below the 104 of 833 TF / 8 TB/s) on the HBM
+    roof: algorithmic operand bytes per point x the delta chain's points / mean launch time, with its
+    fraction of the split MFMA peak beside it (its MACs from pnr_timing_read kind 6: units of 65,536
+    MACs = 131,072 FLOP)."""
     best = None
     for name, (launches, ms, units) in kt.items():
         if name not in ('mlp_fwd', 'mlp_bwd', 'wgrad_group'):
@@ -407,6 +420,20 @@ def kernel_roofline(kt, prec, el_s, traffic_units=True):
             'k_mlp_bwd': 'k_mlp_bwd',
             'k_mlp_bwd16': 'k_mlp_bwd16', 'k_wgrad16_group': 'k_wgrad16_group'}
     traffic = pmc_traffic(tkey[best['kernel']], best['points']) if traffic_units and best['points'] else None
+    if best['kernel'] == 'k_wgrad16_group' and best['points']:
+        bpp = WGRAD_B_PER_POINT + (WGRAD_FC_B_PER_POINT if fc else 0)
+        fpp = WGRAD_FLOP_PER_POINT + (WGRAD_FC_FLOP_PER_POINT if fc else 0)
+        gbs = bpp * best['points'] / (best['avg_ms'] * 1e-3) / 1e9
+        return {'bound': 'hbm', 'achieved': round(gbs, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                'frac': round(gbs / HBM_PEAK_GBS, 4), 'traffic': traffic,
+                'kernel': best['kernel'], 'avg_launch_ms': round(best['avg_ms'], 3), 'launches': best['launches'],
+                'kernel_share_of_step': round(best['share_of_step'], 3),
+                'byte_basis': f'algorithmic fp32 operand bytes, {bpp:,} per training point x {best["points"]:,.0f} '
+                              'points per launch (bench.py WGRAD_B_PER_POINT); traffic = PMC bytes per launch',
+                'arithmetic_intensity': round(fpp / bpp, 1), 'ridge_flop_per_byte': round(best['peak'] * 1e3 /
+                                                                                         HBM_PEAK_GBS, 1),
+                'achieved_tflops': round(best['achieved'], 2),
+                'frac_of_split_peak': round(best['achieved'] / best['peak'], 4)}
     return {'bound': 'mfma', 'achieved': round(best['achieved'], 2), 'peak': round(best['peak'], 1),
             'unit': 'TFLOP/s', 'frac': round(best['achieved'] / best['peak'], 4), 'traffic': traffic,
             'kernel': best['kernel'], 'avg_launch_ms': round(best['avg_ms'], 3), 'launches': best['launches'],
@@ -705,7 +732,7 @@ def map_points_extra(pnr, plib, slam, params, bound, pose, dev, ddp, lib, n=W * 
     out = {'workload': 'S-map with neural points: c_dim=32 decoder, IDW k=8 r=2 mm gather, fc_c injection, '
                        'feature + decoder Adam', 'rays': n, 'points': int(xyz.shape[0]),
            'value': round(n * steps / el, 1), 'unit': 'rays/s', 'ms_per_step': round(el / steps * 1e3, 3),
-           'steps': steps, 'roofline': kernel_roofline(kt, prec, el, traffic_units=False),
+           'steps': steps, 'roofline': kernel_roofline(kt, prec, el, traffic_units=False, fc=True),
            'kernel_rooflines': kernel_table(kt, prec, el, steps, fc=True),
            'kernels': {k: {'launches': v[0], 'ms': round(v[1], 3), 'units': v[2]} for k, v in kt.items()}}
     if 'gather_bwd' in kt:
