@@ -661,20 +661,66 @@ __global__ __launch_bounds__(64 * kRedWaves) void k_part_reduce(const float* __r
 struct ReduceJobs {
   ReduceJob j[kMaxReduceJobs];
   int first[kMaxReduceJobs + 1];  // first block of each job; first[n] = grid
+  int vec[kMaxReduceJobs];        // 1: the job's elements go 4 per lane (float4 partial rows)
   int n;
 };
 
 // every job of a backward chunk in one launch: block b belongs to the job whose block range holds it,
-// then the same fixed-order reduction as k_part_reduce
+// then the same fixed-order reduction as k_part_reduce.  A job whose partial rows are whole float4s
+// (nr pw and pw multiples of 4, 16-B aligned regions: every GEMM job) runs 4 consecutive elements per
+// lane, 256 per block -- the same chains and order per element, a quarter of the blocks and load
+// instructions (the partial tiles are the launch's bytes: 55 MB at the room0 batch)
 __global__ __launch_bounds__(64 * kRedWaves) void k_part_reduce_multi(ReduceJobs J) {
-  __shared__ float red[kRedWaves][64];
+  __shared__ float4 red[kRedWaves][64];
   int q = 0;
   while (q + 1 < J.n && (int)blockIdx.x >= J.first[q + 1]) ++q;
   const ReduceJob& jb = J.j[q];
   const int lane = threadIdx.x & 63, v = threadIdx.x >> 6;
   const int64_t E = (int64_t)jb.nr * jb.pw;
-  const int64_t nmain = (E + 63) / 64;
   const int64_t blk = (int64_t)blockIdx.x - J.first[q];
+  if (J.vec[q]) {
+    const int64_t nmain = (E + 255) / 256;
+    const bool is_bias = blk >= nmain;
+    const int64_t e = (is_bias ? blk - nmain : blk) * 256 + 4 * lane;
+    const float* src = is_bias ? jb.pbias : jb.part;
+    const int64_t stride = is_bias ? jb.nr : E;
+    const bool any = is_bias ? (jb.bias != nullptr && e < jb.nr) : e < E;  // all 4 in range (E, nr: x 4)
+    float4 s0 = make_float4(0.f, 0.f, 0.f, 0.f), s1 = s0;
+    if (any) {
+      int g = v;
+#pragma unroll 4
+      for (; g + kRedWaves < jb.nwg; g += 2 * kRedWaves) {
+        const float4 a = *reinterpret_cast<const float4*>(src + (int64_t)g * stride + e);
+        const float4 b = *reinterpret_cast<const float4*>(src + (int64_t)(g + kRedWaves) * stride + e);
+        s0.x += a.x; s0.y += a.y; s0.z += a.z; s0.w += a.w;
+        s1.x += b.x; s1.y += b.y; s1.z += b.z; s1.w += b.w;
+      }
+      if (g < jb.nwg) {
+        const float4 a = *reinterpret_cast<const float4*>(src + (int64_t)g * stride + e);
+        s0.x += a.x; s0.y += a.y; s0.z += a.z; s0.w += a.w;
+      }
+    }
+    red[v][lane] = make_float4(s0.x + s1.x, s0.y + s1.y, s0.z + s1.z, s0.w + s1.w);
+    __syncthreads();
+    if (v == 0 && any) {
+      float4 t = red[0][lane];
+#pragma unroll
+      for (int i = 1; i < kRedWaves; ++i) {
+        const float4 u = red[i][lane];
+        t.x += u.x; t.y += u.y; t.z += u.z; t.w += u.w;
+      }
+      const float sv[4] = {t.x, t.y, t.z, t.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int64_t ek = e + k;
+        if (!is_bias && (int)(ek % jb.pw) >= jb.nb) continue;  // padding columns (W0: 93 of 96)
+        float* dst = is_bias ? jb.bias + ek : jb.C + (ek / jb.pw) * jb.ldc + ek % jb.pw;
+        *dst = (jb.overwrite ? 0.f : *dst) + sv[k];
+      }
+    }
+    return;
+  }
+  const int64_t nmain = (E + 63) / 64;
   const bool is_bias = blk >= nmain;
   const int64_t e = (is_bias ? blk - nmain : blk) * 64 + lane;
   const float* src = is_bias ? jb.pbias : jb.part;
@@ -690,12 +736,12 @@ __global__ __launch_bounds__(64 * kRedWaves) void k_part_reduce_multi(ReduceJobs
     }
     if (g < jb.nwg) s0 += src[(int64_t)g * stride + e];
   }
-  red[v][lane] = s0 + s1;
+  red[v][lane].x = s0 + s1;
   __syncthreads();
   if (v == 0 && ok) {
-    float s = red[0][lane];
+    float s = red[0][lane].x;
 #pragma unroll
-    for (int i = 1; i < kRedWaves; ++i) s += red[i][lane];
+    for (int i = 1; i < kRedWaves; ++i) s += red[i][lane].x;
     float* dst = is_bias ? jb.bias + e : jb.C + (e / jb.pw) * jb.ldc + e % jb.pw;
     *dst = (jb.overwrite ? 0.f : *dst) + s;
   }
@@ -704,13 +750,20 @@ __global__ __launch_bounds__(64 * kRedWaves) void k_part_reduce_multi(ReduceJobs
 int launch_part_reduce_multi(const ReduceJob* jobs, int n, hipStream_t st) {
   if (n <= 0) return 0;
   if (n > kMaxReduceJobs) return PNR_E_ARG;
+  static const bool vec_ok = !(getenv("PNR_REDUCE_VEC") && getenv("PNR_REDUCE_VEC")[0] == '0');
   ReduceJobs J{};
   int blocks = 0;
   for (int i = 0; i < n; ++i) {
-    J.j[i] = jobs[i];
+    const ReduceJob& r = jobs[i];
+    J.j[i] = r;
     J.first[i] = blocks;
-    const int64_t nmain = ((int64_t)jobs[i].nr * jobs[i].pw + 63) / 64;
-    blocks += (int)(nmain + (jobs[i].bias ? (jobs[i].nr + 63) / 64 : 0));
+    const int64_t E = (int64_t)r.nr * r.pw;
+    const bool vec = vec_ok && E % 4 == 0 && r.pw % 4 == 0 && r.nr % 4 == 0 &&
+                     reinterpret_cast<uintptr_t>(r.part) % 16 == 0 &&
+                     (r.bias == nullptr || reinterpret_cast<uintptr_t>(r.pbias) % 16 == 0);
+    J.vec[i] = vec ? 1 : 0;
+    const int epb = vec ? 256 : 64;
+    blocks += (int)((E + epb - 1) / epb + (r.bias ? (r.nr + epb - 1) / epb : 0));
   }
   J.first[n] = blocks;
   J.n = n;
