@@ -105,17 +105,21 @@ def synth_batch(n, rank, pose, dev, seed=0):
     return (ro.contiguous().to(dev), rd.contiguous().to(dev), gt.to(dev), col.to(dev))
 
 
-def pmc_traffic(kernel, units_per_launch):
+def pmc_traffic(kernel, units_per_launch, workload=None):
     """HBM bytes per launch of `kernel` from the newest committed PMC measurement that holds it
     (profiles/r*_traffic.json, written by tools/traffic_json.py from separate FETCH_SIZE / WRITE_SIZE
     rocprofv3 passes): measured bytes per unit x units per launch, or None.  Files are ordered by
     name (round, then pass letter); a newer file measuring other kernels does not hide an older
     measurement of this one."""
     import glob
-    for f in sorted(glob.glob(os.path.join(REPO, 'profiles', 'r*_traffic.json')), reverse=True):
-        t = json.load(open(f)).get(kernel)
-        if t:
-            return round((t['fetch_B'] + t['write_B']) * units_per_launch)
+    files = sorted(glob.glob(os.path.join(REPO, 'profiles', 'r*_traffic*.json')), reverse=True)
+    # a measurement of this workload first (the room0 batch: its split-K partial tiles are a larger
+    # share of the grouped launch's bytes than at S-map), then any
+    for key in ([f'{kernel}@{workload}'] if workload else []) + [kernel]:
+        for f in files:
+            t = json.load(open(f)).get(key)
+            if t:
+                return round((t['fetch_B'] + t['write_B']) * units_per_launch)
     return None
 
 
@@ -385,7 +389,7 @@ def timed(step, steps, warmup, ddp, lib):
     return el, kt
 
 
-def kernel_roofline(kt, prec, el_s, traffic_units=True, fc=False):
+def kernel_roofline(kt, prec, el_s, traffic_units=True, fc=False, workload=None):
     """Roofline of the dominant hand-written kernel of the step -- the one with the most device time
     among the fused forward, the delta chain and the grouped weight-gradient launch -- per launch.
     The MLP kernels (arithmetic intensity above the machine balance) on the MFMA roof: algorithmic
@@ -419,7 +423,8 @@ def kernel_roofline(kt, prec, el_s, traffic_units=True, fc=False):
     tkey = {'k_mlp_fwd': 'k_mlp_fwd_train', 'k_mlp_fwd16': 'k_mlp_fwd16_train', 'k_mlp_fwd16w': 'k_mlp_fwd16_train',
             'k_mlp_bwd': 'k_mlp_bwd',
             'k_mlp_bwd16': 'k_mlp_bwd16', 'k_wgrad16_group': 'k_wgrad16_group'}
-    traffic = pmc_traffic(tkey[best['kernel']], best['points']) if traffic_units and best['points'] else None
+    traffic = (pmc_traffic(tkey[best['kernel']], best['points'], workload) if traffic_units and best['points']
+               else None)
     if best['kernel'] == 'k_wgrad16_group' and best['points']:
         bpp = WGRAD_B_PER_POINT + (WGRAD_FC_B_PER_POINT if fc else 0)
         fpp = WGRAD_FLOP_PER_POINT + (WGRAD_FC_FLOP_PER_POINT if fc else 0)
@@ -699,7 +704,7 @@ def room0_extra(pnr, params, bound, pose, dev, ddp, lib, steps=100, warmup=5, cp
                          + ('157.3 TF (fp32 MFMA)' if prec == 'fp32' else '833 TF (f16 MFMA / 3)'),
            'decoder_precision': prec, 'dtype': DTYPE[prec],
            'eager_ms_per_iter': round(el_e / 20 * 1e3, 4),
-           'roofline': kernel_roofline(kt, prec, el_e, traffic_units=prec != 'fp32'),
+           'roofline': kernel_roofline(kt, prec, el_e, traffic_units=prec != 'fp32', workload='room0'),
            'kernel_rooflines': kernel_table(kt, prec, el_e, 20) if prec != 'fp32' else None,
            'kernel_profile': 'profiles/r06_room0_timeline.txt, profiles/r06_room0_kernel_stats.csv (rocprofv3 of '
                              'the graph replay)'}
