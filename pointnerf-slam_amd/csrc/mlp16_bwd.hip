@@ -40,6 +40,9 @@ struct BwdGeo {
 #ifndef PNR_BWD_NBUF
 #define PNR_BWD_NBUF 4
 #endif
+  // (a 5-slot ring, 160 KiB, built in round 6 gave wrong f16x3 gradients -- up to 5% of max|g_x| --
+  // and no speed: tools/_r06ad.sh; the step program's waits are verified for at most 4 slots)
+  static_assert(PNR_BWD_NBUF >= 3 && PNR_BWD_NBUF <= 4, "delta-chain DMA ring: 3 or 4 slots");
   static constexpr int kNbuf = HASC ? 4 : PNR_BWD_NBUF;  // 5 x 36 KiB would not fit
   // PIPE: the forward's step pipeline (barrier + DMA mid-step, the next step's fragments read ahead).
   // The feature variant keeps one barrier + DMA at the top of each step: the pipeline spills 61
